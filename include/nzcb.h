@@ -1,0 +1,138 @@
+/*
+ * nzcb — MI355X-native PLONK prover for the nzcb circom circuit (C-ABI).
+ *
+ * This is the drop-in boundary under the reference's prover call:
+ *   snarkjs.plonk.prove(zkeyFileName, witnessFileName, logger)      [EXT] snarkjs 0.4.12
+ *   snarkjs.plonk.fullProve(input, wasmFile, zkeyFileName, logger)  [EXT]
+ * pinned at /root/reference/package.json:18 and /root/reference/yarn.lock:7279-7292,
+ * whose keys are produced at /root/reference/Makefile:54-62.
+ * The N-API addon in nzcb-circom_amd/js/ binds these functions one-to-one
+ * (see INTEGRATION.md). Plain pointers and sizes only; the caller owns every
+ * buffer; nothing is retained after a call returns.
+ *
+ * Byte layouts
+ *   zkey / wtns : snarkjs 0.4 binary files, unchanged.
+ *   proof       : NZCB_PROOF_BYTES = 9 G1 affine points (A,B,C,Z,T1,T2,T3,Wxi,Wxiw),
+ *                 each x||y as 32-byte little-endian normal-form integers
+ *                 (infinity = 64 zero bytes), then 7 Fr evaluations
+ *                 (eval_a,eval_b,eval_c,eval_s1,eval_s2,eval_zw,eval_r), 32 B LE each.
+ *   public      : nPublic x 32-byte LE Fr (= witness[1..nPublic]).
+ *   blinding    : 11 x 32-byte LE Fr (b1..b11) or NULL = all zero (deterministic).
+ *                 snarkjs draws them with Fr.random(); pass random bytes for
+ *                 zero-knowledge, fixed bytes for bit-exact tests.
+ */
+#ifndef NZCB_H
+#define NZCB_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NZCB_PROOF_BYTES (9 * 64 + 7 * 32)
+#define NZCB_BLINDING_BYTES (11 * 32)
+
+/* Error codes; messages reproduce the snarkjs 0.4.12 exception text. */
+enum {
+  NZCB_OK = 0,
+  NZCB_ERR_ARG = 1,
+  NZCB_ERR_FORMAT = 2,
+  NZCB_ERR_NOT_PLONK = 3,     /* "zkey file is not plonk" */
+  NZCB_ERR_CURVE = 4,         /* "Curve of the witness does not match the curve of the proving key" */
+  NZCB_ERR_WITNESS_LEN = 5,   /* "Invalid witness length. Circuit: ..., witness: ..., ..." */
+  NZCB_ERR_COPY = 6,          /* "Copy constraints does not match" */
+  NZCB_ERR_T_DIV = 7,         /* "T Polynomial is not divisible" */
+  NZCB_ERR_TZ = 8,            /* "Tz Polynomial is not well calculated" */
+  NZCB_ERR_DIVPOL = 9,        /* "Polinomial does not divide" */
+  NZCB_ERR_HIP = 10,
+  NZCB_ERR_INTERNAL = 11
+};
+
+typedef struct nzcb_err {
+  int code;
+  char msg[256];
+} nzcb_err;
+
+typedef struct nzcb_ctx nzcb_ctx;
+typedef void (*nzcb_log_fn)(void* user, const char* msg);
+
+/* Library identity / devices. */
+const char* nzcb_version(void);
+int nzcb_device_count(void);
+
+/* ---- Prover (replaces snarkjs plonk_prove) ---------- */
+
+/* Parse a snarkjs 0.4 PLONK zkey and upload it to `device` (HBM-resident,
+ * context-owned). Replaces the zkey read in snarkjs plonk_prove.js [EXT]. */
+nzcb_ctx* nzcb_ctx_create(const uint8_t* zkey, size_t zkey_len, int device, nzcb_err* err);
+void nzcb_ctx_destroy(nzcb_ctx* ctx);
+
+/* Optional progress logger (snarkjs `logger.debug` lines). */
+void nzcb_ctx_set_logger(nzcb_ctx* ctx, nzcb_log_fn fn, void* user);
+
+/* Include the public inputs in the beta transcript (1, default)
+ * or hash A||B||C only (0). */
+void nzcb_ctx_set_transcript_public(nzcb_ctx* ctx, int on);
+
+/* Context facts: domain size, nPublic, nVars, nAdditions, nConstraints. */
+int nzcb_ctx_info(const nzcb_ctx* ctx, uint32_t out[5]);
+
+/* One proof. wtns = snarkjs .wtns bytes. proof_out: NZCB_PROOF_BYTES.
+ * pub_out: pub_cap >= 32 * nPublic bytes. Returns NZCB_OK or an error code. */
+int nzcb_prove(nzcb_ctx* ctx, const uint8_t* wtns, size_t wtns_len, const uint8_t* blinding, uint8_t* proof_out,
+               uint8_t* pub_out, size_t pub_cap, nzcb_err* err);
+
+/* Same with the witness given as nWitness x 32-byte LE field elements (no file header). */
+int nzcb_prove_witness(nzcb_ctx* ctx, const uint8_t* witness, size_t n_witness, const uint8_t* blinding,
+                       uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_err* err);
+
+/* Wall-clock milliseconds of the last proof's phases:
+ * [0] total [1] witness upload+additions+ABC [2] round1 [3] round2 [4] round3 [5] round4 [6] round5
+ * [7] all MSMs [8] all NTTs. Returns the number of values written. */
+int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap);
+
+/* snarkjs-format JSON ({proof}, [publicSignals]) from the binary outputs. */
+int nzcb_proof_to_json(const uint8_t* proof, char* out, size_t cap);
+int nzcb_public_to_json(const uint8_t* pub, int n_public, char* out, size_t cap);
+
+/* ---- Synthetic circuit + setup ------- */
+/* Builds the seeded synthetic circuit of oracle/synth.py and its snarkjs-0.4
+ * PLONK zkey with trapdoor tau (32-byte LE normal) on `device`. Buffers are
+ * malloc'ed by the library; free them with nzcb_free. */
+int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints,
+                     const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len, uint8_t** wtns_out,
+                     size_t* wtns_len, nzcb_err* err);
+void nzcb_free(void* p);
+
+/* ---- Kernel-level entry points (tests / microbench) */
+typedef struct nzcb_engine nzcb_engine;
+nzcb_engine* nzcb_engine_create(int device, int max_log_ntt, size_t max_msm_points, nzcb_err* err);
+void nzcb_engine_destroy(nzcb_engine* e);
+/* Host-buffer variants. Field elements are 32-byte LE Montgomery ("LEM", zkey layout). */
+int nzcb_engine_ntt(nzcb_engine* e, const uint8_t* in_lem, uint8_t* out_lem, int log_n, int inverse, nzcb_err* err);
+/* bases: n x 64-byte LEM affine; scalars: n x 32 B LE (Montgomery if scalars_mont);
+ * out: 64-byte affine x||y LE normal (infinity = zeros). */
+int nzcb_engine_msm(nzcb_engine* e, const uint8_t* bases_lem, const uint8_t* scalars, size_t n, int scalars_mont,
+                    uint8_t* out_affine, nzcb_err* err);
+/* Device-resident variants for benchmarks (pointers from nzcb_dev_alloc). */
+void* nzcb_dev_alloc(size_t bytes);
+void nzcb_dev_free(void* p);
+int nzcb_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int nzcb_memcpy_d2h(void* dst, const void* src, size_t bytes);
+int nzcb_engine_ntt_dev(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, nzcb_err* err);
+int nzcb_engine_msm_dev(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
+                        uint8_t* out_affine, nzcb_err* err);
+/* Average milliseconds per call of `reps` back-to-back device NTTs, timed with HIP
+ * events on the engine's stream. */
+int nzcb_engine_time_ntt(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, int reps, double* ms,
+                         nzcb_err* err);
+/* Field self-test helpers: out[i] = a[i] * b[i] (Montgomery, device), n elements. */
+int nzcb_engine_fr_mul(nzcb_engine* e, const uint8_t* a_lem, const uint8_t* b_lem, uint8_t* out_lem, size_t n,
+                       int field_q, nzcb_err* err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,196 @@
+// C-ABI: engine, device memory and kernel-level entry points (include/nzcb.h).
+#include <cstring>
+#include <vector>
+
+#include "../../include/nzcb.h"
+#include "engine.h"
+
+namespace nzcb {
+
+Engine::Engine(int dev, int max_log_ntt, size_t max_msm_points) : device(dev) {
+  NZ_HIP(hipSetDevice(dev));
+  NZ_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  if (max_log_ntt >= 0) ntt_tables.init(max_log_ntt, stream);
+  if (max_msm_points) msm_scratch.init(max_msm_points);
+}
+
+Engine::~Engine() {
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+void set_err(nzcb_err* err, int code, const char* msg) {
+  if (!err) return;
+  err->code = code;
+  std::snprintf(err->msg, sizeof(err->msg), "%s", msg);
+}
+
+}  // namespace nzcb
+
+using namespace nzcb;
+
+struct nzcb_engine {
+  Engine eng;
+  nzcb_engine(int d, int l, size_t m) : eng(d, l, m) {}
+};
+
+#define NZ_GUARD_BEGIN try {
+#define NZ_GUARD_END(err)                                   \
+  }                                                         \
+  catch (const nzcb::Error& e) {                            \
+    set_err(err, e.code, e.what());                         \
+    return e.code;                                          \
+  }                                                         \
+  catch (const std::exception& e) {                         \
+    set_err(err, NZCB_ERR_INTERNAL, e.what());              \
+    return NZCB_ERR_INTERNAL;                               \
+  }
+
+__global__ void fe_mul_kernel_r(const Fr* a, const Fr* b, Fr* o, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) o[i] = a[i] * b[i];
+}
+__global__ void fe_mul_kernel_q(const Fq* a, const Fq* b, Fq* o, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) o[i] = a[i] * b[i];
+}
+
+static void affine_out(const G1xyzz& r, uint8_t* out) {
+  G1Affine a = xyzz_to_affine(r);
+  Fq x = a.is_inf() ? Fq::zero() : from_mont(a.x);
+  Fq y = a.is_inf() ? Fq::zero() : from_mont(a.y);
+  std::memcpy(out, x.v, 32);
+  std::memcpy(out + 32, y.v, 32);
+}
+
+extern "C" {
+
+const char* nzcb_version(void) { return "nzcb-mi355x 0.1.0 (gfx950)"; }
+
+int nzcb_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void nzcb_free(void* p) { std::free(p); }
+
+nzcb_engine* nzcb_engine_create(int device, int max_log_ntt, size_t max_msm_points, nzcb_err* err) {
+  try {
+    return new nzcb_engine(device, max_log_ntt, max_msm_points);
+  } catch (const nzcb::Error& e) {
+    set_err(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+  }
+  return nullptr;
+}
+
+void nzcb_engine_destroy(nzcb_engine* e) { delete e; }
+
+void* nzcb_dev_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  return p;
+}
+void nzcb_dev_free(void* p) {
+  if (p) (void)hipFree(p);
+}
+int nzcb_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : NZCB_ERR_HIP;
+}
+int nzcb_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : NZCB_ERR_HIP;
+}
+
+int nzcb_engine_ntt_dev(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  ntt(g.ntt_tables, (const Fr*)in, (Fr*)out, log_n, inverse != 0, g.stream);
+  NZ_HIP(hipStreamSynchronize(g.stream));
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_engine_ntt(nzcb_engine* e, const uint8_t* in_lem, uint8_t* out_lem, int log_n, int inverse, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  size_t n = size_t(1) << log_n;
+  DevBuf<Fr> a(n), b(n);
+  NZ_HIP(hipMemcpyAsync(a.p, in_lem, n * 32, hipMemcpyHostToDevice, g.stream));
+  ntt(g.ntt_tables, a.p, b.p, log_n, inverse != 0, g.stream);
+  NZ_HIP(hipMemcpyAsync(out_lem, b.p, n * 32, hipMemcpyDeviceToHost, g.stream));
+  NZ_HIP(hipStreamSynchronize(g.stream));
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_engine_time_ntt(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, int reps, double* ms,
+                         nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  hipEvent_t e0, e1;
+  NZ_HIP(hipEventCreate(&e0));
+  NZ_HIP(hipEventCreate(&e1));
+  NZ_HIP(hipEventRecord(e0, g.stream));
+  for (int i = 0; i < reps; i++) ntt(g.ntt_tables, (const Fr*)in, (Fr*)out, log_n, inverse != 0, g.stream);
+  NZ_HIP(hipEventRecord(e1, g.stream));
+  NZ_HIP(hipEventSynchronize(e1));
+  float t = 0;
+  NZ_HIP(hipEventElapsedTime(&t, e0, e1));
+  *ms = t / (reps > 0 ? reps : 1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_engine_msm_dev(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
+                        uint8_t* out_affine, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  G1xyzz r = msm(g.msm_scratch, (const G1Affine*)bases, (const Fr*)scalars, n, scalars_mont != 0, g.stream);
+  affine_out(r, out_affine);
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_engine_msm(nzcb_engine* e, const uint8_t* bases_lem, const uint8_t* scalars, size_t n, int scalars_mont,
+                    uint8_t* out_affine, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  DevBuf<G1Affine> b(n ? n : 1);
+  DevBuf<Fr> s(n ? n : 1);
+  NZ_HIP(hipMemcpyAsync(b.p, bases_lem, n * 64, hipMemcpyHostToDevice, g.stream));
+  NZ_HIP(hipMemcpyAsync(s.p, scalars, n * 32, hipMemcpyHostToDevice, g.stream));
+  G1xyzz r = msm(g.msm_scratch, b.p, s.p, n, scalars_mont != 0, g.stream);
+  affine_out(r, out_affine);
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_engine_fr_mul(nzcb_engine* e, const uint8_t* a_lem, const uint8_t* b_lem, uint8_t* out_lem, size_t n,
+                       int field_q, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  DevBuf<Fr> a(n), b(n), o(n);
+  NZ_HIP(hipMemcpyAsync(a.p, a_lem, n * 32, hipMemcpyHostToDevice, g.stream));
+  NZ_HIP(hipMemcpyAsync(b.p, b_lem, n * 32, hipMemcpyHostToDevice, g.stream));
+  if (field_q)
+    hipLaunchKernelGGL(fe_mul_kernel_q, dim3(grid_for(n, 256)), dim3(256), 0, g.stream, (const Fq*)a.p,
+                       (const Fq*)b.p, (Fq*)o.p, n);
+  else
+    hipLaunchKernelGGL(fe_mul_kernel_r, dim3(grid_for(n, 256)), dim3(256), 0, g.stream, a.p, b.p, o.p, n);
+  NZ_HIP(hipGetLastError());
+  NZ_HIP(hipMemcpyAsync(out_lem, o.p, n * 32, hipMemcpyDeviceToHost, g.stream));
+  NZ_HIP(hipStreamSynchronize(g.stream));
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+}  // extern "C"

@@ -1,0 +1,166 @@
+// C-ABI: prover context, proofs and snarkjs-format JSON (include/nzcb.h).
+#include <cstring>
+#include <string>
+
+#include "../../include/nzcb.h"
+#include "prover.h"
+
+namespace nzcb {
+void set_err(nzcb_err* err, int code, const char* msg);
+}
+using namespace nzcb;
+
+struct nzcb_ctx {
+  std::unique_ptr<Prover> p;
+  nzcb_log_fn log_fn = nullptr;
+  void* log_user = nullptr;
+};
+
+namespace {
+
+int fail(nzcb_err* err, int code, const char* msg) {
+  set_err(err, code, msg);
+  return code;
+}
+
+std::string dec_le(const uint8_t* le32) {
+  uint32_t v[8];
+  std::memcpy(v, le32, 32);
+  std::string s;
+  bool nz = true;
+  while (nz) {
+    uint64_t rem = 0;
+    nz = false;
+    for (int i = 7; i >= 0; i--) {
+      uint64_t cur = (rem << 32) | v[i];
+      v[i] = (uint32_t)(cur / 10);
+      rem = cur % 10;
+      if (v[i]) nz = true;
+    }
+    s.push_back((char)('0' + rem));
+  }
+  return std::string(s.rbegin(), s.rend());
+}
+
+bool all_zero(const uint8_t* p, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (p[i]) return false;
+  return true;
+}
+
+std::string g1_json(const uint8_t* p) {
+  if (all_zero(p, 64)) return "[\"0\",\"1\",\"0\"]";
+  return "[\"" + dec_le(p) + "\",\"" + dec_le(p + 32) + "\",\"1\"]";
+}
+
+int copy_out(const std::string& s, char* out, size_t cap) {
+  if (!out || cap < s.size() + 1) return (int)(s.size() + 1);
+  std::memcpy(out, s.c_str(), s.size() + 1);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+nzcb_ctx* nzcb_ctx_create(const uint8_t* zkey, size_t zkey_len, int device, nzcb_err* err) {
+  try {
+    auto* c = new nzcb_ctx();
+    c->p.reset(new Prover(zkey, zkey_len, device));
+    if (err) err->code = 0;
+    return c;
+  } catch (const Error& e) {
+    set_err(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+  }
+  return nullptr;
+}
+
+void nzcb_ctx_destroy(nzcb_ctx* ctx) { delete ctx; }
+
+void nzcb_ctx_set_logger(nzcb_ctx* ctx, nzcb_log_fn fn, void* user) {
+  if (!ctx) return;
+  ctx->log_fn = fn;
+  ctx->log_user = user;
+  if (fn)
+    ctx->p->log = [ctx](const std::string& m) { ctx->log_fn(ctx->log_user, m.c_str()); };
+  else
+    ctx->p->log = nullptr;
+}
+
+void nzcb_ctx_set_transcript_public(nzcb_ctx* ctx, int on) {
+  if (ctx) ctx->p->transcript_public = on != 0;
+}
+
+int nzcb_ctx_info(const nzcb_ctx* ctx, uint32_t out[5]) {
+  if (!ctx || !out) return NZCB_ERR_ARG;
+  const Prover& p = *ctx->p;
+  out[0] = p.n;
+  out[1] = p.nPublic;
+  out[2] = p.nVars;
+  out[3] = p.nAdditions;
+  out[4] = p.nConstraints;
+  return 0;
+}
+
+int nzcb_prove_witness(nzcb_ctx* ctx, const uint8_t* witness, size_t n_witness, const uint8_t* blinding,
+                       uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_err* err) {
+  if (!ctx || !witness || !proof_out) return fail(err, NZCB_ERR_ARG, "null argument");
+  if (pub_cap < 32 * (size_t)ctx->p->nPublic || (!pub_out && ctx->p->nPublic))
+    return fail(err, NZCB_ERR_ARG, "public output buffer too small");
+  try {
+    ctx->p->prove(witness, n_witness, blinding, proof_out, pub_out);
+    if (err) err->code = 0;
+    return 0;
+  } catch (const Error& e) {
+    return fail(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, NZCB_ERR_INTERNAL, e.what());
+  }
+}
+
+int nzcb_prove(nzcb_ctx* ctx, const uint8_t* wtns, size_t wtns_len, const uint8_t* blinding, uint8_t* proof_out,
+               uint8_t* pub_out, size_t pub_cap, nzcb_err* err) {
+  if (!ctx || !wtns) return fail(err, NZCB_ERR_ARG, "null argument");
+  try {
+    Wtns w = parse_wtns(wtns, wtns_len);
+    if (!w.q_is_r)
+      return fail(err, NZCB_ERR_CURVE, "Curve of the witness does not match the curve of the proving key");
+    return nzcb_prove_witness(ctx, w.values, w.nWitness, blinding, proof_out, pub_out, pub_cap, err);
+  } catch (const Error& e) {
+    return fail(err, e.code, e.what());
+  }
+}
+
+int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap) {
+  if (!ctx || !ms) return 0;
+  int k = cap < 9 ? cap : 9;
+  for (int i = 0; i < k; i++) ms[i] = ctx->p->tm[i];
+  return k;
+}
+
+int nzcb_proof_to_json(const uint8_t* proof, char* out, size_t cap) {
+  if (!proof) return -1;
+  static const char* pts[7] = {"A", "B", "C", "Z", "T1", "T2", "T3"};
+  static const char* evs[7] = {"eval_a", "eval_b", "eval_c", "eval_s1", "eval_s2", "eval_zw", "eval_r"};
+  std::string s = "{";
+  for (int i = 0; i < 7; i++) s += std::string("\"") + pts[i] + "\":" + g1_json(proof + 64 * i) + ",";
+  for (int i = 0; i < 7; i++) s += std::string("\"") + evs[i] + "\":\"" + dec_le(proof + 9 * 64 + 32 * i) + "\",";
+  s += "\"Wxi\":" + g1_json(proof + 7 * 64) + ",";
+  s += "\"Wxiw\":" + g1_json(proof + 8 * 64) + ",";
+  s += "\"protocol\":\"plonk\",\"curve\":\"bn128\"}";
+  return copy_out(s, out, cap);
+}
+
+int nzcb_public_to_json(const uint8_t* pub, int n_public, char* out, size_t cap) {
+  std::string s = "[";
+  for (int i = 0; i < n_public; i++) {
+    if (i) s += ",";
+    s += "\"" + dec_le(pub + 32 * i) + "\"";
+  }
+  s += "]";
+  return copy_out(s, out, cap);
+}
+
+}  // extern "C"

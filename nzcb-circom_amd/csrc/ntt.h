@@ -1,0 +1,23 @@
+// Fr radix-2 NTT / iNTT over natural-order data.
+#pragma once
+#include "common.h"
+
+namespace nzcb {
+
+// Roots of unity, ffjavascript convention: w[28] = 5^((r-1)/2^28), w[k-1] = w[k]^2.
+Fr fr_root_of_unity(int k);  // Montgomery form
+
+struct NttTables {
+  int max_log = 0;
+  DevBuf<Fr> fwd;  // fwd[i] = w^i,  i < 2^(max_log-1), w = w[max_log]
+  DevBuf<Fr> inv;  // inv[i] = w^-i
+  void init(int max_log, hipStream_t st);
+};
+
+// out = NTT(in) (inverse: out = (1/N) * iNTT(in)), N = 2^log_n <= 2^max_log.
+// Natural order in and out; in != out required (first pass gathers in bit-reversed order).
+// scale (optional, Montgomery) multiplies every input element on load.
+void ntt(const NttTables& t, const Fr* in, Fr* out, int log_n, bool inverse, hipStream_t st,
+         const Fr* scale = nullptr);
+
+}  // namespace nzcb

@@ -1,0 +1,179 @@
+// Fr NTT for gfx950: LDS-tiled radix-2 passes, up to 8 stages per HBM round trip.
+//
+// Replaces ffjavascript Fr.fft / Fr.ifft (wasmcurves frm_fftMix / fftJoin /
+// fftFinal). Semantics: natural order in and out,
+// fft: A[i] = sum_j a[j] w^(ij); ifft: a[j] = N^-1 sum_i A[i] w^(-ij), w = w[log2 N].
+//
+// Plan for N = 2^L (DIT): pass 0 gathers 2^q-element blocks in bit-reversed
+// order (bit reversal fused into the load: a tile is 2^q rows x C consecutive
+// columns, so every row load is C*32 contiguous bytes) and runs stages 0..q-1
+// in LDS; later passes run stages s..s+q-1 on tiles of 2^q rows (stride 2^s)
+// x C consecutive columns, in place. L = 23 -> 3 passes of <= 8 stages, each one
+// read + one write of the array (algorithmic 64 B per element per pass).
+#include "ntt.h"
+
+#include <vector>
+
+namespace nzcb {
+
+static constexpr int kTileElems = 2048;  // 64 KiB of Fr per workgroup
+static constexpr int kNttThreads = 256;
+
+Fr fr_root_of_unity(int k) {
+  Fr w;
+  const uint32_t w28[8] = {0x725b19f0u, 0x9bd61b6eu, 0x41112ed4u, 0x402d111eu,
+                           0x8ef62abcu, 0x00e0a7ebu, 0xa58a7e85u, 0x2a3c09f0u};
+  for (int i = 0; i < 8; i++) w.v[i] = w28[i];
+  w = to_mont(w);
+  for (int j = 28; j > k; j--) w = sqr(w);
+  return w;
+}
+
+__device__ __forceinline__ uint32_t bit_rev(uint32_t x, int bits) {
+  return bits ? (__brev(x) >> (32 - bits)) : 0u;
+}
+
+__global__ void __launch_bounds__(kNttThreads)
+ntt_table_kernel(Fr* __restrict__ out, const Fr* __restrict__ lo, const Fr* __restrict__ hi, size_t count) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  out[i] = lo[i & 2047] * hi[i >> 11];
+}
+
+void NttTables::init(int L, hipStream_t st) {
+  max_log = L;
+  size_t half = L >= 1 ? (size_t(1) << (L - 1)) : 1;
+  fwd.alloc(half);
+  inv.alloc(half);
+  for (int dir = 0; dir < 2; dir++) {
+    Fr w = fr_root_of_unity(L);
+    if (dir) w = inverse(w);
+    size_t nlo = half < 2048 ? half : 2048;
+    size_t nhi = (half + 2047) / 2048;
+    std::vector<Fr> lo(2048, Fr::one()), hi(nhi, Fr::one());
+    for (size_t i = 1; i < nlo; i++) lo[i] = lo[i - 1] * w;
+    Fr w2048 = pow_u64(w, 2048);
+    for (size_t i = 1; i < nhi; i++) hi[i] = hi[i - 1] * w2048;
+    DevBuf<Fr> dlo(2048), dhi(nhi);
+    NZ_HIP(hipMemcpyAsync(dlo.p, lo.data(), 2048 * sizeof(Fr), hipMemcpyHostToDevice, st));
+    NZ_HIP(hipMemcpyAsync(dhi.p, hi.data(), nhi * sizeof(Fr), hipMemcpyHostToDevice, st));
+    Fr* dst = dir ? inv.p : fwd.p;
+    hipLaunchKernelGGL(ntt_table_kernel, dim3(grid_for(half, kNttThreads)), dim3(kNttThreads), 0, st, dst,
+                       dlo.p, dhi.p, half);
+    NZ_HIP(hipGetLastError());
+    NZ_HIP(hipStreamSynchronize(st));
+  }
+}
+
+// One pass: stages [s, s+q) on tiles of (2^q rows) x (2^logC columns).
+__global__ void __launch_bounds__(kNttThreads)
+ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int Lmax,
+                int s, int q, int logC, int first, Fr scale, int do_scale) {
+  extern __shared__ Fr tile[];
+  const int C = 1 << logC;
+  const int rows = 1 << q;
+  const int n_el = rows << logC;
+  const size_t t = blockIdx.x;
+  size_t base = 0, c0 = 0, lo0 = 0;
+  if (first) {
+    c0 = t << logC;
+    for (int e = threadIdx.x; e < n_el; e += blockDim.x) {
+      int j = e >> logC, c = e & (C - 1);
+      size_t src = ((size_t)bit_rev((uint32_t)j, q) << (L - q)) + c0 + c;
+      Fr v = in[src];
+      if (do_scale) v = v * scale;
+      tile[e] = v;
+    }
+  } else {
+    size_t groups_lo = ((size_t)1 << s) >> logC;
+    size_t hi = t / groups_lo;
+    lo0 = (t % groups_lo) << logC;
+    base = (hi << (s + q)) + lo0;
+    for (int e = threadIdx.x; e < n_el; e += blockDim.x) {
+      int j = e >> logC, c = e & (C - 1);
+      tile[e] = in[base + ((size_t)j << s) + c];
+    }
+  }
+  __syncthreads();
+  for (int st = 0; st < q; st++) {
+    const int half = 1 << st;
+    const int g = s + st;  // global stage: butterfly span 2^g
+    const int tw_shift = Lmax - g - 1;
+    for (int b = threadIdx.x; b < (n_el >> 1); b += blockDim.x) {
+      int c = b & (C - 1);
+      int pr = b >> logC;
+      int low = pr & (half - 1);
+      int j0 = ((pr >> st) << (st + 1)) | low;
+      int j1 = j0 + half;
+      size_t k = first ? (size_t)low : (((size_t)low << s) + lo0 + c);
+      Fr w = tw[k << tw_shift];
+      Fr x0 = tile[(j0 << logC) + c];
+      Fr x1 = tile[(j1 << logC) + c] * w;
+      tile[(j0 << logC) + c] = x0 + x1;
+      tile[(j1 << logC) + c] = x0 - x1;
+    }
+    __syncthreads();
+  }
+  if (first) {
+    for (int e = threadIdx.x; e < n_el; e += blockDim.x) {
+      int j = e & (rows - 1), c = e >> q;
+      size_t dst = ((size_t)bit_rev((uint32_t)(c0 + c), L - q) << q) + j;
+      out[dst] = tile[(j << logC) + c];
+    }
+  } else {
+    for (int e = threadIdx.x; e < n_el; e += blockDim.x) {
+      int j = e >> logC, c = e & (C - 1);
+      out[base + ((size_t)j << s) + c] = tile[e];
+    }
+  }
+}
+
+void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hipStream_t st, const Fr* scale) {
+  if (L > t.max_log) throw Error(NZCB_ERR_ARG, "ntt size exceeds table");
+  if (in == out) throw Error(NZCB_ERR_ARG, "ntt requires in != out");
+  const Fr* tw = inverse_dir ? t.inv.p : t.fwd.p;
+  Fr sc = Fr::one();
+  int do_scale = 0;
+  if (inverse_dir) {
+    // N^-1 in Montgomery form
+    Fr n_m = to_mont([&] { Fr x = Fr::zero(); x.v[0] = 1; return x; }());
+    Fr two = n_m + n_m;
+    Fr nn = pow_u64(two, (uint64_t)L);
+    sc = inverse(nn);
+    do_scale = 1;
+  }
+  if (scale) {
+    sc = do_scale ? sc * *scale : *scale;
+    do_scale = 1;
+  }
+  if (L == 0) {
+    // N = 1: copy (with scale)
+    hipLaunchKernelGGL(ntt_pass_kernel, dim3(1), dim3(kNttThreads), sizeof(Fr), st, in, out, tw, 0, t.max_log, 0, 0,
+                       0, 1, sc, do_scale);
+    NZ_HIP(hipGetLastError());
+    return;
+  }
+  int q1 = L < 8 ? L : 8;
+  int cols = 1 << (L - q1);
+  int logC1 = 0;
+  while ((1 << (logC1 + 1)) <= cols && ((1 << (q1 + logC1 + 1)) <= kTileElems)) logC1++;
+  size_t tiles = (size_t)cols >> logC1;
+  size_t lds = (size_t(1) << (q1 + logC1)) * sizeof(Fr);
+  hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)tiles), dim3(kNttThreads), lds, st, in, out, tw, L, t.max_log,
+                     0, q1, logC1, 1, sc, do_scale);
+  NZ_HIP(hipGetLastError());
+  int s = q1;
+  while (s < L) {
+    int q = (L - s) < 8 ? (L - s) : 8;
+    int logC = 0;
+    while (logC + 1 <= s && (1 << (q + logC + 1)) <= kTileElems) logC++;
+    size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
+    size_t lds2 = (size_t(1) << (q + logC)) * sizeof(Fr);
+    hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)ntiles), dim3(kNttThreads), lds2, st, out, out, tw, L,
+                       t.max_log, s, q, logC, 0, sc, 0);
+    NZ_HIP(hipGetLastError());
+    s += q;
+  }
+}
+
+}  // namespace nzcb

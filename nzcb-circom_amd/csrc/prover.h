@@ -1,0 +1,70 @@
+// Device-resident PLONK prover (snarkjs 0.4.12 plonk_prove restated for gfx950).
+#pragma once
+#include <chrono>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+#include "zkey.h"
+
+namespace nzcb {
+
+struct AddRec {  // one addition, reordered by dependency level
+  uint32_t ai, bi, dst, pad;
+  Fr ac, bc;
+};
+
+struct Prover {
+  // zkey facts
+  uint32_t n = 0, n4 = 0, nVars = 0, nPublic = 0, nAdditions = 0, nConstraints = 0, nWit = 0;
+  int power = 0;
+  Fr k1, k2, wn, w2;
+  std::vector<uint32_t> add_level_start;  // offsets into d_adds per level
+  bool transcript_public = true;
+  std::function<void(const std::string&)> log;
+
+  std::unique_ptr<Engine> eng;
+  // resident zkey data (LEM, as in the file)
+  DevBuf<G1Affine> ptau;
+  DevBuf<Fr> qm, ql, qr, qo, qc;  // [n coefs | 4n evals]
+  DevBuf<Fr> sigma;               // 3 x [n | 4n]
+  DevBuf<Fr> lagrange;            // nLagrange x [n | 4n]
+  DevBuf<uint32_t> amap, bmap, cmap;
+  DevBuf<AddRec> adds;
+  DevBuf<Fr> root_lo, root_hi;    // w4^j, w4^(4096 k)
+  // per-proof working set
+  DevBuf<Fr> wit;                 // nVars (witness + internal), Montgomery
+  DevBuf<Fr> wtns_in;             // raw witness upload (normal form)
+  DevBuf<Fr> A, B, C, Z;          // n
+  DevBuf<Fr> pol_a, pol_b, pol_c, pol_z;  // n+2 / n+3
+  DevBuf<Fr> A4, B4, C4, Z4, T, Tz, t, tz, pad4;  // 4n
+  DevBuf<Fr> pol_r, pol_wxi, pol_wxiw;    // n+3, n+6, n+3
+  DevBuf<Fr> blind;               // 12 (index 0 unused)
+  DevBuf<Fr> scan_tmp;            // recursive scan levels
+  DevBuf<Fr> eval_part;           // partial sums of polynomial evaluations
+  DevBuf<uint32_t> flags;
+  std::vector<Fr> host_part;
+
+  // timings of the last proof (ms)
+  double tm[9] = {0};
+
+  Prover(const uint8_t* zkey, size_t len, int device);
+  // witness: nWit x 32-byte LE normal-form values; blinding: 11 x 32-byte LE or null
+  void prove(const uint8_t* witness, size_t n_witness, const uint8_t* blinding, uint8_t* proof_out,
+             uint8_t* pub_out);
+
+ private:
+  hipStream_t st() const { return eng->stream; }
+  void to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb);
+  G1Affine commit(const Fr* coefs, size_t len);
+  Fr eval_poly(const Fr* p, size_t len, const Fr& x);
+  void prefix_product(Fr* x, size_t m, Fr* level_tmp);
+  void suffix_linear(Fr* x, size_t m, const Fr& d, Fr* level_tmp);
+  void div_pol1(const Fr* src, size_t m, const Fr& d, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit);
+  double ms_since(std::chrono::steady_clock::time_point t0);
+  double msm_ms = 0, ntt_ms = 0;
+};
+
+}  // namespace nzcb

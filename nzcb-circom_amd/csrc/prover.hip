@@ -1,0 +1,896 @@
+// PLONK prover rounds 1-5 on gfx950 (snarkjs 0.4.12 plonk_prove restated).
+//
+// Reference: snarkjs@0.4.12 src/plonk_prove.js [EXT] (/root/reference/yarn.lock:7279-7292),
+// called by the reference's dapp / CLI on the zkey built at /root/reference/Makefile:59-62.
+// Row-by-row spec: SURVEY.md §8a a3-a12. Every value below is a unique field or
+// affine-curve element, so with the same blinding scalars the proof bytes are the
+// ones snarkjs would print (parity pinned here against oracle/plonk.py).
+//
+// Design: the zkey is uploaded once (HBM-resident, LEM bytes as in the file) and
+// every per-proof array stays on the device; the host only runs the Fiat-Shamir
+// transcript (keccak over ~1 KB), the per-MSM window fold and a handful of Fr
+// scalars. All data is kept in Montgomery form; MSM digit extraction converts.
+// Sequential JS loops of the reference become parallel scans:
+//   * Z grand product  -> chunked batch inversion + exclusive prefix-product scan
+//   * divPol1          -> suffix linear-recurrence scan y_i = x_i + d*y_{i+1}
+//   * evalPol (Horner) -> chunked Horner * x^(chunk start) + tree sum
+#include "prover.h"
+
+#include <cstring>
+
+#include "keccak.h"
+
+namespace nzcb {
+
+static constexpr int kT = 256;
+static constexpr uint32_t kZeroRef = 0xffffffffu;
+static constexpr int kScanChunk = 32;
+static constexpr int kEvalChunk = 64;
+
+// ----------------------------------------------------------------------------
+// kernels
+// ----------------------------------------------------------------------------
+__global__ void k_wit_to_mont(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = (i == 0) ? Fr::zero() : to_mont(in[i]);  // "First element in plonk is not used"
+}
+
+__global__ void k_additions(const AddRec* __restrict__ recs, uint32_t count, Fr* __restrict__ wit) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const AddRec r = recs[i];
+  Fr a = r.ai == kZeroRef ? Fr::zero() : wit[r.ai];
+  Fr b = r.bi == kZeroRef ? Fr::zero() : wit[r.bi];
+  wit[r.dst] = r.ac * a + r.bc * b;
+}
+
+__global__ void k_build_abc(const uint32_t* __restrict__ am, const uint32_t* __restrict__ bm,
+                            const uint32_t* __restrict__ cm, uint32_t nc, uint32_t n, const Fr* __restrict__ wit,
+                            uint32_t nvars, Fr* __restrict__ A, Fr* __restrict__ B, Fr* __restrict__ C) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fr a = Fr::zero(), b = Fr::zero(), c = Fr::zero();
+  if (i < nc) {
+    uint32_t ia = am[i], ib = bm[i], ic = cm[i];
+    if (ia < nvars) a = wit[ia];
+    if (ib < nvars) b = wit[ib];
+    if (ic < nvars) c = wit[ic];
+  }
+  A[i] = a;
+  B[i] = b;
+  C[i] = c;
+}
+
+__global__ void k_pad(const Fr* __restrict__ src, size_t n, Fr* __restrict__ dst, size_t n4) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  dst[i] = i < n ? src[i] : Fr::zero();
+}
+
+struct BlindIdx {
+  int idx[3];
+  int count;
+};
+
+// p1 = p + (sum_k pz_k X^k)(X^n - 1): pol[n+k] = pz_k, pol[k] -= pz_k  (to4T)
+__global__ void k_blind(Fr* pol, size_t n, const Fr* __restrict__ bl, BlindIdx bi) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int k = 0; k < bi.count; k++) {
+    Fr b = bl[bi.idx[k]];
+    pol[n + k] = b;
+    pol[k] = pol[k] - b;
+  }
+}
+
+// w4^i from two small tables (4n-th roots of unity)
+__device__ __forceinline__ Fr root4(const Fr* __restrict__ lo, const Fr* __restrict__ hi, size_t i) {
+  return lo[i & 4095] * hi[i >> 12];
+}
+
+struct PermArgs {
+  Fr beta, gamma, k1, k2;
+};
+
+// Round 2: num_i / den_i with chunked Montgomery batch inversion.
+__global__ void __launch_bounds__(kT)
+k_perm_ratio(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
+             const Fr* __restrict__ sigma, size_t n, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi,
+             PermArgs pa, Fr* __restrict__ ratio, Fr* __restrict__ den_s, Fr* __restrict__ pre_s) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t s = t * kScanChunk;
+  if (s >= n) return;
+  size_t e = s + kScanChunk < n ? s + kScanChunk : n;
+  const Fr* s1 = sigma + n;           // sigma1 evals (4n), read at stride 4
+  const Fr* s2 = sigma + 5 * n + n;
+  const Fr* s3 = sigma + 10 * n + n;
+  Fr pre = Fr::one();
+  for (size_t i = s; i < e; i++) {
+    Fr w = root4(rlo, rhi, 4 * i);
+    Fr bw = pa.beta * w;
+    Fr a = A[i], b = B[i], c = C[i];
+    Fr num = (a + bw + pa.gamma) * (b + pa.k1 * bw + pa.gamma);
+    num = num * (c + pa.k2 * bw + pa.gamma);
+    Fr den = (a + pa.beta * s1[4 * i] + pa.gamma) * (b + pa.beta * s2[4 * i] + pa.gamma);
+    den = den * (c + pa.beta * s3[4 * i] + pa.gamma);
+    ratio[i] = num;
+    den_s[i] = den;
+    pre = pre * den;
+    pre_s[i] = pre;
+  }
+  Fr inv = inverse(pre);
+  for (size_t i = e; i-- > s;) {
+    Fr before = (i > s) ? pre_s[i - 1] : Fr::one();
+    Fr dinv = inv * before;
+    inv = inv * den_s[i];
+    ratio[i] = ratio[i] * dinv;
+  }
+}
+
+// exclusive prefix products: chunk products, small single-block scan, apply
+__global__ void k_chunk_prod(const Fr* __restrict__ x, size_t m, Fr* __restrict__ out) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t s = t * kScanChunk;
+  if (s >= m) return;
+  size_t e = s + kScanChunk < m ? s + kScanChunk : m;
+  Fr p = Fr::one();
+  for (size_t i = s; i < e; i++) p = p * x[i];
+  out[t] = p;
+}
+
+// in place exclusive product scan of m <= 1024 values; total -> *total
+__global__ void __launch_bounds__(1024) k_scan_mul_small(Fr* x, int m, Fr* total) {
+  __shared__ Fr buf[1024];
+  int i = threadIdx.x;
+  Fr v = i < m ? x[i] : Fr::one();
+  buf[i] = v;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    Fr o = (i >= d) ? buf[i - d] : Fr::one();
+    __syncthreads();
+    if (i >= d) buf[i] = buf[i] * o;
+    __syncthreads();
+  }
+  // buf[i] = inclusive product; exclusive = buf[i-1]
+  if (i < m) x[i] = (i == 0) ? Fr::one() : buf[i - 1];
+  if (i == 1023) *total = buf[1023];
+}
+
+__global__ void k_apply_prod(Fr* __restrict__ x, size_t m, const Fr* __restrict__ pref) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t s = t * kScanChunk;
+  if (s >= m) return;
+  size_t e = s + kScanChunk < m ? s + kScanChunk : m;
+  Fr p = pref[t];
+  for (size_t i = s; i < e; i++) {
+    Fr v = x[i];
+    x[i] = p;
+    p = p * v;
+  }
+}
+
+// suffix linear recurrence y_i = x_i + d*y_{i+1} (y_m = 0), chunk-local pass
+__global__ void k_lin_local(Fr* __restrict__ x, size_t m, Fr d, Fr* __restrict__ heads) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t s = t * kScanChunk;
+  if (s >= m) return;
+  size_t e = s + kScanChunk < m ? s + kScanChunk : m;
+  Fr y = Fr::zero();
+  for (size_t i = e; i-- > s;) {
+    y = x[i] + d * y;
+    x[i] = y;
+  }
+  heads[t] = y;
+}
+
+__global__ void __launch_bounds__(1024) k_lin_small(Fr* x, int m, Fr d) {
+  __shared__ Fr buf[1024];
+  int i = threadIdx.x;
+  buf[i] = i < m ? x[i] : Fr::zero();
+  Fr dk = d;
+  __syncthreads();
+  for (int k = 1; k < 1024; k <<= 1) {
+    Fr o = (i + k < 1024) ? buf[i + k] : Fr::zero();
+    __syncthreads();
+    buf[i] = buf[i] + dk * o;
+    dk = sqr(dk);
+    __syncthreads();
+  }
+  if (i < m) x[i] = buf[i];
+}
+
+// add the carry from the next chunk: y_i += d^(e-i) * Y_e
+__global__ void k_lin_apply(Fr* __restrict__ x, size_t m, Fr d, const Fr* __restrict__ heads, size_t nheads) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t s = t * kScanChunk;
+  if (s >= m || t + 1 >= nheads) return;
+  size_t e = s + kScanChunk < m ? s + kScanChunk : m;
+  Fr carry = heads[t + 1];
+  Fr pw = d;
+  for (size_t i = e; i-- > s;) {
+    x[i] = x[i] + pw * carry;
+    pw = pw * d;
+  }
+}
+
+struct QArgs {
+  Fr beta, gamma, alpha, alpha2, k1, k2, wn;
+  Fr b[10];
+  Fr Z1[4], Z2[4], Z3[4];
+};
+
+__device__ __forceinline__ void mul4(const Fr& a, const Fr& b, const Fr& c, const Fr& d, const Fr& ap,
+                                     const Fr& bp, const Fr& cp, const Fr& dp, int p, const QArgs& q, Fr& r,
+                                     Fr& rz) {
+  Fr a_b = a * b, a_bp = a * bp, ap_b = ap * b, ap_bp = ap * bp;
+  Fr c_d = c * d, c_dp = c * dp, cp_d = cp * d, cp_dp = cp * dp;
+  r = a_b * c_d;
+  Fr a0 = ap_b * c_d + a_bp * c_d + a_b * cp_d + a_b * c_dp;
+  rz = a0;
+  if (p) {
+    Fr a1 = ap_bp * c_d + ap_b * cp_d + ap_b * c_dp + a_bp * cp_d + a_bp * c_dp + a_b * cp_dp;
+    Fr a2 = a_bp * cp_dp + ap_b * cp_dp + ap_bp * c_dp + ap_bp * cp_d;
+    Fr a3 = ap_bp * cp_dp;
+    rz = rz + q.Z1[p] * a1 + q.Z2[p] * a2 + q.Z3[p] * a3;
+  }
+}
+
+// Round 3 quotient evaluations over the 4n domain
+__global__ void __launch_bounds__(kT)
+k_quotient(const Fr* __restrict__ A4, const Fr* __restrict__ B4, const Fr* __restrict__ C4,
+           const Fr* __restrict__ Z4, const Fr* __restrict__ qm, const Fr* __restrict__ ql,
+           const Fr* __restrict__ qr, const Fr* __restrict__ qo, const Fr* __restrict__ qc,
+           const Fr* __restrict__ sigma, const Fr* __restrict__ lag, uint32_t npub, const Fr* __restrict__ Apub,
+           size_t n, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi, QArgs q, Fr* __restrict__ T,
+           Fr* __restrict__ Tz) {
+  const size_t n4 = 4 * n;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const Fr a = A4[i], b = B4[i], c = C4[i], z = Z4[i];
+  const Fr zw = Z4[(i + 4) & (n4 - 1)];
+  const Fr w = root4(rlo, rhi, i);
+  const Fr ap = q.b[2] + q.b[1] * w;
+  const Fr bp = q.b[4] + q.b[3] * w;
+  const Fr cp = q.b[6] + q.b[5] * w;
+  const Fr w2 = sqr(w);
+  const Fr zp = q.b[7] * w2 + q.b[8] * w + q.b[9];
+  const Fr wW = w * q.wn;
+  const Fr wW2 = sqr(wW);
+  const Fr zWp = q.b[7] * wW2 + q.b[8] * wW + q.b[9];
+  Fr pl = Fr::zero();
+  for (uint32_t j = 0; j < npub; j++) pl = pl - lag[(size_t)j * 5 * n + n + i] * Apub[j];
+  const int p = (int)(i & 3);
+  const Fr vqm = qm[n + i], vql = ql[n + i], vqr = qr[n + i], vqo = qo[n + i], vqc = qc[n + i];
+  Fr e1 = a * b * vqm;
+  Fr e1z = a * bp + ap * b;
+  if (p) e1z = e1z + q.Z1[p] * (ap * bp);
+  e1z = e1z * vqm;
+  e1 = e1 + a * vql + b * vqr + c * vqo + pl + vqc;
+  e1z = e1z + ap * vql + bp * vqr + cp * vqo;
+  const Fr betaw = q.beta * w;
+  Fr e2, e2z, e3, e3z;
+  mul4(a + betaw + q.gamma, b + betaw * q.k1 + q.gamma, c + betaw * q.k2 + q.gamma, z, ap, bp, cp, zp, p, q, e2,
+       e2z);
+  const Fr s1 = sigma[n + i], s2 = sigma[6 * n + i], s3 = sigma[11 * n + i];
+  mul4(a + q.beta * s1 + q.gamma, b + q.beta * s2 + q.gamma, c + q.beta * s3 + q.gamma, zw, ap, bp, cp, zWp, p, q,
+       e3, e3z);
+  e2 = e2 * q.alpha;
+  e2z = e2z * q.alpha;
+  e3 = e3 * q.alpha;
+  e3z = e3z * q.alpha;
+  const Fr l1 = lag[n + i];
+  const Fr e4 = (z - Fr::one()) * l1 * q.alpha2;
+  const Fr e4z = zp * l1 * q.alpha2;
+  T[i] = e1 + e2 - e3 + e4;
+  Tz[i] = e1z + e2z - e3z + e4z;
+}
+
+// t'[j + kn] = -sum_{k'<=k} t[j + k'n] (division by X^n - 1), divisibility checks, + tz
+__global__ void k_div_zh(Fr* __restrict__ t, const Fr* __restrict__ tz, size_t n, uint32_t* flags) {
+  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  Fr acc = Fr::zero();
+  uint32_t f = 0;
+  for (int k = 0; k < 4; k++) {
+    size_t i = j + (size_t)k * n;
+    acc = acc - t[i];
+    if (i > 3 * n - 4 && !acc.is_zero()) f |= 1u;  // "T Polynomial is not divisible"
+    Fr v = acc;
+    Fr z = tz[i];
+    if (i > 3 * n + 5) {
+      if (!z.is_zero()) f |= 2u;  // "Tz Polynomial is not well calculated"
+    } else {
+      v = v + z;
+    }
+    t[i] = v;
+  }
+  if (f) atomicOr(flags, f);
+}
+
+// chunked Horner: partial[block] = sum over the block's chunks of p(chunk) * x^(chunk start)
+__global__ void __launch_bounds__(kT)
+k_eval(const Fr* __restrict__ p, size_t len, Fr x, Fr xK, Fr* __restrict__ partial) {
+  __shared__ Fr sh[kT];
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t s = t * kEvalChunk;
+  Fr acc = Fr::zero();
+  if (s < len) {
+    size_t e = s + kEvalChunk < len ? s + kEvalChunk : len;
+    for (size_t i = e; i-- > s;) acc = acc * x + p[i];
+    acc = acc * pow_u64(xK, (uint64_t)t);
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int stride = kT / 2; stride > 0; stride >>= 1) {
+    if ((int)threadIdx.x < stride) sh[threadIdx.x] = sh[threadIdx.x] + sh[threadIdx.x + stride];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+struct RArgs {
+  Fr coefz, coef_ab, ea, eb, ec, coefs3;
+};
+
+// Round 4 linearisation polynomial r (n+3 coefficients)
+__global__ void k_pol_r(const Fr* __restrict__ pz, const Fr* __restrict__ qm, const Fr* __restrict__ ql,
+                        const Fr* __restrict__ qr, const Fr* __restrict__ qo, const Fr* __restrict__ qc,
+                        const Fr* __restrict__ s3, size_t n, RArgs r, Fr* __restrict__ out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n + 3) return;
+  Fr v = r.coefz * pz[i];
+  if (i < n) {
+    v = v + r.coef_ab * qm[i] + r.ea * ql[i] + r.eb * qr[i] + r.ec * qo[i] + qc[i];
+    v = v - r.coefs3 * s3[i];
+  }
+  out[i] = v;
+}
+
+struct WArgs {
+  Fr xim, xi2m, v[7], w0sub;
+};
+
+// Round 5 opening polynomial before division (n+6 coefficients)
+__global__ void k_pol_wxi(const Fr* __restrict__ t, const Fr* __restrict__ pr, const Fr* __restrict__ pa,
+                          const Fr* __restrict__ pb, const Fr* __restrict__ pc, const Fr* __restrict__ s1,
+                          const Fr* __restrict__ s2, size_t n, WArgs wa, Fr* __restrict__ out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n + 6) return;
+  Fr w = wa.xi2m * t[2 * n + i];
+  if (i < n) w = w + wa.xim * t[n + i] + t[i];
+  if (i < n + 3) w = w + wa.v[1] * pr[i];
+  if (i < n + 2) w = w + wa.v[2] * pa[i] + wa.v[3] * pb[i] + wa.v[4] * pc[i];
+  if (i < n) w = w + wa.v[5] * s1[i] + wa.v[6] * s2[i];
+  if (i == 0) w = w - wa.w0sub;
+  out[i] = w;
+}
+
+// dst[i] = src[i+1] (i < m-1), dst[m-1] = 0: divPol1 input for the suffix recurrence
+__global__ void k_shift_down(const Fr* __restrict__ src, size_t m, Fr* __restrict__ dst) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  dst[i] = (i + 1 < m) ? src[i + 1] : Fr::zero();
+}
+
+// "Polinomial does not divide": P0 == -d * q0
+__global__ void k_div_check(const Fr* __restrict__ src, Fr p0_adjust, const Fr* __restrict__ q, Fr d,
+                            uint32_t* flags, uint32_t bit) {
+  if (threadIdx.x || blockIdx.x) return;
+  Fr p0 = src[0] - p0_adjust;
+  if (!(p0 + d * q[0]).is_zero()) atomicOr(flags, bit);
+}
+
+__global__ void k_root_table(Fr* __restrict__ out, Fr base, size_t count) {
+  // out[i] = base^i, i < count (count <= 4096; one thread per entry)
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  out[i] = pow_u64(base, i);
+}
+
+// ----------------------------------------------------------------------------
+// host helpers
+// ----------------------------------------------------------------------------
+static Fr fr_from_le_normal(const uint8_t* p) {
+  Fr x;
+  std::memcpy(x.v, p, 32);
+  // reduce (values from files may be >= r only if malformed; keep exact for < 2^256)
+  for (int k = 0; k < 6; k++) {
+    Fr y = reduce_once(x);
+    if (y == x) break;
+    x = y;
+  }
+  return to_mont(x);
+}
+
+static void fr_to_le_normal(const Fr& m, uint8_t* out) {
+  Fr x = from_mont(m);
+  std::memcpy(out, x.v, 32);
+}
+
+static void fr_to_be(const Fr& m, uint8_t* out) {
+  uint8_t le[32];
+  fr_to_le_normal(m, le);
+  for (int i = 0; i < 32; i++) out[i] = le[31 - i];
+}
+
+static void g1_uncompressed(const G1Affine& a, uint8_t* out) {
+  if (a.is_inf()) {
+    std::memset(out, 0, 64);
+    out[0] = 0x40;
+    return;
+  }
+  Fq x = from_mont(a.x), y = from_mont(a.y);
+  for (int i = 0; i < 32; i++) {
+    out[i] = ((const uint8_t*)x.v)[31 - i];
+    out[32 + i] = ((const uint8_t*)y.v)[31 - i];
+  }
+}
+
+static Fr hash_to_fr(const std::vector<uint8_t>& data) {
+  uint8_t h[32];
+  keccak256(data.data(), data.size(), h);
+  uint8_t le[32];
+  for (int i = 0; i < 32; i++) le[i] = h[31 - i];
+  return fr_from_le_normal(le);
+}
+
+static std::string fr_dec(const Fr& m) {
+  Fr x = from_mont(m);
+  uint32_t v[8];
+  std::memcpy(v, x.v, 32);
+  std::string s;
+  bool nz = true;
+  while (nz) {
+    uint64_t rem = 0;
+    nz = false;
+    for (int i = 7; i >= 0; i--) {
+      uint64_t cur = (rem << 32) | v[i];
+      v[i] = (uint32_t)(cur / 10);
+      rem = cur % 10;
+      if (v[i]) nz = true;
+    }
+    s.push_back((char)('0' + rem));
+  }
+  return std::string(s.rbegin(), s.rend());
+}
+
+static Fr fr_small(uint64_t k) {
+  Fr x = Fr::zero();
+  x.v[0] = (uint32_t)k;
+  x.v[1] = (uint32_t)(k >> 32);
+  return to_mont(x);
+}
+
+double Prover::ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// ----------------------------------------------------------------------------
+// context creation: parse + upload the zkey once
+// ----------------------------------------------------------------------------
+Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
+  Zkey z = parse_zkey(zkey_bytes, len);
+  n = z.domainSize;
+  n4 = 4 * n;
+  power = z.power;
+  nVars = z.nVars;
+  nPublic = z.nPublic;
+  nAdditions = z.nAdditions;
+  nConstraints = z.nConstraints;
+  if (nAdditions > nVars) throw Error(NZCB_ERR_FORMAT, "nAdditions > nVars");
+  nWit = nVars - nAdditions;
+  k1 = z.k1;
+  k2 = z.k2;
+  wn = fr_root_of_unity(power);
+  w2 = fr_root_of_unity(2);
+  eng.reset(new Engine(device, power + 2, (size_t)n + 6));
+  hipStream_t s = st();
+  auto up = [&](auto& buf, const Section& sec) {
+    using T = typename std::remove_reference<decltype(*buf.p)>::type;
+    buf.alloc(sec.len / sizeof(T) ? sec.len / sizeof(T) : 1);
+    if (sec.len) NZ_HIP(hipMemcpyAsync(buf.p, sec.p, sec.len, hipMemcpyHostToDevice, s));
+  };
+  up(ptau, z.ptau);
+  up(qm, z.qm);
+  up(ql, z.ql);
+  up(qr, z.qr);
+  up(qo, z.qo);
+  up(qc, z.qc);
+  up(sigma, z.sigma);
+  up(lagrange, z.lagrange);
+  up(amap, z.amap);
+  up(bmap, z.bmap);
+  up(cmap, z.cmap);
+  // additions: zero out forward references (snarkjs reads not-yet-computed internal
+  // signals as 0), then order by dependency level so each level is one parallel launch
+  {
+    std::vector<uint32_t> level(nAdditions, 0);
+    std::vector<AddRec> recs(nAdditions);
+    uint32_t maxlev = 0;
+    for (uint32_t k = 0; k < nAdditions; k++) {
+      const uint8_t* p = z.additions.p + (size_t)k * 72;
+      AddRec r;
+      std::memcpy(&r.ai, p, 4);
+      std::memcpy(&r.bi, p + 4, 4);
+      std::memcpy(r.ac.v, p + 8, 32);
+      std::memcpy(r.bc.v, p + 40, 32);
+      r.dst = nWit + k;
+      r.pad = 0;
+      uint32_t lv = 0;
+      for (uint32_t* ref : {&r.ai, &r.bi}) {
+        if (*ref >= nVars) *ref = kZeroRef;
+        else if (*ref >= nWit) {
+          uint32_t kk = *ref - nWit;
+          if (kk >= k) *ref = kZeroRef;
+          else lv = std::max(lv, level[kk] + 1);
+        }
+      }
+      level[k] = lv;
+      maxlev = std::max(maxlev, lv);
+      recs[k] = r;
+    }
+    std::vector<uint32_t> cnt(maxlev + 2, 0);
+    for (uint32_t k = 0; k < nAdditions; k++) cnt[level[k] + 1]++;
+    for (uint32_t l = 1; l < cnt.size(); l++) cnt[l] += cnt[l - 1];
+    add_level_start.assign(cnt.begin(), cnt.end());
+    std::vector<AddRec> sorted(nAdditions);
+    std::vector<uint32_t> cur(cnt.begin(), cnt.end());
+    for (uint32_t k = 0; k < nAdditions; k++) sorted[cur[level[k]]++] = recs[k];
+    adds.alloc(nAdditions ? nAdditions : 1);
+    if (nAdditions)
+      NZ_HIP(hipMemcpyAsync(adds.p, sorted.data(), nAdditions * sizeof(AddRec), hipMemcpyHostToDevice, s));
+    NZ_HIP(hipStreamSynchronize(s));
+  }
+  // 4n-th roots: w4^i = lo[i & 4095] * hi[i >> 12]
+  Fr w4 = fr_root_of_unity(power + 2);
+  size_t nlo = 4096, nhi = (n4 + 4095) / 4096;
+  root_lo.alloc(nlo);
+  root_hi.alloc(nhi);
+  hipLaunchKernelGGL(k_root_table, dim3(grid_for(nlo, kT)), dim3(kT), 0, s, root_lo.p, w4, nlo);
+  hipLaunchKernelGGL(k_root_table, dim3(grid_for(nhi, kT)), dim3(kT), 0, s, root_hi.p, pow_u64(w4, 4096), nhi);
+  NZ_HIP(hipGetLastError());
+  // working set
+  wit.alloc(nVars ? nVars : 1);
+  wtns_in.alloc(nWit ? nWit : 1);
+  A.alloc(n); B.alloc(n); C.alloc(n); Z.alloc(n);
+  pol_a.alloc(n + 2); pol_b.alloc(n + 2); pol_c.alloc(n + 2); pol_z.alloc(n + 3);
+  A4.alloc(n4); B4.alloc(n4); C4.alloc(n4); Z4.alloc(n4);
+  T.alloc(n4); Tz.alloc(n4); t.alloc(n4); tz.alloc(n4); pad4.alloc(n4);
+  pol_r.alloc(n + 3); pol_wxi.alloc(n + 6); pol_wxiw.alloc(n + 3);
+  blind.alloc(12);
+  size_t lv = 0, m = n4;
+  while (m > 1024) { m = (m + kScanChunk - 1) / kScanChunk; lv += m; }
+  scan_tmp.alloc(lv + 2048);
+  size_t nblocks = ((size_t)3 * n + 6 + (size_t)kT * kEvalChunk - 1) / ((size_t)kT * kEvalChunk) + 1;
+  eval_part.alloc(nblocks);
+  host_part.resize(nblocks);
+  flags.alloc(1);
+  NZ_HIP(hipStreamSynchronize(s));
+}
+
+// ----------------------------------------------------------------------------
+// building blocks
+// ----------------------------------------------------------------------------
+void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb) {
+  hipStream_t s = st();
+  auto t0 = std::chrono::steady_clock::now();
+  ntt(eng->ntt_tables, evals, coefs, power, true, s);
+  hipLaunchKernelGGL(k_pad, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, coefs, (size_t)n, pad4.p, (size_t)n4);
+  ntt(eng->ntt_tables, pad4.p, evals4, power + 2, false, s);
+  BlindIdx bi;
+  bi.count = nb;
+  for (int k = 0; k < nb; k++) bi.idx[k] = bidx[k];
+  hipLaunchKernelGGL(k_blind, dim3(1), dim3(64), 0, s, coefs, (size_t)n, blind.p, bi);
+  NZ_HIP(hipGetLastError());
+  NZ_HIP(hipStreamSynchronize(s));
+  ntt_ms += ms_since(t0);
+}
+
+G1Affine Prover::commit(const Fr* coefs, size_t len) {
+  auto t0 = std::chrono::steady_clock::now();
+  G1xyzz r = msm(eng->msm_scratch, ptau.p, coefs, len, true, st());
+  msm_ms += ms_since(t0);
+  return xyzz_to_affine(r);
+}
+
+Fr Prover::eval_poly(const Fr* p, size_t len, const Fr& x) {
+  hipStream_t s = st();
+  size_t nthreads = (len + kEvalChunk - 1) / kEvalChunk;
+  size_t nblocks = (nthreads + kT - 1) / kT;
+  if (nblocks > host_part.size()) throw Error(NZCB_ERR_INTERNAL, "eval partial buffer too small");
+  Fr xK = pow_u64(x, kEvalChunk);
+  hipLaunchKernelGGL(k_eval, dim3((unsigned)nblocks), dim3(kT), 0, s, p, len, x, xK, eval_part.p);
+  NZ_HIP(hipGetLastError());
+  NZ_HIP(hipMemcpyAsync(host_part.data(), eval_part.p, nblocks * sizeof(Fr), hipMemcpyDeviceToHost, s));
+  NZ_HIP(hipStreamSynchronize(s));
+  Fr acc = Fr::zero();
+  for (size_t b = 0; b < nblocks; b++) acc = acc + host_part[b];
+  return acc;
+}
+
+void Prover::prefix_product(Fr* x, size_t m, Fr* level_tmp) {
+  hipStream_t s = st();
+  if (m <= 1024) {
+    hipLaunchKernelGGL(k_scan_mul_small, dim3(1), dim3(1024), 0, s, x, (int)m, level_tmp + 1024);
+    NZ_HIP(hipGetLastError());
+    return;
+  }
+  size_t nc = (m + kScanChunk - 1) / kScanChunk;
+  hipLaunchKernelGGL(k_chunk_prod, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, level_tmp);
+  prefix_product(level_tmp, nc, level_tmp + nc);
+  hipLaunchKernelGGL(k_apply_prod, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, level_tmp);
+  NZ_HIP(hipGetLastError());
+}
+
+void Prover::suffix_linear(Fr* x, size_t m, const Fr& d, Fr* level_tmp) {
+  hipStream_t s = st();
+  if (m <= 1024) {
+    hipLaunchKernelGGL(k_lin_small, dim3(1), dim3(1024), 0, s, x, (int)m, d);
+    NZ_HIP(hipGetLastError());
+    return;
+  }
+  size_t nc = (m + kScanChunk - 1) / kScanChunk;
+  hipLaunchKernelGGL(k_lin_local, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, d, level_tmp);
+  // heads obey Y_c = h_c + d^K * Y_{c+1}
+  suffix_linear(level_tmp, nc, pow_u64(d, kScanChunk), level_tmp + nc);
+  hipLaunchKernelGGL(k_lin_apply, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, d, level_tmp, nc);
+  NZ_HIP(hipGetLastError());
+}
+
+void Prover::div_pol1(const Fr* src, size_t m, const Fr& d, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit) {
+  hipStream_t s = st();
+  hipLaunchKernelGGL(k_shift_down, dim3(grid_for(m, kT, 1u << 30)), dim3(kT), 0, s, src, m, dst);
+  suffix_linear(dst, m, d, scan_tmp.p);
+  hipLaunchKernelGGL(k_div_check, dim3(1), dim3(64), 0, s, src, p0_adjust, dst, d, flags.p, flag_bit);
+  NZ_HIP(hipGetLastError());
+}
+
+// ----------------------------------------------------------------------------
+// prove
+// ----------------------------------------------------------------------------
+void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blinding, uint8_t* proof_out,
+                   uint8_t* pub_out) {
+  if (n_witness != nWit) {
+    throw Error(NZCB_ERR_WITNESS_LEN, "Invalid witness length. Circuit: " + std::to_string(nVars) +
+                                          ", witness: " + std::to_string(n_witness) + ", " +
+                                          std::to_string(nAdditions));
+  }
+  NZ_HIP(hipSetDevice(eng->device));
+  hipStream_t s = st();
+  msm_ms = ntt_ms = 0;
+  auto T0 = std::chrono::steady_clock::now();
+  auto lg = [&](const std::string& m) { if (log) log(m); };
+  // blinding scalars b1..b11 (Montgomery); index 0 unused
+  Fr bl[12];
+  bl[0] = Fr::zero();
+  for (int i = 1; i <= 11; i++) bl[i] = blinding ? fr_from_le_normal(blinding + 32 * (i - 1)) : Fr::zero();
+  NZ_HIP(hipMemcpyAsync(blind.p, bl, sizeof(bl), hipMemcpyHostToDevice, s));
+  NZ_HIP(hipMemsetAsync(flags.p, 0, sizeof(uint32_t), s));
+
+  lg("Reading Wtns");
+  NZ_HIP(hipMemcpyAsync(wtns_in.p, witness, (size_t)nWit * 32, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_wit_to_mont, dim3(grid_for(nWit, kT, 1u << 30)), dim3(kT), 0, s, wtns_in.p, wit.p,
+                     (size_t)nWit);
+  for (size_t l = 0; l + 1 < add_level_start.size(); l++) {
+    uint32_t a0 = add_level_start[l], a1 = add_level_start[l + 1];
+    if (a1 > a0)
+      hipLaunchKernelGGL(k_additions, dim3(grid_for(a1 - a0, kT, 1u << 30)), dim3(kT), 0, s, adds.p + a0, a1 - a0,
+                         wit.p);
+  }
+  hipLaunchKernelGGL(k_build_abc, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, amap.p, bmap.p, cmap.p,
+                     nConstraints, n, wit.p, nVars, A.p, B.p, C.p);
+  NZ_HIP(hipGetLastError());
+  NZ_HIP(hipStreamSynchronize(s));
+  tm[1] = ms_since(T0);
+
+  // ---------------- round 1 ----------------
+  auto t1 = std::chrono::steady_clock::now();
+  G1Affine pA, pB, pC, pZ, pT1, pT2, pT3, pWxi, pWxiw;
+  {
+    const int ba[2] = {2, 1}, bb[2] = {4, 3}, bc[2] = {6, 5};
+    to4t(A.p, pol_a.p, A4.p, ba, 2);
+    to4t(B.p, pol_b.p, B4.p, bb, 2);
+    to4t(C.p, pol_c.p, C4.p, bc, 2);
+    lg("multiexp A");
+    pA = commit(pol_a.p, n + 2);
+    lg("multiexp B");
+    pB = commit(pol_b.p, n + 2);
+    lg("multiexp C");
+    pC = commit(pol_c.p, n + 2);
+  }
+  tm[2] = ms_since(t1);
+
+  // ---------------- round 2 ----------------
+  auto t2 = std::chrono::steady_clock::now();
+  Fr beta, gamma;
+  std::vector<Fr> Apub(nPublic);
+  if (nPublic) {
+    NZ_HIP(hipMemcpyAsync(Apub.data(), A.p, nPublic * sizeof(Fr), hipMemcpyDeviceToHost, s));
+    NZ_HIP(hipStreamSynchronize(s));
+  }
+  {
+    std::vector<uint8_t> tr;
+    if (transcript_public) {
+      for (uint32_t i = 0; i < nPublic; i++) {
+        uint8_t be[32];
+        fr_to_be(Apub[i], be);
+        tr.insert(tr.end(), be, be + 32);
+      }
+    }
+    for (const G1Affine* p : {&pA, &pB, &pC}) {
+      uint8_t u[64];
+      g1_uncompressed(*p, u);
+      tr.insert(tr.end(), u, u + 64);
+    }
+    beta = hash_to_fr(tr);
+    lg("beta: " + fr_dec(beta));
+    std::vector<uint8_t> tr2(32);
+    fr_to_be(beta, tr2.data());
+    gamma = hash_to_fr(tr2);
+    lg("gamma: " + fr_dec(gamma));
+  }
+  {
+    PermArgs pa{beta, gamma, k1, k2};
+    size_t nchunks = (n + kScanChunk - 1) / kScanChunk;
+    hipLaunchKernelGGL(k_perm_ratio, dim3(grid_for(nchunks, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, sigma.p,
+                       (size_t)n, root_lo.p, root_hi.p, pa, Z.p, T.p, Tz.p);
+    NZ_HIP(hipGetLastError());
+    // keep the last ratio to form the total product Z[n] = prod of all ratios
+    Fr last_ratio;
+    NZ_HIP(hipMemcpyAsync(&last_ratio, Z.p + (n - 1), sizeof(Fr), hipMemcpyDeviceToHost, s));
+    prefix_product(Z.p, n, scan_tmp.p);
+    Fr last_pref;
+    NZ_HIP(hipMemcpyAsync(&last_pref, Z.p + (n - 1), sizeof(Fr), hipMemcpyDeviceToHost, s));
+    NZ_HIP(hipStreamSynchronize(s));
+    if (last_pref * last_ratio != Fr::one()) throw Error(NZCB_ERR_COPY, "Copy constraints does not match");
+    const int bz[3] = {9, 8, 7};
+    to4t(Z.p, pol_z.p, Z4.p, bz, 3);
+    lg("multiexp Z");
+    pZ = commit(pol_z.p, n + 3);
+  }
+  tm[3] = ms_since(t2);
+
+  // ---------------- round 3 ----------------
+  auto t3 = std::chrono::steady_clock::now();
+  Fr alpha;
+  {
+    std::vector<uint8_t> tr(64);
+    g1_uncompressed(pZ, tr.data());
+    alpha = hash_to_fr(tr);
+    lg("alpha: " + fr_dec(alpha));
+  }
+  {
+    QArgs q;
+    q.beta = beta;
+    q.gamma = gamma;
+    q.alpha = alpha;
+    q.alpha2 = alpha * alpha;
+    q.k1 = k1;
+    q.k2 = k2;
+    q.wn = wn;
+    for (int i = 0; i < 10; i++) q.b[i] = bl[i];
+    Fr one = Fr::one(), two = fr_small(2), four = fr_small(4), eight = fr_small(8);
+    q.Z1[0] = q.Z2[0] = q.Z3[0] = Fr::zero();
+    q.Z1[1] = w2 - one;
+    q.Z1[2] = neg(two);
+    q.Z1[3] = neg(one) - w2;
+    q.Z2[1] = neg(two * w2);
+    q.Z2[2] = four;
+    q.Z2[3] = two * w2;
+    q.Z3[1] = two + two * w2;
+    q.Z3[2] = neg(eight);
+    q.Z3[3] = two - two * w2;
+    auto tq = std::chrono::steady_clock::now();
+    hipLaunchKernelGGL(k_quotient, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, A4.p, B4.p, C4.p, Z4.p, qm.p,
+                       ql.p, qr.p, qo.p, qc.p, sigma.p, lagrange.p, nPublic, A.p, (size_t)n, root_lo.p, root_hi.p, q,
+                       T.p, Tz.p);
+    NZ_HIP(hipGetLastError());
+    ntt(eng->ntt_tables, T.p, t.p, power + 2, true, s);
+    ntt(eng->ntt_tables, Tz.p, tz.p, power + 2, true, s);
+    hipLaunchKernelGGL(k_div_zh, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, t.p, tz.p, (size_t)n, flags.p);
+    NZ_HIP(hipGetLastError());
+    uint32_t f = 0;
+    NZ_HIP(hipMemcpyAsync(&f, flags.p, 4, hipMemcpyDeviceToHost, s));
+    NZ_HIP(hipStreamSynchronize(s));
+    ntt_ms += ms_since(tq);
+    if (f & 1u) throw Error(NZCB_ERR_T_DIV, "T Polynomial is not divisible");
+    if (f & 2u) throw Error(NZCB_ERR_TZ, "Tz Polynomial is not well calculated");
+    lg("multiexp T1");
+    pT1 = commit(t.p, n);
+    lg("multiexp T2");
+    pT2 = commit(t.p + n, n);
+    lg("multiexp T3");
+    pT3 = commit(t.p + 2 * (size_t)n, n + 6);
+  }
+  tm[4] = ms_since(t3);
+
+  // ---------------- round 4 ----------------
+  auto t4 = std::chrono::steady_clock::now();
+  Fr xi, ea, eb, ec, es1, es2, et, ezw, er, xim;
+  {
+    std::vector<uint8_t> tr(192);
+    g1_uncompressed(pT1, tr.data());
+    g1_uncompressed(pT2, tr.data() + 64);
+    g1_uncompressed(pT3, tr.data() + 128);
+    xi = hash_to_fr(tr);
+    lg("xi: " + fr_dec(xi));
+    ea = eval_poly(pol_a.p, n + 2, xi);
+    eb = eval_poly(pol_b.p, n + 2, xi);
+    ec = eval_poly(pol_c.p, n + 2, xi);
+    es1 = eval_poly(sigma.p, n, xi);
+    es2 = eval_poly(sigma.p + 5 * (size_t)n, n, xi);
+    et = eval_poly(t.p, 3 * (size_t)n + 6, xi);
+    ezw = eval_poly(pol_z.p, n + 3, xi * wn);
+    Fr coef_ab = ea * eb;
+    Fr betaxi = beta * xi;
+    Fr e2 = (ea + betaxi + gamma) * (eb + betaxi * k1 + gamma);
+    e2 = e2 * (ec + betaxi * k2 + gamma) * alpha;
+    Fr e3 = (ea + beta * es1 + gamma) * (eb + beta * es2 + gamma);
+    e3 = e3 * beta * ezw * alpha;
+    xim = xi;
+    for (int i = 0; i < power; i++) xim = sqr(xim);
+    Fr eval_l1 = (xim - Fr::one()) * inverse((xi - Fr::one()) * fr_small(n));
+    Fr e4 = eval_l1 * (alpha * alpha);
+    RArgs ra{e2 + e4, coef_ab, ea, eb, ec, e3};
+    hipLaunchKernelGGL(k_pol_r, dim3(grid_for(n + 3, kT, 1u << 30)), dim3(kT), 0, s, pol_z.p, qm.p, ql.p, qr.p,
+                       qo.p, qc.p, sigma.p + 10 * (size_t)n, (size_t)n, ra, pol_r.p);
+    NZ_HIP(hipGetLastError());
+    er = eval_poly(pol_r.p, n + 3, xi);
+  }
+  tm[5] = ms_since(t4);
+
+  // ---------------- round 5 ----------------
+  auto t5 = std::chrono::steady_clock::now();
+  {
+    std::vector<uint8_t> tr(7 * 32);
+    const Fr* ev[7] = {&ea, &eb, &ec, &es1, &es2, &ezw, &er};
+    for (int i = 0; i < 7; i++) fr_to_be(*ev[i], tr.data() + 32 * i);
+    WArgs wa;
+    wa.v[0] = Fr::zero();
+    wa.v[1] = hash_to_fr(tr);
+    lg("v: " + fr_dec(wa.v[1]));
+    for (int i = 2; i <= 6; i++) wa.v[i] = wa.v[i - 1] * wa.v[1];
+    wa.xim = xim;
+    wa.xi2m = xim * xim;
+    wa.w0sub = et + wa.v[1] * er + wa.v[2] * ea + wa.v[3] * eb + wa.v[4] * ec + wa.v[5] * es1 + wa.v[6] * es2;
+    hipLaunchKernelGGL(k_pol_wxi, dim3(grid_for(n + 6, kT, 1u << 30)), dim3(kT), 0, s, t.p, pol_r.p, pol_a.p,
+                       pol_b.p, pol_c.p, sigma.p, sigma.p + 5 * (size_t)n, (size_t)n, wa, T.p);
+    NZ_HIP(hipGetLastError());
+    div_pol1(T.p, n + 6, xi, Fr::zero(), pol_wxi.p, 4u);
+    div_pol1(pol_z.p, n + 3, xi * wn, ezw, pol_wxiw.p, 4u);
+    uint32_t f = 0;
+    NZ_HIP(hipMemcpyAsync(&f, flags.p, 4, hipMemcpyDeviceToHost, s));
+    NZ_HIP(hipStreamSynchronize(s));
+    if (f & 4u) throw Error(NZCB_ERR_DIVPOL, "Polinomial does not divide");
+    lg("multiexp Wxi");
+    pWxi = commit(pol_wxi.p, n + 6);
+    lg("multiexp Wxiw");
+    pWxiw = commit(pol_wxiw.p, n + 3);
+  }
+  tm[6] = ms_since(t5);
+  tm[0] = ms_since(T0);
+  tm[7] = msm_ms;
+  tm[8] = ntt_ms;
+
+  // ---------------- output ----------------
+  const G1Affine* pts[9] = {&pA, &pB, &pC, &pZ, &pT1, &pT2, &pT3, &pWxi, &pWxiw};
+  for (int i = 0; i < 9; i++) {
+    uint8_t* o = proof_out + 64 * i;
+    if (pts[i]->is_inf()) {
+      std::memset(o, 0, 64);
+    } else {
+      Fq x = from_mont(pts[i]->x), y = from_mont(pts[i]->y);
+      std::memcpy(o, x.v, 32);
+      std::memcpy(o + 32, y.v, 32);
+    }
+  }
+  const Fr* ev[7] = {&ea, &eb, &ec, &es1, &es2, &ezw, &er};
+  for (int i = 0; i < 7; i++) fr_to_le_normal(*ev[i], proof_out + 9 * 64 + 32 * i);
+  for (uint32_t i = 0; i < nPublic; i++) {
+    // publicSignals = witness[1..nPublic] as given (normal form, reduced)
+    Fr m = fr_from_le_normal(witness + 32 * (size_t)(i + 1));
+    fr_to_le_normal(m, pub_out + 32 * (size_t)i);
+  }
+}
+
+}  // namespace nzcb

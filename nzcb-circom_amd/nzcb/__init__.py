@@ -1,0 +1,347 @@
+"""ctypes binding of ``libnzcb.so`` (the C-ABI in ``include/nzcb.h``).
+
+Host-side mirror of the reference's prover interface for this path
+(snarkjs 0.4.12 ``plonk.prove(zkeyFileName, witnessFileName, logger)`` [EXT],
+``/root/reference/package.json:18``): ``plonk.prove`` takes a
+zkey and a witness (paths or bytes) and returns ``{proof, publicSignals}`` in
+snarkjs's decimal-string JSON layout, raising with snarkjs's error text.
+
+The library is the product: there is no CPU fallback. Loading fails loudly when
+``lib/libnzcb.so`` has not been built, and every compute call needs a HIP device.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+from ctypes import POINTER, c_char, c_double, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NZCB_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libnzcb.so"))
+
+PROOF_BYTES = 9 * 64 + 7 * 32
+BLINDING_BYTES = 11 * 32
+
+ERROR_NAMES = {
+    0: "OK", 1: "ARG", 2: "FORMAT", 3: "NOT_PLONK", 4: "CURVE", 5: "WITNESS_LEN", 6: "COPY",
+    7: "T_DIV", 8: "TZ", 9: "DIVPOL", 10: "HIP", 11: "INTERNAL",
+}
+
+EXPORTED_SYMBOLS = [
+    "nzcb_version", "nzcb_device_count", "nzcb_ctx_create", "nzcb_ctx_destroy", "nzcb_ctx_set_logger",
+    "nzcb_ctx_set_transcript_public", "nzcb_ctx_info", "nzcb_prove", "nzcb_prove_witness",
+    "nzcb_ctx_last_timings", "nzcb_proof_to_json", "nzcb_public_to_json", "nzcb_synth_setup", "nzcb_free",
+    "nzcb_engine_create", "nzcb_engine_destroy", "nzcb_engine_ntt", "nzcb_engine_msm", "nzcb_dev_alloc",
+    "nzcb_dev_free", "nzcb_memcpy_h2d", "nzcb_memcpy_d2h", "nzcb_engine_ntt_dev", "nzcb_engine_msm_dev",
+    "nzcb_engine_time_ntt", "nzcb_engine_fr_mul",
+]
+
+
+class NzcbError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+        self.name = ERROR_NAMES.get(code, str(code))
+
+
+class _Err(ctypes.Structure):
+    _fields_ = [("code", c_int), ("msg", c_char * 256)]
+
+
+LOG_FN = ctypes.CFUNCTYPE(None, c_void_p, ctypes.c_char_p)
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load the shared library (raises OSError if it is missing)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    lib = ctypes.CDLL(path or LIB_PATH)
+    u8p = POINTER(c_uint8)
+    sigs = {
+        "nzcb_version": (ctypes.c_char_p, []),
+        "nzcb_device_count": (c_int, []),
+        "nzcb_ctx_create": (c_void_p, [u8p, c_size_t, c_int, POINTER(_Err)]),
+        "nzcb_ctx_destroy": (None, [c_void_p]),
+        "nzcb_ctx_set_logger": (None, [c_void_p, LOG_FN, c_void_p]),
+        "nzcb_ctx_set_transcript_public": (None, [c_void_p, c_int]),
+        "nzcb_ctx_info": (c_int, [c_void_p, POINTER(c_uint32)]),
+        "nzcb_prove": (c_int, [c_void_p, u8p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
+        "nzcb_prove_witness": (c_int, [c_void_p, u8p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
+        "nzcb_ctx_last_timings": (c_int, [c_void_p, POINTER(c_double), c_int]),
+        "nzcb_proof_to_json": (c_int, [u8p, ctypes.c_char_p, c_size_t]),
+        "nzcb_public_to_json": (c_int, [u8p, c_int, ctypes.c_char_p, c_size_t]),
+        "nzcb_synth_setup": (c_int, [c_int, c_int, c_int, c_uint64, c_uint32, u8p, c_int,
+                                     POINTER(POINTER(c_uint8)), POINTER(c_size_t),
+                                     POINTER(POINTER(c_uint8)), POINTER(c_size_t), POINTER(_Err)]),
+        "nzcb_free": (None, [c_void_p]),
+        "nzcb_engine_create": (c_void_p, [c_int, c_int, c_size_t, POINTER(_Err)]),
+        "nzcb_engine_destroy": (None, [c_void_p]),
+        "nzcb_engine_ntt": (c_int, [c_void_p, u8p, u8p, c_int, c_int, POINTER(_Err)]),
+        "nzcb_engine_msm": (c_int, [c_void_p, u8p, u8p, c_size_t, c_int, u8p, POINTER(_Err)]),
+        "nzcb_dev_alloc": (c_void_p, [c_size_t]),
+        "nzcb_dev_free": (None, [c_void_p]),
+        "nzcb_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_size_t]),
+        "nzcb_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_size_t]),
+        "nzcb_engine_ntt_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, POINTER(_Err)]),
+        "nzcb_engine_msm_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, u8p, POINTER(_Err)]),
+        "nzcb_engine_time_ntt": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, POINTER(c_double),
+                                         POINTER(_Err)]),
+        "nzcb_engine_fr_mul": (c_int, [c_void_p, u8p, u8p, u8p, c_size_t, c_int, POINTER(_Err)]),
+    }
+    lib.missing_symbols = []
+    for name, (res, args) in sigs.items():
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            lib.missing_symbols.append(name)
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _buf(data: bytes):
+    return (c_uint8 * len(data)).from_buffer_copy(data) if data else (c_uint8 * 1)()
+
+
+def _out(n: int):
+    return (c_uint8 * max(n, 1))()
+
+
+def _check(rc: int, err: _Err):
+    if rc != 0:
+        raise NzcbError(rc, err.msg.decode(errors="replace"))
+
+
+def version() -> str:
+    return load().nzcb_version().decode()
+
+
+def device_count() -> int:
+    return load().nzcb_device_count()
+
+
+class Engine:
+    """Kernel-level access (NTT, MSM, field mul) for tests and microbenchmarks."""
+
+    def __init__(self, device: int = 0, max_log_ntt: int = 12, max_msm_points: int = 1 << 12):
+        self.lib = load()
+        err = _Err()
+        self.h = self.lib.nzcb_engine_create(device, max_log_ntt, max_msm_points, ctypes.byref(err))
+        if not self.h:
+            raise NzcbError(err.code, err.msg.decode(errors="replace"))
+
+    def close(self):
+        if self.h:
+            self.lib.nzcb_engine_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def ntt(self, data_lem: bytes, log_n: int, inverse: bool = False) -> bytes:
+        n = 1 << log_n
+        assert len(data_lem) == 32 * n
+        out = _out(32 * n)
+        err = _Err()
+        _check(self.lib.nzcb_engine_ntt(self.h, _buf(data_lem), out, log_n, int(inverse), ctypes.byref(err)), err)
+        return bytes(out)
+
+    def msm(self, bases_lem: bytes, scalars: bytes, scalars_mont: bool = False) -> bytes:
+        n = len(scalars) // 32
+        assert len(bases_lem) == 64 * n
+        out = _out(64)
+        err = _Err()
+        _check(self.lib.nzcb_engine_msm(self.h, _buf(bases_lem), _buf(scalars), n, int(scalars_mont), out,
+                                        ctypes.byref(err)), err)
+        return bytes(out)
+
+    def field_mul(self, a_lem: bytes, b_lem: bytes, field_q: bool = False) -> bytes:
+        n = len(a_lem) // 32
+        out = _out(32 * n)
+        err = _Err()
+        _check(self.lib.nzcb_engine_fr_mul(self.h, _buf(a_lem), _buf(b_lem), out, n, int(field_q),
+                                           ctypes.byref(err)), err)
+        return bytes(out)
+
+    def time_ntt(self, dev_in: int, dev_out: int, log_n: int, inverse: bool, reps: int) -> float:
+        ms = c_double()
+        err = _Err()
+        _check(self.lib.nzcb_engine_time_ntt(self.h, dev_in, dev_out, log_n, int(inverse), reps, ctypes.byref(ms),
+                                             ctypes.byref(err)), err)
+        return ms.value
+
+    def msm_dev(self, dev_bases: int, dev_scalars: int, n: int, scalars_mont: bool) -> bytes:
+        out = _out(64)
+        err = _Err()
+        _check(self.lib.nzcb_engine_msm_dev(self.h, dev_bases, dev_scalars, n, int(scalars_mont), out,
+                                            ctypes.byref(err)), err)
+        return bytes(out)
+
+
+def dev_alloc(nbytes: int) -> int:
+    p = load().nzcb_dev_alloc(nbytes)
+    if not p:
+        raise NzcbError(10, "hipMalloc failed")
+    return p
+
+
+def dev_free(p: int):
+    load().nzcb_dev_free(p)
+
+
+def h2d(dst: int, data: bytes):
+    buf = ctypes.create_string_buffer(data, len(data))
+    rc = load().nzcb_memcpy_h2d(dst, buf, len(data))
+    if rc:
+        raise NzcbError(rc, "h2d failed")
+
+
+def d2h(src: int, nbytes: int) -> bytes:
+    buf = ctypes.create_string_buffer(nbytes)
+    rc = load().nzcb_memcpy_d2h(buf, src, nbytes)
+    if rc:
+        raise NzcbError(rc, "d2h failed")
+    return buf.raw
+
+
+def _read(x) -> bytes:
+    """snarkjs accepts a file name or {type: "mem", data}; here: path, bytes or {"type": "mem", "data": ...}."""
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        return bytes(x)
+    if isinstance(x, dict) and x.get("type") == "mem":
+        return bytes(x["data"])
+    with open(x, "rb") as f:
+        return f.read()
+
+
+class ProverContext:
+    """A zkey uploaded once to one GPU (``nzcb_ctx_create``); prove many witnesses against it."""
+
+    def __init__(self, zkey, device: int = 0, logger=None, transcript_public: bool = True):
+        self.lib = load()
+        data = _read(zkey)
+        err = _Err()
+        self.h = self.lib.nzcb_ctx_create(_buf(data), len(data), device, ctypes.byref(err))
+        if not self.h:
+            raise NzcbError(err.code, err.msg.decode(errors="replace"))
+        info = (c_uint32 * 5)()
+        self.lib.nzcb_ctx_info(self.h, info)
+        self.domain_size, self.n_public, self.n_vars, self.n_additions, self.n_constraints = list(info)
+        self._logcb = None
+        if logger is not None:
+            self.set_logger(logger)
+        if not transcript_public:
+            self.lib.nzcb_ctx_set_transcript_public(self.h, 0)
+
+    def set_logger(self, logger):
+        fn = getattr(logger, "debug", logger)
+        self._logcb = LOG_FN(lambda _u, m: fn(m.decode()))
+        self.lib.nzcb_ctx_set_logger(self.h, self._logcb, None)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.nzcb_ctx_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def prove_raw(self, wtns, blinding: bytes | None = None):
+        """Returns (proof_bytes, public_bytes) in the C-ABI layout."""
+        data = _read(wtns)
+        proof = _out(PROOF_BYTES)
+        pub = _out(32 * self.n_public)
+        err = _Err()
+        bl = _buf(blinding) if blinding is not None else None
+        if blinding is not None and len(blinding) != BLINDING_BYTES:
+            raise ValueError("blinding must be 11 x 32 bytes")
+        _check(self.lib.nzcb_prove(self.h, _buf(data), len(data), bl, proof, pub, 32 * self.n_public,
+                                   ctypes.byref(err)), err)
+        return bytes(proof), bytes(pub)[:32 * self.n_public]
+
+    def prove_witness_raw(self, witness_le: bytes, blinding: bytes | None = None):
+        n = len(witness_le) // 32
+        proof = _out(PROOF_BYTES)
+        pub = _out(32 * self.n_public)
+        err = _Err()
+        bl = _buf(blinding) if blinding is not None else None
+        _check(self.lib.nzcb_prove_witness(self.h, _buf(witness_le), n, bl, proof, pub, 32 * self.n_public,
+                                           ctypes.byref(err)), err)
+        return bytes(proof), bytes(pub)[:32 * self.n_public]
+
+    def prove(self, wtns, blinding: bytes | None = None):
+        """snarkjs-shaped result: {"proof": {...}, "publicSignals": [...]}."""
+        proof, pub = self.prove_raw(wtns, blinding)
+        return {"proof": proof_to_json(proof), "publicSignals": public_to_json(pub, self.n_public)}
+
+    def last_timings(self):
+        ms = (c_double * 9)()
+        k = self.lib.nzcb_ctx_last_timings(self.h, ms, 9)
+        names = ["total", "witness", "round1", "round2", "round3", "round4", "round5", "msm", "ntt"]
+        return dict(zip(names[:k], list(ms)[:k]))
+
+
+def proof_to_json(proof: bytes) -> dict:
+    lib = load()
+    cap = 8192
+    out = ctypes.create_string_buffer(cap)
+    rc = lib.nzcb_proof_to_json(_buf(proof), out, cap)
+    if rc:
+        raise NzcbError(1, "json buffer too small")
+    return json.loads(out.value.decode())
+
+
+def public_to_json(pub: bytes, n_public: int) -> list:
+    lib = load()
+    cap = 80 * n_public + 8
+    out = ctypes.create_string_buffer(cap)
+    rc = lib.nzcb_public_to_json(_buf(pub), n_public, out, cap)
+    if rc:
+        raise NzcbError(1, "json buffer too small")
+    return json.loads(out.value.decode())
+
+
+class plonk:
+    """snarkjs-compatible entry points (``snarkjs.plonk.prove`` [EXT])."""
+
+    @staticmethod
+    def prove(zkeyFileName, witnessFileName, logger=None, device: int = 0, blinding: bytes | None = None):
+        ctx = ProverContext(zkeyFileName, device=device, logger=logger)
+        try:
+            if blinding is None:
+                blinding = random_blinding()
+            return ctx.prove(witnessFileName, blinding)
+        finally:
+            ctx.close()
+
+
+def random_blinding() -> bytes:
+    """11 uniform Fr scalars (snarkjs ``Fr.random()``), 32-byte LE each."""
+    import secrets
+    r = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+    return b"".join((secrets.randbelow(r)).to_bytes(32, "little") for _ in range(11))
+
+
+def synth_setup(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,
+                n_constraints: int = 0, tau: int = 0x6E7A6362746175, device: int = 0):
+    """Seeded synthetic circuit + zkey built on the GPU (``nzcb_synth_setup``). Returns (zkey, wtns) bytes."""
+    lib = load()
+    zp = POINTER(c_uint8)()
+    wp = POINTER(c_uint8)()
+    zl = c_size_t()
+    wl = c_size_t()
+    err = _Err()
+    taub = _buf(int(tau).to_bytes(32, "little"))
+    rc = lib.nzcb_synth_setup(power, n_public, n_inputs, seed, n_constraints, taub, device, ctypes.byref(zp),
+                              ctypes.byref(zl), ctypes.byref(wp), ctypes.byref(wl), ctypes.byref(err))
+    _check(rc, err)
+    try:
+        zkey = ctypes.string_at(zp, zl.value)
+        wtns = ctypes.string_at(wp, wl.value)
+    finally:
+        lib.nzcb_free(ctypes.cast(zp, c_void_p))
+        lib.nzcb_free(ctypes.cast(wp, c_void_p))
+    return zkey, wtns

@@ -1,0 +1,157 @@
+"""GPU PLONK prover parity through the C-ABI (nzcb_ctx_create / nzcb_prove).
+
+Bit-exact against (a) the committed golden fixtures made by the CPU oracle and
+(b) the oracle run live on fresh seeded circuits. Error paths reproduce
+snarkjs 0.4.12's exception text.
+"""
+import json
+import os
+import struct
+
+import pytest
+
+import nzcb
+from oracle import binfmt, plonk, synth
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _gold(name):
+    with open(os.path.join(GOLD, f"{name}.json")) as f:
+        meta = json.load(f)
+    with open(os.path.join(GOLD, f"{name}.zkey"), "rb") as f:
+        zkey = f.read()
+    with open(os.path.join(GOLD, f"{name}.wtns"), "rb") as f:
+        wtns = f.read()
+    return meta, zkey, wtns
+
+
+@pytest.mark.parametrize("name", ["p5", "p8"])
+@pytest.mark.parametrize("bl", ["zero", "fixed"])
+def test_golden_proof_bits(name, bl):
+    meta, zkey, wtns = _gold(name)
+    exp = meta["proofs"][bl]
+    ctx = nzcb.ProverContext(zkey)
+    blinding = bytes.fromhex(exp["blinding"]) if exp["blinding"] else None
+    proof, pub = ctx.prove_raw(wtns, blinding)
+    assert proof.hex() == exp["proof_bin"]
+    res = ctx.prove(wtns, blinding)
+    assert res["proof"] == exp["proof"]
+    assert res["publicSignals"] == exp["publicSignals"]
+    # keys in snarkjs order
+    assert list(res["proof"].keys()) == list(exp["proof"].keys())
+    ctx.close()
+
+
+def test_repeat_proofs_same_context():
+    meta, zkey, wtns = _gold("p8")
+    exp = meta["proofs"]["fixed"]
+    ctx = nzcb.ProverContext(zkey)
+    bl = bytes.fromhex(exp["blinding"])
+    for _ in range(3):
+        proof, _ = ctx.prove_raw(wtns, bl)
+        assert proof.hex() == exp["proof_bin"]
+
+
+@pytest.mark.parametrize("power,seed,npub,nin", [(4, 11, 1, 2), (6, 12, 3, 5), (10, 13, 3, 8), (11, 14, 5, 16)])
+def test_live_oracle(power, seed, npub, nin):
+    c = synth.synth_circuit(power, npub, nin, seed=seed)
+    tau = 1000003 + seed
+    zk = plonk.setup(c, tau)
+    zkey = binfmt.write_zkey(zk)
+    wtns = binfmt.write_wtns(c["witness"])
+    bl = [(seed * 7919 + i * 104729) % plonk.R_MOD if hasattr(plonk, "R_MOD") else 0 for i in range(11)]
+    from oracle.bn254 import R_MOD
+    bl = [(seed * 7919 + i * 104729 + (i << 200)) % R_MOD for i in range(11)]
+    proof, pub = plonk.prove(zk, c["witness"], bl)
+    ctx = nzcb.ProverContext(zkey)
+    got, gpub = ctx.prove_raw(wtns, b"".join(x.to_bytes(32, "little") for x in bl))
+    assert got == plonk.proof_to_bytes(proof)
+    assert gpub == b"".join(x.to_bytes(32, "little") for x in pub)
+    assert plonk.verify_with_trapdoor(zk, pub, plonk.proof_from_bytes(got), tau)
+
+
+def test_transcript_without_public_inputs():
+    c = synth.synth_circuit(7, 3, 4, seed=21)
+    zk = plonk.setup(c, 4242)
+    proof, pub = plonk.prove(zk, c["witness"], synth.fixed_blindings(), transcript_pub=False)
+    ctx = nzcb.ProverContext(binfmt.write_zkey(zk), transcript_public=False)
+    got, _ = ctx.prove_raw(binfmt.write_wtns(c["witness"]),
+                           b"".join(x.to_bytes(32, "little") for x in synth.fixed_blindings()))
+    assert got == plonk.proof_to_bytes(proof)
+
+
+def test_logger_lines():
+    meta, zkey, wtns = _gold("p5")
+    lines = []
+    ctx = nzcb.ProverContext(zkey, logger=lines.append)
+    ctx.prove_raw(wtns)
+    assert "multiexp A" in lines and any(x.startswith("beta: ") for x in lines)
+
+
+def test_error_witness_length():
+    meta, zkey, wtns = _gold("p5")
+    w = binfmt.read_wtns(wtns)["witness"][:-1]
+    ctx = nzcb.ProverContext(zkey)
+    with pytest.raises(nzcb.NzcbError) as ei:
+        ctx.prove_raw(binfmt.write_wtns(w))
+    assert ei.value.name == "WITNESS_LEN"
+    assert str(ei.value).startswith("Invalid witness length. Circuit: ")
+
+
+def test_error_bad_witness_not_divisible():
+    meta, zkey, wtns = _gold("p8")
+    w = binfmt.read_wtns(wtns)["witness"]
+    w[20] = (w[20] + 1)
+    ctx = nzcb.ProverContext(zkey)
+    with pytest.raises(nzcb.NzcbError) as ei:
+        ctx.prove_raw(binfmt.write_wtns(w))
+    assert str(ei.value) == "T Polynomial is not divisible"
+
+
+def test_error_copy_constraints():
+    meta, zkey, wtns = _gold("p8")
+    zk = binfmt.read_zkey(zkey)
+    # rewire one A-wire of a gate to a different signal: the permutation no longer matches
+    zk["aMap"][40] = zk["aMap"][41] if zk["aMap"][41] != zk["aMap"][40] else 1
+    ctx = nzcb.ProverContext(binfmt.write_zkey(zk))
+    with pytest.raises(nzcb.NzcbError) as ei:
+        ctx.prove_raw(wtns)
+    assert str(ei.value) == "Copy constraints does not match"
+
+
+def test_error_not_plonk_and_curve():
+    meta, zkey, wtns = _gold("p5")
+    bad = bytearray(zkey)
+    # section 1 payload (protocol id) starts after the file header (12) + section header (12)
+    struct.pack_into("<I", bad, 24, 1)
+    with pytest.raises(nzcb.NzcbError) as ei:
+        nzcb.ProverContext(bytes(bad))
+    assert str(ei.value) == "zkey file is not plonk"
+    ctx = nzcb.ProverContext(zkey)
+    w = bytearray(wtns)
+    # wtns section 1: n8 at offset 24, q at 28..60
+    w[28] ^= 1
+    with pytest.raises(nzcb.NzcbError) as ei:
+        ctx.prove_raw(bytes(w))
+    assert str(ei.value) == "Curve of the witness does not match the curve of the proving key"
+
+
+def test_plonk_prove_api_random_blinding_verifies(tmp_path):
+    meta, zkey, wtns = _gold("p8")
+    zp = tmp_path / "c.zkey"
+    wp = tmp_path / "c.wtns"
+    zp.write_bytes(zkey)
+    wp.write_bytes(wtns)
+    res = nzcb.plonk.prove(str(zp), str(wp))
+    proof = res["proof"]
+    zk = binfmt.read_zkey(zkey)
+    p = {}
+    for k in plonk.PROOF_POINTS:
+        v = proof[k]
+        p[k] = None if v[2] == "0" else (int(v[0]), int(v[1]))
+    for k in plonk.PROOF_EVALS:
+        p[k] = int(proof[k])
+    pub = [int(x) for x in res["publicSignals"]]
+    assert plonk.verify_with_trapdoor(zk, pub, p, meta["tau"])
