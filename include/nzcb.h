@@ -88,10 +88,20 @@ int nzcb_prove(nzcb_ctx* ctx, const uint8_t* wtns, size_t wtns_len, const uint8_
 int nzcb_prove_witness(nzcb_ctx* ctx, const uint8_t* witness, size_t n_witness, const uint8_t* blinding,
                        uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_err* err);
 
+/* Same with the witness already resident in HBM: dev_witness is a device pointer
+ * (nzcb_dev_alloc) holding nWitness x 32-byte LE normal-form values. */
+int nzcb_prove_device(nzcb_ctx* ctx, const void* dev_witness, size_t n_witness, const uint8_t* blinding,
+                      uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_err* err);
+
 /* Wall-clock milliseconds of the last proof's phases:
  * [0] total [1] witness upload+additions+ABC [2] round1 [3] round2 [4] round3 [5] round4 [6] round5
  * [7] all MSMs [8] all NTTs. Returns the number of values written. */
 int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap);
+
+/* HIP-event timing of the MSM bucket-accumulation kernel (the dominant kernel):
+ * out = {total ms, launches, MSM points, bucket entries} accumulated since the last
+ * reset; enable = 1 / 0 turns timing on / off and resets, -1 only reads. */
+int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]);
 
 /* snarkjs-format JSON ({proof}, [publicSignals]) from the binary outputs. */
 int nzcb_proof_to_json(const uint8_t* proof, char* out, size_t cap);

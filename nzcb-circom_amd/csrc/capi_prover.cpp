@@ -120,6 +120,22 @@ int nzcb_prove_witness(nzcb_ctx* ctx, const uint8_t* witness, size_t n_witness, 
   }
 }
 
+int nzcb_prove_device(nzcb_ctx* ctx, const void* dev_witness, size_t n_witness, const uint8_t* blinding,
+                      uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_err* err) {
+  if (!ctx || !dev_witness || !proof_out) return fail(err, NZCB_ERR_ARG, "null argument");
+  if (pub_cap < 32 * (size_t)ctx->p->nPublic || (!pub_out && ctx->p->nPublic))
+    return fail(err, NZCB_ERR_ARG, "public output buffer too small");
+  try {
+    ctx->p->prove((const uint8_t*)dev_witness, n_witness, blinding, proof_out, pub_out, true);
+    if (err) err->code = 0;
+    return 0;
+  } catch (const Error& e) {
+    return fail(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, NZCB_ERR_INTERNAL, e.what());
+  }
+}
+
 int nzcb_prove(nzcb_ctx* ctx, const uint8_t* wtns, size_t wtns_len, const uint8_t* blinding, uint8_t* proof_out,
                uint8_t* pub_out, size_t pub_cap, nzcb_err* err) {
   if (!ctx || !wtns) return fail(err, NZCB_ERR_ARG, "null argument");
@@ -138,6 +154,23 @@ int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap) {
   int k = cap < 9 ? cap : 9;
   for (int i = 0; i < k; i++) ms[i] = ctx->p->tm[i];
   return k;
+}
+
+int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
+  if (!ctx) return NZCB_ERR_ARG;
+  MsmScratch& sc = ctx->p->eng->msm_scratch;
+  if (out) {
+    out[0] = sc.prof_ms;
+    out[1] = (double)sc.prof_launches;
+    out[2] = (double)sc.prof_points;
+    out[3] = (double)sc.prof_entries;
+  }
+  if (enable >= 0) {
+    sc.prof = enable != 0;
+    sc.prof_ms = 0;
+    sc.prof_launches = sc.prof_points = sc.prof_entries = 0;
+  }
+  return 0;
 }
 
 int nzcb_proof_to_json(const uint8_t* proof, char* out, size_t cap) {

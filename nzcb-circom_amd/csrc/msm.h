@@ -20,6 +20,11 @@ struct MsmScratch {
   DevBuf<uint8_t> scan_tmp;
   size_t scan_tmp_bytes = 0;
   std::vector<G1xyzz> host_win;
+  // optional HIP-event timing of the bucket-accumulation kernel (bench.py roofline)
+  bool prof = false;
+  double prof_ms = 0;
+  uint64_t prof_launches = 0, prof_points = 0, prof_entries = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
   void init(size_t max_points);
 };
 

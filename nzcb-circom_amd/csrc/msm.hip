@@ -279,10 +279,18 @@ G1xyzz msm(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, b
   digits_dispatch(c, scalars, n, mont ? 1 : 0, sc, st, true);
   const size_t max_entries = n * (size_t)nw;
   const size_t nthreads = (max_entries + kChunk - 1) / kChunk;
+  if (sc.prof) {
+    if (!sc.ev0) {
+      NZ_HIP(hipEventCreate(&sc.ev0));
+      NZ_HIP(hipEventCreate(&sc.ev1));
+    }
+    NZ_HIP(hipEventRecord(sc.ev0, st));
+  }
   hipLaunchKernelGGL(msm_accumulate_kernel, dim3(grid_for(nthreads, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0,
                      st, bases, sc.sorted.p, sc.offsets.p, nkeys, nthreads, sc.buckets.p, sc.carry_own.p,
                      sc.carry_cont.p, sc.own_key.p);
   NZ_HIP(hipGetLastError());
+  if (sc.prof) NZ_HIP(hipEventRecord(sc.ev1, st));
   hipLaunchKernelGGL(msm_fixup_kernel, dim3(grid_for(nthreads, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0, st,
                      sc.offsets.p, sc.own_key.p, sc.carry_own.p, sc.carry_cont.p, nthreads, sc.buckets.p);
   NZ_HIP(hipGetLastError());
@@ -295,6 +303,16 @@ G1xyzz msm(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, b
   NZ_HIP(hipGetLastError());
   NZ_HIP(hipMemcpyAsync(sc.host_win.data(), sc.win.p, nw * sizeof(G1xyzz), hipMemcpyDeviceToHost, st));
   NZ_HIP(hipStreamSynchronize(st));
+  if (sc.prof) {
+    float t = 0;
+    NZ_HIP(hipEventElapsedTime(&t, sc.ev0, sc.ev1));
+    uint32_t total = 0;
+    NZ_HIP(hipMemcpy(&total, sc.offsets.p + nkeys, 4, hipMemcpyDeviceToHost));
+    sc.prof_ms += t;
+    sc.prof_launches++;
+    sc.prof_points += n;
+    sc.prof_entries += total;
+  }
   G1xyzz res = G1xyzz::inf();
   for (int w = nw - 1; w >= 0; w--) {
     for (int i = 0; i < c; i++) res = xyzz_dbl(res);

@@ -52,8 +52,9 @@ struct Prover {
 
   Prover(const uint8_t* zkey, size_t len, int device);
   // witness: nWit x 32-byte LE normal-form values; blinding: 11 x 32-byte LE or null
+  // witness_on_device: `witness` is a device pointer (HBM-resident input, no PCIe copy)
   void prove(const uint8_t* witness, size_t n_witness, const uint8_t* blinding, uint8_t* proof_out,
-             uint8_t* pub_out);
+             uint8_t* pub_out, bool witness_on_device = false);
 
  private:
   hipStream_t st() const { return eng->stream; }

@@ -649,7 +649,7 @@ void Prover::div_pol1(const Fr* src, size_t m, const Fr& d, const Fr& p0_adjust,
 // prove
 // ----------------------------------------------------------------------------
 void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blinding, uint8_t* proof_out,
-                   uint8_t* pub_out) {
+                   uint8_t* pub_out, bool witness_on_device) {
   if (n_witness != nWit) {
     throw Error(NZCB_ERR_WITNESS_LEN, "Invalid witness length. Circuit: " + std::to_string(nVars) +
                                           ", witness: " + std::to_string(n_witness) + ", " +
@@ -668,8 +668,12 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   NZ_HIP(hipMemsetAsync(flags.p, 0, sizeof(uint32_t), s));
 
   lg("Reading Wtns");
-  NZ_HIP(hipMemcpyAsync(wtns_in.p, witness, (size_t)nWit * 32, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_wit_to_mont, dim3(grid_for(nWit, kT, 1u << 30)), dim3(kT), 0, s, wtns_in.p, wit.p,
+  const Fr* wsrc = (const Fr*)witness;
+  if (!witness_on_device) {
+    NZ_HIP(hipMemcpyAsync(wtns_in.p, witness, (size_t)nWit * 32, hipMemcpyHostToDevice, s));
+    wsrc = wtns_in.p;
+  }
+  hipLaunchKernelGGL(k_wit_to_mont, dim3(grid_for(nWit, kT, 1u << 30)), dim3(kT), 0, s, wsrc, wit.p,
                      (size_t)nWit);
   for (size_t l = 0; l + 1 < add_level_start.size(); l++) {
     uint32_t a0 = add_level_start[l], a1 = add_level_start[l + 1];
@@ -886,9 +890,18 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   }
   const Fr* ev[7] = {&ea, &eb, &ec, &es1, &es2, &ezw, &er};
   for (int i = 0; i < 7; i++) fr_to_le_normal(*ev[i], proof_out + 9 * 64 + 32 * i);
+  std::vector<uint8_t> pubw((size_t)nPublic * 32);
+  if (nPublic) {
+    if (witness_on_device) {
+      NZ_HIP(hipMemcpyAsync(pubw.data(), witness + 32, pubw.size(), hipMemcpyDeviceToHost, s));
+      NZ_HIP(hipStreamSynchronize(s));
+    } else {
+      std::memcpy(pubw.data(), witness + 32, pubw.size());
+    }
+  }
   for (uint32_t i = 0; i < nPublic; i++) {
     // publicSignals = witness[1..nPublic] as given (normal form, reduced)
-    Fr m = fr_from_le_normal(witness + 32 * (size_t)(i + 1));
+    Fr m = fr_from_le_normal(pubw.data() + 32 * (size_t)i);
     fr_to_le_normal(m, pub_out + 32 * (size_t)i);
   }
 }

@@ -29,7 +29,8 @@ ERROR_NAMES = {
 
 EXPORTED_SYMBOLS = [
     "nzcb_version", "nzcb_device_count", "nzcb_ctx_create", "nzcb_ctx_destroy", "nzcb_ctx_set_logger",
-    "nzcb_ctx_set_transcript_public", "nzcb_ctx_info", "nzcb_prove", "nzcb_prove_witness",
+    "nzcb_ctx_set_transcript_public", "nzcb_ctx_info", "nzcb_prove", "nzcb_prove_witness", "nzcb_prove_device",
+    "nzcb_ctx_kernel_stats",
     "nzcb_ctx_last_timings", "nzcb_proof_to_json", "nzcb_public_to_json", "nzcb_synth_setup", "nzcb_free",
     "nzcb_engine_create", "nzcb_engine_destroy", "nzcb_engine_ntt", "nzcb_engine_msm", "nzcb_dev_alloc",
     "nzcb_dev_free", "nzcb_memcpy_h2d", "nzcb_memcpy_d2h", "nzcb_engine_ntt_dev", "nzcb_engine_msm_dev",
@@ -70,6 +71,8 @@ def load(path: str | None = None):
         "nzcb_ctx_info": (c_int, [c_void_p, POINTER(c_uint32)]),
         "nzcb_prove": (c_int, [c_void_p, u8p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
         "nzcb_prove_witness": (c_int, [c_void_p, u8p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
+        "nzcb_prove_device": (c_int, [c_void_p, c_void_p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
+        "nzcb_ctx_kernel_stats": (c_int, [c_void_p, c_int, POINTER(c_double)]),
         "nzcb_ctx_last_timings": (c_int, [c_void_p, POINTER(c_double), c_int]),
         "nzcb_proof_to_json": (c_int, [u8p, ctypes.c_char_p, c_size_t]),
         "nzcb_public_to_json": (c_int, [u8p, c_int, ctypes.c_char_p, c_size_t]),
@@ -221,11 +224,15 @@ def _read(x) -> bytes:
 class ProverContext:
     """A zkey uploaded once to one GPU (``nzcb_ctx_create``); prove many witnesses against it."""
 
-    def __init__(self, zkey, device: int = 0, logger=None, transcript_public: bool = True):
+    def __init__(self, zkey, device: int = 0, logger=None, transcript_public: bool = True, _raw=None):
         self.lib = load()
-        data = _read(zkey)
         err = _Err()
-        self.h = self.lib.nzcb_ctx_create(_buf(data), len(data), device, ctypes.byref(err))
+        if _raw is not None:            # (pointer, length) owned by the caller: no host copy
+            self.h = self.lib.nzcb_ctx_create(ctypes.cast(_raw[0], POINTER(c_uint8)), _raw[1], device,
+                                              ctypes.byref(err))
+        else:
+            data = _read(zkey)
+            self.h = self.lib.nzcb_ctx_create(_buf(data), len(data), device, ctypes.byref(err))
         if not self.h:
             raise NzcbError(err.code, err.msg.decode(errors="replace"))
         info = (c_uint32 * 5)()
@@ -271,6 +278,22 @@ class ProverContext:
         _check(self.lib.nzcb_prove_witness(self.h, _buf(witness_le), n, bl, proof, pub, 32 * self.n_public,
                                            ctypes.byref(err)), err)
         return bytes(proof), bytes(pub)[:32 * self.n_public]
+
+    def prove_device_raw(self, dev_witness: int, n_witness: int, blinding: bytes | None = None):
+        """Witness already resident in HBM (device pointer, normal-form LE values)."""
+        proof = _out(PROOF_BYTES)
+        pub = _out(32 * self.n_public)
+        err = _Err()
+        bl = _buf(blinding) if blinding is not None else None
+        _check(self.lib.nzcb_prove_device(self.h, dev_witness, n_witness, bl, proof, pub, 32 * self.n_public,
+                                          ctypes.byref(err)), err)
+        return bytes(proof), bytes(pub)[:32 * self.n_public]
+
+    def kernel_stats(self, enable: int = -1):
+        """MSM bucket-accumulation kernel timing: (ms, launches, points, entries); enable 1/0 resets."""
+        out = (c_double * 4)()
+        self.lib.nzcb_ctx_kernel_stats(self.h, enable, out)
+        return tuple(out)
 
     def prove(self, wtns, blinding: bytes | None = None):
         """snarkjs-shaped result: {"proof": {...}, "publicSignals": [...]}."""
@@ -325,6 +348,28 @@ def random_blinding() -> bytes:
     return b"".join((secrets.randbelow(r)).to_bytes(32, "little") for _ in range(11))
 
 
+def synth_context(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,
+                  n_constraints: int = 0, tau: int = 0x6E7A6362746175, device: int = 0):
+    """Build the synthetic circuit's zkey on `device` and upload it straight into a
+    ProverContext without copying the (multi-GB) zkey through Python. Returns (ctx, wtns bytes)."""
+    lib = load()
+    zp = POINTER(c_uint8)()
+    wp = POINTER(c_uint8)()
+    zl = c_size_t()
+    wl = c_size_t()
+    err = _Err()
+    taub = _buf(int(tau).to_bytes(32, "little"))
+    _check(lib.nzcb_synth_setup(power, n_public, n_inputs, seed, n_constraints, taub, device, ctypes.byref(zp),
+                                ctypes.byref(zl), ctypes.byref(wp), ctypes.byref(wl), ctypes.byref(err)), err)
+    try:
+        ctx = ProverContext(None, device=device, _raw=(zp, zl.value))
+        wtns = ctypes.string_at(wp, wl.value)
+    finally:
+        lib.nzcb_free(ctypes.cast(zp, c_void_p))
+        lib.nzcb_free(ctypes.cast(wp, c_void_p))
+    return ctx, wtns
+
+
 def synth_setup(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,
                 n_constraints: int = 0, tau: int = 0x6E7A6362746175, device: int = 0):
     """Seeded synthetic circuit + zkey built on the GPU (``nzcb_synth_setup``). Returns (zkey, wtns) bytes."""
@@ -345,3 +390,25 @@ def synth_setup(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x
         lib.nzcb_free(ctypes.cast(zp, c_void_p))
         lib.nzcb_free(ctypes.cast(wp, c_void_p))
     return zkey, wtns
+
+
+def synth_setup_raw(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,
+                    n_constraints: int = 0, tau: int = 0x6E7A6362746175, device: int = 0):
+    """Like synth_setup but returns library-owned host buffers (zkey_ptr, zkey_len, wtns_ptr, wtns_len)
+    without copying them into Python; release with free_raw()."""
+    lib = load()
+    zp = POINTER(c_uint8)()
+    wp = POINTER(c_uint8)()
+    zl = c_size_t()
+    wl = c_size_t()
+    err = _Err()
+    taub = _buf(int(tau).to_bytes(32, "little"))
+    _check(lib.nzcb_synth_setup(power, n_public, n_inputs, seed, n_constraints, taub, device, ctypes.byref(zp),
+                                ctypes.byref(zl), ctypes.byref(wp), ctypes.byref(wl), ctypes.byref(err)), err)
+    return (ctypes.cast(zp, c_void_p).value, zl.value, ctypes.cast(wp, c_void_p).value, wl.value)
+
+
+def free_raw(raw):
+    lib = load()
+    lib.nzcb_free(raw[0])
+    lib.nzcb_free(raw[2])

@@ -7,8 +7,8 @@ and its r1cs/ptau cannot be built offline (circom, snarkjs and the ptau are
 [EXT], SURVEY.md §7 "Hard parts"). SURVEY.md §8d config 3 therefore
 prescribes a *synthetic satisfied circuit* with a seeded tau. This module
 defines that circuit family bit-exactly; the HIP library's
-``nzcb_synth_setup`` (``nzcb-circom_amd/csrc/synth.cpp``) implements the same
-generator and ``tests/test_synth_parity.py`` checks the two agree byte for
+``nzcb_synth_setup`` (``nzcb-circom_amd/csrc/synth.hip``) implements the same
+generator and ``tests/test_gpu_synth.py`` checks the two agree byte for
 byte on the zkey and wtns they emit.
 
 Gate shape follows what snarkjs ``plonk setup`` emits from an r1cs
@@ -110,6 +110,8 @@ def synth_circuit(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 
         cons.append((s, 0, 0, 0, 1, 0, 0, 0))
     for _ in range(n_constraints - n_public):
         kind = rng.below(8)
+        if kind == 7 and unused_pos < len(unused):
+            kind = 0    # additions read only signals that already sit on a gate wire
         a = pick()
         b = pick()
         if kind == 7:

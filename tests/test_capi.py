@@ -1,0 +1,51 @@
+"""C-ABI library: loads without a GPU, exports every function include/nzcb.h
+declares, and its host-only helpers (JSON formatting) match the oracle."""
+import json
+import os
+import re
+
+import pytest
+
+import nzcb
+from oracle import plonk
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _declared():
+    with open(os.path.join(ROOT, "include", "nzcb.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(nzcb_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_header():
+    lib = nzcb.load()
+    declared = _declared()
+    assert len(declared) >= 25
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert missing == []
+    assert set(nzcb.EXPORTED_SYMBOLS) <= set(declared)
+    assert lib.missing_symbols == []
+    assert "gfx950" in nzcb.version()
+
+
+@pytest.mark.parametrize("name", ["p5", "p8"])
+def test_proof_json_matches_oracle(name):
+    with open(os.path.join(GOLD, f"{name}.json")) as f:
+        meta = json.load(f)
+    for bl in ("zero", "fixed"):
+        exp = meta["proofs"][bl]
+        got = nzcb.proof_to_json(bytes.fromhex(exp["proof_bin"]))
+        assert got == exp["proof"]
+        assert list(got.keys()) == list(exp["proof"].keys())
+        pub = b"".join(int(x).to_bytes(32, "little") for x in exp["publicSignals"])
+        assert nzcb.public_to_json(pub, 3) == exp["publicSignals"]
+
+
+def test_infinity_point_json():
+    proof = bytearray(bytes.fromhex(json.load(open(os.path.join(GOLD, "p5.json")))["proofs"]["zero"]["proof_bin"]))
+    proof[0:64] = bytes(64)
+    assert nzcb.proof_to_json(bytes(proof))["A"] == ["0", "1", "0"]
+    assert plonk.proof_to_json_obj(plonk.proof_from_bytes(bytes(proof)))["A"] == ["0", "1", "0"]

@@ -1,0 +1,31 @@
+"""nzcb_synth_setup (GPU) emits the same zkey / wtns bytes as the CPU oracle's
+synth_circuit + plonk.setup + binfmt writers (oracle/synth.py, oracle/plonk.py)."""
+import pytest
+
+import nzcb
+from oracle import binfmt, plonk, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("power,npub,nin,seed,ncons", [(4, 1, 2, 5, 0), (6, 3, 4, 6, 0), (8, 3, 8, 7, 200),
+                                                       (9, 0, 3, 8, 0)])
+def test_synth_setup_bytes(power, npub, nin, seed, ncons):
+    tau = 0x1234567 + seed
+    zkey, wtns = nzcb.synth_setup(power, npub, nin, seed, ncons, tau)
+    c = synth.synth_circuit(power, npub, nin, seed=seed, n_constraints=ncons or None)
+    zk = plonk.setup(c, tau)
+    assert wtns == binfmt.write_wtns(c["witness"])
+    assert zkey == binfmt.write_zkey(zk)
+
+
+def test_synth_setup_proves_and_verifies():
+    tau = 777
+    zkey, wtns = nzcb.synth_setup(12, 3, 8, 99, 0, tau)
+    ctx = nzcb.ProverContext(zkey)
+    bl = b"".join(x.to_bytes(32, "little") for x in synth.fixed_blindings())
+    proof, pub = ctx.prove_raw(wtns, bl)
+    zk = binfmt.read_zkey(zkey)
+    p = plonk.proof_from_bytes(proof)
+    pubv = [int.from_bytes(pub[i:i + 32], "little") for i in range(0, len(pub), 32)]
+    assert plonk.verify_with_trapdoor(zk, pubv, p, tau)
