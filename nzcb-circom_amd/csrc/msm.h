@@ -19,6 +19,11 @@ struct MsmScratch {
   DevBuf<G1xyzz> win;         // per-window sums
   DevBuf<uint8_t> scan_tmp;
   size_t scan_tmp_bytes = 0;
+  // radix-sort bucketing (default; NZCB_MSM_SORT=atomic selects the histogram+scatter path)
+  bool use_radix = true;
+  DevBuf<uint32_t> keys_in, keys_out, vals_in;
+  DevBuf<uint8_t> sort_tmp;
+  size_t sort_tmp_bytes = 0;
   std::vector<G1xyzz> host_win;
   // optional HIP-event timing of the bucket-accumulation kernel (bench.py roofline)
   bool prof = false;

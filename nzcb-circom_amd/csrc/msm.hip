@@ -24,6 +24,8 @@
 #include "msm.h"
 
 #include <hipcub/hipcub.hpp>
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 namespace nzcb {
@@ -93,6 +95,49 @@ msm_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, uint32_t*
       sorted[pos] = (uint32_t)i | (sign << 31);
     });
   }
+}
+
+// Radix-sort path: every (scalar, window) pair gets a fixed slot w*n + i, so no
+// atomics are needed; zero digits get the sentinel key nkeys and sort last.
+template <int C>
+__global__ void __launch_bounds__(kMsmThreads)
+msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, uint32_t* __restrict__ keys,
+                uint32_t* __restrict__ vals) {
+  constexpr int NW = (255 + C - 1) / C;
+  constexpr uint32_t NB = 1u << (C - 1);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    Fr s = scalars[i];
+    if (mont) s = from_mont(s);
+    uint32_t k[NW];
+    uint32_t v[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      k[w] = NW * NB;
+      v[w] = (uint32_t)i;
+    }
+    for_each_digit<C>(s, [&](int w, uint32_t b, uint32_t sign) {
+      k[w] = (uint32_t)w * NB + b;
+      v[w] = (uint32_t)i | (sign << 31);
+    });
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      keys[(size_t)w * n + i] = k[w];
+      vals[(size_t)w * n + i] = v[w];
+    }
+  }
+}
+
+// offsets[k] = first position of key >= k in the sorted key array (k = 0..nkeys)
+__global__ void __launch_bounds__(kMsmThreads)
+msm_offsets_kernel(const uint32_t* __restrict__ skeys, size_t m, uint32_t nkeys, uint32_t* __restrict__ offsets) {
+  size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > nkeys) return;
+  size_t lo = 0, hi = m;
+  while (lo < hi) {
+    size_t mid = (lo + hi) >> 1;
+    if (skeys[mid] < k) lo = mid + 1; else hi = mid;
+  }
+  offsets[k] = (uint32_t)lo;
 }
 
 // largest k in [0, nkeys) with offsets[k] <= pos  (offsets[nkeys] > pos)
@@ -217,6 +262,15 @@ void MsmScratch::init(size_t maxp) {
   offsets.alloc(max_keys + 1);
   cursor.alloc(max_keys + 1);
   sorted.alloc(max_entries);
+  keys_in.alloc(max_entries);
+  keys_out.alloc(max_entries);
+  vals_in.alloc(max_entries);
+  const char* m = std::getenv("NZCB_MSM_SORT");
+  use_radix = !(m && std::string(m) == "atomic");
+  sort_tmp_bytes = 0;
+  NZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp_bytes, keys_in.p, keys_out.p, vals_in.p, sorted.p,
+                                            max_entries, 0, 21));
+  sort_tmp.alloc(sort_tmp_bytes + 16);
   buckets.alloc(max_keys);
   size_t nthreads = (max_entries + kChunk - 1) / kChunk + 1;
   carry_own.alloc(nthreads);
@@ -233,7 +287,10 @@ void MsmScratch::init(size_t maxp) {
 template <int C>
 static void launch_digits(const Fr* scalars, size_t n, int mont, MsmScratch& sc, hipStream_t st, bool scatter) {
   unsigned g = grid_for(n, kMsmThreads, 8192);
-  if (!scatter)
+  if (sc.use_radix)
+    hipLaunchKernelGGL(msm_keys_kernel<C>, dim3(grid_for(n, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0, st,
+                       scalars, n, mont, sc.keys_in.p, sc.vals_in.p);
+  else if (!scatter)
     hipLaunchKernelGGL(msm_count_kernel<C>, dim3(g), dim3(kMsmThreads), 0, st, scalars, n, mont, sc.counts.p);
   else
     hipLaunchKernelGGL(msm_scatter_kernel<C>, dim3(g), dim3(kMsmThreads), 0, st, scalars, n, mont, sc.cursor.p,
@@ -271,13 +328,25 @@ G1xyzz msm(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, b
   const int nw = num_windows(c);
   const uint32_t nb = 1u << (c - 1);
   const uint32_t nkeys = nb * (uint32_t)nw;
-  NZ_HIP(hipMemsetAsync(sc.counts.p, 0, (nkeys + 1) * sizeof(uint32_t), st));
-  digits_dispatch(c, scalars, n, mont ? 1 : 0, sc, st, false);
-  size_t tmp = sc.scan_tmp_bytes;
-  NZ_HIP(hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp.p, tmp, sc.counts.p, sc.offsets.p, (int)(nkeys + 1), st));
-  NZ_HIP(hipMemcpyAsync(sc.cursor.p, sc.offsets.p, (nkeys + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-  digits_dispatch(c, scalars, n, mont ? 1 : 0, sc, st, true);
   const size_t max_entries = n * (size_t)nw;
+  if (sc.use_radix) {
+    digits_dispatch(c, scalars, n, mont ? 1 : 0, sc, st, false);
+    int end_bit = 1;
+    while ((1u << end_bit) <= nkeys) end_bit++;
+    size_t tmp = sc.sort_tmp_bytes;
+    NZ_HIP(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp.p, tmp, sc.keys_in.p, sc.keys_out.p, sc.vals_in.p,
+                                              sc.sorted.p, max_entries, 0, end_bit, st));
+    hipLaunchKernelGGL(msm_offsets_kernel, dim3(grid_for((size_t)nkeys + 1, kMsmThreads, 1u << 30)),
+                       dim3(kMsmThreads), 0, st, sc.keys_out.p, max_entries, nkeys, sc.offsets.p);
+    NZ_HIP(hipGetLastError());
+  } else {
+    NZ_HIP(hipMemsetAsync(sc.counts.p, 0, (nkeys + 1) * sizeof(uint32_t), st));
+    digits_dispatch(c, scalars, n, mont ? 1 : 0, sc, st, false);
+    size_t tmp = sc.scan_tmp_bytes;
+    NZ_HIP(hipcub::DeviceScan::ExclusiveSum(sc.scan_tmp.p, tmp, sc.counts.p, sc.offsets.p, (int)(nkeys + 1), st));
+    NZ_HIP(hipMemcpyAsync(sc.cursor.p, sc.offsets.p, (nkeys + 1) * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    digits_dispatch(c, scalars, n, mont ? 1 : 0, sc, st, true);
+  }
   const size_t nthreads = (max_entries + kChunk - 1) / kChunk;
   if (sc.prof) {
     if (!sc.ev0) {

@@ -34,12 +34,16 @@ struct Prover {
   DevBuf<uint32_t> amap, bmap, cmap;
   DevBuf<AddRec> adds;
   DevBuf<Fr> root_lo, root_hi;    // w4^j, w4^(4096 k)
+  DevBuf<Fr> x_lo;                // g * w4^j (coset points, with root_hi)
+  DevBuf<Fr> g_lo, g_hi, gi_lo, gi_hi;  // g^j, g^-j split tables
+  Fr zh_inv[4];
+  DevBuf<Fr> cq, cs, cl;          // coset evaluations: Qm..Qc (5 x 4n), sigma1..3 (3 x 4n), L_j (nl x 4n)
   // per-proof working set
   DevBuf<Fr> wit;                 // nVars (witness + internal), Montgomery
   DevBuf<Fr> wtns_in;             // raw witness upload (normal form)
   DevBuf<Fr> A, B, C, Z;          // n
   DevBuf<Fr> pol_a, pol_b, pol_c, pol_z;  // n+2 / n+3
-  DevBuf<Fr> A4, B4, C4, Z4, T, Tz, t, tz, pad4;  // 4n
+  DevBuf<Fr> A4, B4, C4, Z4, T, Tz, t, pad4;  // 4n (A4..Z4: coset evaluations)
   DevBuf<Fr> pol_r, pol_wxi, pol_wxiw;    // n+3, n+6, n+3
   DevBuf<Fr> blind;               // 12 (index 0 unused)
   DevBuf<Fr> scan_tmp;            // recursive scan levels
