@@ -1,5 +1,6 @@
 // C-ABI: prover context, proofs and snarkjs-format JSON (include/nzcb.h).
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../../include/nzcb.h"
@@ -14,6 +15,7 @@ struct nzcb_ctx {
   std::unique_ptr<Prover> p;
   nzcb_log_fn log_fn = nullptr;
   void* log_user = nullptr;
+  std::mutex mu;  // proofs on one context are serialized (SURVEY.md §8b "Threading")
 };
 
 namespace {
@@ -110,6 +112,7 @@ int nzcb_prove_witness(nzcb_ctx* ctx, const uint8_t* witness, size_t n_witness, 
   if (pub_cap < 32 * (size_t)ctx->p->nPublic || (!pub_out && ctx->p->nPublic))
     return fail(err, NZCB_ERR_ARG, "public output buffer too small");
   try {
+    std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->p->prove(witness, n_witness, blinding, proof_out, pub_out);
     if (err) err->code = 0;
     return 0;
@@ -126,6 +129,7 @@ int nzcb_prove_device(nzcb_ctx* ctx, const void* dev_witness, size_t n_witness, 
   if (pub_cap < 32 * (size_t)ctx->p->nPublic || (!pub_out && ctx->p->nPublic))
     return fail(err, NZCB_ERR_ARG, "public output buffer too small");
   try {
+    std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->p->prove((const uint8_t*)dev_witness, n_witness, blinding, proof_out, pub_out, true);
     if (err) err->code = 0;
     return 0;
@@ -158,17 +162,21 @@ int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap) {
 
 int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
   if (!ctx) return NZCB_ERR_ARG;
-  MsmScratch& sc = ctx->p->eng->msm_scratch;
   if (out) {
-    out[0] = sc.prof_ms;
-    out[1] = (double)sc.prof_launches;
-    out[2] = (double)sc.prof_points;
-    out[3] = (double)sc.prof_entries;
+    for (int i = 0; i < 4; i++) out[i] = 0;
+    for (auto& m : ctx->p->msc) {
+      out[0] += m->prof_ms;
+      out[1] += (double)m->prof_launches;
+      out[2] += (double)m->prof_points;
+      out[3] += (double)m->prof_entries;
+    }
   }
   if (enable >= 0) {
-    sc.prof = enable != 0;
-    sc.prof_ms = 0;
-    sc.prof_launches = sc.prof_points = sc.prof_entries = 0;
+    for (auto& m : ctx->p->msc) {
+      m->prof = enable != 0;
+      m->prof_ms = 0;
+      m->prof_launches = m->prof_points = m->prof_entries = 0;
+    }
   }
   return 0;
 }

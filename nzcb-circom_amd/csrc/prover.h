@@ -26,6 +26,12 @@ struct Prover {
   std::function<void(const std::string&)> log;
 
   std::unique_ptr<Engine> eng;
+  // commitment pipeline: one MSM scratch + stream per concurrently running commitment
+  static constexpr int kSlots = 3;
+  std::unique_ptr<MsmScratch> msc[kSlots];
+  hipStream_t aux[kSlots] = {nullptr, nullptr, nullptr};
+  hipEvent_t ready[kSlots] = {nullptr, nullptr, nullptr};
+  ~Prover();
   // resident zkey data (LEM, as in the file)
   DevBuf<G1Affine> ptau;
   DevBuf<Fr> qm, ql, qr, qo, qc;  // [n coefs | 4n evals]
@@ -63,7 +69,8 @@ struct Prover {
  private:
   hipStream_t st() const { return eng->stream; }
   void to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb);
-  G1Affine commit(const Fr* coefs, size_t len);
+  void commit_start(int slot, const Fr* coefs, size_t len);
+  G1Affine commit_finish(int slot);
   Fr eval_poly(const Fr* p, size_t len, const Fr& x);
   void prefix_product(Fr* x, size_t m, Fr* level_tmp);
   void suffix_linear(Fr* x, size_t m, const Fr& d, Fr* level_tmp);

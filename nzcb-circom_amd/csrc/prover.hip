@@ -414,6 +414,16 @@ static Fr fr_small(uint64_t k) {
   return to_mont(x);
 }
 
+Prover::~Prover() {
+  for (int i = 0; i < kSlots; i++) {
+    if (aux[i]) {
+      (void)hipStreamSynchronize(aux[i]);
+      (void)hipStreamDestroy(aux[i]);
+    }
+    if (ready[i]) (void)hipEventDestroy(ready[i]);
+  }
+}
+
 double Prover::ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -436,7 +446,13 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   k2 = z.k2;
   wn = fr_root_of_unity(power);
   w2 = fr_root_of_unity(2);
-  eng.reset(new Engine(device, power + 2, (size_t)n + 6));
+  eng.reset(new Engine(device, power + 2, 0));
+  for (int i = 0; i < kSlots; i++) {
+    msc[i].reset(new MsmScratch());
+    msc[i]->init((size_t)n + 6);
+    NZ_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
+    NZ_HIP(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
+  }
   hipStream_t s = st();
   auto up = [&](auto& buf, const Section& sec) {
     using T = typename std::remove_reference<decltype(*buf.p)>::type;
@@ -572,13 +588,21 @@ void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int n
                      (size_t)n4, g_lo.p, g_hi.p);
   ntt(eng->ntt_tables, pad4.p, evals4, power + 2, false, s);
   NZ_HIP(hipGetLastError());
-  NZ_HIP(hipStreamSynchronize(s));
-  ntt_ms += ms_since(t0);
+  ntt_ms += ms_since(t0);  // host enqueue time only (kernels run asynchronously)
 }
 
-G1Affine Prover::commit(const Fr* coefs, size_t len) {
+// Commitments run on their own streams: the MSM of one polynomial overlaps the NTTs
+// of the next and the other MSMs of the same round (their sort / reduction kernels are
+// latency-bound and fill the gaps of the compute-bound bucket accumulation).
+void Prover::commit_start(int slot, const Fr* coefs, size_t len) {
+  NZ_HIP(hipEventRecord(ready[slot], st()));
+  NZ_HIP(hipStreamWaitEvent(aux[slot], ready[slot], 0));
+  msm_enqueue(*msc[slot], ptau.p, coefs, len, true, aux[slot]);
+}
+
+G1Affine Prover::commit_finish(int slot) {
   auto t0 = std::chrono::steady_clock::now();
-  G1xyzz r = msm(eng->msm_scratch, ptau.p, coefs, len, true, st());
+  G1xyzz r = msm_finish(*msc[slot], aux[slot]);
   msm_ms += ms_since(t0);
   return xyzz_to_affine(r);
 }
@@ -683,14 +707,17 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   {
     const int ba[2] = {2, 1}, bb[2] = {4, 3}, bc[2] = {6, 5};
     to4t(A.p, pol_a.p, A4.p, ba, 2);
-    to4t(B.p, pol_b.p, B4.p, bb, 2);
-    to4t(C.p, pol_c.p, C4.p, bc, 2);
     lg("multiexp A");
-    pA = commit(pol_a.p, n + 2);
+    commit_start(0, pol_a.p, n + 2);
+    to4t(B.p, pol_b.p, B4.p, bb, 2);
     lg("multiexp B");
-    pB = commit(pol_b.p, n + 2);
+    commit_start(1, pol_b.p, n + 2);
+    to4t(C.p, pol_c.p, C4.p, bc, 2);
     lg("multiexp C");
-    pC = commit(pol_c.p, n + 2);
+    commit_start(2, pol_c.p, n + 2);
+    pA = commit_finish(0);
+    pB = commit_finish(1);
+    pC = commit_finish(2);
   }
   tm[2] = ms_since(t1);
 
@@ -740,7 +767,8 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     const int bz[3] = {9, 8, 7};
     to4t(Z.p, pol_z.p, Z4.p, bz, 3);
     lg("multiexp Z");
-    pZ = commit(pol_z.p, n + 3);
+    commit_start(0, pol_z.p, n + 3);
+    pZ = commit_finish(0);
   }
   tm[3] = ms_since(t2);
 
@@ -776,11 +804,14 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     ntt_ms += ms_since(tq);
     if (f & 1u) throw Error(NZCB_ERR_T_DIV, "T Polynomial is not divisible");
     lg("multiexp T1");
-    pT1 = commit(t.p, n);
+    commit_start(0, t.p, n);
     lg("multiexp T2");
-    pT2 = commit(t.p + n, n);
+    commit_start(1, t.p + n, n);
     lg("multiexp T3");
-    pT3 = commit(t.p + 2 * (size_t)n, n + 6);
+    commit_start(2, t.p + 2 * (size_t)n, n + 6);
+    pT1 = commit_finish(0);
+    pT2 = commit_finish(1);
+    pT3 = commit_finish(2);
   }
   tm[4] = ms_since(t3);
 
@@ -837,15 +868,17 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
                        pol_b.p, pol_c.p, sigma.p, sigma.p + 5 * (size_t)n, (size_t)n, wa, T.p);
     NZ_HIP(hipGetLastError());
     div_pol1(T.p, n + 6, xi, Fr::zero(), pol_wxi.p, 4u);
+    lg("multiexp Wxi");
+    commit_start(0, pol_wxi.p, n + 6);
     div_pol1(pol_z.p, n + 3, xi * wn, ezw, pol_wxiw.p, 4u);
+    lg("multiexp Wxiw");
+    commit_start(1, pol_wxiw.p, n + 3);
     uint32_t f = 0;
     NZ_HIP(hipMemcpyAsync(&f, flags.p, 4, hipMemcpyDeviceToHost, s));
     NZ_HIP(hipStreamSynchronize(s));
+    pWxi = commit_finish(0);
+    pWxiw = commit_finish(1);
     if (f & 4u) throw Error(NZCB_ERR_DIVPOL, "Polinomial does not divide");
-    lg("multiexp Wxi");
-    pWxi = commit(pol_wxi.p, n + 6);
-    lg("multiexp Wxiw");
-    pWxiw = commit(pol_wxiw.p, n + 3);
   }
   tm[6] = ms_since(t5);
   tm[0] = ms_since(T0);

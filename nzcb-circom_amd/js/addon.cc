@@ -1,0 +1,224 @@
+// N-API addon: the Node.js side of the drop-in boundary.
+//
+// The reference's host is Node.js: its proofs come from snarkjs.plonk.prove /
+// plonk.fullProve [EXT] (snarkjs 0.4.12, /root/reference/package.json:18). This
+// addon binds the C-ABI in include/nzcb.h one-to-one; index.js wraps it in the
+// snarkjs-compatible Promise API. Proving runs in napi_async_work on the libuv
+// pool so the event loop is never blocked; the optional logger is called back on
+// the main thread through a thread-safe function.
+#define NAPI_VERSION 6
+#include <node_api.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../include/nzcb.h"
+
+#define CHECK(call)                                                    \
+  do {                                                                 \
+    if ((call) != napi_ok) {                                           \
+      napi_throw_error(env, nullptr, "nzcb addon: N-API call failed"); \
+      return nullptr;                                                  \
+    }                                                                  \
+  } while (0)
+
+namespace {
+
+struct Ctx {
+  nzcb_ctx* ctx = nullptr;
+};
+
+void ctx_finalize(napi_env, void* data, void*) {
+  Ctx* c = static_cast<Ctx*>(data);
+  if (c->ctx) nzcb_ctx_destroy(c->ctx);
+  delete c;
+}
+
+napi_value make_error(napi_env env, int code, const char* msg) {
+  napi_value m, err, c;
+  napi_create_string_utf8(env, msg, NAPI_AUTO_LENGTH, &m);
+  napi_create_error(env, nullptr, m, &err);
+  napi_create_int32(env, code, &c);
+  napi_set_named_property(env, err, "code", c);
+  return err;
+}
+
+// createContext(zkey: Buffer, device: number) -> external
+napi_value CreateContext(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  void* data = nullptr;
+  size_t len = 0;
+  CHECK(napi_get_buffer_info(env, argv[0], &data, &len));
+  int32_t device = 0;
+  if (argc > 1) napi_get_value_int32(env, argv[1], &device);
+  nzcb_err err{};
+  nzcb_ctx* ctx = nzcb_ctx_create(static_cast<const uint8_t*>(data), len, device, &err);
+  if (!ctx) {
+    napi_throw(env, make_error(env, err.code, err.msg));
+    return nullptr;
+  }
+  Ctx* c = new Ctx();
+  c->ctx = ctx;
+  napi_value ext;
+  CHECK(napi_create_external(env, c, ctx_finalize, nullptr, &ext));
+  return ext;
+}
+
+struct ProveWork {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  napi_ref ctx_ref = nullptr, wtns_ref = nullptr;
+  napi_threadsafe_function tsfn = nullptr;
+  Ctx* c = nullptr;
+  const uint8_t* wtns = nullptr;
+  size_t wtns_len = 0;
+  bool has_blinding = false;
+  uint8_t blinding[NZCB_BLINDING_BYTES];
+  uint8_t proof[NZCB_PROOF_BYTES];
+  uint8_t pub[32 * 64];
+  uint32_t npub = 0;
+  int rc = 0;
+  nzcb_err err{};
+};
+
+void log_trampoline(void* user, const char* msg) {
+  ProveWork* w = static_cast<ProveWork*>(user);
+  if (!w->tsfn) return;
+  char* copy = strdup(msg);
+  if (napi_call_threadsafe_function(w->tsfn, copy, napi_tsfn_blocking) != napi_ok) free(copy);
+}
+
+void call_logger(napi_env env, napi_value fn, void*, void* data) {
+  char* msg = static_cast<char*>(data);
+  if (env && fn) {
+    napi_value s, undef;
+    napi_create_string_utf8(env, msg, NAPI_AUTO_LENGTH, &s);
+    napi_get_undefined(env, &undef);
+    napi_call_function(env, undef, fn, 1, &s, nullptr);
+  }
+  free(msg);
+}
+
+void prove_execute(napi_env, void* data) {
+  ProveWork* w = static_cast<ProveWork*>(data);
+  uint32_t info[5];
+  nzcb_ctx_info(w->c->ctx, info);
+  w->npub = info[1];
+  if (w->npub > 64) {
+    w->rc = NZCB_ERR_ARG;
+    std::snprintf(w->err.msg, sizeof(w->err.msg), "too many public signals for the addon buffer");
+    return;
+  }
+  nzcb_ctx_set_logger(w->c->ctx, w->tsfn ? log_trampoline : nullptr, w);
+  w->rc = nzcb_prove(w->c->ctx, w->wtns, w->wtns_len, w->has_blinding ? w->blinding : nullptr, w->proof, w->pub,
+                     sizeof(w->pub), &w->err);
+  nzcb_ctx_set_logger(w->c->ctx, nullptr, nullptr);
+}
+
+void prove_complete(napi_env env, napi_status, void* data) {
+  ProveWork* w = static_cast<ProveWork*>(data);
+  if (w->rc) {
+    napi_reject_deferred(env, w->deferred, make_error(env, w->rc, w->err.msg));
+  } else {
+    std::string pj(8192, '\0'), uj(96 * 64 + 8, '\0');
+    nzcb_proof_to_json(w->proof, &pj[0], pj.size());
+    nzcb_public_to_json(w->pub, (int)w->npub, &uj[0], uj.size());
+    napi_value obj, a, b;
+    napi_create_object(env, &obj);
+    napi_create_string_utf8(env, pj.c_str(), NAPI_AUTO_LENGTH, &a);
+    napi_create_string_utf8(env, uj.c_str(), NAPI_AUTO_LENGTH, &b);
+    napi_set_named_property(env, obj, "proof", a);
+    napi_set_named_property(env, obj, "publicSignals", b);
+    napi_resolve_deferred(env, w->deferred, obj);
+  }
+  if (w->tsfn) napi_release_threadsafe_function(w->tsfn, napi_tsfn_release);
+  napi_delete_reference(env, w->ctx_ref);
+  napi_delete_reference(env, w->wtns_ref);
+  napi_delete_async_work(env, w->work);
+  delete w;
+}
+
+// prove(ctx, wtns: Buffer, blinding: Buffer|null, logger: Function|null) -> Promise<{proof, publicSignals}> (JSON strings)
+napi_value Prove(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  ProveWork* w = new ProveWork();
+  CHECK(napi_get_value_external(env, argv[0], reinterpret_cast<void**>(&w->c)));
+  void* wd = nullptr;
+  CHECK(napi_get_buffer_info(env, argv[1], &wd, &w->wtns_len));
+  w->wtns = static_cast<const uint8_t*>(wd);
+  CHECK(napi_create_reference(env, argv[0], 1, &w->ctx_ref));
+  CHECK(napi_create_reference(env, argv[1], 1, &w->wtns_ref));
+  napi_valuetype t;
+  if (argc > 2 && napi_typeof(env, argv[2], &t) == napi_ok && t == napi_object) {
+    void* bd = nullptr;
+    size_t bl = 0;
+    if (napi_get_buffer_info(env, argv[2], &bd, &bl) == napi_ok && bl == NZCB_BLINDING_BYTES) {
+      std::memcpy(w->blinding, bd, bl);
+      w->has_blinding = true;
+    }
+  }
+  if (argc > 3 && napi_typeof(env, argv[3], &t) == napi_ok && t == napi_function) {
+    napi_value name;
+    napi_create_string_utf8(env, "nzcb-logger", NAPI_AUTO_LENGTH, &name);
+    CHECK(napi_create_threadsafe_function(env, argv[3], nullptr, name, 0, 1, nullptr, nullptr, nullptr, call_logger,
+                                          &w->tsfn));
+  }
+  napi_value promise, rname;
+  CHECK(napi_create_promise(env, &w->deferred, &promise));
+  napi_create_string_utf8(env, "nzcb-prove", NAPI_AUTO_LENGTH, &rname);
+  CHECK(napi_create_async_work(env, nullptr, rname, prove_execute, prove_complete, w, &w->work));
+  CHECK(napi_queue_async_work(env, w->work));
+  return promise;
+}
+
+napi_value Info(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c = nullptr;
+  CHECK(napi_get_value_external(env, argv[0], reinterpret_cast<void**>(&c)));
+  uint32_t v[5];
+  nzcb_ctx_info(c->ctx, v);
+  napi_value obj;
+  napi_create_object(env, &obj);
+  const char* names[5] = {"domainSize", "nPublic", "nVars", "nAdditions", "nConstraints"};
+  for (int i = 0; i < 5; i++) {
+    napi_value x;
+    napi_create_uint32(env, v[i], &x);
+    napi_set_named_property(env, obj, names[i], x);
+  }
+  return obj;
+}
+
+napi_value Version(napi_env env, napi_callback_info) {
+  napi_value s;
+  napi_create_string_utf8(env, nzcb_version(), NAPI_AUTO_LENGTH, &s);
+  return s;
+}
+
+napi_value DeviceCount(napi_env env, napi_callback_info) {
+  napi_value s;
+  napi_create_int32(env, nzcb_device_count(), &s);
+  return s;
+}
+
+napi_value Init(napi_env env, napi_value exports) {
+  napi_property_descriptor props[] = {
+      {"createContext", nullptr, CreateContext, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"prove", nullptr, Prove, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"info", nullptr, Info, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
+  };
+  napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
+  return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

@@ -1,0 +1,186 @@
+'use strict';
+// snarkjs-compatible PLONK API on the MI355X prover (SURVEY.md §8b).
+//
+// Drop-in for the two calls the reference's callers make into snarkjs 0.4.12
+// (/root/reference/package.json:18; the dapp and the `snarkjs plonk prove|fullprove`
+// CLI, README.md:50-53):
+//   plonk.prove(zkeyFileName, witnessFileName, logger)       -> Promise<{proof, publicSignals}>
+//   plonk.fullProve(input, wasmFile, zkeyFileName, logger)   -> Promise<{proof, publicSignals}>
+// File arguments accept a path, a Buffer/Uint8Array, or {type: "mem", data}.
+// Blinding scalars are drawn like snarkjs's Fr.random() unless options.blinding
+// (11 x 32-byte LE Buffer) is given -- fixed blinding makes proofs bit-reproducible.
+const fs = require('fs');
+const path = require('path');
+const crypto = require('crypto');
+
+const addon = require(path.join(__dirname, 'build', 'nzcb.node'));
+
+const R = BigInt('21888242871839275222246405745257275088548364400416034343698204186575808495617');
+const BLINDING_BYTES = 11 * 32;
+
+function readBin(x) {
+  if (typeof x === 'string') return fs.readFileSync(x);
+  if (x && x.type === 'mem') return Buffer.from(x.data);
+  if (x instanceof Uint8Array) return Buffer.from(x);
+  throw new Error('expected a file name, a buffer or {type: "mem", data}');
+}
+
+function randomBlinding() {
+  const out = Buffer.alloc(BLINDING_BYTES);
+  const mask = (BigInt(1) << BigInt(254)) - BigInt(1);
+  for (let i = 0; i < 11; i++) {
+    let v;
+    do {
+      v = BigInt('0x' + crypto.randomBytes(32).toString('hex')) & mask;
+    } while (v >= R);
+    for (let j = 0; j < 32; j++) {
+      out[32 * i + j] = Number(v & BigInt(255));
+      v >>= BigInt(8);
+    }
+  }
+  return out;
+}
+
+// One HBM-resident context per (zkey content, device): the zkey is uploaded once.
+const contexts = new Map();
+function contextFor(zkeyBuf, device) {
+  const key = crypto.createHash('sha256').update(zkeyBuf).digest('hex') + ':' + device;
+  let ctx = contexts.get(key);
+  if (!ctx) {
+    ctx = addon.createContext(zkeyBuf, device);
+    contexts.set(key, ctx);
+  }
+  return ctx;
+}
+
+function loggerFn(logger) {
+  if (!logger) return null;
+  if (typeof logger === 'function') return logger;
+  if (typeof logger.debug === 'function') return (m) => logger.debug(m);
+  return null;
+}
+
+async function prove(zkeyFileName, witnessFileName, logger, options) {
+  options = options || {};
+  const zkey = readBin(zkeyFileName);
+  const wtns = readBin(witnessFileName);
+  const ctx = contextFor(zkey, options.device || 0);
+  const blinding = options.blinding ? Buffer.from(options.blinding) : randomBlinding();
+  if (blinding.length !== BLINDING_BYTES) throw new Error('blinding must be 11 x 32 bytes');
+  const res = await addon.prove(ctx, wtns, blinding, loggerFn(logger));
+  return { proof: JSON.parse(res.proof), publicSignals: JSON.parse(res.publicSignals) };
+}
+
+// ---------------------------------------------------------------------------
+// Witness calculation from a circom 2.0.x witness .wasm (circom_runtime 0.1.17
+// WitnessCalculatorBuilder / calculateWTNSBin interface, SURVEY.md §2 [EXT]).
+// Parity unpinned: no circom artefact exists offline to test against.
+// ---------------------------------------------------------------------------
+function fnvHash(str) {
+  const M = BigInt(2) ** BigInt(64);
+  let h = BigInt('0xCBF29CE484222325');
+  for (let i = 0; i < str.length; i++) {
+    h ^= BigInt(str.charCodeAt(i));
+    h = (h * BigInt('0x100000001B3')) % M;
+  }
+  return h.toString(16).padStart(16, '0');
+}
+
+function flatArray(a) {
+  const res = [];
+  (function fill(x) {
+    if (Array.isArray(x)) x.forEach(fill);
+    else res.push(x);
+  })(a);
+  return res;
+}
+
+async function wtnsCalculate(input, wasmFile) {
+  const code = readBin(wasmFile);
+  let instance;
+  let errStr = '';
+  const getMessage = () => {
+    let msg = '';
+    let c = instance.exports.getMessageChar();
+    while (c !== 0) {
+      msg += String.fromCharCode(c);
+      c = instance.exports.getMessageChar();
+    }
+    return msg;
+  };
+  const errors = ['', 'Signal not found.', 'Too many signals set.', 'Signal already set.', 'Assert Failed.',
+    'Not enough memory.', 'Input signal array access exceeds the size.'];
+  const mod = await WebAssembly.compile(code);
+  instance = await WebAssembly.instantiate(mod, {
+    runtime: {
+      exceptionHandler: (c) => { throw new Error((errors[c] || 'Unknown error.') + '\n' + errStr); },
+      printErrorMessage: () => { errStr += getMessage() + '\n'; },
+      writeBufferMessage: () => { getMessage(); },
+      showSharedRWMemory: () => {},
+    },
+  });
+  const ex = instance.exports;
+  const n32 = ex.getFieldNumLen32();
+  ex.getRawPrime();
+  let prime = BigInt(0);
+  for (let j = n32 - 1; j >= 0; j--) prime = (prime << BigInt(32)) | BigInt(ex.readSharedRWMemory(j) >>> 0);
+  const witnessSize = ex.getWitnessSize();
+  ex.init(0);
+  let counter = 0;
+  for (const k of Object.keys(input)) {
+    const h = fnvHash(k);
+    const hMSB = parseInt(h.slice(0, 8), 16);
+    const hLSB = parseInt(h.slice(8, 16), 16);
+    const vals = flatArray(input[k]);
+    const size = ex.getInputSignalSize(hMSB, hLSB);
+    if (size < 0) throw new Error(`Signal ${k} not found\n`);
+    if (vals.length < size) throw new Error(`Not enough values for input signal ${k}\n`);
+    if (vals.length > size) throw new Error(`Too many values for input signal ${k}\n`);
+    for (let i = 0; i < vals.length; i++) {
+      let v = BigInt(vals[i]) % prime;
+      if (v < BigInt(0)) v += prime;
+      for (let j = 0; j < n32; j++) {
+        ex.writeSharedRWMemory(j, Number(v & BigInt(0xffffffff)));
+        v >>= BigInt(32);
+      }
+      ex.setInputSignal(hMSB, hLSB, i);
+      counter++;
+    }
+  }
+  if (ex.getInputSize && counter < ex.getInputSize()) {
+    throw new Error(`Not all inputs have been set. Only ${counter} out of ${ex.getInputSize()}`);
+  }
+  const n8 = n32 * 4;
+  const out = Buffer.alloc(12 + 12 + 4 + n8 + 4 + 12 + witnessSize * n8);
+  let o = 0;
+  out.write('wtns', 0, 'latin1'); o = 4;
+  out.writeUInt32LE(2, o); o += 4;
+  out.writeUInt32LE(2, o); o += 4;
+  out.writeUInt32LE(1, o); o += 4;
+  out.writeUInt32LE(8 + n8, o); out.writeUInt32LE(0, o + 4); o += 8;
+  out.writeUInt32LE(n8, o); o += 4;
+  ex.getRawPrime();
+  for (let j = 0; j < n32; j++) { out.writeUInt32LE(ex.readSharedRWMemory(j) >>> 0, o); o += 4; }
+  out.writeUInt32LE(witnessSize, o); o += 4;
+  out.writeUInt32LE(2, o); o += 4;
+  const s2 = witnessSize * n8;
+  out.writeUInt32LE(s2 % 0x100000000, o); out.writeUInt32LE(Math.floor(s2 / 0x100000000), o + 4); o += 8;
+  for (let i = 0; i < witnessSize; i++) {
+    ex.getWitness(i);
+    for (let j = 0; j < n32; j++) { out.writeUInt32LE(ex.readSharedRWMemory(j) >>> 0, o); o += 4; }
+  }
+  return out;
+}
+
+async function fullProve(input, wasmFile, zkeyFileName, logger, options) {
+  const wtns = await wtnsCalculate(input, wasmFile);
+  return prove(zkeyFileName, { type: 'mem', data: wtns }, logger, options);
+}
+
+module.exports = {
+  plonk: { prove, fullProve },
+  wtns: { calculate: wtnsCalculate },
+  version: addon.version,
+  deviceCount: addon.deviceCount,
+  _addon: addon,
+};
