@@ -138,6 +138,14 @@ int nzcb_engine_msm_dev(nzcb_engine* e, const void* bases, const void* scalars, 
  * events on the engine's stream. */
 int nzcb_engine_time_ntt(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, int reps, double* ms,
                          nzcb_err* err);
+/* Microbench inputs: n pseudo-random Fr (Montgomery, < 2^253)
+ * from `seed`, and [s_i]G1 bases (LEM affine) from Montgomery scalars. Device pointers. */
+int nzcb_engine_random_fr(nzcb_engine* e, void* dev_out, size_t n, uint64_t seed, nzcb_err* err);
+int nzcb_engine_fixed_base(nzcb_engine* e, const void* dev_scalars_mont, size_t n, void* dev_out, nzcb_err* err);
+/* Average wall ms per MSM over `reps` (host-synchronised) and the average bucket-
+ * accumulation kernel ms (HIP events). */
+int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont, int reps,
+                         double* ms, double* acc_ms, nzcb_err* err);
 /* Field self-test helpers: out[i] = a[i] * b[i] (Montgomery, device), n elements. */
 int nzcb_engine_fr_mul(nzcb_engine* e, const uint8_t* a_lem, const uint8_t* b_lem, uint8_t* out_lem, size_t n,
                        int field_q, nzcb_err* err);

@@ -1,4 +1,5 @@
 // C-ABI: engine, device memory and kernel-level entry points (include/nzcb.h).
+#include <chrono>
 #include <cstring>
 #include <vector>
 
@@ -52,6 +53,25 @@ __global__ void fe_mul_kernel_r(const Fr* a, const Fr* b, Fr* o, size_t n) {
 __global__ void fe_mul_kernel_q(const Fq* a, const Fq* b, Fq* o, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) o[i] = a[i] * b[i];
+}
+
+// uniform-ish Fr in Montgomery form: 253 random bits (< r) from a splitmix64 stream per element
+__global__ void random_fr_kernel(Fr* out, size_t n, uint64_t seed) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t x = seed ^ (0x9E3779B97F4A7C15ULL * (i + 1));
+  Fr v;
+  for (int k = 0; k < 4; k++) {
+    x += 0x9E3779B97F4A7C15ULL;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    v.v[2 * k] = (uint32_t)z;
+    v.v[2 * k + 1] = (uint32_t)(z >> 32);
+  }
+  v.v[7] &= 0x1fffffffu;
+  out[i] = to_mont(v);
 }
 
 static void affine_out(const G1xyzz& r, uint8_t* out) {
@@ -169,6 +189,46 @@ int nzcb_engine_msm(nzcb_engine* e, const uint8_t* bases_lem, const uint8_t* sca
   NZ_HIP(hipMemcpyAsync(s.p, scalars, n * 32, hipMemcpyHostToDevice, g.stream));
   G1xyzz r = msm(g.msm_scratch, b.p, s.p, n, scalars_mont != 0, g.stream);
   affine_out(r, out_affine);
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_engine_random_fr(nzcb_engine* e, void* dev_out, size_t n, uint64_t seed, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  hipLaunchKernelGGL(random_fr_kernel, dim3(grid_for(n, 256, 1u << 30)), dim3(256), 0, g.stream, (Fr*)dev_out, n,
+                     seed);
+  NZ_HIP(hipGetLastError());
+  NZ_HIP(hipStreamSynchronize(g.stream));
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_engine_fixed_base(nzcb_engine* e, const void* dev_scalars_mont, size_t n, void* dev_out, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  launch_fixed_base((const Fr*)dev_scalars_mont, n, (G1Affine*)dev_out, g.stream);
+  NZ_HIP(hipStreamSynchronize(g.stream));
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont, int reps,
+                         double* ms, double* acc_ms, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  MsmScratch& sc = g.msm_scratch;
+  sc.prof = true;
+  sc.prof_ms = 0;
+  sc.prof_launches = 0;
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < reps; i++) (void)msm(sc, (const G1Affine*)bases, (const Fr*)scalars, n, scalars_mont != 0, g.stream);
+  *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / (reps ? reps : 1);
+  *acc_ms = sc.prof_ms / (sc.prof_launches ? sc.prof_launches : 1);
+  sc.prof = false;
   return 0;
   NZ_GUARD_END(err)
 }

@@ -5,6 +5,9 @@
 
 namespace nzcb {
 
+// [s_i] G1 (LEM affine) for Montgomery scalars, one thread per point (synth.hip).
+void launch_fixed_base(const Fr* scalars_mont, size_t n, G1Affine* out, hipStream_t st);
+
 struct Engine {
   int device = 0;
   hipStream_t stream = nullptr;

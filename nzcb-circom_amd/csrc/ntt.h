@@ -9,8 +9,10 @@ Fr fr_root_of_unity(int k);  // Montgomery form
 
 struct NttTables {
   int max_log = 0;
-  DevBuf<Fr> fwd;  // fwd[i] = w^i,  i < 2^(max_log-1), w = w[max_log]
-  DevBuf<Fr> inv;  // inv[i] = w^-i
+  // Per-stage compact twiddles: stage g (butterfly span 2^g) uses w_{2^(g+1)}^k,
+  // k < 2^g, stored contiguously at offset 2^g - 1, so the twiddles of consecutive
+  // butterflies of a stage are consecutive in memory (coalesced 32-byte loads).
+  DevBuf<Fr> fwd, inv;  // 2^max_log - 1 entries each
   void init(int max_log, hipStream_t st);
 };
 

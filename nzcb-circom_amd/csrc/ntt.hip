@@ -10,6 +10,13 @@
 // in LDS; later passes run stages s..s+q-1 on tiles of 2^q rows (stride 2^s)
 // x C consecutive columns, in place. L = 23 -> 3 passes of <= 8 stages, each one
 // read + one write of the array (algorithmic 64 B per element per pass).
+//
+// The pass is bound by Montgomery products (one per butterfly), so the kernel is
+// shaped for issue rate: 512 threads per 64 KiB tile (2 tiles per CU -> 4 waves
+// per SIMD), each thread's butterflies of a stage issue their twiddle loads
+// together before touching LDS, twiddles come from per-stage compact tables
+// (consecutive butterflies -> consecutive twiddles), and stage 0's unit twiddles
+// are skipped.
 #include "ntt.h"
 
 #include <vector>
@@ -17,7 +24,8 @@
 namespace nzcb {
 
 static constexpr int kTileElems = 2048;  // 64 KiB of Fr per workgroup
-static constexpr int kNttThreads = 256;
+static constexpr int kNttThreads = 512;
+static constexpr int kBfPerThread = kTileElems / 2 / kNttThreads;  // 2
 
 Fr fr_root_of_unity(int k) {
   Fr w;
@@ -33,18 +41,31 @@ __device__ __forceinline__ uint32_t bit_rev(uint32_t x, int bits) {
   return bits ? (__brev(x) >> (32 - bits)) : 0u;
 }
 
-__global__ void __launch_bounds__(kNttThreads)
+// full[i] = lo[i & 2047] * hi[i >> 11] = W^i for i < 2^(L-1)
+__global__ void __launch_bounds__(256)
 ntt_table_kernel(Fr* __restrict__ out, const Fr* __restrict__ lo, const Fr* __restrict__ hi, size_t count) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   out[i] = lo[i & 2047] * hi[i >> 11];
 }
 
+// compact[2^g - 1 + k] = full[k << (L - g - 1)], g < L, k < 2^g
+__global__ void __launch_bounds__(256)
+ntt_stage_table_kernel(Fr* __restrict__ out, const Fr* __restrict__ full, int L, size_t count) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  int g = 63 - __clzll((unsigned long long)(i + 1));  // i + 1 in [2^g, 2^(g+1))
+  size_t k = i + 1 - ((size_t)1 << g);
+  out[i] = full[k << (L - g - 1)];
+}
+
 void NttTables::init(int L, hipStream_t st) {
   max_log = L;
-  size_t half = L >= 1 ? (size_t(1) << (L - 1)) : 1;
-  fwd.alloc(half);
-  inv.alloc(half);
+  const size_t half = L >= 1 ? (size_t(1) << (L - 1)) : 1;
+  const size_t total = (size_t(1) << L) - 1;
+  fwd.alloc(total ? total : 1);
+  inv.alloc(total ? total : 1);
+  DevBuf<Fr> full(half);
   for (int dir = 0; dir < 2; dir++) {
     Fr w = fr_root_of_unity(L);
     if (dir) w = inverse(w);
@@ -57,9 +78,11 @@ void NttTables::init(int L, hipStream_t st) {
     DevBuf<Fr> dlo(2048), dhi(nhi);
     NZ_HIP(hipMemcpyAsync(dlo.p, lo.data(), 2048 * sizeof(Fr), hipMemcpyHostToDevice, st));
     NZ_HIP(hipMemcpyAsync(dhi.p, hi.data(), nhi * sizeof(Fr), hipMemcpyHostToDevice, st));
-    Fr* dst = dir ? inv.p : fwd.p;
-    hipLaunchKernelGGL(ntt_table_kernel, dim3(grid_for(half, kNttThreads)), dim3(kNttThreads), 0, st, dst,
-                       dlo.p, dhi.p, half);
+    hipLaunchKernelGGL(ntt_table_kernel, dim3(grid_for(half, 256, 1u << 30)), dim3(256), 0, st, full.p, dlo.p, dhi.p,
+                       half);
+    if (total)
+      hipLaunchKernelGGL(ntt_stage_table_kernel, dim3(grid_for(total, 256, 1u << 30)), dim3(256), 0, st,
+                         dir ? inv.p : fwd.p, full.p, L, total);
     NZ_HIP(hipGetLastError());
     NZ_HIP(hipStreamSynchronize(st));
   }
@@ -67,17 +90,18 @@ void NttTables::init(int L, hipStream_t st) {
 
 // One pass: stages [s, s+q) on tiles of (2^q rows) x (2^logC columns).
 __global__ void __launch_bounds__(kNttThreads)
-ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int Lmax,
-                int s, int q, int logC, int first, Fr scale, int do_scale) {
+ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int s, int q, int logC, int first, Fr scale,
+                int do_scale) {
   extern __shared__ Fr tile[];
   const int C = 1 << logC;
   const int rows = 1 << q;
   const int n_el = rows << logC;
+  const int tid = threadIdx.x;
   const size_t t = blockIdx.x;
   size_t base = 0, c0 = 0, lo0 = 0;
   if (first) {
     c0 = t << logC;
-    for (int e = threadIdx.x; e < n_el; e += blockDim.x) {
+    for (int e = tid; e < n_el; e += kNttThreads) {
       int j = e >> logC, c = e & (C - 1);
       size_t src = ((size_t)bit_rev((uint32_t)j, q) << (L - q)) + c0 + c;
       Fr v = in[src];
@@ -89,39 +113,52 @@ ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int Lma
     size_t hi = t / groups_lo;
     lo0 = (t % groups_lo) << logC;
     base = (hi << (s + q)) + lo0;
-    for (int e = threadIdx.x; e < n_el; e += blockDim.x) {
+    for (int e = tid; e < n_el; e += kNttThreads) {
       int j = e >> logC, c = e & (C - 1);
       tile[e] = in[base + ((size_t)j << s) + c];
     }
   }
   __syncthreads();
+  const int nbf = n_el >> 1;
+#pragma unroll 1
   for (int st = 0; st < q; st++) {
     const int half = 1 << st;
     const int g = s + st;  // global stage: butterfly span 2^g
-    const int tw_shift = Lmax - g - 1;
-    for (int b = threadIdx.x; b < (n_el >> 1); b += blockDim.x) {
-      int c = b & (C - 1);
-      int pr = b >> logC;
-      int low = pr & (half - 1);
-      int j0 = ((pr >> st) << (st + 1)) | low;
-      int j1 = j0 + half;
-      size_t k = first ? (size_t)low : (((size_t)low << s) + lo0 + c);
-      Fr w = tw[k << tw_shift];
-      Fr x0 = tile[(j0 << logC) + c];
-      Fr x1 = tile[(j1 << logC) + c] * w;
-      tile[(j0 << logC) + c] = x0 + x1;
-      tile[(j1 << logC) + c] = x0 - x1;
+    const Fr* __restrict__ twg = tw + (((size_t)1 << g) - 1);
+    Fr w[kBfPerThread];
+    int i0[kBfPerThread], i1[kBfPerThread];
+    bool act[kBfPerThread];
+#pragma unroll
+    for (int u = 0; u < kBfPerThread; u++) {
+      const int b = tid + u * kNttThreads;
+      act[u] = b < nbf;
+      const int c = b & (C - 1);
+      const int pr = b >> logC;
+      const int low = pr & (half - 1);
+      const int j0 = ((pr >> st) << (st + 1)) | low;
+      i0[u] = (j0 << logC) + c;
+      i1[u] = ((j0 + half) << logC) + c;
+      const size_t k = first ? (size_t)low : (((size_t)low << s) + lo0 + c);
+      if (act[u] && g) w[u] = twg[k];
+    }
+#pragma unroll
+    for (int u = 0; u < kBfPerThread; u++) {
+      if (!act[u]) continue;
+      const Fr x0 = tile[i0[u]];
+      const Fr x1 = g ? tile[i1[u]] * w[u] : tile[i1[u]];
+      tile[i0[u]] = x0 + x1;
+      tile[i1[u]] = x0 - x1;
     }
     __syncthreads();
   }
   if (first) {
-    for (int e = threadIdx.x; e < n_el; e += blockDim.x) {
+    for (int e = tid; e < n_el; e += kNttThreads) {
       int j = e & (rows - 1), c = e >> q;
       size_t dst = ((size_t)bit_rev((uint32_t)(c0 + c), L - q) << q) + j;
       out[dst] = tile[(j << logC) + c];
     }
   } else {
-    for (int e = threadIdx.x; e < n_el; e += blockDim.x) {
+    for (int e = tid; e < n_el; e += kNttThreads) {
       int j = e >> logC, c = e & (C - 1);
       out[base + ((size_t)j << s) + c] = tile[e];
     }
@@ -135,11 +172,8 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   Fr sc = Fr::one();
   int do_scale = 0;
   if (inverse_dir) {
-    // N^-1 in Montgomery form
-    Fr n_m = to_mont([&] { Fr x = Fr::zero(); x.v[0] = 1; return x; }());
-    Fr two = n_m + n_m;
-    Fr nn = pow_u64(two, (uint64_t)L);
-    sc = inverse(nn);
+    Fr two = Fr::one() + Fr::one();
+    sc = inverse(pow_u64(two, (uint64_t)L));  // N^-1
     do_scale = 1;
   }
   if (scale) {
@@ -147,9 +181,8 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
     do_scale = 1;
   }
   if (L == 0) {
-    // N = 1: copy (with scale)
-    hipLaunchKernelGGL(ntt_pass_kernel, dim3(1), dim3(kNttThreads), sizeof(Fr), st, in, out, tw, 0, t.max_log, 0, 0,
-                       0, 1, sc, do_scale);
+    hipLaunchKernelGGL(ntt_pass_kernel, dim3(1), dim3(kNttThreads), sizeof(Fr), st, in, out, tw, 0, 0, 0, 0, 1, sc,
+                       do_scale);
     NZ_HIP(hipGetLastError());
     return;
   }
@@ -159,8 +192,8 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   while ((1 << (logC1 + 1)) <= cols && ((1 << (q1 + logC1 + 1)) <= kTileElems)) logC1++;
   size_t tiles = (size_t)cols >> logC1;
   size_t lds = (size_t(1) << (q1 + logC1)) * sizeof(Fr);
-  hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)tiles), dim3(kNttThreads), lds, st, in, out, tw, L, t.max_log,
-                     0, q1, logC1, 1, sc, do_scale);
+  hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)tiles), dim3(kNttThreads), lds, st, in, out, tw, L, 0, q1, logC1,
+                     1, sc, do_scale);
   NZ_HIP(hipGetLastError());
   int s = q1;
   while (s < L) {
@@ -169,8 +202,8 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
     while (logC + 1 <= s && (1 << (q + logC + 1)) <= kTileElems) logC++;
     size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
     size_t lds2 = (size_t(1) << (q + logC)) * sizeof(Fr);
-    hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)ntiles), dim3(kNttThreads), lds2, st, out, out, tw, L,
-                       t.max_log, s, q, logC, 0, sc, 0);
+    hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)ntiles), dim3(kNttThreads), lds2, st, out, out, tw, L, s, q,
+                       logC, 0, sc, 0);
     NZ_HIP(hipGetLastError());
     s += q;
   }

@@ -272,6 +272,12 @@ Circuit build_circuit(int power, uint32_t n_public, uint32_t n_inputs, uint64_t 
 
 }  // namespace
 
+// [s_i] G1 as LEM affine on `st` (microbench bases; PTau generation below)
+void launch_fixed_base(const Fr* scalars_mont, size_t n, G1Affine* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_fixed_base, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, st, scalars_mont, n, out);
+  NZ_HIP(hipGetLastError());
+}
+
 // The whole setup; returns (zkey, wtns) as malloc'ed buffers.
 static void synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_cons, const uint8_t* tau_le,
                         int device, uint8_t** zk_out, size_t* zk_len, uint8_t** wt_out, size_t* wt_len) {

@@ -34,7 +34,8 @@ EXPORTED_SYMBOLS = [
     "nzcb_ctx_last_timings", "nzcb_proof_to_json", "nzcb_public_to_json", "nzcb_synth_setup", "nzcb_free",
     "nzcb_engine_create", "nzcb_engine_destroy", "nzcb_engine_ntt", "nzcb_engine_msm", "nzcb_dev_alloc",
     "nzcb_dev_free", "nzcb_memcpy_h2d", "nzcb_memcpy_d2h", "nzcb_engine_ntt_dev", "nzcb_engine_msm_dev",
-    "nzcb_engine_time_ntt", "nzcb_engine_fr_mul",
+    "nzcb_engine_time_ntt", "nzcb_engine_fr_mul", "nzcb_engine_random_fr", "nzcb_engine_fixed_base",
+    "nzcb_engine_time_msm",
 ]
 
 
@@ -93,6 +94,10 @@ def load(path: str | None = None):
         "nzcb_engine_time_ntt": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, POINTER(c_double),
                                          POINTER(_Err)]),
         "nzcb_engine_fr_mul": (c_int, [c_void_p, u8p, u8p, u8p, c_size_t, c_int, POINTER(_Err)]),
+        "nzcb_engine_random_fr": (c_int, [c_void_p, c_void_p, c_size_t, c_uint64, POINTER(_Err)]),
+        "nzcb_engine_fixed_base": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, POINTER(_Err)]),
+        "nzcb_engine_time_msm": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, POINTER(c_double),
+                                         POINTER(c_double), POINTER(_Err)]),
     }
     lib.missing_symbols = []
     for name, (res, args) in sigs.items():
@@ -176,6 +181,22 @@ class Engine:
         _check(self.lib.nzcb_engine_time_ntt(self.h, dev_in, dev_out, log_n, int(inverse), reps, ctypes.byref(ms),
                                              ctypes.byref(err)), err)
         return ms.value
+
+    def random_fr(self, dev_out: int, n: int, seed: int):
+        err = _Err()
+        _check(self.lib.nzcb_engine_random_fr(self.h, dev_out, n, seed, ctypes.byref(err)), err)
+
+    def fixed_base(self, dev_scalars: int, n: int, dev_out: int):
+        err = _Err()
+        _check(self.lib.nzcb_engine_fixed_base(self.h, dev_scalars, n, dev_out, ctypes.byref(err)), err)
+
+    def time_msm(self, dev_bases: int, dev_scalars: int, n: int, scalars_mont: bool, reps: int):
+        ms = c_double()
+        acc = c_double()
+        err = _Err()
+        _check(self.lib.nzcb_engine_time_msm(self.h, dev_bases, dev_scalars, n, int(scalars_mont), reps,
+                                             ctypes.byref(ms), ctypes.byref(acc), ctypes.byref(err)), err)
+        return ms.value, acc.value
 
     def msm_dev(self, dev_bases: int, dev_scalars: int, n: int, scalars_mont: bool) -> bytes:
         out = _out(64)

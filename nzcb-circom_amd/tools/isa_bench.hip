@@ -1,0 +1,97 @@
+// Instruction-throughput probe for the Montgomery-product building blocks on gfx950:
+// v_mad_u64_u32, v_addc_co_u32, s_nop, v_fma_f64, v_mul_lo_u32, v_mul_hi_u32.
+// Full-chip throughput (many waves) of 16 independent instructions per asm block.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#define REP16(x) x x x x x x x x x x x x x x x x
+
+template <int K>
+__global__ void probe(uint64_t* out, int iters) {
+  uint64_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  uint32_t x = threadIdx.x * 3 + 1, y = threadIdx.x * 7 + 5;
+  double d0 = x, d1 = y, d2 = x + 1.0, d3 = y + 1.0, d4 = 0.5, d5 = 0.25, d6 = 0.125, d7 = 2.0;
+  uint32_t h = 0;
+  for (int i = 0; i < iters; i++) {
+    if (K == 0) {  // 16 x v_mad_u64_u32 (8 independent accumulators, 2 rounds)
+      asm volatile(
+          "v_mad_u64_u32 %0, vcc, %8, %9, %0\n v_mad_u64_u32 %1, vcc, %8, %9, %1\n"
+          "v_mad_u64_u32 %2, vcc, %8, %9, %2\n v_mad_u64_u32 %3, vcc, %8, %9, %3\n"
+          "v_mad_u64_u32 %4, vcc, %8, %9, %4\n v_mad_u64_u32 %5, vcc, %8, %9, %5\n"
+          "v_mad_u64_u32 %6, vcc, %8, %9, %6\n v_mad_u64_u32 %7, vcc, %8, %9, %7\n"
+          "v_mad_u64_u32 %0, vcc, %8, %9, %0\n v_mad_u64_u32 %1, vcc, %8, %9, %1\n"
+          "v_mad_u64_u32 %2, vcc, %8, %9, %2\n v_mad_u64_u32 %3, vcc, %8, %9, %3\n"
+          "v_mad_u64_u32 %4, vcc, %8, %9, %4\n v_mad_u64_u32 %5, vcc, %8, %9, %5\n"
+          "v_mad_u64_u32 %6, vcc, %8, %9, %6\n v_mad_u64_u32 %7, vcc, %8, %9, %7\n"
+          : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+          : "v"(x), "v"(y)
+          : "vcc");
+    } else if (K == 1) {  // 16 x v_add_co_u32
+      asm volatile(REP16("v_add_co_u32 %0, vcc, %0, %1\n") : "+v"(x) : "v"(y) : "vcc");
+    } else if (K == 2) {  // 16 x s_nop 1
+      asm volatile(REP16("s_nop 1\n"));
+    } else if (K == 3) {  // 16 x v_fma_f64 (8 independent)
+      asm volatile(
+          "v_fma_f64 %0, %0, %8, %9\n v_fma_f64 %1, %1, %8, %9\n v_fma_f64 %2, %2, %8, %9\n v_fma_f64 %3, %3, %8, %9\n"
+          "v_fma_f64 %4, %4, %8, %9\n v_fma_f64 %5, %5, %8, %9\n v_fma_f64 %6, %6, %8, %9\n v_fma_f64 %7, %7, %8, %9\n"
+          "v_fma_f64 %0, %0, %8, %9\n v_fma_f64 %1, %1, %8, %9\n v_fma_f64 %2, %2, %8, %9\n v_fma_f64 %3, %3, %8, %9\n"
+          "v_fma_f64 %4, %4, %8, %9\n v_fma_f64 %5, %5, %8, %9\n v_fma_f64 %6, %6, %8, %9\n v_fma_f64 %7, %7, %8, %9\n"
+          : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7)
+          : "v"(0.999), "v"(0.001));
+    } else if (K == 4) {  // 16 x v_mul_lo_u32
+      asm volatile(REP16("v_mul_lo_u32 %0, %0, %1\n") : "+v"(x) : "v"(y));
+    } else if (K == 5) {  // 16 x v_mul_hi_u32
+      asm volatile(REP16("v_mul_hi_u32 %0, %0, %1\n") : "+v"(x) : "v"(y));
+    } else if (K == 6) {  // 8 x (mad; s_nop 1; addc) as in field.h mac
+      asm volatile(
+          "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
+          "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
+          "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
+          "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
+          "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
+          "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
+          "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
+          "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
+          : "+v"(a0), "+v"(h)
+          : "v"(x), "v"(y)
+          : "s20", "s21");
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ x ^ h ^
+                                               (uint64_t)(d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7);
+}
+
+template <int K>
+double run(uint64_t* d, int blocks, int threads, int iters) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  probe<K><<<blocks, threads>>>(d, 2);
+  (void)hipDeviceSynchronize();
+  (void)hipEventRecord(e0);
+  probe<K><<<blocks, threads>>>(d, iters);
+  (void)hipEventRecord(e1);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  return ms;
+}
+
+int main() {
+  const int blocks = 256 * 8, threads = 256, iters = 4000;
+  uint64_t* d;
+  (void)hipMalloc(&d, (size_t)blocks * threads * 8);
+  const char* names[7] = {"v_mad_u64_u32", "v_add_co_u32", "s_nop 1", "v_fma_f64", "v_mul_lo_u32", "v_mul_hi_u32",
+                          "mac(mad;nop;addc)"};
+  double ms[7] = {run<0>(d, blocks, threads, iters), run<1>(d, blocks, threads, iters), run<2>(d, blocks, threads, iters),
+                  run<3>(d, blocks, threads, iters), run<4>(d, blocks, threads, iters), run<5>(d, blocks, threads, iters),
+                  run<6>(d, blocks, threads, iters)};
+  const double waves = (double)blocks * threads / 64;
+  for (int k = 0; k < 7; k++) {
+    double n_instr = waves * iters * (k == 6 ? 8 : 16);  // wave-instructions (mac = one mad+nop+addc group)
+    double simd_cycles = ms[k] * 1e-3 * 2.4e9 * 1024;    // 256 CUs x 4 SIMDs at 2.4 GHz
+    printf("%-20s %8.3f ms  %6.2f SIMD-cycles per wave-instruction\n", names[k], ms[k], simd_cycles / n_instr);
+  }
+  return 0;
+}

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Kernel microbenchmarks (BASELINE.json configs[1]: BN254 G1 MSM + Fr NTT on one
+MI355X, 2^18..2^24). One JSON line per (kernel, size) with HBM-roofline figures:
+MSM 96 B/point (64 B affine base + 32 B scalar), NTT 64 B/element/transform
+(SURVEY.md §8d). Inputs: pseudo-random Fr scalars, bases [s_i]G1."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import nzcb  # noqa: E402
+
+PEAK = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--min-log", type=int, default=18)
+    ap.add_argument("--max-log", type=int, default=24)
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    nmax = 1 << args.max_log
+    eng = nzcb.Engine(0, max_log_ntt=args.max_log, max_msm_points=nmax)
+    sc = nzcb.dev_alloc(nmax * 32)
+    out = nzcb.dev_alloc(nmax * 32)
+    bases = nzcb.dev_alloc(nmax * 64)
+    eng.random_fr(sc, nmax, 0x6E7A6362)
+    eng.fixed_base(sc, nmax, bases)
+    for lg in range(args.min_log, args.max_log + 1):
+        n = 1 << lg
+        for inv in (False, True):
+            ms = eng.time_ntt(sc, out, lg, inv, args.reps)
+            gbs = 64 * n / (ms / 1e3) / 1e9
+            print(json.dumps({"kernel": "intt" if inv else "ntt", "log_n": lg, "ms": round(ms, 4),
+                              "elements_per_s": round(n / (ms / 1e3), 1), "GBs": round(gbs, 1),
+                              "frac": round(gbs / PEAK, 4)}), flush=True)
+        ms, acc = eng.time_msm(bases, sc, n, True, args.reps)
+        gbs = 96 * n / (ms / 1e3) / 1e9
+        print(json.dumps({"kernel": "msm", "log_n": lg, "ms": round(ms, 4), "accumulate_ms": round(acc, 4),
+                          "points_per_s": round(n / (ms / 1e3), 1), "GBs": round(gbs, 1),
+                          "frac": round(gbs / PEAK, 5)}), flush=True)
+    for p in (sc, out, bases):
+        nzcb.dev_free(p)
+
+
+if __name__ == "__main__":
+    main()
