@@ -8,6 +8,9 @@ proof on one GPU), batch-sharded with no collective across ranks (configs[3]).
 A "step" is one full proof (snarkjs plonk_prove rounds 1-5) of one
 witness whose values are already resident in HBM when the timed region starts;
 the 800-byte proof and the public signals are copied back to the host inside it.
+The K timed proofs are one nzcb_prove_batch call: --lanes proofs are in flight
+on each GPU (lanes share the HBM-resident proving key; SURVEY.md §8e batch mode),
+so one proof's latency-bound phases overlap another's compute.
 The circuit is the seeded synthetic nzcp_live stand-in:
 the real nzcp_live_final.zkey / circom witness cannot be built offline.
 
@@ -35,6 +38,10 @@ PROOF_BYTES_PER_N = 7104       # algorithmic bytes per proof = 7
 NZCP_INPUTS = 2970             # nzcp_live input signals (toBeSigned bits + len + data)
 SEED = 0x6E7A6362
 TAU = 0x6E7A6362746175
+# Product-scanning Montgomery product: 128 (v_mad_u64_u32 + v_addc_co_u32) pairs per
+# 8x32-bit product, 4 SIMD-cycles per wave64 instruction (profiles/r1_isa_bench.txt),
+# 1024 SIMDs at ~2.0 GHz under load: 1024 * 2.0e9 * 64 / (256 * 4) = 128 G products/s.
+VALU_MULT_BOUND_GS = 128.0
 
 
 def blinding_for(step: int) -> bytes:
@@ -59,6 +66,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--power", type=int, default=21, help="log2 PLONK domain (nzcp_live: 21)")
+    ap.add_argument("--lanes", type=int, default=2, help="proofs in flight per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -87,22 +95,30 @@ def main():
             torch.cuda.synchronize(local)
             dist.barrier()
 
-    for i in range(args.warmup):
-        ctx.prove_device_raw(dev_w, nwit, blinding_for(1000 + i))
-    # PCIe-inclusive rate (host witness) for DESIGN.md, one proof, not the reported value
-    t_h = time.time()
+    # single-proof latency (one lane) and the PCIe-inclusive rate (host witness) for
+    # DESIGN.md; neither is the reported value
+    ctx.prove_device_raw(dev_w, nwit, blinding_for(998))
+    t_l = time.perf_counter()
+    ctx.prove_device_raw(dev_w, nwit, blinding_for(997))
+    latency_ms = (time.perf_counter() - t_l) * 1e3
+    single_timings = ctx.last_timings()
+    t_h = time.perf_counter()
     ctx.prove_witness_raw(wtns[76:76 + nwit * 32], blinding_for(999))
-    pcie_ms = (time.time() - t_h) * 1e3
+    pcie_ms = (time.perf_counter() - t_h) * 1e3
+    ctx.set_lanes(args.lanes)
+    if args.warmup:
+        nw = max(args.warmup, args.lanes)
+        ctx.prove_batch_raw([dev_w] * nw, n_witness=nwit, blindings=[blinding_for(1000 + i) for i in range(nw)],
+                            on_device=True)
     ctx.kernel_stats(1)
     blinds = [blinding_for(i) for i in range(args.steps)]
     barrier()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ctx.prove_device_raw(dev_w, nwit, blinds[i])
+    proofs = ctx.prove_batch_raw([dev_w] * args.steps, n_witness=nwit, blindings=blinds, on_device=True)
     barrier()
     elapsed = time.perf_counter() - t0
+    assert len({p for p, _ in proofs}) == args.steps  # distinct blindings -> distinct proofs
     kms, klaunch, kpoints, kentries = ctx.kernel_stats(0)
-    timings = ctx.last_timings()
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
@@ -115,9 +131,12 @@ def main():
     if rank == 0:
         avg_launch_ms = kms / max(klaunch, 1)
         pts_per_launch = kpoints / max(klaunch, 1)
+        ent_per_launch = kentries / max(klaunch, 1)
         achieved = MSM_BYTES_PER_POINT * pts_per_launch / (avg_launch_ms / 1e3) / 1e9 if avg_launch_ms else 0.0
+        # VALU view of the same kernel: 10 Fq Montgomery products per XYZZ mixed addition
+        mults_per_s = 10 * ent_per_launch / (avg_launch_ms / 1e3) if avg_launch_ms else 0.0
         traffic = None
-        tf = os.environ.get("NZCB_TRAFFIC_JSON")
+        tf = os.environ.get("NZCB_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "accumulate_traffic.json"))
         if tf and os.path.exists(tf):
             with open(tf) as f:
                 traffic = json.load(f).get("bytes_per_launch")
@@ -150,6 +169,7 @@ def main():
                 "n_additions": ctx.n_additions,
                 "proofs_per_gpu": args.steps,
                 "parallelism": f"batch-shard x{world} (no collective)",
+                "proofs_in_flight_per_gpu": args.lanes,
             },
             "roofline": {
                 "kernel": "msm_accumulate_kernel (Pippenger bucket accumulation)",
@@ -163,13 +183,18 @@ def main():
                 "launches": int(klaunch),
                 "points_per_launch": int(pts_per_launch),
                 "bytes_per_point": MSM_BYTES_PER_POINT,
+                "bucket_entries_per_launch": int(ent_per_launch),
+                "valu": {"fq_mont_mul_per_s": round(mults_per_s / 1e9, 2), "unit": "G/s",
+                         "bound_mad_addc": VALU_MULT_BOUND_GS,
+                         "frac": round(mults_per_s / 1e9 / VALU_MULT_BOUND_GS, 4)},
             },
             "proof_roofline": {
                 "algorithmic_bytes": PROOF_BYTES_PER_N * n,
                 "achieved_GBs": round(proof_gbs, 2),
                 "frac": round(proof_gbs / HBM_PEAK_GBS, 5),
             },
-            "phase_ms_last_proof": {k: round(v, 3) for k, v in timings.items()},
+            "single_proof_latency_ms": round(latency_ms, 3),
+            "phase_ms_single_proof": {k: round(v, 3) for k, v in single_timings.items()},
             "pcie_inclusive_ms": round(pcie_ms, 3),
             "setup_s": round(setup_s, 2),
             "cpu_baseline": cpu,

@@ -93,6 +93,22 @@ int nzcb_prove_witness(nzcb_ctx* ctx, const uint8_t* witness, size_t n_witness, 
 int nzcb_prove_device(nzcb_ctx* ctx, const void* dev_witness, size_t n_witness, const uint8_t* blinding,
                       uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_err* err);
 
+/* Proof lanes (default 1): each extra lane is a per-proof working set + streams on
+ * the context's device (~6.5 GB at n = 2^21) sharing the HBM-resident proving key,
+ * so nzcb_prove_batch keeps `lanes` proofs in flight and one proof's latency-bound
+ * phases (Fiat-Shamir host steps, bucket reductions) overlap another's compute. */
+int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err);
+int nzcb_ctx_lanes(const nzcb_ctx* ctx);
+
+/* `count` independent proofs over the context's lanes (SURVEY.md §8b nzcb_prove_batch,
+ * §8e batch mode). witnesses[i]: nWitness x 32-byte LE normal-form values, host memory,
+ * or device pointers when witness_on_device. blindings: count x NZCB_BLINDING_BYTES or
+ * NULL (all zero). proofs_out: count x NZCB_PROOF_BYTES. pubs_out: count x pub_stride
+ * (pub_stride >= 32 * nPublic). Returns the error of the lowest failing index. */
+int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witness, int count, int witness_on_device,
+                     const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out, size_t pub_stride,
+                     nzcb_err* err);
+
 /* Wall-clock milliseconds of the last proof's phases:
  * [0] total [1] witness upload+additions+ABC [2] round1 [3] round2 [4] round3 [5] round4 [6] round5
  * [7] all MSMs [8] all NTTs. Returns the number of values written. */
@@ -146,6 +162,16 @@ int nzcb_engine_fixed_base(nzcb_engine* e, const void* dev_scalars_mont, size_t 
  * accumulation kernel ms (HIP events). */
 int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont, int reps,
                          double* ms, double* acc_ms, nzcb_err* err);
+/* Fixed-base schedule (the prover's): builds the shifted-base table of the first
+ * n_table bases (2^(20w) multiples, 13 rows), then runs the MSM of the first n.
+ * One-shot (table and scratch freed on return); for parity tests. */
+int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
+                              int scalars_mont, uint8_t* out_affine, nzcb_err* err);
+/* Per-phase MSM timing (HIP events, average over reps after one warm-up):
+ * out[0] wall ms, out[1..7] keys, sort, offsets, accumulate, finalize, reduce, sums,
+ * out[8] table build ms (fixed_base only). */
+int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
+                          int fixed_base, int reps, double* out, nzcb_err* err);
 /* Field self-test helpers: out[i] = a[i] * b[i] (Montgomery, device), n elements. */
 int nzcb_engine_fr_mul(nzcb_engine* e, const uint8_t* a_lem, const uint8_t* b_lem, uint8_t* out_lem, size_t n,
                        int field_q, nzcb_err* err);

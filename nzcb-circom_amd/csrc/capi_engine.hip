@@ -1,6 +1,7 @@
 // C-ABI: engine, device memory and kernel-level entry points (include/nzcb.h).
 #include <chrono>
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include "../../include/nzcb.h"
@@ -229,6 +230,59 @@ int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars,
   *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / (reps ? reps : 1);
   *acc_ms = sc.prof_ms / (sc.prof_launches ? sc.prof_launches : 1);
   sc.prof = false;
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
+                              int scalars_mont, uint8_t* out_affine, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  if (n > n_table) throw Error(NZCB_ERR_ARG, "msm larger than its base table");
+  MsmBaseTable t;
+  t.build((const G1Affine*)bases, n_table, kFixedBaseWindow, g.stream);
+  MsmScratch sc;
+  sc.init(n ? n : 1, true);
+  G1xyzz r = msm(sc, (const G1Affine*)bases, (const Fr*)scalars, n, scalars_mont != 0, g.stream, &t);
+  affine_out(r, out_affine);
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
+                          int fixed_base, int reps, double* out, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  std::unique_ptr<MsmBaseTable> t;
+  std::unique_ptr<MsmScratch> own;
+  MsmScratch* sc = &g.msm_scratch;
+  double table_ms = 0;
+  if (fixed_base) {
+    auto t0 = std::chrono::steady_clock::now();
+    t.reset(new MsmBaseTable());
+    t->build((const G1Affine*)bases, n, kFixedBaseWindow, g.stream);
+    NZ_HIP(hipStreamSynchronize(g.stream));
+    table_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    own.reset(new MsmScratch());
+    own->init(n, true);
+    sc = own.get();
+  }
+  (void)msm(*sc, (const G1Affine*)bases, (const Fr*)scalars, n, scalars_mont != 0, g.stream, t.get());  // warm-up
+  sc->prof = true;
+  sc->prof_phases = true;
+  sc->prof_ms = 0;
+  sc->prof_launches = 0;
+  for (double& x : sc->phase_ms) x = 0;
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < reps; i++)
+    (void)msm(*sc, (const G1Affine*)bases, (const Fr*)scalars, n, scalars_mont != 0, g.stream, t.get());
+  const double r = reps > 0 ? reps : 1;
+  out[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / r;
+  for (int i = 0; i < 7; i++) out[1 + i] = sc->phase_ms[i] / r;
+  out[8] = table_ms;
+  sc->prof = sc->prof_phases = false;
   return 0;
   NZ_GUARD_END(err)
 }

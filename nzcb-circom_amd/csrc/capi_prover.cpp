@@ -1,7 +1,10 @@
 // C-ABI: prover context, proofs and snarkjs-format JSON (include/nzcb.h).
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/nzcb.h"
 #include "prover.h"
@@ -12,10 +15,13 @@ void set_err(nzcb_err* err, int code, const char* msg);
 using namespace nzcb;
 
 struct nzcb_ctx {
-  std::unique_ptr<Prover> p;
+  std::unique_ptr<Prover> p;                   // lane 0: owns the HBM-resident proving key
+  std::vector<std::unique_ptr<Prover>> extra;  // lanes 1..: share it (nzcb_ctx_set_lanes)
   nzcb_log_fn log_fn = nullptr;
   void* log_user = nullptr;
-  std::mutex mu;  // proofs on one context are serialized (SURVEY.md §8b "Threading")
+  std::mutex mu;  // calls on one context are serialized (SURVEY.md §8b "Threading")
+  Prover* lane(size_t i) { return i == 0 ? p.get() : extra[i - 1].get(); }
+  size_t lanes() const { return 1 + extra.size(); }
 };
 
 namespace {
@@ -83,16 +89,90 @@ void nzcb_ctx_destroy(nzcb_ctx* ctx) { delete ctx; }
 
 void nzcb_ctx_set_logger(nzcb_ctx* ctx, nzcb_log_fn fn, void* user) {
   if (!ctx) return;
+  std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->log_fn = fn;
   ctx->log_user = user;
-  if (fn)
-    ctx->p->log = [ctx](const std::string& m) { ctx->log_fn(ctx->log_user, m.c_str()); };
-  else
-    ctx->p->log = nullptr;
+  for (size_t i = 0; i < ctx->lanes(); i++) {
+    if (fn)
+      ctx->lane(i)->log = [ctx](const std::string& m) { ctx->log_fn(ctx->log_user, m.c_str()); };
+    else
+      ctx->lane(i)->log = nullptr;
+  }
 }
 
 void nzcb_ctx_set_transcript_public(nzcb_ctx* ctx, int on) {
-  if (ctx) ctx->p->transcript_public = on != 0;
+  if (!ctx) return;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  for (size_t i = 0; i < ctx->lanes(); i++) ctx->lane(i)->transcript_public = on != 0;
+}
+
+int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err) {
+  if (!ctx || lanes < 1 || lanes > 16) return fail(err, NZCB_ERR_ARG, "lanes must be in 1..16");
+  try {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    while (ctx->lanes() > (size_t)lanes) ctx->extra.pop_back();
+    while (ctx->lanes() < (size_t)lanes) {
+      ctx->extra.emplace_back(new Prover(*ctx->p, (int)ctx->lanes()));
+      Prover* q = ctx->extra.back().get();
+      q->log = ctx->p->log;
+    }
+    if (err) err->code = 0;
+    return 0;
+  } catch (const Error& e) {
+    return fail(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, NZCB_ERR_INTERNAL, e.what());
+  }
+}
+
+int nzcb_ctx_lanes(const nzcb_ctx* ctx) { return ctx ? (int)ctx->lanes() : 0; }
+
+int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witness, int count, int witness_on_device,
+                     const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out, size_t pub_stride,
+                     nzcb_err* err) {
+  if (!ctx || count < 0 || (count && (!witnesses || !proofs_out))) return fail(err, NZCB_ERR_ARG, "null argument");
+  const size_t npub = ctx->p->nPublic;
+  if (npub && (!pubs_out || pub_stride < 32 * npub)) return fail(err, NZCB_ERR_ARG, "public output buffer too small");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::atomic<int> next(0);
+  std::atomic<int> first_bad(count);
+  std::vector<int> codes(count, 0);
+  std::vector<std::string> msgs(count);
+  auto worker = [&](Prover* pr) {
+    for (;;) {
+      const int i = next.fetch_add(1);
+      if (i >= count || i > first_bad.load()) return;
+      try {
+        pr->prove((const uint8_t*)witnesses[i], n_witness,
+                  blindings ? blindings + (size_t)i * NZCB_BLINDING_BYTES : nullptr,
+                  proofs_out + (size_t)i * NZCB_PROOF_BYTES, npub ? pubs_out + (size_t)i * pub_stride : nullptr,
+                  witness_on_device != 0);
+      } catch (const Error& e) {
+        codes[i] = e.code;
+        msgs[i] = e.what();
+      } catch (const std::exception& e) {
+        codes[i] = NZCB_ERR_INTERNAL;
+        msgs[i] = e.what();
+      }
+      if (codes[i]) {
+        int cur = first_bad.load();
+        while (i < cur && !first_bad.compare_exchange_weak(cur, i)) {
+        }
+      }
+    }
+  };
+  const size_t nl = std::min(ctx->lanes(), (size_t)(count > 0 ? count : 1));
+  std::vector<std::thread> th;
+  for (size_t l = 1; l < nl; l++) th.emplace_back(worker, ctx->lane(l));
+  worker(ctx->lane(0));
+  for (auto& t : th) t.join();
+  const int bad = first_bad.load();
+  if (bad < count) {
+    std::string m = "proof " + std::to_string(bad) + ": " + msgs[bad];
+    return fail(err, codes[bad], m.c_str());
+  }
+  if (err) err->code = 0;
+  return 0;
 }
 
 int nzcb_ctx_info(const nzcb_ctx* ctx, uint32_t out[5]) {
@@ -164,19 +244,21 @@ int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
   if (!ctx) return NZCB_ERR_ARG;
   if (out) {
     for (int i = 0; i < 4; i++) out[i] = 0;
-    for (auto& m : ctx->p->msc) {
-      out[0] += m->prof_ms;
-      out[1] += (double)m->prof_launches;
-      out[2] += (double)m->prof_points;
-      out[3] += (double)m->prof_entries;
-    }
+    for (size_t l = 0; l < ctx->lanes(); l++)
+      for (auto& m : ctx->lane(l)->msc) {
+        out[0] += m->prof_ms;
+        out[1] += (double)m->prof_launches;
+        out[2] += (double)m->prof_points;
+        out[3] += (double)m->prof_entries;
+      }
   }
   if (enable >= 0) {
-    for (auto& m : ctx->p->msc) {
-      m->prof = enable != 0;
-      m->prof_ms = 0;
-      m->prof_launches = m->prof_points = m->prof_entries = 0;
-    }
+    for (size_t l = 0; l < ctx->lanes(); l++)
+      for (auto& m : ctx->lane(l)->msc) {
+        m->prof = enable != 0;
+        m->prof_ms = 0;
+        m->prof_launches = m->prof_points = m->prof_entries = 0;
+      }
   }
   return 0;
 }

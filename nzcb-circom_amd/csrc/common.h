@@ -34,13 +34,14 @@ template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  bool owned = true;  // false: a view of another buffer (shared proving-key data)
   DevBuf() = default;
   explicit DevBuf(size_t count) { alloc(count); }
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
-  DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n), owned(o.owned) { o.p = nullptr; o.n = 0; }
   DevBuf& operator=(DevBuf&& o) noexcept {
-    if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+    if (this != &o) { release(); p = o.p; n = o.n; owned = o.owned; o.p = nullptr; o.n = 0; }
     return *this;
   }
   ~DevBuf() { release(); }
@@ -48,9 +49,16 @@ struct DevBuf {
     release();
     if (count) NZ_HIP(hipMalloc(&p, count * sizeof(T)));
     n = count;
+    owned = true;
+  }
+  void alias(const DevBuf& o) {
+    release();
+    p = o.p;
+    n = o.n;
+    owned = false;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p && owned) (void)hipFree(p);
     p = nullptr;
     n = 0;
   }

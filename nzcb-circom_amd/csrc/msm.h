@@ -7,46 +7,64 @@
 
 namespace nzcb {
 
+// Precomputed shifted bases for fixed-base MSMs (the prover's PTau): row w holds
+// 2^(c*w) * B_i (LEM affine), so every window's digits land in ONE bucket set and
+// the per-window bucket reductions and the window Horner disappear.
+struct MsmBaseTable {
+  DevBuf<G1Affine> q;
+  size_t n = 0, stride = 0;
+  int c = 0, nw = 0;
+  void build(const G1Affine* bases, size_t n, int c, hipStream_t st);
+};
+
+// Window size of the table-based (fixed-base) MSM.
+constexpr int kFixedBaseWindow = 20;
+
 struct MsmScratch {
   size_t max_points = 0;
-  DevBuf<uint32_t> offsets;   // first sorted position of each (window, bucket) key, + total at the end
-  DevBuf<uint32_t> sorted;    // point index | sign << 31, grouped by bucket
+  DevBuf<uint32_t> offsets;   // first sorted position of each bucket key, + total at the end
+  DevBuf<uint32_t> sorted;    // base index | sign << 31, grouped by bucket
   DevBuf<uint32_t> keys_in, keys_out, vals_in;
   DevBuf<uint8_t> sort_tmp;
   size_t sort_tmp_bytes = 0;
   DevBuf<G1xyzz> buckets;     // buckets whose entries lie in one accumulation chunk
   DevBuf<G1xyzz> carry_own;   // per chunk: partial sum of a bucket that starts in the chunk and spills over
   DevBuf<G1xyzz> carry_cont;  // per chunk: partial sum of a bucket that began in an earlier chunk
-  DevBuf<G1xyzz> seg_tot;     // per (window, segment): sum_j (j+1) * bucket_j
-  DevBuf<G1xyzz> seg_run;     // per (window, segment): sum_j bucket_j
-  DevBuf<G1xyzz> win;         // per (window, sum slot): see msm_window_sums_kernel
+  DevBuf<G1xyzz> seg_tot;     // per (bucket set, segment): sum_j (j+1) * bucket_j
+  DevBuf<G1xyzz> seg_run;     // per (bucket set, segment): sum_j bucket_j
+  DevBuf<G1xyzz> parts;       // per (set, sum slot, part): partial plain sums
+  DevBuf<G1xyzz> win;         // per (set, sum slot): see msm_sums_kernel
   G1xyzz* host_win = nullptr;  // pinned
   size_t host_win_cap = 0;
   // shape of the MSM in flight (set by msm_enqueue, used by msm_finish)
-  int cur_c = 0, cur_nw = 0, cur_nbits = 0, cur_seglen = 0;
+  int cur_c = 0, cur_nsets = 0, cur_nbits = 0, cur_seglen = 0;
   size_t cur_n = 0;
   uint32_t cur_nkeys = 0;
-  // optional HIP-event timing of the bucket-accumulation kernel (bench.py roofline)
-  bool prof = false;
+  // optional HIP-event timing: accumulation kernel (bench.py roofline) and, with
+  // prof_phases, every phase (keys, sort, offsets, accumulate, finalize, reduce, sums)
+  bool prof = false, prof_phases = false;
   double prof_ms = 0;
+  double phase_ms[7] = {0, 0, 0, 0, 0, 0, 0};
   uint64_t prof_launches = 0, prof_points = 0, prof_entries = 0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  void init(size_t max_points);
+  hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  void init(size_t max_points, bool fixed_base = false);
   ~MsmScratch();
 };
 
-// Window size used for an MSM of n points.
+// Window size of the generic (variable-base) MSM of n points.
 int msm_window_bits(size_t n);
 
 // Enqueue the whole MSM sum_i s_i * B_i on `st` (no host sync); msm_finish waits for
-// it and folds the per-window sums on the host. bases: zkey PTau layout (LEM affine).
-// scalars: Fr, Montgomery form if scalars_mont.
+// it and folds the bucket-set sums on the host. bases: zkey PTau layout (LEM affine).
+// scalars: Fr, Montgomery form if scalars_mont. With `table` (built from the same
+// bases, n <= table->n) the fixed-base schedule is used.
 void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, bool scalars_mont,
-                 hipStream_t st);
+                 hipStream_t st, const MsmBaseTable* table = nullptr);
 G1xyzz msm_finish(MsmScratch& sc, hipStream_t st);
 
-inline G1xyzz msm(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, bool mont, hipStream_t st) {
-  msm_enqueue(sc, bases, scalars, n, mont, st);
+inline G1xyzz msm(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, bool mont, hipStream_t st,
+                  const MsmBaseTable* table = nullptr) {
+  msm_enqueue(sc, bases, scalars, n, mont, st, table);
   return msm_finish(sc, st);
 }
 

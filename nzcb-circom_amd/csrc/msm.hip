@@ -6,25 +6,31 @@
 // (16 bits at 2^21) on CPU workers. The result is a unique group element, so
 // any correct schedule is bit-exact after conversion to affine.
 //
-// Pipeline (one stream, no host sync until the window sums):
+// Two schedules share the kernels:
+//  * generic (variable bases): c-bit windows, one bucket set per window
+//    (key = window * 2^(c-1) + |digit| - 1), host Horner over the windows;
+//  * fixed-base (the prover's PTau): a table of shifted bases 2^(20w) * B_i
+//    (MsmBaseTable) turns the 13 windows of 20 bits into ONE set of 2^19 buckets
+//    (key = |digit| - 1, value = row w of the table): 13 instead of 16 bucket
+//    additions per scalar, and a single bucket reduction.
+//
+// Pipeline (one stream, no host sync until the bucket-set sums):
 //  1. keys:       thread per scalar -> signed c-bit digits; (scalar, window) pair i
-//                 gets the fixed slot w*n+i, key = window*2^(c-1) + |digit|-1
-//                 (zero digits get a sentinel key that sorts last) -- no atomics
-//  2. sort:       rocPRIM radix sort of (key, index|sign) on ceil(log2 keys) bits
+//                 gets the fixed slot w*n+i; zero digits get a sentinel key that
+//                 sorts last -- no atomics
+//  2. sort:       rocPRIM radix sort of (key, base index|sign) on ceil(log2 keys) bits
 //  3. offsets:    bucket start positions by binary search in the sorted keys
 //  4. accumulate: thread per fixed 32-entry chunk of the sorted stream (load balance
 //                 independent of the digit distribution): XYZZ mixed adds of the
 //                 gathered affine bases; bucket runs inside one chunk are written
 //                 directly, runs crossing a chunk edge go to per-chunk carries
-//  5. reduce:     thread per (window, 16-bucket segment): rebuilds each bucket (one
-//                 store or carries) and runs sum/weighted-sum from the top bucket
-//  6. sums:       one workgroup per (window, slot): slot 0 sums the segments'
-//                 weighted sums, slot b+1 sums the running sums of segments whose
-//                 index has bit b set (the segment-offset weights, in binary)
-//  7. host:       per window W = T + 16 * sum_b 2^b R_b, then Horner over windows
-// Bases are read straight from the zkey PTau layout (64 B LEM affine); the
-// 2^21-point table is 128 MiB and stays resident in the 256 MiB Infinity Cache
-// across the 16 windows' random gathers.
+//  5. finalize:   thread per bucket spanning chunks: owner carry + continuations
+//  6. reduce:     thread per (set, 8-bucket segment): running sum / weighted sum
+//  7. sums:       slot 0 sums the segments' weighted sums, slot b+1 sums the running
+//                 sums of segments whose index has bit b set (the segment-offset
+//                 weights, in binary); two levels of block tree sums
+//  8. host:       per set W = T + 8 * sum_b 2^b R_b, then Horner over the sets
+// Generic bases are read straight from the zkey PTau layout (64 B LEM affine).
 #include "msm.h"
 
 #include <hipcub/hipcub.hpp>
@@ -34,6 +40,9 @@ namespace nzcb {
 static constexpr int kMsmThreads = 256;
 static constexpr uint32_t kChunk = 32;
 static constexpr int kSegLen = 8;
+static constexpr int kSumThreads = 256;  // level-1 sums: block size
+static constexpr int kSumPer = 4;        // level-1 sums: sequential adds per thread
+static constexpr int kPartThreads = 64;  // level-2 sums: block size
 
 int msm_window_bits(size_t n) {
   if (n >= (size_t(1) << 18)) return 16;
@@ -71,12 +80,14 @@ __device__ __forceinline__ void for_each_digit(const Fr& s, F&& f) {
   }
 }
 
-template <int C>
+// FIXED: key = bucket, value = table row w (stride) + i; else key = w * NB + bucket, value = i
+template <int C, bool FIXED>
 __global__ void __launch_bounds__(kMsmThreads)
-msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, uint32_t* __restrict__ keys,
+msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t stride, uint32_t* __restrict__ keys,
                 uint32_t* __restrict__ vals) {
   constexpr int NW = (255 + C - 1) / C;
   constexpr uint32_t NB = 1u << (C - 1);
+  constexpr uint32_t SENTINEL = FIXED ? NB : NW * NB;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     Fr s = scalars[i];
     if (mont) s = from_mont(s);
@@ -84,12 +95,17 @@ msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, uint32_t* __
     uint32_t v[NW];
 #pragma unroll
     for (int w = 0; w < NW; w++) {
-      k[w] = NW * NB;
+      k[w] = SENTINEL;
       v[w] = (uint32_t)i;
     }
     for_each_digit<C>(s, [&](int w, uint32_t b, uint32_t sign) {
-      k[w] = (uint32_t)w * NB + b;
-      v[w] = (uint32_t)i | (sign << 31);
+      if (FIXED) {
+        k[w] = b;
+        v[w] = (uint32_t)((size_t)w * stride + i) | (sign << 31);
+      } else {
+        k[w] = (uint32_t)w * NB + b;
+        v[w] = (uint32_t)i | (sign << 31);
+      }
     });
 #pragma unroll
     for (int w = 0; w < NW; w++) {
@@ -180,12 +196,12 @@ msm_bucket_finalize_kernel(const uint32_t* __restrict__ offsets, uint32_t nkeys,
   buckets[k] = v;
 }
 
-// thread per (window, L-bucket segment): run = sum_j B_j, tot = sum_j (j+1) B_j
+// thread per (set, L-bucket segment): run = sum_j B_j, tot = sum_j (j+1) B_j
 __global__ void __launch_bounds__(kMsmThreads)
 msm_bucket_reduce_kernel(const G1xyzz* __restrict__ buckets, const uint32_t* __restrict__ offsets, int nb,
-                         int seglen, int nseg, int nw, G1xyzz* __restrict__ seg_tot, G1xyzz* __restrict__ seg_run) {
+                         int seglen, int nseg, int nsets, G1xyzz* __restrict__ seg_tot, G1xyzz* __restrict__ seg_run) {
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (size_t)nw * nseg) return;
+  if (t >= (size_t)nsets * nseg) return;
   const int w = (int)(t / nseg);
   const int g = (int)(t % nseg);
   const size_t base = (size_t)w * nb + (size_t)g * seglen;
@@ -208,40 +224,25 @@ msm_bucket_reduce_kernel(const G1xyzz* __restrict__ buckets, const uint32_t* __r
   seg_run[t] = run;  // sum_j bucket_{g*L+j}
 }
 
-// workgroup (w, j): j = 0 -> sum_g seg_tot[w][g]; j = b+1 -> sum of seg_run[w][g] over g with bit b set
-__global__ void __launch_bounds__(kMsmThreads)
-msm_window_sums_kernel(const G1xyzz* __restrict__ seg_tot, const G1xyzz* __restrict__ seg_run, int nseg,
-                       int nslots, G1xyzz* __restrict__ out) {
-  __shared__ G1xyzz sh[kMsmThreads];
-  const int w = blockIdx.x / nslots;
-  const int j = blockIdx.x % nslots;
+// Block tree sum with a single EC-addition site: `per` sequential steps in which
+// load(step, rhs) supplies the thread's next term, then log2(T) LDS tree levels.
+template <int T, class Load>
+__device__ __forceinline__ G1xyzz block_sum(int per, G1xyzz* sh, Load&& load) {
+  constexpr int LG = T == 256 ? 8 : T == 128 ? 7 : T == 64 ? 6 : 5;
   const int tid = threadIdx.x;
-  const int count = j == 0 ? nseg : nseg >> 1;
-  const int nacc = (count + kMsmThreads - 1) / kMsmThreads;
-  int lg = 0;
-  while ((1 << lg) < kMsmThreads) lg++;
   G1xyzz acc = G1xyzz::inf();
-  for (int step = 0; step < nacc + lg; step++) {
-    if (step == nacc) {
+  for (int step = 0; step < per + LG; step++) {
+    if (step == per) {
       sh[tid] = acc;
       __syncthreads();
     }
     bool doit;
     G1xyzz lhs, rhs;
-    if (step < nacc) {
-      const int q = tid + step * kMsmThreads;
-      doit = q < count;
-      if (doit) {
-        int g = q;
-        if (j) {
-          const int b = j - 1;
-          g = ((q >> b) << (b + 1)) | (1 << b) | (q & ((1 << b) - 1));
-        }
-        rhs = j ? seg_run[(size_t)w * nseg + g] : seg_tot[(size_t)w * nseg + g];
-        lhs = acc;
-      }
+    if (step < per) {
+      doit = load(step, rhs);
+      lhs = acc;
     } else {
-      const int stride = (kMsmThreads >> 1) >> (step - nacc);
+      const int stride = (T >> 1) >> (step - per);
       doit = tid < stride;
       if (doit) {
         lhs = sh[tid];
@@ -250,39 +251,132 @@ msm_window_sums_kernel(const G1xyzz* __restrict__ seg_tot, const G1xyzz* __restr
     }
     G1xyzz r;
     if (doit) r = xyzz_add(lhs, rhs);
-    if (step < nacc) {
+    if (step < per) {
       if (doit) acc = r;
     } else {
       if (doit) sh[tid] = r;
       __syncthreads();
     }
   }
-  if (tid == 0) out[blockIdx.x] = sh[0];
+  return sh[0];
 }
 
-static void msm_shape(size_t n, int& c, int& nw, uint32_t& nb, int& seglen, int& nseg, int& nbits) {
-  c = msm_window_bits(n);
+// level 1: block (set w, slot j, part p). Slot 0 sums seg_tot[w][g] over all g; slot b+1
+// sums seg_run[w][g] over the g with bit b set. Part p covers kSumPer * T terms.
+__global__ void __launch_bounds__(kSumThreads)
+msm_sums_kernel(const G1xyzz* __restrict__ seg_tot, const G1xyzz* __restrict__ seg_run, int nseg, int nslots,
+                int nparts, G1xyzz* __restrict__ parts) {
+  __shared__ G1xyzz sh[kSumThreads];
+  const int p = blockIdx.x % nparts;
+  const int wj = blockIdx.x / nparts;
+  const int j = wj % nslots;
+  const int w = wj / nslots;
+  const int count = j == 0 ? nseg : nseg >> 1;
+  const G1xyzz r = block_sum<kSumThreads>(kSumPer, sh, [&](int step, G1xyzz& rhs) {
+    const int q = (p * kSumPer + step) * kSumThreads + (int)threadIdx.x;
+    if (q >= count) return false;
+    int g = q;
+    if (j) {
+      const int b = j - 1;
+      g = ((q >> b) << (b + 1)) | (1 << b) | (q & ((1 << b) - 1));
+    }
+    rhs = j ? seg_run[(size_t)w * nseg + g] : seg_tot[(size_t)w * nseg + g];
+    return true;
+  });
+  if (threadIdx.x == 0) parts[blockIdx.x] = r;
+}
+
+// level 2: block per (set, slot) sums its nparts partials
+__global__ void __launch_bounds__(kPartThreads)
+msm_parts_kernel(const G1xyzz* __restrict__ parts, int nparts, G1xyzz* __restrict__ out) {
+  __shared__ G1xyzz sh[kPartThreads];
+  const int per = (nparts + kPartThreads - 1) / kPartThreads;
+  const G1xyzz r = block_sum<kPartThreads>(per, sh, [&](int step, G1xyzz& rhs) {
+    const int q = step * kPartThreads + (int)threadIdx.x;
+    if (q >= nparts) return false;
+    rhs = parts[(size_t)blockIdx.x * nparts + q];
+    return true;
+  });
+  if (threadIdx.x == 0) out[blockIdx.x] = r;
+}
+
+// Shifted-base table: row w = 2^(c*w) * B_i, thread per base (c doublings per row,
+// one Fermat inversion per stored affine point).
+__global__ void __launch_bounds__(kMsmThreads)
+msm_table_kernel(const G1Affine* __restrict__ bases, size_t n, size_t stride, int c, int nw, G1Affine* __restrict__ q) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const G1Affine P = bases[i];
+  q[i] = P;
+  if (P.is_inf()) {
+    for (int w = 1; w < nw; w++) q[(size_t)w * stride + i] = P;
+    return;
+  }
+  G1xyzz acc = xyzz_from_affine(P);
+  for (int w = 1; w < nw; w++) {
+    for (int k = 0; k < c; k++) acc = xyzz_dbl(acc);
+    const Fq ti = inverse(acc.ZZ * acc.ZZZ);
+    G1Affine r;
+    r.x = acc.X * (acc.ZZZ * ti);
+    r.y = acc.Y * (acc.ZZ * ti);
+    q[(size_t)w * stride + i] = r;
+  }
+}
+
+void MsmBaseTable::build(const G1Affine* bases, size_t npts, int cbits, hipStream_t st) {
+  n = npts;
+  stride = npts;
+  c = cbits;
   nw = num_windows(c);
-  nb = 1u << (c - 1);
-  seglen = (int)(nb < (uint32_t)kSegLen ? nb : kSegLen);
-  nseg = (int)(nb / seglen);
-  nbits = 0;
-  while ((1 << nbits) < nseg) nbits++;
+  if ((size_t)nw * stride >= (size_t(1) << 31)) throw Error(NZCB_ERR_ARG, "msm table too large for 31-bit indices");
+  q.alloc((size_t)nw * stride);
+  hipLaunchKernelGGL(msm_table_kernel, dim3(grid_for(n, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0, st, bases, n,
+                     stride, c, nw, q.p);
+  NZ_HIP(hipGetLastError());
 }
 
-void MsmScratch::init(size_t maxp) {
+struct MsmPlan {
+  int c, nw, nsets, seglen, nseg, nbits, nslots, nparts;
+  uint32_t nb, nkeys;
+  size_t entries;
+};
+
+static MsmPlan make_plan(size_t n, const MsmBaseTable* t) {
+  MsmPlan p;
+  p.c = t ? t->c : msm_window_bits(n);
+  p.nw = num_windows(p.c);
+  p.nsets = t ? 1 : p.nw;
+  p.nb = 1u << (p.c - 1);
+  p.nkeys = p.nb * (uint32_t)p.nsets;
+  p.seglen = (int)(p.nb < (uint32_t)kSegLen ? p.nb : kSegLen);
+  p.nseg = (int)(p.nb / p.seglen);
+  p.nbits = 0;
+  while ((1 << p.nbits) < p.nseg) p.nbits++;
+  p.nslots = p.nbits + 1;
+  p.nparts = (p.nseg + kSumThreads * kSumPer - 1) / (kSumThreads * kSumPer);
+  p.entries = n * (size_t)p.nw;
+  return p;
+}
+
+void MsmScratch::init(size_t maxp, bool fixed_base) {
   max_points = maxp;
-  size_t max_entries = 0, max_keys = 0, max_seg = 0, max_slots = 0;
+  size_t max_entries = 0, max_keys = 0, max_seg = 0, max_slots = 0, max_parts = 0;
+  auto fit = [&](const MsmPlan& p) {
+    max_entries = std::max(max_entries, p.entries);
+    max_keys = std::max(max_keys, (size_t)p.nkeys);
+    max_seg = std::max(max_seg, (size_t)p.nseg * p.nsets);
+    max_slots = std::max(max_slots, (size_t)p.nslots * p.nsets);
+    max_parts = std::max(max_parts, (size_t)p.nslots * p.nsets * p.nparts);
+  };
   for (size_t n = 1;; n <<= 1) {
     size_t m = n < maxp ? n : maxp;
-    int c, nw, seglen, nseg, nbits;
-    uint32_t nb;
-    msm_shape(m, c, nw, nb, seglen, nseg, nbits);
-    max_entries = std::max(max_entries, m * nw);
-    max_keys = std::max(max_keys, (size_t)nb * nw);
-    max_seg = std::max(max_seg, (size_t)nseg * nw);
-    max_slots = std::max(max_slots, (size_t)(nbits + 1) * nw);
+    fit(make_plan(m, nullptr));
     if (m == maxp) break;
+  }
+  if (fixed_base) {
+    MsmBaseTable t;
+    t.c = kFixedBaseWindow;
+    fit(make_plan(maxp, &t));
   }
   offsets.alloc(max_keys + 1);
   sorted.alloc(max_entries);
@@ -299,6 +393,7 @@ void MsmScratch::init(size_t maxp) {
   carry_cont.alloc(nthreads);
   seg_tot.alloc(max_seg);
   seg_run.alloc(max_seg);
+  parts.alloc(max_parts);
   win.alloc(max_slots);
   host_win_cap = max_slots;
   NZ_HIP(hipHostMalloc((void**)&host_win, max_slots * sizeof(G1xyzz), hipHostMallocDefault));
@@ -306,20 +401,26 @@ void MsmScratch::init(size_t maxp) {
 
 MsmScratch::~MsmScratch() {
   if (host_win) (void)hipHostFree(host_win);
-  if (ev0) (void)hipEventDestroy(ev0);
-  if (ev1) (void)hipEventDestroy(ev1);
+  for (auto& e : ev)
+    if (e) (void)hipEventDestroy(e);
 }
 
-template <int C>
-static void launch_keys(const Fr* scalars, size_t n, int mont, MsmScratch& sc, hipStream_t st) {
-  hipLaunchKernelGGL(msm_keys_kernel<C>, dim3(grid_for(n, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0, st,
-                     scalars, n, mont, sc.keys_in.p, sc.vals_in.p);
+template <int C, bool FIXED>
+static void launch_keys(const Fr* scalars, size_t n, int mont, size_t stride, MsmScratch& sc, hipStream_t st) {
+  hipLaunchKernelGGL((msm_keys_kernel<C, FIXED>), dim3(grid_for(n, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0, st,
+                     scalars, n, mont, stride, sc.keys_in.p, sc.vals_in.p);
   NZ_HIP(hipGetLastError());
 }
 
-static void keys_dispatch(int c, const Fr* scalars, size_t n, int mont, MsmScratch& sc, hipStream_t st) {
+static void keys_dispatch(int c, const Fr* scalars, size_t n, int mont, const MsmBaseTable* t, MsmScratch& sc,
+                          hipStream_t st) {
+  if (t) {
+    if (c != kFixedBaseWindow) throw Error(NZCB_ERR_INTERNAL, "bad fixed-base msm window");
+    launch_keys<kFixedBaseWindow, true>(scalars, n, mont, t->stride, sc, st);
+    return;
+  }
   switch (c) {
-#define NZ_CASE(K) case K: launch_keys<K>(scalars, n, mont, sc, st); break;
+#define NZ_CASE(K) case K: launch_keys<K, false>(scalars, n, mont, 0, sc, st); break;
     NZ_CASE(4) NZ_CASE(5) NZ_CASE(6) NZ_CASE(7) NZ_CASE(8) NZ_CASE(9) NZ_CASE(10) NZ_CASE(11) NZ_CASE(12)
     NZ_CASE(13) NZ_CASE(14) NZ_CASE(15) NZ_CASE(16)
 #undef NZ_CASE
@@ -339,74 +440,93 @@ G1Affine xyzz_to_affine(const G1xyzz& p) {
   return r;
 }
 
-void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, bool mont, hipStream_t st) {
+void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, bool mont, hipStream_t st,
+                 const MsmBaseTable* table) {
   sc.cur_n = n;
   if (n == 0) return;
   if (n > sc.max_points) throw Error(NZCB_ERR_ARG, "msm larger than scratch");
-  int c, nw, seglen, nseg, nbits;
-  uint32_t nb;
-  msm_shape(n, c, nw, nb, seglen, nseg, nbits);
-  const uint32_t nkeys = nb * (uint32_t)nw;
-  sc.cur_c = c;
-  sc.cur_nw = nw;
-  sc.cur_nbits = nbits;
-  sc.cur_seglen = seglen;
-  sc.cur_nkeys = nkeys;
-  const size_t entries = n * (size_t)nw;
-  keys_dispatch(c, scalars, n, mont ? 1 : 0, sc, st);
+  if (table && n > table->n) throw Error(NZCB_ERR_ARG, "msm larger than its base table");
+  const MsmPlan p = make_plan(n, table);
+  if (p.entries > sc.sorted.n || p.nkeys + 1 > sc.offsets.n)
+    throw Error(NZCB_ERR_ARG, "msm scratch was not sized for this schedule");
+  const G1Affine* gather = table ? table->q.p : bases;
+  sc.cur_c = p.c;
+  sc.cur_nsets = p.nsets;
+  sc.cur_nbits = p.nbits;
+  sc.cur_seglen = p.seglen;
+  sc.cur_nkeys = p.nkeys;
+  const bool phases = sc.prof && sc.prof_phases;
+  if (sc.prof && !sc.ev[0])
+    for (auto& e : sc.ev) NZ_HIP(hipEventCreate(&e));
+  auto mark = [&](int i) {
+    if (phases) NZ_HIP(hipEventRecord(sc.ev[i], st));
+  };
+  mark(0);
+  keys_dispatch(p.c, scalars, n, mont ? 1 : 0, table, sc, st);
+  mark(1);
   int end_bit = 1;
-  while ((1u << end_bit) <= nkeys) end_bit++;
+  while ((1u << end_bit) <= p.nkeys) end_bit++;
   size_t tmp = sc.sort_tmp_bytes;
   NZ_HIP(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp.p, tmp, sc.keys_in.p, sc.keys_out.p, sc.vals_in.p,
-                                            sc.sorted.p, entries, 0, end_bit, st));
-  hipLaunchKernelGGL(msm_offsets_kernel, dim3(grid_for((size_t)nkeys + 1, kMsmThreads, 1u << 30)), dim3(kMsmThreads),
-                     0, st, sc.keys_out.p, entries, nkeys, sc.offsets.p);
+                                            sc.sorted.p, p.entries, 0, end_bit, st));
+  mark(2);
+  hipLaunchKernelGGL(msm_offsets_kernel, dim3(grid_for((size_t)p.nkeys + 1, kMsmThreads, 1u << 30)),
+                     dim3(kMsmThreads), 0, st, sc.keys_out.p, p.entries, p.nkeys, sc.offsets.p);
   NZ_HIP(hipGetLastError());
-  const size_t nthreads = (entries + kChunk - 1) / kChunk;
-  if (sc.prof) {
-    if (!sc.ev0) {
-      NZ_HIP(hipEventCreate(&sc.ev0));
-      NZ_HIP(hipEventCreate(&sc.ev1));
-    }
-    NZ_HIP(hipEventRecord(sc.ev0, st));
-  }
+  const size_t nthreads = (p.entries + kChunk - 1) / kChunk;
+  if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[3], st));
   hipLaunchKernelGGL(msm_accumulate_kernel, dim3(grid_for(nthreads, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0,
-                     st, bases, sc.sorted.p, sc.offsets.p, nkeys, nthreads, sc.buckets.p, sc.carry_own.p,
+                     st, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads, sc.buckets.p, sc.carry_own.p,
                      sc.carry_cont.p);
   NZ_HIP(hipGetLastError());
-  if (sc.prof) NZ_HIP(hipEventRecord(sc.ev1, st));
-  hipLaunchKernelGGL(msm_bucket_finalize_kernel, dim3(grid_for(nkeys, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0,
-                     st, sc.offsets.p, nkeys, sc.carry_own.p, sc.carry_cont.p, sc.buckets.p);
+  if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[4], st));
+  hipLaunchKernelGGL(msm_bucket_finalize_kernel, dim3(grid_for(p.nkeys, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0,
+                     st, sc.offsets.p, p.nkeys, sc.carry_own.p, sc.carry_cont.p, sc.buckets.p);
   NZ_HIP(hipGetLastError());
-  hipLaunchKernelGGL(msm_bucket_reduce_kernel, dim3(grid_for((size_t)nw * nseg, kMsmThreads, 1u << 30)),
-                     dim3(kMsmThreads), 0, st, sc.buckets.p, sc.offsets.p, (int)nb, seglen, nseg, nw, sc.seg_tot.p,
-                     sc.seg_run.p);
+  mark(5);
+  hipLaunchKernelGGL(msm_bucket_reduce_kernel, dim3(grid_for((size_t)p.nsets * p.nseg, kMsmThreads, 1u << 30)),
+                     dim3(kMsmThreads), 0, st, sc.buckets.p, sc.offsets.p, (int)p.nb, p.seglen, p.nseg, p.nsets,
+                     sc.seg_tot.p, sc.seg_run.p);
   NZ_HIP(hipGetLastError());
-  const int nslots = nbits + 1;
-  hipLaunchKernelGGL(msm_window_sums_kernel, dim3(nw * nslots), dim3(kMsmThreads), 0, st, sc.seg_tot.p, sc.seg_run.p,
-                     nseg, nslots, sc.win.p);
+  mark(6);
+  hipLaunchKernelGGL(msm_sums_kernel, dim3(p.nsets * p.nslots * p.nparts), dim3(kSumThreads), 0, st, sc.seg_tot.p,
+                     sc.seg_run.p, p.nseg, p.nslots, p.nparts, sc.parts.p);
   NZ_HIP(hipGetLastError());
-  NZ_HIP(hipMemcpyAsync(sc.host_win, sc.win.p, (size_t)nw * nslots * sizeof(G1xyzz), hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(msm_parts_kernel, dim3(p.nsets * p.nslots), dim3(kPartThreads), 0, st, sc.parts.p, p.nparts,
+                     sc.win.p);
+  NZ_HIP(hipGetLastError());
+  mark(7);
+  NZ_HIP(hipMemcpyAsync(sc.host_win, sc.win.p, (size_t)p.nsets * p.nslots * sizeof(G1xyzz), hipMemcpyDeviceToHost,
+                        st));
 }
 
 G1xyzz msm_finish(MsmScratch& sc, hipStream_t st) {
   if (sc.cur_n == 0) return G1xyzz::inf();
   NZ_HIP(hipStreamSynchronize(st));
-  const int c = sc.cur_c, nw = sc.cur_nw, nslots = sc.cur_nbits + 1;
+  const int c = sc.cur_c, nsets = sc.cur_nsets, nslots = sc.cur_nbits + 1;
   if (sc.prof) {
     float t = 0;
-    NZ_HIP(hipEventElapsedTime(&t, sc.ev0, sc.ev1));
+    NZ_HIP(hipEventElapsedTime(&t, sc.ev[3], sc.ev[4]));
     uint32_t total = 0;
-    NZ_HIP(hipMemcpy(&total, sc.offsets.p + sc.cur_nkeys, 4, hipMemcpyDeviceToHost));
+    NZ_HIP(hipMemcpyAsync(&total, sc.offsets.p + sc.cur_nkeys, 4, hipMemcpyDeviceToHost, st));
+    NZ_HIP(hipStreamSynchronize(st));
     sc.prof_ms += t;
     sc.prof_launches++;
     sc.prof_points += sc.cur_n;
     sc.prof_entries += total;
+    if (sc.prof_phases) {
+      // keys, sort, offsets, accumulate, finalize, reduce, sums
+      for (int i = 0; i < 7; i++) {
+        float ms = 0;
+        NZ_HIP(hipEventElapsedTime(&ms, sc.ev[i], sc.ev[i + 1]));
+        sc.phase_ms[i] += ms;
+      }
+    }
   }
   int lg_seg = 0;
   while ((1 << lg_seg) < sc.cur_seglen) lg_seg++;
   G1xyzz res = G1xyzz::inf();
-  for (int w = nw - 1; w >= 0; w--) {
+  for (int w = nsets - 1; w >= 0; w--) {
     const G1xyzz* s = sc.host_win + (size_t)w * nslots;
     // sum_g g * run_g = sum_b 2^b R_b  (Horner over the bits), times the segment length
     G1xyzz acc = G1xyzz::inf();
@@ -416,7 +536,8 @@ G1xyzz msm_finish(MsmScratch& sc, hipStream_t st) {
     }
     for (int i = 0; i < lg_seg; i++) acc = xyzz_dbl(acc);
     const G1xyzz W = xyzz_add(acc, s[0]);
-    for (int i = 0; i < c; i++) res = xyzz_dbl(res);
+    if (nsets > 1)
+      for (int i = 0; i < c; i++) res = xyzz_dbl(res);
     res = xyzz_add(res, W);
   }
   return res;

@@ -34,6 +34,7 @@ struct Prover {
   ~Prover();
   // resident zkey data (LEM, as in the file)
   DevBuf<G1Affine> ptau;
+  MsmBaseTable ptab;  // shifted PTau bases for the fixed-base MSM schedule
   DevBuf<Fr> qm, ql, qr, qo, qc;  // [n coefs | 4n evals]
   DevBuf<Fr> sigma;               // 3 x [n | 4n]
   DevBuf<Fr> lagrange;            // nLagrange x [n | 4n]
@@ -61,6 +62,7 @@ struct Prover {
   double tm[9] = {0};
 
   Prover(const uint8_t* zkey, size_t len, int device);
+  Prover(const Prover& primary, int lane);  // extra lane sharing primary's proving key
   // witness: nWit x 32-byte LE normal-form values; blinding: 11 x 32-byte LE or null
   // witness_on_device: `witness` is a device pointer (HBM-resident input, no PCIe copy)
   void prove(const uint8_t* witness, size_t n_witness, const uint8_t* blinding, uint8_t* proof_out,
@@ -68,6 +70,8 @@ struct Prover {
 
  private:
   hipStream_t st() const { return eng->stream; }
+  void init_slots();
+  void alloc_workspace();
   void to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb);
   void commit_start(int slot, const Fr* coefs, size_t len);
   G1Affine commit_finish(int slot);

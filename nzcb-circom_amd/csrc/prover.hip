@@ -447,12 +447,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   wn = fr_root_of_unity(power);
   w2 = fr_root_of_unity(2);
   eng.reset(new Engine(device, power + 2, 0));
-  for (int i = 0; i < kSlots; i++) {
-    msc[i].reset(new MsmScratch());
-    msc[i]->init((size_t)n + 6);
-    NZ_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
-    NZ_HIP(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
-  }
+  init_slots();
   hipStream_t s = st();
   auto up = [&](auto& buf, const Section& sec) {
     using T = typename std::remove_reference<decltype(*buf.p)>::type;
@@ -460,6 +455,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     if (sec.len) NZ_HIP(hipMemcpyAsync(buf.p, sec.p, sec.len, hipMemcpyHostToDevice, s));
   };
   up(ptau, z.ptau);
+  ptab.build(ptau.p, ptau.n, kFixedBaseWindow, s);
   up(qm, z.qm);
   up(ql, z.ql);
   up(qr, z.qr);
@@ -536,13 +532,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
       p = p * w4n;
     }
   }
-  // working set
-  wit.alloc(nVars ? nVars : 1);
-  wtns_in.alloc(nWit ? nWit : 1);
-  A.alloc(n); B.alloc(n); C.alloc(n); Z.alloc(n);
-  pol_a.alloc(n + 2); pol_b.alloc(n + 2); pol_c.alloc(n + 2); pol_z.alloc(n + 3);
-  A4.alloc(n4); B4.alloc(n4); C4.alloc(n4); Z4.alloc(n4);
-  T.alloc(n4); Tz.alloc(n4); t.alloc(n4); pad4.alloc(n4);
+  alloc_workspace();
   // coset evaluations of the fixed polynomials from the zkey coefficients (once per context)
   {
     const uint32_t nl = nPublic > 0 ? nPublic : 1;
@@ -560,6 +550,26 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     for (uint32_t j = 0; j < nl; j++) coset_eval(lagrange.p + (size_t)j * 5 * n, cl.p + (size_t)j * n4);
     NZ_HIP(hipGetLastError());
   }
+  NZ_HIP(hipStreamSynchronize(s));
+}
+
+void Prover::init_slots() {
+  for (int i = 0; i < kSlots; i++) {
+    msc[i].reset(new MsmScratch());
+    msc[i]->init((size_t)n + 6, true);
+    NZ_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
+    NZ_HIP(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
+  }
+}
+
+// per-proof working set (one per lane)
+void Prover::alloc_workspace() {
+  wit.alloc(nVars ? nVars : 1);
+  wtns_in.alloc(nWit ? nWit : 1);
+  A.alloc(n); B.alloc(n); C.alloc(n); Z.alloc(n);
+  pol_a.alloc(n + 2); pol_b.alloc(n + 2); pol_c.alloc(n + 2); pol_z.alloc(n + 3);
+  A4.alloc(n4); B4.alloc(n4); C4.alloc(n4); Z4.alloc(n4);
+  T.alloc(n4); Tz.alloc(n4); t.alloc(n4); pad4.alloc(n4);
   pol_r.alloc(n + 3); pol_wxi.alloc(n + 6); pol_wxiw.alloc(n + 3);
   blind.alloc(12);
   size_t lv = 0, m = n4;
@@ -569,7 +579,31 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   eval_part.alloc(nblocks);
   host_part.resize(nblocks);
   flags.alloc(1);
-  NZ_HIP(hipStreamSynchronize(s));
+}
+
+// An extra proof lane on the primary's device: shares the HBM-resident proving key
+// (zkey sections, shifted PTau table, coset evaluations, root tables) read-only and
+// owns its streams, MSM scratch and per-proof working set.
+Prover::Prover(const Prover& pk, int) {
+  n = pk.n; n4 = pk.n4; nVars = pk.nVars; nPublic = pk.nPublic; nAdditions = pk.nAdditions;
+  nConstraints = pk.nConstraints; nWit = pk.nWit; power = pk.power;
+  k1 = pk.k1; k2 = pk.k2; wn = pk.wn; w2 = pk.w2;
+  add_level_start = pk.add_level_start;
+  transcript_public = pk.transcript_public;
+  for (int k = 0; k < 4; k++) zh_inv[k] = pk.zh_inv[k];
+  NZ_HIP(hipSetDevice(pk.eng->device));
+  eng.reset(new Engine(pk.eng->device, power + 2, 0));
+  init_slots();
+  ptau.alias(pk.ptau);
+  ptab.q.alias(pk.ptab.q);
+  ptab.n = pk.ptab.n; ptab.stride = pk.ptab.stride; ptab.c = pk.ptab.c; ptab.nw = pk.ptab.nw;
+  qm.alias(pk.qm); ql.alias(pk.ql); qr.alias(pk.qr); qo.alias(pk.qo); qc.alias(pk.qc);
+  sigma.alias(pk.sigma); lagrange.alias(pk.lagrange);
+  amap.alias(pk.amap); bmap.alias(pk.bmap); cmap.alias(pk.cmap); adds.alias(pk.adds);
+  root_lo.alias(pk.root_lo); root_hi.alias(pk.root_hi); x_lo.alias(pk.x_lo);
+  g_lo.alias(pk.g_lo); g_hi.alias(pk.g_hi); gi_lo.alias(pk.gi_lo); gi_hi.alias(pk.gi_hi);
+  cq.alias(pk.cq); cs.alias(pk.cs); cl.alias(pk.cl);
+  alloc_workspace();
 }
 
 // ----------------------------------------------------------------------------
@@ -597,7 +631,7 @@ void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int n
 void Prover::commit_start(int slot, const Fr* coefs, size_t len) {
   NZ_HIP(hipEventRecord(ready[slot], st()));
   NZ_HIP(hipStreamWaitEvent(aux[slot], ready[slot], 0));
-  msm_enqueue(*msc[slot], ptau.p, coefs, len, true, aux[slot]);
+  msm_enqueue(*msc[slot], ptau.p, coefs, len, true, aux[slot], &ptab);
 }
 
 G1Affine Prover::commit_finish(int slot) {

@@ -35,7 +35,8 @@ EXPORTED_SYMBOLS = [
     "nzcb_engine_create", "nzcb_engine_destroy", "nzcb_engine_ntt", "nzcb_engine_msm", "nzcb_dev_alloc",
     "nzcb_dev_free", "nzcb_memcpy_h2d", "nzcb_memcpy_d2h", "nzcb_engine_ntt_dev", "nzcb_engine_msm_dev",
     "nzcb_engine_time_ntt", "nzcb_engine_fr_mul", "nzcb_engine_random_fr", "nzcb_engine_fixed_base",
-    "nzcb_engine_time_msm",
+    "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
+    "nzcb_ctx_lanes", "nzcb_prove_batch",
 ]
 
 
@@ -74,6 +75,10 @@ def load(path: str | None = None):
         "nzcb_prove_witness": (c_int, [c_void_p, u8p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
         "nzcb_prove_device": (c_int, [c_void_p, c_void_p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
         "nzcb_ctx_kernel_stats": (c_int, [c_void_p, c_int, POINTER(c_double)]),
+        "nzcb_ctx_set_lanes": (c_int, [c_void_p, c_int, POINTER(_Err)]),
+        "nzcb_ctx_lanes": (c_int, [c_void_p]),
+        "nzcb_prove_batch": (c_int, [c_void_p, POINTER(c_void_p), c_size_t, c_int, c_int, u8p, u8p, u8p, c_size_t,
+                                     POINTER(_Err)]),
         "nzcb_ctx_last_timings": (c_int, [c_void_p, POINTER(c_double), c_int]),
         "nzcb_proof_to_json": (c_int, [u8p, ctypes.c_char_p, c_size_t]),
         "nzcb_public_to_json": (c_int, [u8p, c_int, ctypes.c_char_p, c_size_t]),
@@ -98,6 +103,10 @@ def load(path: str | None = None):
         "nzcb_engine_fixed_base": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, POINTER(_Err)]),
         "nzcb_engine_time_msm": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, POINTER(c_double),
                                          POINTER(c_double), POINTER(_Err)]),
+        "nzcb_engine_msm_fixed_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_int, u8p,
+                                              POINTER(_Err)]),
+        "nzcb_engine_time_msm2": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_int,
+                                          POINTER(c_double), POINTER(_Err)]),
     }
     lib.missing_symbols = []
     for name, (res, args) in sigs.items():
@@ -197,6 +206,27 @@ class Engine:
         _check(self.lib.nzcb_engine_time_msm(self.h, dev_bases, dev_scalars, n, int(scalars_mont), reps,
                                              ctypes.byref(ms), ctypes.byref(acc), ctypes.byref(err)), err)
         return ms.value, acc.value
+
+    MSM_PHASES = ("keys", "sort", "offsets", "accumulate", "finalize", "reduce", "sums")
+
+    def time_msm_phases(self, dev_bases: int, dev_scalars: int, n: int, scalars_mont: bool, fixed_base: bool,
+                        reps: int) -> dict:
+        """Wall ms per MSM and HIP-event ms per phase (generic or fixed-base schedule)."""
+        out = (c_double * 9)()
+        err = _Err()
+        _check(self.lib.nzcb_engine_time_msm2(self.h, dev_bases, dev_scalars, n, int(scalars_mont), int(fixed_base),
+                                              reps, out, ctypes.byref(err)), err)
+        d = {"wall": out[0], "table_build": out[8]}
+        d.update({k: out[1 + i] for i, k in enumerate(self.MSM_PHASES)})
+        return d
+
+    def msm_fixed_dev(self, dev_bases: int, n_table: int, dev_scalars: int, n: int, scalars_mont: bool) -> bytes:
+        """Fixed-base (shifted-table) MSM of the first n of n_table device bases."""
+        out = _out(64)
+        err = _Err()
+        _check(self.lib.nzcb_engine_msm_fixed_dev(self.h, dev_bases, n_table, dev_scalars, n, int(scalars_mont), out,
+                                                  ctypes.byref(err)), err)
+        return bytes(out)
 
     def msm_dev(self, dev_bases: int, dev_scalars: int, n: int, scalars_mont: bool) -> bytes:
         out = _out(64)
@@ -309,6 +339,43 @@ class ProverContext:
         _check(self.lib.nzcb_prove_device(self.h, dev_witness, n_witness, bl, proof, pub, 32 * self.n_public,
                                           ctypes.byref(err)), err)
         return bytes(proof), bytes(pub)[:32 * self.n_public]
+
+    def set_lanes(self, lanes: int):
+        """Proofs kept in flight by prove_batch (extra lanes share the resident proving key)."""
+        err = _Err()
+        _check(self.lib.nzcb_ctx_set_lanes(self.h, lanes, ctypes.byref(err)), err)
+
+    @property
+    def lanes(self) -> int:
+        return self.lib.nzcb_ctx_lanes(self.h)
+
+    def prove_batch_raw(self, witnesses, n_witness: int | None = None, blindings=None, on_device: bool = False):
+        """Independent proofs over the lanes. witnesses: list of bytes (host) or device
+        pointers (on_device). blindings: list of 352-byte values / None. Returns [(proof, pub)]."""
+        count = len(witnesses)
+        keep = []
+        ptrs = (c_void_p * max(count, 1))()
+        for i, w in enumerate(witnesses):
+            if on_device:
+                ptrs[i] = w
+            else:
+                b = _buf(w)
+                keep.append(b)
+                ptrs[i] = ctypes.cast(b, c_void_p).value
+                if n_witness is None:
+                    n_witness = len(w) // 32
+        bl = None
+        if blindings is not None:
+            bl = _buf(b"".join(x if x is not None else bytes(352) for x in blindings))
+        proofs = _out(PROOF_BYTES * count)
+        stride = 32 * max(self.n_public, 1)
+        pubs = _out(stride * count)
+        err = _Err()
+        _check(self.lib.nzcb_prove_batch(self.h, ptrs, n_witness or 0, count, int(on_device), bl, proofs, pubs,
+                                         stride, ctypes.byref(err)), err)
+        P, Q = bytes(proofs), bytes(pubs)
+        return [(P[i * PROOF_BYTES:(i + 1) * PROOF_BYTES], Q[i * stride:i * stride + 32 * self.n_public])
+                for i in range(count)]
 
     def kernel_stats(self, enable: int = -1):
         """MSM bucket-accumulation kernel timing: (ms, launches, points, entries); enable 1/0 resets."""

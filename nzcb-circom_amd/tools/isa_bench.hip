@@ -13,6 +13,8 @@ __global__ void probe(uint64_t* out, int iters) {
   uint32_t x = threadIdx.x * 3 + 1, y = threadIdx.x * 7 + 5;
   double d0 = x, d1 = y, d2 = x + 1.0, d3 = y + 1.0, d4 = 0.5, d5 = 0.25, d6 = 0.125, d7 = 2.0;
   uint32_t h = 0;
+  uint32_t r0 = x, r1 = x + 1, r2 = x + 2, r3 = x + 3, r4 = x + 4, r5 = x + 5, r6 = x + 6, r7 = x + 7;
+  float f0 = x, f1 = y, f2 = 1.f, f3 = 2.f, f4 = 3.f, f5 = 4.f, f6 = 5.f, f7 = 6.f;
   for (int i = 0; i < iters; i++) {
     if (K == 0) {  // 16 x v_mad_u64_u32 (8 independent accumulators, 2 rounds)
       asm volatile(
@@ -43,6 +45,47 @@ __global__ void probe(uint64_t* out, int iters) {
       asm volatile(REP16("v_mul_lo_u32 %0, %0, %1\n") : "+v"(x) : "v"(y));
     } else if (K == 5) {  // 16 x v_mul_hi_u32
       asm volatile(REP16("v_mul_hi_u32 %0, %0, %1\n") : "+v"(x) : "v"(y));
+    } else if (K == 7) {  // 16 x v_add_u32, 8 independent
+      asm volatile(REP16("v_add_u32 %0, %0, %8\n v_add_u32 %1, %1, %8\n v_add_u32 %2, %2, %8\n v_add_u32 %3, %3, %8\n"
+                         "v_add_u32 %4, %4, %8\n v_add_u32 %5, %5, %8\n v_add_u32 %6, %6, %8\n v_add_u32 %7, %7, %8\n")
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y));
+    } else if (K == 8) {  // v_add_co_u32, 8 independent
+      asm volatile(REP16("v_add_co_u32 %0, vcc, %0, %8\n v_add_co_u32 %1, vcc, %1, %8\n v_add_co_u32 %2, vcc, %2, %8\n"
+                         "v_add_co_u32 %3, vcc, %3, %8\n v_add_co_u32 %4, vcc, %4, %8\n v_add_co_u32 %5, vcc, %5, %8\n"
+                         "v_add_co_u32 %6, vcc, %6, %8\n v_add_co_u32 %7, vcc, %7, %8\n")
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y) : "vcc");
+    } else if (K == 9) {  // v_addc_co_u32 (VOP2, vcc in/out), 8 independent
+      asm volatile(REP16("v_addc_co_u32 %0, vcc, %0, %8, vcc\n v_addc_co_u32 %1, vcc, %1, %8, vcc\n"
+                         "v_addc_co_u32 %2, vcc, %2, %8, vcc\n v_addc_co_u32 %3, vcc, %3, %8, vcc\n"
+                         "v_addc_co_u32 %4, vcc, %4, %8, vcc\n v_addc_co_u32 %5, vcc, %5, %8, vcc\n"
+                         "v_addc_co_u32 %6, vcc, %6, %8, vcc\n v_addc_co_u32 %7, vcc, %7, %8, vcc\n")
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y) : "vcc");
+    } else if (K == 10) {  // v_add3_u32, 8 independent
+      asm volatile(REP16("v_add3_u32 %0, %0, %8, %9\n v_add3_u32 %1, %1, %8, %9\n v_add3_u32 %2, %2, %8, %9\n"
+                         "v_add3_u32 %3, %3, %8, %9\n v_add3_u32 %4, %4, %8, %9\n v_add3_u32 %5, %5, %8, %9\n"
+                         "v_add3_u32 %6, %6, %8, %9\n v_add3_u32 %7, %7, %8, %9\n")
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y), "v"(x));
+    } else if (K == 11) {  // v_mad_u32_u24, 8 independent
+      asm volatile(REP16("v_mad_u32_u24 %0, %0, %8, %9\n v_mad_u32_u24 %1, %1, %8, %9\n v_mad_u32_u24 %2, %2, %8, %9\n"
+                         "v_mad_u32_u24 %3, %3, %8, %9\n v_mad_u32_u24 %4, %4, %8, %9\n v_mad_u32_u24 %5, %5, %8, %9\n"
+                         "v_mad_u32_u24 %6, %6, %8, %9\n v_mad_u32_u24 %7, %7, %8, %9\n")
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y), "v"(x));
+    } else if (K == 12) {  // v_mul_lo_u32, 8 independent
+      asm volatile(REP16("v_mul_lo_u32 %0, %0, %8\n v_mul_lo_u32 %1, %1, %8\n v_mul_lo_u32 %2, %2, %8\n"
+                         "v_mul_lo_u32 %3, %3, %8\n v_mul_lo_u32 %4, %4, %8\n v_mul_lo_u32 %5, %5, %8\n"
+                         "v_mul_lo_u32 %6, %6, %8\n v_mul_lo_u32 %7, %7, %8\n")
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y));
+    } else if (K == 13) {  // v_fma_f32, 8 independent (reference: 2 cycles per wave64)
+      asm volatile(REP16("v_fma_f32 %0, %0, %8, %9\n v_fma_f32 %1, %1, %8, %9\n v_fma_f32 %2, %2, %8, %9\n"
+                         "v_fma_f32 %3, %3, %8, %9\n v_fma_f32 %4, %4, %8, %9\n v_fma_f32 %5, %5, %8, %9\n"
+                         "v_fma_f32 %6, %6, %8, %9\n v_fma_f32 %7, %7, %8, %9\n")
+                   : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5), "+v"(f6), "+v"(f7)
+                   : "v"(0.999f), "v"(0.001f));
+    } else if (K == 14) {  // v_mad_u64_u32 + v_addc_co_u32 pairs, 4 independent column chains
+      asm volatile(REP16("v_mad_u64_u32 %0, s[20:21], %8, %9, %0\n v_mad_u64_u32 %1, s[22:23], %8, %9, %1\n"
+                         "v_addc_co_u32_e64 %4, s[20:21], %4, 0, s[20:21]\n v_addc_co_u32_e64 %5, s[22:23], %5, 0, s[22:23]\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(x), "v"(y)
+                   : "s20", "s21", "s22", "s23");
     } else if (K == 6) {  // 8 x (mad; s_nop 1; addc) as in field.h mac
       asm volatile(
           "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
@@ -59,7 +102,9 @@ __global__ void probe(uint64_t* out, int iters) {
     }
   }
   out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7 ^ x ^ h ^
-                                               (uint64_t)(d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7);
+                                               (uint64_t)(d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7) ^
+                                               (r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7) ^
+                                               (uint64_t)(f0 + f1 + f2 + f3 + f4 + f5 + f6 + f7);
 }
 
 template <int K>
@@ -82,14 +127,24 @@ int main() {
   const int blocks = 256 * 8, threads = 256, iters = 4000;
   uint64_t* d;
   (void)hipMalloc(&d, (size_t)blocks * threads * 8);
-  const char* names[7] = {"v_mad_u64_u32", "v_add_co_u32", "s_nop 1", "v_fma_f64", "v_mul_lo_u32", "v_mul_hi_u32",
-                          "mac(mad;nop;addc)"};
-  double ms[7] = {run<0>(d, blocks, threads, iters), run<1>(d, blocks, threads, iters), run<2>(d, blocks, threads, iters),
-                  run<3>(d, blocks, threads, iters), run<4>(d, blocks, threads, iters), run<5>(d, blocks, threads, iters),
-                  run<6>(d, blocks, threads, iters)};
+  const int NK = 15;
+  const char* names[NK] = {"v_mad_u64_u32 x8", "v_add_co_u32 chain", "s_nop 1", "v_fma_f64 x8", "v_mul_lo_u32 chain",
+                           "v_mul_hi_u32 chain", "mac(mad;nop;addc)", "v_add_u32 x8", "v_add_co_u32 x8",
+                           "v_addc_co_u32 x8", "v_add3_u32 x8", "v_mad_u32_u24 x8", "v_mul_lo_u32 x8",
+                           "v_fma_f32 x8", "mad,mad,addc,addc x2"};
+  double ms[NK] = {run<0>(d, blocks, threads, iters), run<1>(d, blocks, threads, iters), run<2>(d, blocks, threads, iters),
+                   run<3>(d, blocks, threads, iters), run<4>(d, blocks, threads, iters), run<5>(d, blocks, threads, iters),
+                   run<6>(d, blocks, threads, iters), run<7>(d, blocks, threads, iters / 8),
+                   run<8>(d, blocks, threads, iters / 8), run<9>(d, blocks, threads, iters / 8),
+                   run<10>(d, blocks, threads, iters / 8), run<11>(d, blocks, threads, iters / 8),
+                   run<12>(d, blocks, threads, iters / 8), run<13>(d, blocks, threads, iters / 8),
+                   run<14>(d, blocks, threads, iters / 4)};
   const double waves = (double)blocks * threads / 64;
-  for (int k = 0; k < 7; k++) {
-    double n_instr = waves * iters * (k == 6 ? 8 : 16);  // wave-instructions (mac = one mad+nop+addc group)
+  for (int k = 0; k < NK; k++) {
+    // wave-instructions per iteration (mac = one mad+nop+addc group)
+    double per = k == 6 ? 8 : (k >= 7 && k <= 13) ? 128 : k == 14 ? 64 : 16;
+    int it = k >= 7 && k <= 13 ? iters / 8 : k == 14 ? iters / 4 : iters;
+    double n_instr = waves * it * per;
     double simd_cycles = ms[k] * 1e-3 * 2.4e9 * 1024;    // 256 CUs x 4 SIMDs at 2.4 GHz
     printf("%-20s %8.3f ms  %6.2f SIMD-cycles per wave-instruction\n", names[k], ms[k], simd_cycles / n_instr);
   }

@@ -35,11 +35,14 @@ def main():
             print(json.dumps({"kernel": "intt" if inv else "ntt", "log_n": lg, "ms": round(ms, 4),
                               "elements_per_s": round(n / (ms / 1e3), 1), "GBs": round(gbs, 1),
                               "frac": round(gbs / PEAK, 4)}), flush=True)
-        ms, acc = eng.time_msm(bases, sc, n, True, args.reps)
-        gbs = 96 * n / (ms / 1e3) / 1e9
-        print(json.dumps({"kernel": "msm", "log_n": lg, "ms": round(ms, 4), "accumulate_ms": round(acc, 4),
-                          "points_per_s": round(n / (ms / 1e3), 1), "GBs": round(gbs, 1),
-                          "frac": round(gbs / PEAK, 5)}), flush=True)
+        for fixed in (False, True):
+            ph = eng.time_msm_phases(bases, sc, n, True, fixed, args.reps)
+            ms = ph["wall"]
+            gbs = 96 * n / (ms / 1e3) / 1e9
+            print(json.dumps({"kernel": "msm_fixed_base" if fixed else "msm", "log_n": lg, "ms": round(ms, 4),
+                              "phases_ms": {k: round(v, 4) for k, v in ph.items() if k != "wall"},
+                              "points_per_s": round(n / (ms / 1e3), 1), "GBs": round(gbs, 1),
+                              "frac": round(gbs / PEAK, 5)}), flush=True)
     for p in (sc, out, bases):
         nzcb.dev_free(p)
 

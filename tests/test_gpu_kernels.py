@@ -95,3 +95,54 @@ def test_msm_duplicate_and_negated_points(engine):
     bases = b"".join(bn.g1_to_lem(p) for p in pts)
     got = _affine(engine.msm(bases, b"".join(bn.to_le(s) for s in sc), False))
     assert got == want
+
+
+def _msm_fixed(engine, pts, sc, n_table=None, mont=False):
+    """Fixed-base schedule (shifted-base table, one 2^19-bucket set) via device buffers."""
+    import nzcb
+    n = len(sc)
+    n_table = n_table or n
+    bases = b"".join(bn.g1_to_lem(p) for p in pts[:n_table])
+    scal = _lem(sc, R_MOD) if mont else b"".join(bn.to_le(s) for s in sc)
+    db, ds = nzcb.dev_alloc(len(bases)), nzcb.dev_alloc(max(len(scal), 32))
+    try:
+        nzcb.h2d(db, bases)
+        if scal:
+            nzcb.h2d(ds, scal)
+        return _affine(engine.msm_fixed_dev(db, n_table, ds, n, mont))
+    finally:
+        nzcb.dev_free(db)
+        nzcb.dev_free(ds)
+
+
+@pytest.mark.parametrize("n,kind", [(1, "rand"), (100, "rand"), (2000, "rand"), (300, "zeros"), (300, "ones"),
+                                    (300, "equal"), (300, "rminus1"), (300, "mixed"), (300, "top")])
+def test_msm_fixed_base(engine, n, kind):
+    rng = random.Random(1000 + n + len(kind))
+    pts = _bases(n + 5, n + 1)
+    if kind == "rand":
+        sc = [rng.randrange(R_MOD) for _ in range(n)]
+    elif kind == "zeros":
+        sc = [0] * n
+    elif kind == "ones":
+        sc = [1] * n
+    elif kind == "equal":
+        sc = [rng.randrange(R_MOD)] * n
+    elif kind == "rminus1":
+        sc = [R_MOD - 1] * n
+    elif kind == "top":  # digits at the top window edge: 2^240.., 2^253, half-window carries
+        sc = [rng.choice([1 << 253, (1 << 240) - 1, (1 << 239) * 3, (1 << 19) * 5, R_MOD - (1 << 19)])
+              for _ in range(n)]
+    else:
+        sc = [rng.choice([0, 1, R_MOD - 1, rng.randrange(R_MOD)]) for _ in range(n)]
+    want = bn.msm(pts[:n], sc)
+    # table built over more bases than the MSM uses (as the prover's n+6 PTau table)
+    assert _msm_fixed(engine, pts, sc, n_table=n + 5) == want
+    assert _msm_fixed(engine, pts, sc, n_table=n + 5, mont=True) == want
+
+
+def test_msm_fixed_base_infinity_bases(engine):
+    g = bn.g1_mul(bn.G1_GEN, 777)
+    pts = [g, None, bn.g1_neg(g), g, None, g]
+    sc = [5, 6, 5, 7, 9, R_MOD - 5]
+    assert _msm_fixed(engine, pts, sc) == bn.msm(pts, sc)

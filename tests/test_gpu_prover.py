@@ -155,3 +155,45 @@ def test_plonk_prove_api_random_blinding_verifies(tmp_path):
         p[k] = int(proof[k])
     pub = [int(x) for x in res["publicSignals"]]
     assert plonk.verify_with_trapdoor(zk, pub, p, meta["tau"])
+
+
+def test_batch_lanes_bit_exact():
+    """nzcb_prove_batch over 3 lanes sharing one resident proving key: every proof
+    equals its golden fixture, whatever lane ran it (host and device witnesses)."""
+    meta, zkey, wtns = _gold("p8")
+    w = binfmt.read_wtns(wtns)["witness"]
+    wit = b"".join(x.to_bytes(32, "little") for x in w)
+    ctx = nzcb.ProverContext(zkey)
+    ctx.set_lanes(3)
+    assert ctx.lanes == 3
+    kinds = ["fixed", "zero", "fixed", "fixed", "zero", "zero", "fixed"]
+    bls = [bytes.fromhex(meta["proofs"][k]["blinding"]) if meta["proofs"][k]["blinding"] else None for k in kinds]
+    res = ctx.prove_batch_raw([wit] * len(kinds), blindings=bls)
+    for k, (proof, pub) in zip(kinds, res):
+        assert proof.hex() == meta["proofs"][k]["proof_bin"]
+    dev = nzcb.dev_alloc(len(wit))
+    try:
+        nzcb.h2d(dev, wit)
+        res = ctx.prove_batch_raw([dev] * 4, n_witness=len(w), blindings=bls[:4], on_device=True)
+        for k, (proof, pub) in zip(kinds[:4], res):
+            assert proof.hex() == meta["proofs"][k]["proof_bin"]
+    finally:
+        nzcb.dev_free(dev)
+    # single-proof calls still work after the batch (lane 0)
+    proof, _ = ctx.prove_raw(wtns, bls[0])
+    assert proof.hex() == meta["proofs"]["fixed"]["proof_bin"]
+    ctx.set_lanes(1)
+    assert ctx.lanes == 1
+
+
+def test_batch_reports_lowest_failing_index():
+    meta, zkey, wtns = _gold("p8")
+    w = binfmt.read_wtns(wtns)["witness"]
+    good = b"".join(x.to_bytes(32, "little") for x in w)
+    w[20] = w[20] + 1
+    bad = b"".join(x.to_bytes(32, "little") for x in w)
+    ctx = nzcb.ProverContext(zkey)
+    ctx.set_lanes(2)
+    with pytest.raises(nzcb.NzcbError) as ei:
+        ctx.prove_batch_raw([good, good, bad, good, bad])
+    assert str(ei.value) == "proof 2: T Polynomial is not divisible"
