@@ -18,7 +18,8 @@
 //  1. keys:       thread per scalar -> signed c-bit digits; (scalar, window) pair i
 //                 gets the fixed slot w*n+i; zero digits get a sentinel key that
 //                 sorts last -- no atomics
-//  2. sort:       rocPRIM radix sort of (key, base index|sign) on ceil(log2 keys) bits
+//  2. sort:       rocPRIM onesweep radix sort of (key, base index|sign) on the 20 key
+//                 bits, 10 bits per pass (2 passes instead of the default 8-bit 3)
 //  3. offsets:    bucket start positions by binary search in the sorted keys
 //  4. accumulate: thread per fixed 32-entry chunk of the sorted stream (load balance
 //                 independent of the digit distribution): XYZZ mixed adds of the
@@ -33,11 +34,43 @@
 // Generic bases are read straight from the zkey PTau layout (64 B LEM affine).
 #include "msm.h"
 
-#include <hipcub/hipcub.hpp>
+#include <cstdlib>
+#include <rocprim/rocprim.hpp>
 
 namespace nzcb {
 
 static constexpr int kMsmThreads = 256;
+
+// Onesweep with 10-bit digits: the 20-bit bucket keys take 2 passes over the
+// (key, value) pairs instead of 3 with the library's 8-bit default for gfx950.
+template <unsigned Bits>
+using SortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, Bits,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
+static int sort_bits() {
+  static int bits = [] {
+    const char* e = std::getenv("NZCB_SORT_BITS");
+    int b = e ? std::atoi(e) : 10;
+    return (b == 8 || b == 10 || b == 11) ? b : 10;
+  }();
+  return bits;
+}
+
+static void radix_sort(void* tmp, size_t& tmp_bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                       uint32_t* vout, size_t m, int end_bit, hipStream_t st) {
+  switch (sort_bits()) {
+    case 8:
+      NZ_HIP(rocprim::radix_sort_pairs<SortConfig<8>>(tmp, tmp_bytes, kin, kout, vin, vout, m, 0, end_bit, st));
+      break;
+    case 11:
+      NZ_HIP(rocprim::radix_sort_pairs<SortConfig<11>>(tmp, tmp_bytes, kin, kout, vin, vout, m, 0, end_bit, st));
+      break;
+    default:
+      NZ_HIP(rocprim::radix_sort_pairs<SortConfig<10>>(tmp, tmp_bytes, kin, kout, vin, vout, m, 0, end_bit, st));
+  }
+}
 static constexpr uint32_t kChunk = 32;
 static constexpr int kSegLen = 8;
 static constexpr int kSumThreads = 256;  // level-1 sums: block size
@@ -384,8 +417,7 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
   keys_out.alloc(max_entries);
   vals_in.alloc(max_entries);
   sort_tmp_bytes = 0;
-  NZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp_bytes, keys_in.p, keys_out.p, vals_in.p, sorted.p,
-                                            max_entries, 0, 21));
+  radix_sort(nullptr, sort_tmp_bytes, keys_in.p, keys_out.p, vals_in.p, sorted.p, max_entries, 21, nullptr);
   sort_tmp.alloc(sort_tmp_bytes + 16);
   buckets.alloc(max_keys);
   size_t nthreads = (max_entries + kChunk - 1) / kChunk + 1;
@@ -467,8 +499,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   int end_bit = 1;
   while ((1u << end_bit) <= p.nkeys) end_bit++;
   size_t tmp = sc.sort_tmp_bytes;
-  NZ_HIP(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp.p, tmp, sc.keys_in.p, sc.keys_out.p, sc.vals_in.p,
-                                            sc.sorted.p, p.entries, 0, end_bit, st));
+  radix_sort(sc.sort_tmp.p, tmp, sc.keys_in.p, sc.keys_out.p, sc.vals_in.p, sc.sorted.p, p.entries, end_bit, st);
   mark(2);
   hipLaunchKernelGGL(msm_offsets_kernel, dim3(grid_for((size_t)p.nkeys + 1, kMsmThreads, 1u << 30)),
                      dim3(kMsmThreads), 0, st, sc.keys_out.p, p.entries, p.nkeys, sc.offsets.p);
