@@ -1,0 +1,37 @@
+#!/usr/bin/env node
+'use strict';
+// `snarkjs plonk prove|fullprove` equivalent on the MI355X prover (SURVEY.md §8b):
+//   node cli.js plonk prove     <circuit.zkey> <witness.wtns> <proof.json> <public.json>
+//   node cli.js plonk fullprove <input.json> <circuit.wasm> <circuit.zkey> <proof.json> <public.json>
+// Output JSON is written like snarkjs's CLI (stringifyBigInts, 1-space indent).
+const fs = require('fs');
+const nz = require('./index.js');
+
+function usage() {
+  console.error('usage: cli.js plonk prove <zkey> <wtns> <proof.json> <public.json>\n' +
+                '       cli.js plonk fullprove <input.json> <wasm> <zkey> <proof.json> <public.json>');
+  process.exit(1);
+}
+
+async function main(argv) {
+  if (argv[0] !== 'plonk') usage();
+  const logger = process.env.NZCB_VERBOSE ? { debug: (m) => console.error(m) } : null;
+  let res, out;
+  if (argv[1] === 'prove' && argv.length === 6) {
+    res = await nz.plonk.prove(argv[2], argv[3], logger);
+    out = argv.slice(4);
+  } else if (argv[1] === 'fullprove' && argv.length === 7) {
+    const input = JSON.parse(fs.readFileSync(argv[2], 'utf8'));
+    res = await nz.plonk.fullProve(input, argv[3], argv[4], logger);
+    out = argv.slice(5);
+  } else {
+    usage();
+  }
+  fs.writeFileSync(out[0], JSON.stringify(res.proof, null, 1), 'utf-8');
+  fs.writeFileSync(out[1], JSON.stringify(res.publicSignals, null, 1), 'utf-8');
+}
+
+main(process.argv.slice(2)).then(() => process.exit(0), (e) => {
+  console.error(e && e.message ? e.message : e);
+  process.exit(1);
+});

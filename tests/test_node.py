@@ -70,3 +70,24 @@ const fs = require('fs');
 """
     d = json.loads(run_node(script))
     assert d["msg"] == "T Polynomial is not divisible" and d["code"] == 7
+
+
+@needs_node
+@pytest.mark.gpu
+def test_cli_plonk_prove_verifies(tmp_path):
+    """`node cli.js plonk prove` (the `snarkjs plonk prove` CLI shape): random blinding,
+    proof accepted by the oracle's trapdoor verifier."""
+    from oracle import binfmt, plonk
+    meta = json.load(open(os.path.join(GOLD, "p8.json")))
+    pf, pb = tmp_path / "proof.json", tmp_path / "public.json"
+    p = subprocess.run(["node", os.path.join(JS, "cli.js"), "plonk", "prove", os.path.join(GOLD, "p8.zkey"),
+                        os.path.join(GOLD, "p8.wtns"), str(pf), str(pb)], capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr
+    proof = json.loads(pf.read_text())
+    pub = [int(x) for x in json.loads(pb.read_text())]
+    assert [str(x) for x in pub] == meta["proofs"]["fixed"]["publicSignals"]
+    pt = {k: (None if proof[k][2] == "0" else (int(proof[k][0]), int(proof[k][1]))) for k in plonk.PROOF_POINTS}
+    pt.update({k: int(proof[k]) for k in plonk.PROOF_EVALS})
+    zk = binfmt.read_zkey(open(os.path.join(GOLD, "p8.zkey"), "rb").read())
+    assert plonk.verify_with_trapdoor(zk, pub, pt, meta["tau"])
