@@ -241,7 +241,7 @@ int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table,
   NZ_HIP(hipSetDevice(g.device));
   if (n > n_table) throw Error(NZCB_ERR_ARG, "msm larger than its base table");
   MsmBaseTable t;
-  t.build((const G1Affine*)bases, n_table, kFixedBaseWindow, g.stream);
+  t.build((const G1Affine*)bases, n_table, fixed_base_window(), g.stream);
   MsmScratch sc;
   sc.init(n ? n : 1, true);
   G1xyzz r = msm(sc, (const G1Affine*)bases, (const Fr*)scalars, n, scalars_mont != 0, g.stream, &t);
@@ -262,7 +262,7 @@ int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars
   if (fixed_base) {
     auto t0 = std::chrono::steady_clock::now();
     t.reset(new MsmBaseTable());
-    t->build((const G1Affine*)bases, n, kFixedBaseWindow, g.stream);
+    t->build((const G1Affine*)bases, n, fixed_base_window(), g.stream);
     NZ_HIP(hipStreamSynchronize(g.stream));
     table_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     own.reset(new MsmScratch());

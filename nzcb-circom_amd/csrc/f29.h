@@ -1,0 +1,197 @@
+// BN254 Fq in a redundant radix 2^29 (9 limbs, Montgomery R = 2^261) for the MSM
+// bucket accumulation.
+//
+// Why: on gfx950 v_mad_u64_u32 and v_addc_co_u32 both issue at 4 cycles per wave64
+// instruction (profiles/r1_isa_bench.txt). With 32-bit limbs every partial product
+// needs mad + addc. With 29-bit limbs a partial product is < 2^58 (< 2^60 with one
+// bit of limb slack), so a whole column (<= 18 products plus the carry) stays below
+// 2^64 in one accumulator. That is one v_mad_u64_u32 per partial product, no carry
+// instruction and no final subtraction. tools/mul29bench.hip measures 133.6 G
+// products/s against 103.2 for csrc/field.h.
+//
+// Value invariants (x < 2^257 for every product input, 10p = 0.945 * 2^257):
+//   mul29(a, b): a, b < 2^257 with limbs < 2^30  ->  result < 2p, limbs < 2^29
+//   sub29<K>(a, b) = a + K - b with K = k*p in "borrowed" limbs (every limb >= 2^29 - 1,
+//   so no limb goes negative), b < K, a and b normalized; result normalized
+// Only add/sub/mul are needed by the XYZZ mixed addition (msm.hip).
+#pragma once
+#include "field.h"
+
+namespace nzcb {
+
+struct F29 {
+  uint32_t v[9];
+};
+
+struct Fq29 {
+  static constexpr uint32_t MASK = (1u << 29) - 1;
+  static constexpr uint32_t INV = 0x04866389u;  // -p^-1 mod 2^29
+  static constexpr uint32_t P[9] = {0x187cfd47u, 0x010460b6u, 0x1c72a34fu, 0x02d522d0u, 0x1585d978u,
+                                    0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
+  // k*p in borrowed form (k = 2, 4, 6, 8)
+  static constexpr uint32_t K2[9] = {0x30f9fa8eu, 0x2208c16cu, 0x38e5469du, 0x25aa45a0u, 0x2b0bb2efu,
+                                     0x25b68180u, 0x214dc281u, 0x3cb84c67u, 0x0060c89bu};
+  static constexpr uint32_t K4[9] = {0x21f3f51cu, 0x241182dau, 0x31ca8d3bu, 0x2b548b42u, 0x361765dfu,
+                                     0x2b6d0301u, 0x229b8503u, 0x397098cfu, 0x00c19138u};
+  static constexpr uint32_t K6[9] = {0x32edefaau, 0x261a4447u, 0x2aafd3d9u, 0x30fed0e4u, 0x212318cfu,
+                                     0x31238483u, 0x23e94785u, 0x3628e537u, 0x012259d5u};
+  static constexpr uint32_t K8[9] = {0x23e7ea38u, 0x282305b5u, 0x23951a77u, 0x36a91686u, 0x2c2ecbbfu,
+                                     0x36da0604u, 0x25370a07u, 0x32e1319fu, 0x01832272u};
+  static constexpr uint32_t ONE[9] = {0x157ccc21u, 0x141c2758u, 0x185230d3u, 0x014c0419u, 0x0aa36fb9u,
+                                      0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};  // 2^261 mod p
+  static constexpr uint32_t C256[9] = {0x058f0d9du, 0x1aea1c6eu, 0x11c2cf74u, 0x11d651ebu, 0x1462c0a7u,
+                                       0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0x000e0a77u};  // 2^256 mod p
+};
+
+NZ_HD F29 f29_const(const uint32_t (&c)[9]) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = c[i];
+  return r;
+}
+
+// a * b * 2^-261 mod p (see the invariants above)
+NZ_HD F29 mul29(const F29& a, const F29& b) {
+  using Q = Fq29;
+  uint32_t m[9];
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+#pragma unroll
+    for (int j = 0; j < i; j++) {
+      acc += (uint64_t)a.v[j] * b.v[i - j];
+      acc += (uint64_t)m[j] * Q::P[i - j];
+    }
+    acc += (uint64_t)a.v[i] * b.v[0];
+    m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
+    acc += (uint64_t)m[i] * Q::P[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int i = 9; i < 17; i++) {
+#pragma unroll
+    for (int j = i - 8; j < 9; j++) {
+      acc += (uint64_t)a.v[j] * b.v[i - j];
+      acc += (uint64_t)m[j] * Q::P[i - j];
+    }
+    r.v[i - 9] = (uint32_t)acc & Q::MASK;
+    acc >>= 29;
+  }
+  r.v[8] = (uint32_t)acc;
+  return r;
+}
+
+NZ_HD void norm29(F29& r) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    r.v[i + 1] += r.v[i] >> 29;
+    r.v[i] &= Fq29::MASK;
+  }
+}
+
+// a + K - b, normalized (K borrowed-form multiple of p, b < K)
+NZ_HD F29 sub29(const F29& a, const F29& b, const uint32_t (&K)[9]) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = a.v[i] + K[i] - b.v[i];
+  norm29(r);
+  return r;
+}
+
+// a + b (+ b again when twice), normalized
+NZ_HD F29 add29(const F29& a, const F29& b) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = a.v[i] + b.v[i];
+  norm29(r);
+  return r;
+}
+NZ_HD F29 add2x29(const F29& a, const F29& b) {  // a + 2b
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = a.v[i] + (b.v[i] << 1);
+  norm29(r);
+  return r;
+}
+
+// p - y for a normalized y <= p (negated base ordinate), normalized
+NZ_HD F29 neg29(const F29& y) {
+  F29 r;
+  r.v[0] = Fq29::P[0] + (1u << 29) - y.v[0];
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.v[i] = Fq29::P[i] + (1u << 29) - 1u - y.v[i];
+  r.v[8] = Fq29::P[8] - 1u - y.v[8];
+  norm29(r);
+  return r;
+}
+
+// x == 0 mod p for a product output (normalized, < 2p): x is 0 or p
+NZ_HD bool is0p29(const F29& x) {
+  uint32_t o0 = 0, op = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    o0 |= x.v[i];
+    op |= x.v[i] ^ Fq29::P[i];
+  }
+  return o0 == 0 || op == 0;
+}
+
+// radix change of the same integer (< 2^256, no Montgomery change)
+NZ_HD F29 split29(const Fq& x) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int bit = 29 * i, limb = bit >> 5, sh = bit & 31;
+    uint64_t w = x.v[limb];
+    if (limb + 1 < 8) w |= (uint64_t)x.v[limb + 1] << 32;
+    r.v[i] = (uint32_t)(w >> sh) & Fq29::MASK;
+  }
+  return r;
+}
+NZ_HD Fq join29(const F29& x) {  // x normalized, < 2^256
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int bit = 29 * i, limb = bit >> 5, sh = bit & 31;
+    const uint64_t w = (uint64_t)x.v[i] << sh;
+    r.v[limb] |= (uint32_t)w;
+    if (limb + 1 < 8) r.v[limb + 1] |= (uint32_t)(w >> 32);
+  }
+  return r;
+}
+
+// Montgomery-261 value (any F29 < 2^257) -> canonical Montgomery-256 Fq (csrc/field.h)
+NZ_HD Fq to_fq256(const F29& x) { return reduce_once(join29(mul29(x, f29_const(Fq29::C256)))); }
+
+// XYZZ point with Montgomery-261 coordinates: X < 8p, Y < 4p, ZZ, ZZZ < 2p
+struct Xyzz29 {
+  F29 X, Y, ZZ, ZZZ;
+};
+
+// doubling of an affine point (x, y < p+1, normalized): dbl-2008-s-1 with Z = 1
+NZ_HD Xyzz29 mdbl29(const F29& x, const F29& y) {
+  Xyzz29 r;
+  F29 U;
+#pragma unroll
+  for (int i = 0; i < 9; i++) U.v[i] = y.v[i] << 1;  // < 2p, limbs < 2^30
+  const F29 V = mul29(U, U);
+  const F29 W = mul29(U, V);
+  const F29 S = mul29(x, V);
+  const F29 xx = mul29(x, x);
+  F29 M;
+#pragma unroll
+  for (int i = 0; i < 9; i++) M.v[i] = xx.v[i] * 3u;  // < 6p
+  norm29(M);
+  const F29 t = add29(S, S);                                      // < 4p
+  r.X = sub29(mul29(M, M), t, Fq29::K4);                          // < 6p
+  const F29 d = sub29(S, r.X, Fq29::K8);                          // < 10p
+  r.Y = sub29(mul29(M, d), mul29(W, y), Fq29::K2);                // < 4p
+  r.ZZ = V;
+  r.ZZZ = W;
+  return r;
+}
+
+}  // namespace nzcb

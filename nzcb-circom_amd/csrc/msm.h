@@ -11,14 +11,15 @@ namespace nzcb {
 // 2^(c*w) * B_i (LEM affine), so every window's digits land in ONE bucket set and
 // the per-window bucket reductions and the window Horner disappear.
 struct MsmBaseTable {
-  DevBuf<G1Affine> q;
+  DevBuf<G1Affine> q;  // affine, coordinates x * 2^261 mod p (Montgomery-261, csrc/f29.h)
   size_t n = 0, stride = 0;
   int c = 0, nw = 0;
   void build(const G1Affine* bases, size_t n, int c, hipStream_t st);
 };
 
-// Window size of the table-based (fixed-base) MSM.
-constexpr int kFixedBaseWindow = 20;
+// Window size of the table-based (fixed-base) MSM: 16..20 bits (NZCB_FB_WINDOW
+// overrides the default), i.e. 16..13 table rows and 2^15..2^19 buckets.
+int fixed_base_window();
 
 struct MsmScratch {
   size_t max_points = 0;
@@ -30,6 +31,7 @@ struct MsmScratch {
   DevBuf<G1xyzz> buckets;     // buckets whose entries lie in one accumulation chunk
   DevBuf<G1xyzz> carry_own;   // per chunk: partial sum of a bucket that starts in the chunk and spills over
   DevBuf<G1xyzz> carry_cont;  // per chunk: partial sum of a bucket that began in an earlier chunk
+  DevBuf<uint32_t> large;     // [count, bucket ids...] of buckets with long carry runs
   DevBuf<G1xyzz> seg_tot;     // per (bucket set, segment): sum_j (j+1) * bucket_j
   DevBuf<G1xyzz> seg_run;     // per (bucket set, segment): sum_j bucket_j
   DevBuf<G1xyzz> parts;       // per (set, sum slot, part): partial plain sums

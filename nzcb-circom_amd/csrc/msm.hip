@@ -9,10 +9,12 @@
 // Two schedules share the kernels:
 //  * generic (variable bases): c-bit windows, one bucket set per window
 //    (key = window * 2^(c-1) + |digit| - 1), host Horner over the windows;
-//  * fixed-base (the prover's PTau): a table of shifted bases 2^(20w) * B_i
-//    (MsmBaseTable) turns the 13 windows of 20 bits into ONE set of 2^19 buckets
-//    (key = |digit| - 1, value = row w of the table): 13 instead of 16 bucket
-//    additions per scalar, and a single bucket reduction.
+//  * fixed-base (the prover's PTau): a table of shifted bases 2^(c*w) * B_i
+//    (MsmBaseTable) turns the windows into ONE set of 2^(c-1) buckets (key =
+//    |digit| - 1, value = row w of the table) and a single bucket reduction. c = 17
+//    by default (15 rows, 2^16 buckets): measured against c = 16..20 at 2^21, it
+//    balances the bucket additions (15 per scalar) with the reduction tail. Its accumulation runs in
+//    the carry-free 9 x 29-bit radix of csrc/f29.h (table stored Montgomery-261).
 //
 // Pipeline (one stream, no host sync until the bucket-set sums):
 //  1. keys:       thread per scalar -> signed c-bit digits; (scalar, window) pair i
@@ -33,6 +35,8 @@
 //  8. host:       per set W = T + 8 * sum_b 2^b R_b, then Horner over the sets
 // Generic bases are read straight from the zkey PTau layout (64 B LEM affine).
 #include "msm.h"
+
+#include "f29.h"
 
 #include <cstdlib>
 #include <rocprim/rocprim.hpp>
@@ -76,6 +80,17 @@ static constexpr int kSegLen = 8;
 static constexpr int kSumThreads = 256;  // level-1 sums: block size
 static constexpr int kSumPer = 4;        // level-1 sums: sequential adds per thread
 static constexpr int kPartThreads = 64;  // level-2 sums: block size
+static constexpr uint32_t kSeqSpan = 64;  // finalize: longest carry run summed by one thread
+static constexpr int kLargeBlocks = 256;  // finalize: workgroups for the longer runs
+
+int fixed_base_window() {
+  static const int c = [] {
+    const char* e = std::getenv("NZCB_FB_WINDOW");
+    const int v = e ? std::atoi(e) : 17;
+    return (v >= 16 && v <= 20) ? v : 17;
+  }();
+  return c;
+}
 
 int msm_window_bits(size_t n) {
   if (n >= (size_t(1) << 18)) return 16;
@@ -209,6 +224,93 @@ msm_accumulate_kernel(const G1Affine* __restrict__ bases, const uint32_t* __rest
   }
 }
 
+// Fixed-base schedule: the same chunked accumulation in the redundant radix 2^29
+// (csrc/f29.h) on table bases stored as Montgomery-261 values; buckets are written back
+// in the Montgomery-256 XYZZ layout the reduction kernels use.
+static __device__ __forceinline__ void mdbl29_rare(const F29& x, const F29& y, Xyzz29* out) { *out = mdbl29(x, y); }
+
+__device__ __forceinline__ G1xyzz xyzz29_out(const Xyzz29& a, bool inf) {
+  if (inf) return G1xyzz::inf();
+  G1xyzz r;
+  r.X = to_fq256(a.X);
+  r.Y = to_fq256(a.Y);
+  r.ZZ = to_fq256(a.ZZ);
+  r.ZZZ = to_fq256(a.ZZZ);
+  return r;
+}
+
+template <int WAVES>
+__global__ void __launch_bounds__(kMsmThreads) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
+msm_accumulate29_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
+                        const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
+                        G1xyzz* __restrict__ buckets, G1xyzz* __restrict__ carry_own,
+                        G1xyzz* __restrict__ carry_cont) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nthreads) return;
+  const uint32_t M = offsets[nkeys];
+  const uint32_t s = (uint32_t)t * kChunk;
+  if (s >= M) return;
+  const uint32_t e = (s + kChunk < M) ? s + kChunk : M;
+  uint32_t k = find_key(offsets, nkeys, s);
+  uint32_t kstart = offsets[k], kend = offsets[k + 1];
+  Xyzz29 acc;
+  bool inf = true;
+  for (uint32_t pos = s; pos < e;) {
+    const uint32_t ent = sorted[pos];
+    const G1Affine P = bases[ent & 0x7fffffffu];
+    if (!P.is_inf()) {
+      const F29 x = split29(P.x);
+      F29 y = split29(P.y);
+      if (ent >> 31) y = neg29(y);
+      if (inf) {
+        acc.X = x;
+        acc.Y = y;
+        acc.ZZ = f29_const(Fq29::ONE);
+        acc.ZZZ = f29_const(Fq29::ONE);
+        inf = false;
+      } else {
+        // madd-2008-s (XYZZ + affine): 8 products + 2 squares
+        const F29 U2 = mul29(x, acc.ZZ);
+        const F29 S2 = mul29(y, acc.ZZZ);
+        const F29 Pd = sub29(U2, acc.X, Fq29::K8);   // < 10p
+        const F29 R = sub29(S2, acc.Y, Fq29::K4);    // < 6p
+        const F29 PP = mul29(Pd, Pd);
+        const F29 PPP = mul29(Pd, PP);
+        const F29 ZZ3 = mul29(acc.ZZ, PP);
+        const F29 Q = mul29(acc.X, PP);
+        const F29 RR = mul29(R, R);
+        const F29 X3 = sub29(RR, add2x29(PPP, Q), Fq29::K6);           // < 8p
+        const F29 Y3 = sub29(mul29(R, sub29(Q, X3, Fq29::K8)), mul29(acc.Y, PPP), Fq29::K2);  // < 4p
+        const F29 ZZZ3 = mul29(acc.ZZZ, PPP);
+        if (is0p29(ZZ3)) {  // same abscissa: doubling (equal points) or infinity (opposite)
+          if (is0p29(RR)) mdbl29_rare(x, y, &acc);
+          else inf = true;
+        } else {
+          acc.X = X3;
+          acc.Y = Y3;
+          acc.ZZ = ZZ3;
+          acc.ZZZ = ZZZ3;
+        }
+      }
+    }
+    pos++;
+    if (pos == kend || pos == e) {
+      const bool starts = kstart >= s;
+      const bool ends = kend <= e;
+      const G1xyzz out = xyzz29_out(acc, inf);
+      if (starts && ends) buckets[k] = out;
+      else if (!starts) carry_cont[t] = out;
+      else carry_own[t] = out;
+      inf = true;
+      if (pos < e) {
+        k = find_key(offsets, nkeys, pos);
+        kstart = offsets[k];
+        kend = offsets[k + 1];
+      }
+    }
+  }
+}
+
 // Kernels below keep exactly one inlined EC addition per loop body: an inlined
 // formula is ~3.5k instructions, and several copies in one loop thrash the shared
 // instruction cache (measured: 2.7 ms -> see profiles/ for the single-site form).
@@ -217,13 +319,18 @@ msm_accumulate_kernel(const G1Affine* __restrict__ bases, const uint32_t* __rest
 // the continuation carries of the chunks the bucket spills into (thread per bucket).
 __global__ void __launch_bounds__(kMsmThreads)
 msm_bucket_finalize_kernel(const uint32_t* __restrict__ offsets, uint32_t nkeys, const G1xyzz* __restrict__ carry_own,
-                           const G1xyzz* __restrict__ carry_cont, G1xyzz* __restrict__ buckets) {
+                           const G1xyzz* __restrict__ carry_cont, G1xyzz* __restrict__ buckets,
+                           uint32_t* __restrict__ large) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nkeys) return;
   const uint32_t s = offsets[k], e = offsets[k + 1];
   if (e == s) return;
   const uint32_t c0 = s / kChunk, c1 = (e - 1) / kChunk;
   if (c0 == c1) return;  // the accumulation stored it already
+  if (c1 - c0 > kSeqSpan) {  // long run of carries (skewed digits): a workgroup sums it
+    large[1 + atomicAdd(&large[0], 1u)] = (uint32_t)k;
+    return;
+  }
   G1xyzz v = carry_own[c0];
   for (uint32_t u = c0 + 1; u <= c1; u++) v = xyzz_add(v, carry_cont[u]);
   buckets[k] = v;
@@ -294,6 +401,30 @@ __device__ __forceinline__ G1xyzz block_sum(int per, G1xyzz* sh, Load&& load) {
   return sh[0];
 }
 
+// Buckets listed by the finalize kernel (more than kSeqSpan carries, e.g. many equal
+// digits): one workgroup per bucket, kSumThreads-way partial sums + LDS tree.
+__global__ void __launch_bounds__(kSumThreads)
+msm_bucket_large_kernel(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
+                        const G1xyzz* __restrict__ carry_own, const G1xyzz* __restrict__ carry_cont,
+                        G1xyzz* __restrict__ buckets) {
+  __shared__ G1xyzz sh[kSumThreads];
+  const uint32_t count = large[0];
+  for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
+    const uint32_t k = large[1 + i];
+    const uint32_t c0 = offsets[k] / kChunk, c1 = (offsets[k + 1] - 1) / kChunk;
+    const uint32_t span = c1 - c0 + 1;
+    const int per = (int)((span + kSumThreads - 1) / kSumThreads);
+    const G1xyzz r = block_sum<kSumThreads>(per, sh, [&](int step, G1xyzz& rhs) {
+      const uint32_t u = (uint32_t)step * kSumThreads + threadIdx.x;
+      if (u >= span) return false;
+      rhs = u ? carry_cont[c0 + u] : carry_own[c0];
+      return true;
+    });
+    if (threadIdx.x == 0) buckets[k] = r;
+    __syncthreads();
+  }
+}
+
 // level 1: block (set w, slot j, part p). Slot 0 sums seg_tot[w][g] over all g; slot b+1
 // sums seg_run[w][g] over the g with bit b set. Part p covers kSumPer * T terms.
 __global__ void __launch_bounds__(kSumThreads)
@@ -336,22 +467,23 @@ msm_parts_kernel(const G1xyzz* __restrict__ parts, int nparts, G1xyzz* __restric
 // Shifted-base table: row w = 2^(c*w) * B_i, thread per base (c doublings per row,
 // one Fermat inversion per stored affine point).
 __global__ void __launch_bounds__(kMsmThreads)
-msm_table_kernel(const G1Affine* __restrict__ bases, size_t n, size_t stride, int c, int nw, G1Affine* __restrict__ q) {
+msm_table_kernel(const G1Affine* __restrict__ bases, size_t n, size_t stride, int c, int nw, Fq k261,
+                 G1Affine* __restrict__ q) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const G1Affine P = bases[i];
-  q[i] = P;
   if (P.is_inf()) {
-    for (int w = 1; w < nw; w++) q[(size_t)w * stride + i] = P;
+    for (int w = 0; w < nw; w++) q[(size_t)w * stride + i] = P;
     return;
   }
   G1xyzz acc = xyzz_from_affine(P);
-  for (int w = 1; w < nw; w++) {
-    for (int k = 0; k < c; k++) acc = xyzz_dbl(acc);
+  for (int w = 0; w < nw; w++) {
+    if (w)
+      for (int k = 0; k < c; k++) acc = xyzz_dbl(acc);
     const Fq ti = inverse(acc.ZZ * acc.ZZZ);
-    G1Affine r;
-    r.x = acc.X * (acc.ZZZ * ti);
-    r.y = acc.Y * (acc.ZZ * ti);
+    G1Affine r;  // affine, Montgomery-261 (x * 2^261 = mont256(x * 2^256, 2^261))
+    r.x = acc.X * (acc.ZZZ * ti) * k261;
+    r.y = acc.Y * (acc.ZZ * ti) * k261;
     q[(size_t)w * stride + i] = r;
   }
 }
@@ -363,8 +495,11 @@ void MsmBaseTable::build(const G1Affine* bases, size_t npts, int cbits, hipStrea
   nw = num_windows(c);
   if ((size_t)nw * stride >= (size_t(1) << 31)) throw Error(NZCB_ERR_ARG, "msm table too large for 31-bit indices");
   q.alloc((size_t)nw * stride);
+  Fq thirty_two = Fq::zero();
+  thirty_two.v[0] = 32;
+  const Fq k261 = to_mont(thirty_two);  // 2^261 mod p
   hipLaunchKernelGGL(msm_table_kernel, dim3(grid_for(n, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0, st, bases, n,
-                     stride, c, nw, q.p);
+                     stride, c, nw, k261, q.p);
   NZ_HIP(hipGetLastError());
 }
 
@@ -408,7 +543,7 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
   }
   if (fixed_base) {
     MsmBaseTable t;
-    t.c = kFixedBaseWindow;
+    t.c = fixed_base_window();
     fit(make_plan(maxp, &t));
   }
   offsets.alloc(max_keys + 1);
@@ -422,6 +557,7 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
   buckets.alloc(max_keys);
   size_t nthreads = (max_entries + kChunk - 1) / kChunk + 1;
   carry_own.alloc(nthreads);
+  large.alloc(max_keys + 1);
   carry_cont.alloc(nthreads);
   seg_tot.alloc(max_seg);
   seg_run.alloc(max_seg);
@@ -447,9 +583,14 @@ static void launch_keys(const Fr* scalars, size_t n, int mont, size_t stride, Ms
 static void keys_dispatch(int c, const Fr* scalars, size_t n, int mont, const MsmBaseTable* t, MsmScratch& sc,
                           hipStream_t st) {
   if (t) {
-    if (c != kFixedBaseWindow) throw Error(NZCB_ERR_INTERNAL, "bad fixed-base msm window");
-    launch_keys<kFixedBaseWindow, true>(scalars, n, mont, t->stride, sc, st);
-    return;
+    switch (c) {
+      case 16: launch_keys<16, true>(scalars, n, mont, t->stride, sc, st); return;
+      case 17: launch_keys<17, true>(scalars, n, mont, t->stride, sc, st); return;
+      case 18: launch_keys<18, true>(scalars, n, mont, t->stride, sc, st); return;
+      case 19: launch_keys<19, true>(scalars, n, mont, t->stride, sc, st); return;
+      case 20: launch_keys<20, true>(scalars, n, mont, t->stride, sc, st); return;
+      default: throw Error(NZCB_ERR_INTERNAL, "bad fixed-base msm window");
+    }
   }
   switch (c) {
 #define NZ_CASE(K) case K: launch_keys<K, false>(scalars, n, mont, 0, sc, st); break;
@@ -506,13 +647,22 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   NZ_HIP(hipGetLastError());
   const size_t nthreads = (p.entries + kChunk - 1) / kChunk;
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[3], st));
-  hipLaunchKernelGGL(msm_accumulate_kernel, dim3(grid_for(nthreads, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0,
-                     st, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads, sc.buckets.p, sc.carry_own.p,
-                     sc.carry_cont.p);
+  static const int acc_waves = [] {
+    const char* e = std::getenv("NZCB_ACC29_WAVES");
+    return e ? std::atoi(e) : 4;
+  }();
+  auto acc29 = acc_waves >= 4 ? msm_accumulate29_kernel<4> : msm_accumulate29_kernel<3>;
+  hipLaunchKernelGGL(table ? acc29 : msm_accumulate_kernel,
+                     dim3(grid_for(nthreads, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0, st, gather, sc.sorted.p,
+                     sc.offsets.p, p.nkeys, nthreads, sc.buckets.p, sc.carry_own.p, sc.carry_cont.p);
   NZ_HIP(hipGetLastError());
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[4], st));
+  NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));
   hipLaunchKernelGGL(msm_bucket_finalize_kernel, dim3(grid_for(p.nkeys, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0,
-                     st, sc.offsets.p, p.nkeys, sc.carry_own.p, sc.carry_cont.p, sc.buckets.p);
+                     st, sc.offsets.p, p.nkeys, sc.carry_own.p, sc.carry_cont.p, sc.buckets.p, sc.large.p);
+  NZ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(msm_bucket_large_kernel, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, sc.offsets.p, sc.large.p,
+                     sc.carry_own.p, sc.carry_cont.p, sc.buckets.p);
   NZ_HIP(hipGetLastError());
   mark(5);
   hipLaunchKernelGGL(msm_bucket_reduce_kernel, dim3(grid_for((size_t)p.nsets * p.nseg, kMsmThreads, 1u << 30)),

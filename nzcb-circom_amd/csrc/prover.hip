@@ -455,7 +455,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     if (sec.len) NZ_HIP(hipMemcpyAsync(buf.p, sec.p, sec.len, hipMemcpyHostToDevice, s));
   };
   up(ptau, z.ptau);
-  ptab.build(ptau.p, ptau.n, kFixedBaseWindow, s);
+  ptab.build(ptau.p, ptau.n, fixed_base_window(), s);
   up(qm, z.qm);
   up(ql, z.ql);
   up(qr, z.qr);

@@ -13,6 +13,7 @@ __global__ void probe(uint64_t* out, int iters) {
   uint32_t x = threadIdx.x * 3 + 1, y = threadIdx.x * 7 + 5;
   double d0 = x, d1 = y, d2 = x + 1.0, d3 = y + 1.0, d4 = 0.5, d5 = 0.25, d6 = 0.125, d7 = 2.0;
   uint32_t h = 0;
+  const uint64_t b64 = (uint64_t)threadIdx.x * 977;
   uint32_t r0 = x, r1 = x + 1, r2 = x + 2, r3 = x + 3, r4 = x + 4, r5 = x + 5, r6 = x + 6, r7 = x + 7;
   float f0 = x, f1 = y, f2 = 1.f, f3 = 2.f, f4 = 3.f, f5 = 4.f, f6 = 5.f, f7 = 6.f;
   for (int i = 0; i < iters; i++) {
@@ -86,6 +87,31 @@ __global__ void probe(uint64_t* out, int iters) {
                          "v_addc_co_u32_e64 %4, s[20:21], %4, 0, s[20:21]\n v_addc_co_u32_e64 %5, s[22:23], %5, 0, s[22:23]\n")
                    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(x), "v"(y)
                    : "s20", "s21", "s22", "s23");
+    } else if (K >= 15 && K <= 24) {
+#define NZ_OP8(OP) asm volatile(REP16(OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7)) \
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y), "v"(x))
+#define NZ_OP8W(OP) asm volatile(REP16(OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7)) \
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(y), "v"(x), "v"(b64))
+#define AND(i) "v_and_b32 %" #i ", %" #i ", %8\n"
+#define ALIGN(i) "v_alignbit_b32 %" #i ", %" #i ", %8, 29\n"
+#define SHR(i) "v_lshrrev_b32 %" #i ", 29, %" #i "\n"
+#define MU24(i) "v_mul_u32_u24 %" #i ", %" #i ", %8\n"
+#define MHU24(i) "v_mul_hi_u32_u24 %" #i ", %" #i ", %8\n"
+#define BFE(i) "v_bfe_u32 %" #i ", %" #i ", 3, 29\n"
+#define SHR64(i) "v_lshrrev_b64 %" #i ", 29, %" #i "\n"
+#define LSHLADD64(i) "v_lshl_add_u64 %" #i ", %" #i ", 0, %10\n"
+#define ADD64CO(i) "v_add_co_u32 %" #i ", vcc, %" #i ", %8\n"
+#define CND(i) "v_cndmask_b32 %" #i ", %" #i ", %8, vcc\n"
+      if (K == 15) NZ_OP8(AND);
+      else if (K == 16) NZ_OP8(ALIGN);
+      else if (K == 17) NZ_OP8(SHR);
+      else if (K == 18) NZ_OP8(MU24);
+      else if (K == 19) NZ_OP8(MHU24);
+      else if (K == 20) NZ_OP8(BFE);
+      else if (K == 21) NZ_OP8W(SHR64);
+      else if (K == 22) NZ_OP8W(LSHLADD64);
+      else if (K == 23) NZ_OP8(CND);
+      else NZ_OP8(ADD64CO);
     } else if (K == 6) {  // 8 x (mad; s_nop 1; addc) as in field.h mac
       asm volatile(
           "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
@@ -127,23 +153,30 @@ int main() {
   const int blocks = 256 * 8, threads = 256, iters = 4000;
   uint64_t* d;
   (void)hipMalloc(&d, (size_t)blocks * threads * 8);
-  const int NK = 15;
+  const int NK = 25;
   const char* names[NK] = {"v_mad_u64_u32 x8", "v_add_co_u32 chain", "s_nop 1", "v_fma_f64 x8", "v_mul_lo_u32 chain",
                            "v_mul_hi_u32 chain", "mac(mad;nop;addc)", "v_add_u32 x8", "v_add_co_u32 x8",
                            "v_addc_co_u32 x8", "v_add3_u32 x8", "v_mad_u32_u24 x8", "v_mul_lo_u32 x8",
-                           "v_fma_f32 x8", "mad,mad,addc,addc x2"};
+                           "v_fma_f32 x8", "mad,mad,addc,addc x2", "v_and_b32 x8", "v_alignbit_b32 x8",
+                           "v_lshrrev_b32 x8", "v_mul_u32_u24 x8", "v_mul_hi_u32_u24 x8", "v_bfe_u32 x8",
+                           "v_lshrrev_b64 x8", "v_lshl_add_u64 x8", "v_cndmask_b32 x8", "v_add_co_u32(e32) x8"};
   double ms[NK] = {run<0>(d, blocks, threads, iters), run<1>(d, blocks, threads, iters), run<2>(d, blocks, threads, iters),
                    run<3>(d, blocks, threads, iters), run<4>(d, blocks, threads, iters), run<5>(d, blocks, threads, iters),
                    run<6>(d, blocks, threads, iters), run<7>(d, blocks, threads, iters / 8),
                    run<8>(d, blocks, threads, iters / 8), run<9>(d, blocks, threads, iters / 8),
                    run<10>(d, blocks, threads, iters / 8), run<11>(d, blocks, threads, iters / 8),
                    run<12>(d, blocks, threads, iters / 8), run<13>(d, blocks, threads, iters / 8),
-                   run<14>(d, blocks, threads, iters / 4)};
+                   run<14>(d, blocks, threads, iters / 4),  run<15>(d, blocks, threads, iters / 8),
+                   run<16>(d, blocks, threads, iters / 8), run<17>(d, blocks, threads, iters / 8),
+                   run<18>(d, blocks, threads, iters / 8), run<19>(d, blocks, threads, iters / 8),
+                   run<20>(d, blocks, threads, iters / 8), run<21>(d, blocks, threads, iters / 8),
+                   run<22>(d, blocks, threads, iters / 8), run<23>(d, blocks, threads, iters / 8),
+                   run<24>(d, blocks, threads, iters / 8)};
   const double waves = (double)blocks * threads / 64;
   for (int k = 0; k < NK; k++) {
     // wave-instructions per iteration (mac = one mad+nop+addc group)
-    double per = k == 6 ? 8 : (k >= 7 && k <= 13) ? 128 : k == 14 ? 64 : 16;
-    int it = k >= 7 && k <= 13 ? iters / 8 : k == 14 ? iters / 4 : iters;
+    double per = k == 6 ? 8 : (k >= 7 && k <= 13) || k >= 15 ? 128 : k == 14 ? 64 : 16;
+    int it = (k >= 7 && k <= 13) || k >= 15 ? iters / 8 : k == 14 ? iters / 4 : iters;
     double n_instr = waves * it * per;
     double simd_cycles = ms[k] * 1e-3 * 2.4e9 * 1024;    // 256 CUs x 4 SIMDs at 2.4 GHz
     printf("%-20s %8.3f ms  %6.2f SIMD-cycles per wave-instruction\n", names[k], ms[k], simd_cycles / n_instr);

@@ -146,3 +146,24 @@ def test_msm_fixed_base_infinity_bases(engine):
     pts = [g, None, bn.g1_neg(g), g, None, g]
     sc = [5, 6, 5, 7, 9, R_MOD - 5]
     assert _msm_fixed(engine, pts, sc) == bn.msm(pts, sc)
+
+
+@pytest.mark.parametrize("fixed", [False, True])
+def test_msm_long_carry_runs(engine, fixed):
+    """Equal scalars put every window's entries in one bucket: thousands of accumulation
+    chunks end in carries of one bucket (the finalize kernel's workgroup path)."""
+    n = 5000
+    rng = random.Random(77)
+    pts = _bases(n, 4242)
+    v = rng.randrange(R_MOD)
+    sc = [v] * n
+    acc = None
+    for p in pts:
+        acc = bn.g1_add(acc, p)
+    want = bn.g1_mul(acc, v)
+    if fixed:
+        assert _msm_fixed(engine, pts, sc) == want
+    else:
+        bases = b"".join(bn.g1_to_lem(p) for p in pts)
+        got = _affine(engine.msm(bases, b"".join(bn.to_le(s) for s in sc), False))
+        assert got == want
