@@ -166,8 +166,10 @@ NZ_HD Fq join29(const F29& x) {  // x normalized, < 2^256
 // Montgomery-261 value (any F29 < 2^257) -> canonical Montgomery-256 Fq (csrc/field.h)
 NZ_HD Fq to_fq256(const F29& x) { return reduce_once(join29(mul29(x, f29_const(Fq29::C256)))); }
 
-// XYZZ point with Montgomery-261 coordinates: X < 8p, Y < 4p, ZZ, ZZZ < 2p
-struct Xyzz29 {
+// XYZZ point with Montgomery-261 coordinates: X < 8p, Y < 4p, ZZ, ZZZ < 2p.
+// Stored as 144 bytes; infinity is stored with ZZ = 0 (a finite point's ZZ is never
+// 0 or p).
+struct alignas(16) Xyzz29 {
   F29 X, Y, ZZ, ZZZ;
 };
 

@@ -4,6 +4,7 @@
 
 #include "common.h"
 #include "ec.h"
+#include "f29.h"
 
 namespace nzcb {
 
@@ -31,6 +32,9 @@ struct MsmScratch {
   DevBuf<G1xyzz> buckets;     // buckets whose entries lie in one accumulation chunk
   DevBuf<G1xyzz> carry_own;   // per chunk: partial sum of a bucket that starts in the chunk and spills over
   DevBuf<G1xyzz> carry_cont;  // per chunk: partial sum of a bucket that began in an earlier chunk
+  // fixed-base schedule: the accumulation stores its results unconverted (radix 2^29,
+  // Montgomery-261); the finalize kernel converts them into buckets
+  DevBuf<Xyzz29> buckets29, carry_own29, carry_cont29;
   DevBuf<uint32_t> large;     // [count, bucket ids...] of buckets with long carry runs
   DevBuf<G1xyzz> seg_tot;     // per (bucket set, segment): sum_j (j+1) * bucket_j
   DevBuf<G1xyzz> seg_run;     // per (bucket set, segment): sum_j bucket_j

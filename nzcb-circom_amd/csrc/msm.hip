@@ -81,7 +81,7 @@ static constexpr int kSumThreads = 256;  // level-1 sums: block size
 static constexpr int kSumPer = 4;        // level-1 sums: sequential adds per thread
 static constexpr int kPartThreads = 64;  // level-2 sums: block size
 static constexpr uint32_t kSeqSpan = 64;  // finalize: longest carry run summed by one thread
-static constexpr int kLargeBlocks = 256;  // finalize: workgroups for the longer runs
+static constexpr int kLargeBlocks = 32;  // finalize: workgroups for the longer runs
 
 int fixed_base_window() {
   static const int c = [] {
@@ -225,12 +225,18 @@ msm_accumulate_kernel(const G1Affine* __restrict__ bases, const uint32_t* __rest
 }
 
 // Fixed-base schedule: the same chunked accumulation in the redundant radix 2^29
-// (csrc/f29.h) on table bases stored as Montgomery-261 values; buckets are written back
-// in the Montgomery-256 XYZZ layout the reduction kernels use.
+// (csrc/f29.h) on table bases stored as Montgomery-261 values. Results are stored
+// unconverted (a store per bucket run costs a few instructions; the 4 products of the
+// conversion would run for the whole wave whenever any lane ends a run, i.e. on most
+// iterations) and the finalize kernel converts them to the Montgomery-256 layout.
 static __device__ __forceinline__ void mdbl29_rare(const F29& x, const F29& y, Xyzz29* out) { *out = mdbl29(x, y); }
 
-__device__ __forceinline__ G1xyzz xyzz29_out(const Xyzz29& a, bool inf) {
-  if (inf) return G1xyzz::inf();
+__device__ __forceinline__ G1xyzz load_point(const G1xyzz& p) { return p; }
+__device__ __forceinline__ G1xyzz load_point(const Xyzz29& a) {
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) z |= a.ZZ.v[i];
+  if (!z) return G1xyzz::inf();
   G1xyzz r;
   r.X = to_fq256(a.X);
   r.Y = to_fq256(a.Y);
@@ -243,8 +249,8 @@ template <int WAVES>
 __global__ void __launch_bounds__(kMsmThreads) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 msm_accumulate29_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
                         const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
-                        G1xyzz* __restrict__ buckets, G1xyzz* __restrict__ carry_own,
-                        G1xyzz* __restrict__ carry_cont) {
+                        Xyzz29* __restrict__ buckets, Xyzz29* __restrict__ carry_own,
+                        Xyzz29* __restrict__ carry_cont) {
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nthreads) return;
   const uint32_t M = offsets[nkeys];
@@ -297,7 +303,10 @@ msm_accumulate29_kernel(const G1Affine* __restrict__ bases, const uint32_t* __re
     if (pos == kend || pos == e) {
       const bool starts = kstart >= s;
       const bool ends = kend <= e;
-      const G1xyzz out = xyzz29_out(acc, inf);
+      Xyzz29 out = acc;
+      if (inf)
+#pragma unroll
+        for (int i = 0; i < 9; i++) out.ZZ.v[i] = 0;
       if (starts && ends) buckets[k] = out;
       else if (!starts) carry_cont[t] = out;
       else carry_own[t] = out;
@@ -317,22 +326,28 @@ msm_accumulate29_kernel(const G1Affine* __restrict__ bases, const uint32_t* __re
 
 // Buckets whose entries span several accumulation chunks: owner chunk's carry plus
 // the continuation carries of the chunks the bucket spills into (thread per bucket).
+// P = G1xyzz: the generic accumulation already wrote single-chunk buckets in place;
+// P = Xyzz29: every bucket is converted here (single-chunk ones from `single`).
+template <class P>
 __global__ void __launch_bounds__(kMsmThreads)
-msm_bucket_finalize_kernel(const uint32_t* __restrict__ offsets, uint32_t nkeys, const G1xyzz* __restrict__ carry_own,
-                           const G1xyzz* __restrict__ carry_cont, G1xyzz* __restrict__ buckets,
-                           uint32_t* __restrict__ large) {
+msm_bucket_finalize_kernel(const uint32_t* __restrict__ offsets, uint32_t nkeys, const P* __restrict__ single,
+                           const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
+                           G1xyzz* __restrict__ buckets, uint32_t* __restrict__ large) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nkeys) return;
   const uint32_t s = offsets[k], e = offsets[k + 1];
   if (e == s) return;
   const uint32_t c0 = s / kChunk, c1 = (e - 1) / kChunk;
-  if (c0 == c1) return;  // the accumulation stored it already
+  if (c0 == c1) {  // stored by the accumulation
+    if (single) buckets[k] = load_point(single[k]);
+    return;
+  }
   if (c1 - c0 > kSeqSpan) {  // long run of carries (skewed digits): a workgroup sums it
     large[1 + atomicAdd(&large[0], 1u)] = (uint32_t)k;
     return;
   }
-  G1xyzz v = carry_own[c0];
-  for (uint32_t u = c0 + 1; u <= c1; u++) v = xyzz_add(v, carry_cont[u]);
+  G1xyzz v = load_point(carry_own[c0]);
+  for (uint32_t u = c0 + 1; u <= c1; u++) v = xyzz_add(v, load_point(carry_cont[u]));
   buckets[k] = v;
 }
 
@@ -403,9 +418,10 @@ __device__ __forceinline__ G1xyzz block_sum(int per, G1xyzz* sh, Load&& load) {
 
 // Buckets listed by the finalize kernel (more than kSeqSpan carries, e.g. many equal
 // digits): one workgroup per bucket, kSumThreads-way partial sums + LDS tree.
+template <class P>
 __global__ void __launch_bounds__(kSumThreads)
 msm_bucket_large_kernel(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
-                        const G1xyzz* __restrict__ carry_own, const G1xyzz* __restrict__ carry_cont,
+                        const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
                         G1xyzz* __restrict__ buckets) {
   __shared__ G1xyzz sh[kSumThreads];
   const uint32_t count = large[0];
@@ -417,7 +433,7 @@ msm_bucket_large_kernel(const uint32_t* __restrict__ offsets, const uint32_t* __
     const G1xyzz r = block_sum<kSumThreads>(per, sh, [&](int step, G1xyzz& rhs) {
       const uint32_t u = (uint32_t)step * kSumThreads + threadIdx.x;
       if (u >= span) return false;
-      rhs = u ? carry_cont[c0 + u] : carry_own[c0];
+      rhs = load_point(u ? carry_cont[c0 + u] : carry_own[c0]);
       return true;
     });
     if (threadIdx.x == 0) buckets[k] = r;
@@ -558,6 +574,11 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
   size_t nthreads = (max_entries + kChunk - 1) / kChunk + 1;
   carry_own.alloc(nthreads);
   large.alloc(max_keys + 1);
+  if (fixed_base) {
+    buckets29.alloc(max_keys);
+    carry_own29.alloc(nthreads);
+    carry_cont29.alloc(nthreads);
+  }
   carry_cont.alloc(nthreads);
   seg_tot.alloc(max_seg);
   seg_run.alloc(max_seg);
@@ -651,18 +672,35 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     const char* e = std::getenv("NZCB_ACC29_WAVES");
     return e ? std::atoi(e) : 4;
   }();
-  auto acc29 = acc_waves >= 4 ? msm_accumulate29_kernel<4> : msm_accumulate29_kernel<3>;
-  hipLaunchKernelGGL(table ? acc29 : msm_accumulate_kernel,
-                     dim3(grid_for(nthreads, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0, st, gather, sc.sorted.p,
-                     sc.offsets.p, p.nkeys, nthreads, sc.buckets.p, sc.carry_own.p, sc.carry_cont.p);
+  const dim3 agrid(grid_for(nthreads, kMsmThreads, 1u << 30));
+  if (table) {
+    if (!sc.buckets29.p) throw Error(NZCB_ERR_ARG, "msm scratch was not sized for the fixed-base schedule");
+    hipLaunchKernelGGL(acc_waves >= 4 ? msm_accumulate29_kernel<4> : msm_accumulate29_kernel<3>, agrid,
+                       dim3(kMsmThreads), 0, st, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads,
+                       sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
+  } else {
+    hipLaunchKernelGGL(msm_accumulate_kernel, agrid, dim3(kMsmThreads), 0, st, gather, sc.sorted.p, sc.offsets.p,
+                       p.nkeys, nthreads, sc.buckets.p, sc.carry_own.p, sc.carry_cont.p);
+  }
   NZ_HIP(hipGetLastError());
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[4], st));
   NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));
-  hipLaunchKernelGGL(msm_bucket_finalize_kernel, dim3(grid_for(p.nkeys, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0,
-                     st, sc.offsets.p, p.nkeys, sc.carry_own.p, sc.carry_cont.p, sc.buckets.p, sc.large.p);
-  NZ_HIP(hipGetLastError());
-  hipLaunchKernelGGL(msm_bucket_large_kernel, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, sc.offsets.p, sc.large.p,
-                     sc.carry_own.p, sc.carry_cont.p, sc.buckets.p);
+  const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
+  if (table) {
+    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, sc.offsets.p, p.nkeys,
+                       (const Xyzz29*)sc.buckets29.p, (const Xyzz29*)sc.carry_own29.p,
+                       (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p, sc.large.p);
+    NZ_HIP(hipGetLastError());
+    hipLaunchKernelGGL(msm_bucket_large_kernel<Xyzz29>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, sc.offsets.p,
+                       sc.large.p, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p);
+  } else {
+    hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, sc.offsets.p, p.nkeys,
+                       (const G1xyzz*)nullptr, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p,
+                       sc.buckets.p, sc.large.p);
+    NZ_HIP(hipGetLastError());
+    hipLaunchKernelGGL(msm_bucket_large_kernel<G1xyzz>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, sc.offsets.p,
+                       sc.large.p, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p, sc.buckets.p);
+  }
   NZ_HIP(hipGetLastError());
   mark(5);
   hipLaunchKernelGGL(msm_bucket_reduce_kernel, dim3(grid_for((size_t)p.nsets * p.nseg, kMsmThreads, 1u << 30)),
