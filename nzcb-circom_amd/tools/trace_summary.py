@@ -11,6 +11,8 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--window", type=float, default=0.0, help="only the last N seconds (0 = all)")
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--last", nargs=2, metavar=("KERNEL", "COUNT"),
+                    help="window from the COUNT-th last launch of a kernel whose name contains KERNEL to its last")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -18,7 +20,11 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     t_end = max(e for _, e, _ in rows)
-    if a.window > 0:
+    if a.last:
+        hits = [r for r in rows if a.last[0] in r[2]][-int(a.last[1]):]
+        lo, t_end = hits[0][0], hits[-1][1]
+        rows = [r for r in rows if lo <= r[0] and r[1] <= t_end]
+    elif a.window > 0:
         rows = [r for r in rows if r[0] >= t_end - a.window * 1e9]
     t0 = min(s for s, _, _ in rows)
     busy, cur_s, cur_e = 0, None, None
