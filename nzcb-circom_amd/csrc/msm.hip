@@ -19,9 +19,10 @@
 // Pipeline (one stream, no host sync until the bucket-set sums):
 //  1. keys:       thread per scalar -> signed c-bit digits; (scalar, window) pair i
 //                 gets the fixed slot w*n+i; zero digits get a sentinel key that
-//                 sorts last -- no atomics
-//  2. sort:       rocPRIM onesweep radix sort of (key, base index|sign) on the 20 key
-//                 bits, 10 bits per pass (2 passes instead of the default 8-bit 3)
+//                 sorts last (or, with 16-bit fixed-base keys, bucket 0 and the
+//                 table's infinity point) -- no atomics
+//  2. sort:       rocPRIM onesweep radix sort of (key, base index|sign), 2 passes of
+//                 <= 10 key bits (16-bit keys for the fixed-base c <= 17)
 //  3. offsets:    bucket start positions by binary search in the sorted keys
 //  4. accumulate: thread per fixed 32-entry chunk of the sorted stream (load balance
 //                 independent of the digit distribution): XYZZ mixed adds of the
@@ -45,26 +46,29 @@ namespace nzcb {
 
 static constexpr int kMsmThreads = 256;
 
-// Onesweep with 10-bit digits: the 20-bit bucket keys take 2 passes over the
-// (key, value) pairs instead of 3 with the library's 8-bit default for gfx950.
+// Onesweep with a chosen digit width: the generic path's 20-bit keys take 2 passes of
+// 10 bits instead of 3 with the library's 8-bit default for gfx950.
 template <unsigned Bits>
 using SortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, Bits,
                                         rocprim::block_radix_rank_algorithm::match>>;
 
-static int sort_bits() {
-  static int bits = [] {
+// digit bits per onesweep pass: 8 for 16-bit keys, 10 for the <= 20-bit 32-bit keys
+// (measured at 2^21: 0.51 vs 0.62 ms and 0.55 vs 0.69 ms); NZCB_SORT_BITS overrides
+static int sort_bits(bool k16) {
+  static const int env = [] {
     const char* e = std::getenv("NZCB_SORT_BITS");
-    int b = e ? std::atoi(e) : 10;
-    return (b == 8 || b == 10 || b == 11) ? b : 10;
+    const int b = e ? std::atoi(e) : 0;
+    return (b == 8 || b == 10 || b == 11) ? b : 0;
   }();
-  return bits;
+  return env ? env : k16 ? 8 : 10;
 }
 
-static void radix_sort(void* tmp, size_t& tmp_bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+template <class K>
+static void radix_sort(void* tmp, size_t& tmp_bytes, const K* kin, K* kout, const uint32_t* vin,
                        uint32_t* vout, size_t m, int end_bit, hipStream_t st) {
-  switch (sort_bits()) {
+  switch (sort_bits(sizeof(K) == 2)) {
     case 8:
       NZ_HIP(rocprim::radix_sort_pairs<SortConfig<8>>(tmp, tmp_bytes, kin, kout, vin, vout, m, 0, end_bit, st));
       break;
@@ -128,14 +132,19 @@ __device__ __forceinline__ void for_each_digit(const Fr& s, F&& f) {
   }
 }
 
-// FIXED: key = bucket, value = table row w (stride) + i; else key = w * NB + bucket, value = i
-template <int C, bool FIXED>
+// FIXED: key = bucket, value = table row w (stride) + i; else key = w * NB + bucket, value = i.
+// Zero digits: with 16-bit keys (fixed base, c <= 17) key 0 and the table's infinity
+// point as value (the accumulation skips it), so the keys stay 16 bits; otherwise a
+// sentinel key that sorts after every bucket.
+template <int C, bool FIXED, class K>
 __global__ void __launch_bounds__(kMsmThreads)
-msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t stride, uint32_t* __restrict__ keys,
-                uint32_t* __restrict__ vals) {
+msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t stride, uint32_t skip_val,
+                K* __restrict__ keys, uint32_t* __restrict__ vals) {
   constexpr int NW = (255 + C - 1) / C;
   constexpr uint32_t NB = 1u << (C - 1);
-  constexpr uint32_t SENTINEL = FIXED ? NB : NW * NB;
+  constexpr bool K16 = sizeof(K) == 2;
+  static_assert(!K16 || (FIXED && NB <= 65536), "16-bit keys need a single bucket set of <= 2^16");
+  constexpr uint32_t SENTINEL = K16 ? 0u : FIXED ? NB : NW * NB;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     Fr s = scalars[i];
     if (mont) s = from_mont(s);
@@ -144,7 +153,7 @@ msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t strid
 #pragma unroll
     for (int w = 0; w < NW; w++) {
       k[w] = SENTINEL;
-      v[w] = (uint32_t)i;
+      v[w] = K16 ? skip_val : (uint32_t)i;
     }
     for_each_digit<C>(s, [&](int w, uint32_t b, uint32_t sign) {
       if (FIXED) {
@@ -157,15 +166,16 @@ msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t strid
     });
 #pragma unroll
     for (int w = 0; w < NW; w++) {
-      keys[(size_t)w * n + i] = k[w];
+      keys[(size_t)w * n + i] = (K)k[w];
       vals[(size_t)w * n + i] = v[w];
     }
   }
 }
 
 // offsets[k] = first position of a key >= k in the sorted key array (k = 0..nkeys)
+template <class K>
 __global__ void __launch_bounds__(kMsmThreads)
-msm_offsets_kernel(const uint32_t* __restrict__ skeys, size_t m, uint32_t nkeys, uint32_t* __restrict__ offsets) {
+msm_offsets_kernel(const K* __restrict__ skeys, size_t m, uint32_t nkeys, uint32_t* __restrict__ offsets) {
   size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k > nkeys) return;
   size_t lo = 0, hi = m;
@@ -510,7 +520,8 @@ void MsmBaseTable::build(const G1Affine* bases, size_t npts, int cbits, hipStrea
   c = cbits;
   nw = num_windows(c);
   if ((size_t)nw * stride >= (size_t(1) << 31)) throw Error(NZCB_ERR_ARG, "msm table too large for 31-bit indices");
-  q.alloc((size_t)nw * stride);
+  q.alloc((size_t)nw * stride + 1);  // + the infinity point zero digits point at
+  NZ_HIP(hipMemsetAsync(q.p + (size_t)nw * stride, 0, sizeof(G1Affine), st));
   Fq thirty_two = Fq::zero();
   thirty_two.v[0] = 32;
   const Fq k261 = to_mont(thirty_two);  // 2^261 mod p
@@ -569,6 +580,10 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
   vals_in.alloc(max_entries);
   sort_tmp_bytes = 0;
   radix_sort(nullptr, sort_tmp_bytes, keys_in.p, keys_out.p, vals_in.p, sorted.p, max_entries, 21, nullptr);
+  size_t tmp16 = 0;
+  radix_sort(nullptr, tmp16, (const uint16_t*)keys_in.p, (uint16_t*)keys_out.p, vals_in.p, sorted.p, max_entries, 16,
+             nullptr);
+  sort_tmp_bytes = std::max(sort_tmp_bytes, tmp16);
   sort_tmp.alloc(sort_tmp_bytes + 16);
   buckets.alloc(max_keys);
   size_t nthreads = (max_entries + kChunk - 1) / kChunk + 1;
@@ -594,19 +609,21 @@ MsmScratch::~MsmScratch() {
     if (e) (void)hipEventDestroy(e);
 }
 
-template <int C, bool FIXED>
-static void launch_keys(const Fr* scalars, size_t n, int mont, size_t stride, MsmScratch& sc, hipStream_t st) {
-  hipLaunchKernelGGL((msm_keys_kernel<C, FIXED>), dim3(grid_for(n, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0, st,
-                     scalars, n, mont, stride, sc.keys_in.p, sc.vals_in.p);
+template <int C, bool FIXED, class K = uint32_t>
+static void launch_keys(const Fr* scalars, size_t n, int mont, size_t stride, MsmScratch& sc, hipStream_t st,
+                        uint32_t skip_val = 0) {
+  hipLaunchKernelGGL((msm_keys_kernel<C, FIXED, K>), dim3(grid_for(n, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0,
+                     st, scalars, n, mont, stride, skip_val, (K*)sc.keys_in.p, sc.vals_in.p);
   NZ_HIP(hipGetLastError());
 }
 
 static void keys_dispatch(int c, const Fr* scalars, size_t n, int mont, const MsmBaseTable* t, MsmScratch& sc,
                           hipStream_t st) {
   if (t) {
+    const uint32_t inf_idx = (uint32_t)((size_t)t->nw * t->stride);  // the table's infinity point
     switch (c) {
-      case 16: launch_keys<16, true>(scalars, n, mont, t->stride, sc, st); return;
-      case 17: launch_keys<17, true>(scalars, n, mont, t->stride, sc, st); return;
+      case 16: launch_keys<16, true, uint16_t>(scalars, n, mont, t->stride, sc, st, inf_idx); return;
+      case 17: launch_keys<17, true, uint16_t>(scalars, n, mont, t->stride, sc, st, inf_idx); return;
       case 18: launch_keys<18, true>(scalars, n, mont, t->stride, sc, st); return;
       case 19: launch_keys<19, true>(scalars, n, mont, t->stride, sc, st); return;
       case 20: launch_keys<20, true>(scalars, n, mont, t->stride, sc, st); return;
@@ -658,13 +675,24 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   mark(0);
   keys_dispatch(p.c, scalars, n, mont ? 1 : 0, table, sc, st);
   mark(1);
-  int end_bit = 1;
-  while ((1u << end_bit) <= p.nkeys) end_bit++;
   size_t tmp = sc.sort_tmp_bytes;
-  radix_sort(sc.sort_tmp.p, tmp, sc.keys_in.p, sc.keys_out.p, sc.vals_in.p, sc.sorted.p, p.entries, end_bit, st);
-  mark(2);
-  hipLaunchKernelGGL(msm_offsets_kernel, dim3(grid_for((size_t)p.nkeys + 1, kMsmThreads, 1u << 30)),
-                     dim3(kMsmThreads), 0, st, sc.keys_out.p, p.entries, p.nkeys, sc.offsets.p);
+  const dim3 ogrid(grid_for((size_t)p.nkeys + 1, kMsmThreads, 1u << 30));
+  if (table && p.nkeys <= 65536) {  // 16-bit keys, no sentinel (see msm_keys_kernel)
+    int end_bit = 0;
+    while ((1u << end_bit) < p.nkeys) end_bit++;
+    radix_sort(sc.sort_tmp.p, tmp, (const uint16_t*)sc.keys_in.p, (uint16_t*)sc.keys_out.p, sc.vals_in.p,
+               sc.sorted.p, p.entries, end_bit, st);
+    mark(2);
+    hipLaunchKernelGGL(msm_offsets_kernel<uint16_t>, ogrid, dim3(kMsmThreads), 0, st, (const uint16_t*)sc.keys_out.p,
+                       p.entries, p.nkeys, sc.offsets.p);
+  } else {
+    int end_bit = 1;
+    while ((1u << end_bit) <= p.nkeys) end_bit++;
+    radix_sort(sc.sort_tmp.p, tmp, sc.keys_in.p, sc.keys_out.p, sc.vals_in.p, sc.sorted.p, p.entries, end_bit, st);
+    mark(2);
+    hipLaunchKernelGGL(msm_offsets_kernel<uint32_t>, ogrid, dim3(kMsmThreads), 0, st, sc.keys_out.p, p.entries,
+                       p.nkeys, sc.offsets.p);
+  }
   NZ_HIP(hipGetLastError());
   const size_t nthreads = (p.entries + kChunk - 1) / kChunk;
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[3], st));
