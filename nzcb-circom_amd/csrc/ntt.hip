@@ -13,10 +13,10 @@
 //
 // The pass is bound by Montgomery products (one per butterfly), so the kernel is
 // shaped for issue rate: 512 threads per 64 KiB tile (2 tiles per CU -> 4 waves
-// per SIMD), each thread's butterflies of a stage issue their twiddle loads
-// together before touching LDS, twiddles come from per-stage compact tables
-// (consecutive butterflies -> consecutive twiddles), and stage 0's unit twiddles
-// are skipped.
+// per SIMD), stages are done two at a time as radix-4 groups held in registers
+// (4 elements per thread: half the LDS traffic and barriers of radix-2), twiddles
+// come from per-stage compact tables (consecutive butterflies -> consecutive
+// twiddles), and stage 0's unit twiddles are skipped.
 #include "ntt.h"
 
 #include <vector>
@@ -26,6 +26,7 @@ namespace nzcb {
 static constexpr int kTileElems = 2048;  // 64 KiB of Fr per workgroup
 static constexpr int kNttThreads = 512;
 static constexpr int kBfPerThread = kTileElems / 2 / kNttThreads;  // 2
+static_assert(kTileElems / 4 == kNttThreads, "one radix-4 group per thread");
 
 Fr fr_root_of_unity(int k) {
   Fr w;
@@ -120,34 +121,58 @@ ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int s, 
   }
   __syncthreads();
   const int nbf = n_el >> 1;
-#pragma unroll 1
-  for (int st = 0; st < q; st++) {
-    const int half = 1 << st;
-    const int g = s + st;  // global stage: butterfly span 2^g
+  const Fr one = Fr::one();
+  int st = 0;
+  if (q & 1) {  // odd stage count: one radix-2 stage, then radix-4 pairs of stages
+    const int g = s;
     const Fr* __restrict__ twg = tw + (((size_t)1 << g) - 1);
-    Fr w[kBfPerThread];
-    int i0[kBfPerThread], i1[kBfPerThread];
-    bool act[kBfPerThread];
 #pragma unroll
     for (int u = 0; u < kBfPerThread; u++) {
       const int b = tid + u * kNttThreads;
-      act[u] = b < nbf;
+      if (b >= nbf) continue;
+      const int c = b & (C - 1);
+      const int j0 = b >> logC;  // stage span 1: pairs (2 pr, 2 pr + 1)
+      const int i0 = ((2 * j0) << logC) + c, i1 = ((2 * j0 + 1) << logC) + c;
+      const size_t k = first ? 0 : (lo0 + c);
+      const Fr x0 = tile[i0];
+      const Fr x1 = g ? tile[i1] * twg[k] : tile[i1];
+      tile[i0] = x0 + x1;
+      tile[i1] = x0 - x1;
+    }
+    __syncthreads();
+    st = 1;
+  }
+  // radix-4: stages st and st+1 on 4 elements per thread (half the LDS round trips and
+  // barriers of two radix-2 stages); twiddles: stage g at low, stage g+1 at low, low+h
+  const int ngroups = n_el >> 2;
+#pragma unroll 1
+  for (; st < q; st += 2) {
+    const int h = 1 << st;
+    const int g = s + st;
+    const Fr* __restrict__ twa = tw + (((size_t)1 << g) - 1);
+    const Fr* __restrict__ twb = tw + (((size_t)1 << (g + 1)) - 1);
+    const int b = tid;
+    if (b < ngroups) {
       const int c = b & (C - 1);
       const int pr = b >> logC;
-      const int low = pr & (half - 1);
-      const int j0 = ((pr >> st) << (st + 1)) | low;
-      i0[u] = (j0 << logC) + c;
-      i1[u] = ((j0 + half) << logC) + c;
-      const size_t k = first ? (size_t)low : (((size_t)low << s) + lo0 + c);
-      if (act[u] && g) w[u] = twg[k];
-    }
-#pragma unroll
-    for (int u = 0; u < kBfPerThread; u++) {
-      if (!act[u]) continue;
-      const Fr x0 = tile[i0[u]];
-      const Fr x1 = g ? tile[i1[u]] * w[u] : tile[i1[u]];
-      tile[i0[u]] = x0 + x1;
-      tile[i1[u]] = x0 - x1;
+      const int low = pr & (h - 1);
+      const int j = ((pr >> st) << (st + 2)) | low;
+      const size_t ka = first ? (size_t)low : (((size_t)low << s) + lo0 + c);
+      const size_t kc = first ? (size_t)(low + h) : (((size_t)(low + h) << s) + lo0 + c);
+      const Fr wa = g ? twa[ka] : one;
+      const Fr wb = twb[ka];
+      const Fr wc = twb[kc];
+      const int i0 = (j << logC) + c, i1 = ((j + h) << logC) + c, i2 = ((j + 2 * h) << logC) + c,
+                i3 = ((j + 3 * h) << logC) + c;
+      const Fr x0 = tile[i0], x1 = tile[i1], x2 = tile[i2], x3 = tile[i3];
+      const Fr t1 = g ? x1 * wa : x1;
+      const Fr t3 = g ? x3 * wa : x3;
+      const Fr y0 = x0 + t1, y1 = x0 - t1, y2 = x2 + t3, y3 = x2 - t3;
+      const Fr u2 = y2 * wb, u3 = y3 * wc;
+      tile[i0] = y0 + u2;
+      tile[i2] = y0 - u2;
+      tile[i1] = y1 + u3;
+      tile[i3] = y1 - u3;
     }
     __syncthreads();
   }
