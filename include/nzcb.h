@@ -123,6 +123,23 @@ int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]);
 int nzcb_proof_to_json(const uint8_t* proof, char* out, size_t cap);
 int nzcb_public_to_json(const uint8_t* pub, int n_public, char* out, size_t cap);
 
+/* ---- Verification key, verifier, Solidity calldata ----
+ * Host-only (no GPU needed). Binary verification key, NZCB_VK_BYTES:
+ *   u32 nPublic | u32 power | k1, k2 (Fr, 32 B LE) | Qm Ql Qr Qo Qc S1 S2 S3 (G1 x||y,
+ *   32 B LE each, infinity = zeros) | X_2 (x.c0 x.c1 y.c0 y.c1, 32 B LE) | w (Fr, 32 B LE)
+ * Replaces snarkjs `zkey export verificationkey` (/root/reference/Makefile:56,61). */
+#define NZCB_VK_BYTES (8 + 2 * 32 + 8 * 64 + 4 * 32 + 32)
+int nzcb_vk_from_zkey(const uint8_t* zkey, size_t zkey_len, uint8_t* vk_out, nzcb_err* err);
+/* verification_key.json text (snarkjs layout); returns 0, or the needed size if cap is short. */
+int nzcb_vk_to_json(const uint8_t* vk, char* out, size_t cap);
+/* snarkjs plonk.verify: *valid = 1 if the proof (NZCB_PROOF_BYTES) is valid for the public
+ * signals (n_public x 32 B LE), else 0. transcript_public as nzcb_ctx_set_transcript_public. */
+int nzcb_verify(const uint8_t* vk, const uint8_t* proof, const uint8_t* pub, int n_public, int transcript_public,
+                int* valid, nzcb_err* err);
+/* snarkjs `zkey export soliditycalldata` for PLONK (/root/reference/Makefile:57,62 verifier):
+ * "0x<proof hex>,[\"0x<pub>\",...]"; returns 0, or the needed size if cap is short. */
+int nzcb_proof_to_calldata(const uint8_t* proof, const uint8_t* pub, int n_public, char* out, size_t cap);
+
 /* ---- Synthetic circuit + setup ------- */
 /* Builds the seeded synthetic circuit of oracle/synth.py and its snarkjs-0.4
  * PLONK zkey with trapdoor tau (32-byte LE normal) on `device`. Buffers are

@@ -11,6 +11,27 @@
 
 namespace nzcb {
 void set_err(nzcb_err* err, int code, const char* msg);
+
+// decimal string of a 32-byte little-endian integer (snarkjs stringifyBigInts)
+std::string dec_le32(const uint8_t* le32) {
+  uint32_t v[8];
+  std::memcpy(v, le32, 32);
+  std::string s;
+  bool nz = true;
+  while (nz) {
+    uint64_t rem = 0;
+    nz = false;
+    for (int i = 7; i >= 0; i--) {
+      uint64_t cur = (rem << 32) | v[i];
+      v[i] = (uint32_t)(cur / 10);
+      rem = cur % 10;
+      if (v[i]) nz = true;
+    }
+    s.push_back((char)('0' + rem));
+  }
+  return std::string(s.rbegin(), s.rend());
+}
+
 }
 using namespace nzcb;
 
@@ -31,25 +52,6 @@ int fail(nzcb_err* err, int code, const char* msg) {
   return code;
 }
 
-std::string dec_le(const uint8_t* le32) {
-  uint32_t v[8];
-  std::memcpy(v, le32, 32);
-  std::string s;
-  bool nz = true;
-  while (nz) {
-    uint64_t rem = 0;
-    nz = false;
-    for (int i = 7; i >= 0; i--) {
-      uint64_t cur = (rem << 32) | v[i];
-      v[i] = (uint32_t)(cur / 10);
-      rem = cur % 10;
-      if (v[i]) nz = true;
-    }
-    s.push_back((char)('0' + rem));
-  }
-  return std::string(s.rbegin(), s.rend());
-}
-
 bool all_zero(const uint8_t* p, size_t n) {
   for (size_t i = 0; i < n; i++)
     if (p[i]) return false;
@@ -58,7 +60,7 @@ bool all_zero(const uint8_t* p, size_t n) {
 
 std::string g1_json(const uint8_t* p) {
   if (all_zero(p, 64)) return "[\"0\",\"1\",\"0\"]";
-  return "[\"" + dec_le(p) + "\",\"" + dec_le(p + 32) + "\",\"1\"]";
+  return "[\"" + dec_le32(p) + "\",\"" + dec_le32(p + 32) + "\",\"1\"]";
 }
 
 int copy_out(const std::string& s, char* out, size_t cap) {
@@ -269,7 +271,7 @@ int nzcb_proof_to_json(const uint8_t* proof, char* out, size_t cap) {
   static const char* evs[7] = {"eval_a", "eval_b", "eval_c", "eval_s1", "eval_s2", "eval_zw", "eval_r"};
   std::string s = "{";
   for (int i = 0; i < 7; i++) s += std::string("\"") + pts[i] + "\":" + g1_json(proof + 64 * i) + ",";
-  for (int i = 0; i < 7; i++) s += std::string("\"") + evs[i] + "\":\"" + dec_le(proof + 9 * 64 + 32 * i) + "\",";
+  for (int i = 0; i < 7; i++) s += std::string("\"") + evs[i] + "\":\"" + dec_le32(proof + 9 * 64 + 32 * i) + "\",";
   s += "\"Wxi\":" + g1_json(proof + 7 * 64) + ",";
   s += "\"Wxiw\":" + g1_json(proof + 8 * 64) + ",";
   s += "\"protocol\":\"plonk\",\"curve\":\"bn128\"}";
@@ -280,7 +282,7 @@ int nzcb_public_to_json(const uint8_t* pub, int n_public, char* out, size_t cap)
   std::string s = "[";
   for (int i = 0; i < n_public; i++) {
     if (i) s += ",";
-    s += "\"" + dec_le(pub + 32 * i) + "\"";
+    s += "\"" + dec_le32(pub + 32 * i) + "\"";
   }
   s += "]";
   return copy_out(s, out, cap);

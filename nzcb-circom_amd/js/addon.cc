@@ -207,6 +207,102 @@ napi_value DeviceCount(napi_env env, napi_callback_info) {
   return s;
 }
 
+// buffer argument i -> (data, len); false if not a Buffer
+bool buf_arg(napi_env env, napi_value v, const uint8_t** data, size_t* len) {
+  void* d = nullptr;
+  if (napi_get_buffer_info(env, v, &d, len) != napi_ok) return false;
+  *data = static_cast<const uint8_t*>(d);
+  return true;
+}
+
+napi_value json_string(napi_env env, const std::string& s) {
+  napi_value v;
+  napi_create_string_utf8(env, s.c_str(), s.size(), &v);
+  return v;
+}
+
+// vkFromZkey(zkey: Buffer) -> Buffer (NZCB_VK_BYTES); snarkjs `zkey export verificationkey`
+napi_value VkFromZkey(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  const uint8_t* z;
+  size_t zl;
+  if (argc < 1 || !buf_arg(env, argv[0], &z, &zl)) {
+    napi_throw_type_error(env, nullptr, "vkFromZkey(zkey: Buffer)");
+    return nullptr;
+  }
+  void* out = nullptr;
+  napi_value res;
+  CHECK(napi_create_buffer(env, NZCB_VK_BYTES, &out, &res));
+  nzcb_err err{};
+  if (nzcb_vk_from_zkey(z, zl, static_cast<uint8_t*>(out), &err) != 0) {
+    napi_throw(env, make_error(env, err.code, err.msg));
+    return nullptr;
+  }
+  return res;
+}
+
+// vkToJson(vk: Buffer) -> string (verification_key.json)
+napi_value VkToJson(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  const uint8_t* vk;
+  size_t vl;
+  if (argc < 1 || !buf_arg(env, argv[0], &vk, &vl) || vl != NZCB_VK_BYTES) {
+    napi_throw_type_error(env, nullptr, "vkToJson(vk: Buffer)");
+    return nullptr;
+  }
+  std::string s((size_t)nzcb_vk_to_json(vk, nullptr, 0), '\0');
+  nzcb_vk_to_json(vk, &s[0], s.size());
+  s.resize(std::strlen(s.c_str()));
+  return json_string(env, s);
+}
+
+// verify(vk: Buffer, proof: Buffer, pub: Buffer, transcriptPublic: bool) -> bool (snarkjs plonk.verify)
+napi_value Verify(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  const uint8_t *vk, *proof, *pub;
+  size_t vl, pl, ul;
+  if (argc < 3 || !buf_arg(env, argv[0], &vk, &vl) || !buf_arg(env, argv[1], &proof, &pl) ||
+      !buf_arg(env, argv[2], &pub, &ul) || vl != NZCB_VK_BYTES || pl != NZCB_PROOF_BYTES || ul % 32) {
+    napi_throw_type_error(env, nullptr, "verify(vk: Buffer, proof: Buffer, pub: Buffer, transcriptPublic)");
+    return nullptr;
+  }
+  bool tp = true;
+  if (argc > 3) napi_get_value_bool(env, argv[3], &tp);
+  int valid = 0;
+  nzcb_err err{};
+  if (nzcb_verify(vk, proof, pub, (int)(ul / 32), tp ? 1 : 0, &valid, &err) != 0) {
+    napi_throw(env, make_error(env, err.code, err.msg));
+    return nullptr;
+  }
+  napi_value r;
+  napi_get_boolean(env, valid != 0, &r);
+  return r;
+}
+
+// calldata(proof: Buffer, pub: Buffer) -> string (snarkjs `zkey export soliditycalldata`)
+napi_value Calldata(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  const uint8_t *proof, *pub;
+  size_t pl, ul;
+  if (argc < 2 || !buf_arg(env, argv[0], &proof, &pl) || !buf_arg(env, argv[1], &pub, &ul) ||
+      pl != NZCB_PROOF_BYTES || ul % 32) {
+    napi_throw_type_error(env, nullptr, "calldata(proof: Buffer, pub: Buffer)");
+    return nullptr;
+  }
+  std::string s((size_t)nzcb_proof_to_calldata(proof, pub, (int)(ul / 32), nullptr, 0), '\0');
+  nzcb_proof_to_calldata(proof, pub, (int)(ul / 32), &s[0], s.size());
+  s.resize(std::strlen(s.c_str()));
+  return json_string(env, s);
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"createContext", nullptr, CreateContext, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -214,6 +310,10 @@ napi_value Init(napi_env env, napi_value exports) {
       {"info", nullptr, Info, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"vkFromZkey", nullptr, VkFromZkey, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"vkToJson", nullptr, VkToJson, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"verify", nullptr, Verify, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"calldata", nullptr, Calldata, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

@@ -177,8 +177,54 @@ async function fullProve(input, wasmFile, zkeyFileName, logger, options) {
   return prove(zkeyFileName, { type: 'mem', data: wtns }, logger, options);
 }
 
+// ---------------------------------------------------------------------------
+// Verification key, verifier, Solidity calldata (SURVEY.md §8f ranks 1 and 4):
+// snarkjs zKey.exportVerificationKey / plonk.verify / plonk.exportSolidityCallData.
+// ---------------------------------------------------------------------------
+const PROOF_POINTS = ['A', 'B', 'C', 'Z', 'T1', 'T2', 'T3', 'Wxi', 'Wxiw'];
+const PROOF_EVALS = ['eval_a', 'eval_b', 'eval_c', 'eval_s1', 'eval_s2', 'eval_zw', 'eval_r'];
+const VK_POINTS = ['Qm', 'Ql', 'Qr', 'Qo', 'Qc', 'S1', 'S2', 'S3'];
+
+function le32(x) {
+  let v = BigInt(x);
+  const out = Buffer.alloc(32);
+  for (let i = 0; i < 32; i++) { out[i] = Number(v & BigInt(255)); v >>= BigInt(8); }
+  return out;
+}
+function g1Buf(p) { return String(p[2]) === '0' ? Buffer.alloc(64) : Buffer.concat([le32(p[0]), le32(p[1])]); }
+function proofBuf(proof) {
+  return Buffer.concat(PROOF_POINTS.map((k) => g1Buf(proof[k])).concat(PROOF_EVALS.map((k) => le32(proof[k]))));
+}
+function pubBuf(pub) { return Buffer.concat(pub.map(le32).concat([Buffer.alloc(0)])); }
+function vkBuf(vk) {
+  const head = Buffer.alloc(8);
+  head.writeUInt32LE(Number(vk.nPublic), 0);
+  head.writeUInt32LE(Number(vk.power), 4);
+  const x2 = vk.X_2;
+  return Buffer.concat([head, le32(vk.k1), le32(vk.k2)].concat(VK_POINTS.map((k) => g1Buf(vk[k])))
+    .concat([le32(x2[0][0]), le32(x2[0][1]), le32(x2[1][0]), le32(x2[1][1]), le32(vk.w)]));
+}
+
+async function exportVerificationKey(zkeyFileName) {
+  return JSON.parse(addon.vkToJson(addon.vkFromZkey(readBin(zkeyFileName))));
+}
+
+async function verify(vkVerifier, publicSignals, proof, logger, options) {
+  options = options || {};
+  const tp = options.transcriptPublic === undefined ? true : !!options.transcriptPublic;
+  const ok = addon.verify(vkBuf(vkVerifier), proofBuf(proof), pubBuf(publicSignals), tp);
+  const log = loggerFn(logger);
+  if (log) log(ok ? 'OK!' : 'Invalid proof');
+  return ok;
+}
+
+async function exportSolidityCallData(proof, publicSignals) {
+  return addon.calldata(proofBuf(proof), pubBuf(publicSignals));
+}
+
 module.exports = {
-  plonk: { prove, fullProve },
+  plonk: { prove, fullProve, verify, exportSolidityCallData },
+  zKey: { exportVerificationKey },
   wtns: { calculate: wtnsCalculate },
   version: addon.version,
   deviceCount: addon.deviceCount,

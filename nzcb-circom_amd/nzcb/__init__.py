@@ -21,6 +21,10 @@ LIB_PATH = os.environ.get("NZCB_LIB", os.path.join(os.path.dirname(_HERE), "lib"
 
 PROOF_BYTES = 9 * 64 + 7 * 32
 BLINDING_BYTES = 11 * 32
+VK_BYTES = 8 + 2 * 32 + 8 * 64 + 4 * 32 + 32
+PROOF_POINTS = ("A", "B", "C", "Z", "T1", "T2", "T3", "Wxi", "Wxiw")
+PROOF_EVALS = ("eval_a", "eval_b", "eval_c", "eval_s1", "eval_s2", "eval_zw", "eval_r")
+VK_POINTS = ("Qm", "Ql", "Qr", "Qo", "Qc", "S1", "S2", "S3")
 
 ERROR_NAMES = {
     0: "OK", 1: "ARG", 2: "FORMAT", 3: "NOT_PLONK", 4: "CURVE", 5: "WITNESS_LEN", 6: "COPY",
@@ -36,7 +40,8 @@ EXPORTED_SYMBOLS = [
     "nzcb_dev_free", "nzcb_memcpy_h2d", "nzcb_memcpy_d2h", "nzcb_engine_ntt_dev", "nzcb_engine_msm_dev",
     "nzcb_engine_time_ntt", "nzcb_engine_fr_mul", "nzcb_engine_random_fr", "nzcb_engine_fixed_base",
     "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
-    "nzcb_ctx_lanes", "nzcb_prove_batch",
+    "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_to_json", "nzcb_verify",
+    "nzcb_proof_to_calldata",
 ]
 
 
@@ -76,6 +81,10 @@ def load(path: str | None = None):
         "nzcb_prove_device": (c_int, [c_void_p, c_void_p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
         "nzcb_ctx_kernel_stats": (c_int, [c_void_p, c_int, POINTER(c_double)]),
         "nzcb_ctx_set_lanes": (c_int, [c_void_p, c_int, POINTER(_Err)]),
+        "nzcb_vk_from_zkey": (c_int, [u8p, c_size_t, u8p, POINTER(_Err)]),
+        "nzcb_vk_to_json": (c_int, [u8p, ctypes.c_char_p, c_size_t]),
+        "nzcb_verify": (c_int, [u8p, u8p, u8p, c_int, c_int, POINTER(c_int), POINTER(_Err)]),
+        "nzcb_proof_to_calldata": (c_int, [u8p, u8p, c_int, ctypes.c_char_p, c_size_t]),
         "nzcb_ctx_lanes": (c_int, [c_void_p]),
         "nzcb_prove_batch": (c_int, [c_void_p, POINTER(c_void_p), c_size_t, c_int, c_int, u8p, u8p, u8p, c_size_t,
                                      POINTER(_Err)]),
@@ -415,8 +424,77 @@ def public_to_json(pub: bytes, n_public: int) -> list:
     return json.loads(out.value.decode())
 
 
+def _json_text(fn, *args) -> str:
+    need = fn(*args, None, 0)
+    out = ctypes.create_string_buffer(max(need, 1))
+    rc = fn(*args, out, max(need, 1))
+    if rc != 0:
+        raise NzcbError(11, "json encoding failed")
+    return out.value.decode()
+
+
+def vk_from_zkey(zkey) -> bytes:
+    """Binary verification key (include/nzcb.h NZCB_VK_BYTES) of a zkey (bytes or path)."""
+    data = open(zkey, "rb").read() if isinstance(zkey, str) else zkey
+    out = _out(VK_BYTES)
+    err = _Err()
+    _check(load().nzcb_vk_from_zkey(_buf(data), len(data), out, ctypes.byref(err)), err)
+    return bytes(out)
+
+
+def vk_to_json(vk: bytes) -> dict:
+    """snarkjs verification_key.json object."""
+    import json
+    return json.loads(_json_text(load().nzcb_vk_to_json, _buf(vk)))
+
+
+def _le(x) -> bytes:
+    return int(x).to_bytes(32, "little")
+
+
+def vk_from_json(obj: dict) -> bytes:
+    """verification_key.json (snarkjs layout) -> binary verification key."""
+    def g1(p):
+        return bytes(64) if str(p[2]) == "0" else _le(p[0]) + _le(p[1])
+
+    out = int(obj["nPublic"]).to_bytes(4, "little") + int(obj["power"]).to_bytes(4, "little")
+    out += _le(obj["k1"]) + _le(obj["k2"])
+    out += b"".join(g1(obj[k]) for k in VK_POINTS)
+    (x0, x1), (y0, y1) = obj["X_2"][0], obj["X_2"][1]
+    out += _le(x0) + _le(x1) + _le(y0) + _le(y1) + _le(obj["w"])
+    return out
+
+
+def proof_from_json(obj: dict) -> bytes:
+    """snarkjs proof object -> NZCB_PROOF_BYTES."""
+    def g1(p):
+        return bytes(64) if str(p[2]) == "0" else _le(p[0]) + _le(p[1])
+
+    return b"".join(g1(obj[k]) for k in PROOF_POINTS) + b"".join(_le(obj[k]) for k in PROOF_EVALS)
+
+
+def verify(vk: bytes, proof: bytes, public: bytes, transcript_public: bool = True) -> bool:
+    """Pairing verification of a binary proof; public = nPublic x 32-byte LE."""
+    valid = c_int(0)
+    err = _Err()
+    _check(load().nzcb_verify(_buf(vk), _buf(proof), _buf(public), len(public) // 32, int(transcript_public),
+                              ctypes.byref(valid), ctypes.byref(err)), err)
+    return bool(valid.value)
+
+
+def proof_to_calldata(proof: bytes, public: bytes) -> str:
+    """snarkjs `zkey export soliditycalldata` text for a PLONK proof."""
+    return _json_text(load().nzcb_proof_to_calldata, _buf(proof), _buf(public), len(public) // 32)
+
+
 class plonk:
-    """snarkjs-compatible entry points (``snarkjs.plonk.prove`` [EXT])."""
+    """snarkjs-compatible entry points (``snarkjs.plonk.prove`` / ``verify`` [EXT])."""
+
+    @staticmethod
+    def verify(vk_verifier: dict, publicSignals, proof: dict, transcript_public: bool = True) -> bool:
+        """snarkjs.plonk.verify(vkey, publicSignals, proof) on the JSON objects."""
+        pub = b"".join(_le(x) for x in publicSignals)
+        return verify(vk_from_json(vk_verifier), proof_from_json(proof), pub, transcript_public)
 
     @staticmethod
     def prove(zkeyFileName, witnessFileName, logger=None, device: int = 0, blinding: bytes | None = None):

@@ -516,3 +516,62 @@ def verify_with_trapdoor(vk: dict, public, proof, tau: int, transcript_pub=True)
         return False
     _, lhs, rhs = verify_prepare(vk, public, proof, transcript_pub)
     return bn.g1_mul(lhs, tau) == rhs
+
+
+# ---------------------------------------------------------------------------
+# verification key, pairing verifier, calldata
+# ---------------------------------------------------------------------------
+VK_POINTS = ("Qm", "Ql", "Qr", "Qo", "Qc", "S1", "S2", "S3")
+
+
+def vk_from_zkey(zk: dict) -> dict:
+    """snarkjs 0.4.x `zkey export verificationkey` for PLONK (zkey_export_verificationkey.js
+    [EXT], run at /root/reference/Makefile:56,61): the header facts and the selector /
+    permutation commitments, X_2 = [tau]_2 and the domain generator w."""
+    vk = {"protocol": "plonk", "curve": "bn128", "nPublic": zk["nPublic"], "power": zk["power"],
+          "k1": zk["k1"], "k2": zk["k2"]}
+    for k in VK_POINTS:
+        vk[k] = zk[k]
+    vk["X_2"] = zk["X_2"]
+    vk["w"] = FR_W[zk["power"]]
+    vk["domainSize"] = zk["domainSize"]
+    return vk
+
+
+def vk_to_json_obj(vk: dict) -> dict:
+    """verification_key.json layout (decimal strings, projective "1" coordinates)."""
+    def g1(p):
+        return ["0", "1", "0"] if p is None else [str(p[0]), str(p[1]), "1"]
+
+    out = {"protocol": "plonk", "curve": "bn128", "nPublic": vk["nPublic"], "power": vk["power"],
+           "k1": str(vk["k1"]), "k2": str(vk["k2"])}
+    for k in VK_POINTS:
+        out[k] = g1(vk[k])
+    (x0, x1), (y0, y1) = vk["X_2"]
+    out["X_2"] = [[str(x0), str(x1)], [str(y0), str(y1)], ["1", "0"]]
+    out["w"] = str(vk["w"])
+    return out
+
+
+def verify(vk: dict, public, proof, transcript_pub=True) -> bool:
+    """snarkjs plonk_verify restated with the pairing: e(-lhs, X_2) * e(rhs, [1]_2) == 1
+    (lhs = Wxi + u Wxiw, rhs = xi Wxi + u xi w Wxiw + F - E; see verify_prepare)."""
+    from . import pairing
+    if any(not bn.g1_is_on_curve(proof[k]) for k in PROOF_POINTS):
+        return False
+    if any(not 0 <= proof[k] < R_MOD for k in PROOF_EVALS) or any(not 0 <= x < R_MOD for x in public):
+        return False
+    vk = dict(vk)
+    vk.setdefault("domainSize", 1 << vk["power"])
+    _, lhs, rhs = verify_prepare(vk, public, proof, transcript_pub)
+    return pairing.pairing_check([(bn.g1_neg(lhs), vk["X_2"]), (rhs, bn.G2_GEN)])
+
+
+def solidity_calldata(proof, public) -> str:
+    """snarkjs 0.4.x `zkey export soliditycalldata` for PLONK (plonk_exportsoliditycalldata.js
+    [EXT], consumer at /root/reference/Makefile:57,62): "0x" + the 9 points as uncompressed
+    big-endian x||y and the 7 evaluations big-endian, then the public signals as 0x-hex."""
+    buf = b"".join(bn.g1_to_uncompressed(proof[k]) for k in PROOF_POINTS)
+    buf += b"".join(_fr_be(proof[k]) for k in PROOF_EVALS)
+    pubs = ",".join('"0x%064x"' % x for x in public)
+    return "0x" + buf.hex() + ",[" + pubs + "]"
