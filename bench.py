@@ -86,6 +86,9 @@ def main():
     ap.add_argument("--lanes", type=int, default=2, help="proofs in flight per GPU")
     ap.add_argument("--batch", type=int, default=0,
                     help="fixed total batch sharded over the ranks (configs[3]: 512); default: --steps per rank")
+    ap.add_argument("--msm-devices", default="",
+                    help="configs[4] single-proof mode: split each MSM over these device ids, e.g. 0,1,2,3 "
+                         "(one process; lanes forced to 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -124,6 +127,10 @@ def main():
     t_h = time.perf_counter()
     ctx.prove_witness_raw(wtns[76:76 + nwit * 32], blinding_for(999))
     pcie_ms = (time.perf_counter() - t_h) * 1e3
+    msm_devices = [int(x) for x in args.msm_devices.split(",") if x.strip() != ""]
+    if msm_devices:
+        ctx.set_msm_devices(msm_devices)
+        args.lanes = 1
     ctx.set_lanes(args.lanes)
     if args.warmup:
         nw = max(args.warmup, args.lanes)
@@ -189,6 +196,7 @@ def main():
                 "total_proofs": total_proofs,
                 "parallelism": f"batch-shard x{world} (no collective)",
                 "proofs_in_flight_per_gpu": args.lanes,
+                "msm_devices": msm_devices or None,
             },
             "roofline": {
                 "kernel": "msm_accumulate_kernel (Pippenger bucket accumulation)",

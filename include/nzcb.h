@@ -100,6 +100,13 @@ int nzcb_prove_device(nzcb_ctx* ctx, const void* dev_witness, size_t n_witness, 
 int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err);
 int nzcb_ctx_lanes(const nzcb_ctx* ctx);
 
+/* Single-proof mode across GPUs: every commitment MSM of lane 0
+ * is split by point range over devices[0..ndev) (devices[0] = the context's device); each
+ * other device holds the shifted-base table of its PTau range, receives its scalar slice
+ * by a peer copy over xGMI and returns one 96-byte partial, which the host adds. ndev = 1
+ * restores the single-device schedule. Results are bit-identical either way. */
+int nzcb_ctx_set_msm_devices(nzcb_ctx* ctx, const int* devices, int ndev, nzcb_err* err);
+
 /* `count` independent proofs over the context's lanes (SURVEY.md §8b nzcb_prove_batch,
  * §8e batch mode). witnesses[i]: nWitness x 32-byte LE normal-form values, host memory,
  * or device pointers when witness_on_device. blindings: count x NZCB_BLINDING_BYTES or

@@ -129,6 +129,20 @@ int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err) {
 
 int nzcb_ctx_lanes(const nzcb_ctx* ctx) { return ctx ? (int)ctx->lanes() : 0; }
 
+int nzcb_ctx_set_msm_devices(nzcb_ctx* ctx, const int* devices, int ndev, nzcb_err* err) {
+  if (!ctx || !devices || ndev < 1 || ndev > 64) return fail(err, NZCB_ERR_ARG, "devices: 1..64 ids");
+  try {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->p->set_msm_devices(std::vector<int>(devices, devices + ndev));
+    if (err) err->code = 0;
+    return 0;
+  } catch (const Error& e) {
+    return fail(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, NZCB_ERR_INTERNAL, e.what());
+  }
+}
+
 int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witness, int count, int witness_on_device,
                      const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out, size_t pub_stride,
                      nzcb_err* err) {

@@ -16,6 +16,21 @@ struct AddRec {  // one addition, reordered by dependency level
   Fr ac, bc;
 };
 
+// one proof's MSMs split by point range over several devices
+// of this process. A shard holds the shifted-base table of its PTau range and per-slot
+// MSM scratch; the scalar slice arrives by a device-to-device copy over xGMI and the
+// 96-byte partial comes back to the host, where the partials are added.
+struct MsmShard {
+  static constexpr int kSlots = 3;
+  int device = 0;
+  size_t lo = 0, hi = 0;
+  MsmBaseTable table;
+  std::unique_ptr<MsmScratch> sc[kSlots];
+  DevBuf<Fr> scal[kSlots];
+  hipStream_t st[kSlots] = {nullptr, nullptr, nullptr};
+  ~MsmShard();
+};
+
 struct Prover {
   // zkey facts
   uint32_t n = 0, n4 = 0, nVars = 0, nPublic = 0, nAdditions = 0, nConstraints = 0, nWit = 0;
@@ -63,6 +78,10 @@ struct Prover {
 
   Prover(const uint8_t* zkey, size_t len, int device);
   Prover(const Prover& primary, int lane);  // extra lane sharing primary's proving key
+  // Split every commitment MSM over devices[0] (this prover's device) and the others.
+  void set_msm_devices(const std::vector<int>& devices);
+  std::vector<std::unique_ptr<MsmShard>> shards;
+  size_t own_hi = 0;  // this device's MSM point range is [0, own_hi) when shards exist
   // witness: nWit x 32-byte LE normal-form values; blinding: 11 x 32-byte LE or null
   // witness_on_device: `witness` is a device pointer (HBM-resident input, no PCIe copy)
   void prove(const uint8_t* witness, size_t n_witness, const uint8_t* blinding, uint8_t* proof_out,

@@ -381,6 +381,48 @@ Prover::~Prover() {
   }
 }
 
+MsmShard::~MsmShard() {
+  (void)hipSetDevice(device);
+  for (auto& s : st)
+    if (s) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+}
+
+void Prover::set_msm_devices(const std::vector<int>& devices) {
+  if (devices.empty() || devices[0] != eng->device)
+    throw Error(NZCB_ERR_ARG, "msm devices must start with the context's device");
+  shards.clear();
+  own_hi = 0;
+  const size_t N = ptau.n;  // n + 6 bases
+  const size_t k = devices.size();
+  if (k == 1) return;
+  own_hi = N / k;
+  for (size_t i = 1; i < k; i++) {
+    auto sh = std::make_unique<MsmShard>();
+    sh->device = devices[i];
+    sh->lo = N * i / k;
+    sh->hi = N * (i + 1) / k;
+    const size_t cnt = sh->hi - sh->lo;
+    NZ_HIP(hipSetDevice(sh->device));
+    for (int j = 0; j < MsmShard::kSlots; j++) {
+      NZ_HIP(hipStreamCreateWithFlags(&sh->st[j], hipStreamNonBlocking));
+      sh->sc[j].reset(new MsmScratch());
+      sh->sc[j]->init(cnt, true);
+      sh->scal[j].alloc(cnt);
+    }
+    {  // the shard's PTau range -> its shifted-base table (built on the shard's device)
+      DevBuf<G1Affine> part(cnt);
+      NZ_HIP(hipMemcpyPeerAsync(part.p, sh->device, ptau.p + sh->lo, eng->device, cnt * sizeof(G1Affine), sh->st[0]));
+      sh->table.build(part.p, cnt, fixed_base_window(), sh->st[0]);
+      NZ_HIP(hipStreamSynchronize(sh->st[0]));
+    }
+    shards.push_back(std::move(sh));
+  }
+  NZ_HIP(hipSetDevice(eng->device));
+}
+
 double Prover::ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -588,12 +630,31 @@ void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int n
 void Prover::commit_start(int slot, const Fr* coefs, size_t len) {
   NZ_HIP(hipEventRecord(ready[slot], st()));
   NZ_HIP(hipStreamWaitEvent(aux[slot], ready[slot], 0));
+  if (!shards.empty()) {
+    for (auto& sh : shards) {
+      const size_t cnt = len > sh->lo ? std::min(len, sh->hi) - sh->lo : 0;
+      NZ_HIP(hipSetDevice(sh->device));
+      if (cnt) {
+        NZ_HIP(hipStreamWaitEvent(sh->st[slot], ready[slot], 0));
+        NZ_HIP(hipMemcpyPeerAsync(sh->scal[slot].p, sh->device, coefs + sh->lo, eng->device, cnt * sizeof(Fr),
+                                  sh->st[slot]));
+      }
+      msm_enqueue(*sh->sc[slot], nullptr, sh->scal[slot].p, cnt, true, sh->st[slot], &sh->table);  // cnt 0: no-op
+    }
+    NZ_HIP(hipSetDevice(eng->device));
+    len = std::min(len, own_hi);
+  }
   msm_enqueue(*msc[slot], ptau.p, coefs, len, true, aux[slot], &ptab);
 }
 
 G1Affine Prover::commit_finish(int slot) {
   auto t0 = std::chrono::steady_clock::now();
   G1xyzz r = msm_finish(*msc[slot], aux[slot]);
+  for (auto& sh : shards) {  // partial sums of the other devices' point ranges
+    NZ_HIP(hipSetDevice(sh->device));
+    r = xyzz_add(r, msm_finish(*sh->sc[slot], sh->st[slot]));
+  }
+  if (!shards.empty()) NZ_HIP(hipSetDevice(eng->device));
   msm_ms += ms_since(t0);
   return xyzz_to_affine(r);
 }

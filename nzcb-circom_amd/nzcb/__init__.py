@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_engine_time_ntt", "nzcb_engine_fr_mul", "nzcb_engine_random_fr", "nzcb_engine_fixed_base",
     "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_to_json", "nzcb_verify",
-    "nzcb_proof_to_calldata",
+    "nzcb_proof_to_calldata", "nzcb_ctx_set_msm_devices",
 ]
 
 
@@ -81,6 +81,7 @@ def load(path: str | None = None):
         "nzcb_prove_device": (c_int, [c_void_p, c_void_p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
         "nzcb_ctx_kernel_stats": (c_int, [c_void_p, c_int, POINTER(c_double)]),
         "nzcb_ctx_set_lanes": (c_int, [c_void_p, c_int, POINTER(_Err)]),
+        "nzcb_ctx_set_msm_devices": (c_int, [c_void_p, POINTER(c_int), c_int, POINTER(_Err)]),
         "nzcb_vk_from_zkey": (c_int, [u8p, c_size_t, u8p, POINTER(_Err)]),
         "nzcb_vk_to_json": (c_int, [u8p, ctypes.c_char_p, c_size_t]),
         "nzcb_verify": (c_int, [u8p, u8p, u8p, c_int, c_int, POINTER(c_int), POINTER(_Err)]),
@@ -353,6 +354,12 @@ class ProverContext:
         """Proofs kept in flight by prove_batch (extra lanes share the resident proving key)."""
         err = _Err()
         _check(self.lib.nzcb_ctx_set_lanes(self.h, lanes, ctypes.byref(err)), err)
+
+    def set_msm_devices(self, devices):
+        """Split each commitment MSM over these devices (first = the context's device)."""
+        arr = (c_int * len(devices))(*devices)
+        err = _Err()
+        _check(self.lib.nzcb_ctx_set_msm_devices(self.h, arr, len(devices), ctypes.byref(err)), err)
 
     @property
     def lanes(self) -> int:

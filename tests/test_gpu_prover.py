@@ -197,3 +197,35 @@ def test_batch_reports_lowest_failing_index():
     with pytest.raises(nzcb.NzcbError) as ei:
         ctx.prove_batch_raw([good, good, bad, good, bad])
     assert str(ei.value) == "proof 2: T Polynomial is not divisible"
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_msm_split_over_devices_bit_exact(devices):
+    """commitment MSMs split by point range over several
+    devices (here the same device several times: the partition, the peer copies and the
+    host-side sum of partials are exercised) give the golden proof bits."""
+    meta, zkey, wtns = _gold("p8")
+    ctx = nzcb.ProverContext(zkey)
+    ctx.set_msm_devices(devices)
+    for bl in ("fixed", "zero"):
+        exp = meta["proofs"][bl]
+        blinding = bytes.fromhex(exp["blinding"]) if exp["blinding"] else None
+        proof, _ = ctx.prove_raw(wtns, blinding)
+        assert proof.hex() == exp["proof_bin"]
+    ctx.set_msm_devices([0])
+    proof, _ = ctx.prove_raw(wtns, bytes.fromhex(meta["proofs"]["fixed"]["blinding"]))
+    assert proof.hex() == meta["proofs"]["fixed"]["proof_bin"]
+    with pytest.raises(nzcb.NzcbError):
+        ctx.set_msm_devices([1 if nzcb.device_count() > 1 else 5, 0])
+
+
+def test_msm_split_live_oracle():
+    c = synth.synth_circuit(10, 3, 8, seed=41)
+    zk = plonk.setup(c, 99991)
+    from oracle.bn254 import R_MOD
+    bl = [(41 * 7919 + i * 104729 + (i << 200)) % R_MOD for i in range(11)]
+    proof, pub = plonk.prove(zk, c["witness"], bl)
+    ctx = nzcb.ProverContext(binfmt.write_zkey(zk))
+    ctx.set_msm_devices([0, 0, 0, 0])
+    got, _ = ctx.prove_raw(binfmt.write_wtns(c["witness"]), b"".join(x.to_bytes(32, "little") for x in bl))
+    assert got == plonk.proof_to_bytes(proof)
