@@ -146,6 +146,9 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     assert len({p for p, _ in proofs}) == len(mine)  # distinct blindings -> distinct proofs
+    # full-size parity by a size-independent property: the pairing verifier accepts the
+    # first and last proof of the timed batch (host, outside the timed region)
+    verified = all(nzcb.verify(ctx.vk, proofs[i][0], proofs[i][1]) for i in {0, len(proofs) - 1})
     kms, klaunch, kpoints, kentries = ctx.kernel_stats(0)
     elapsed = max_over_ranks(elapsed, dist, f"cuda:{local}")
     total_proofs = args.batch if args.batch else args.steps * world
@@ -220,6 +223,7 @@ def main():
                 "achieved_GBs": round(proof_gbs, 2),
                 "frac": round(proof_gbs / HBM_PEAK_GBS, 5),
             },
+            "proofs_verified": verified,
             "single_proof_latency_ms": round(latency_ms, 3),
             "phase_ms_single_proof": {k: round(v, 3) for k, v in single_timings.items()},
             "pcie_inclusive_ms": round(pcie_ms, 3),

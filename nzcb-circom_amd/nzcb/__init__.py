@@ -288,14 +288,18 @@ class ProverContext:
     def __init__(self, zkey, device: int = 0, logger=None, transcript_public: bool = True, _raw=None):
         self.lib = load()
         err = _Err()
+        vk = _out(VK_BYTES)
         if _raw is not None:            # (pointer, length) owned by the caller: no host copy
-            self.h = self.lib.nzcb_ctx_create(ctypes.cast(_raw[0], POINTER(c_uint8)), _raw[1], device,
-                                              ctypes.byref(err))
+            zptr, zlen = ctypes.cast(_raw[0], POINTER(c_uint8)), _raw[1]
         else:
             data = _read(zkey)
-            self.h = self.lib.nzcb_ctx_create(_buf(data), len(data), device, ctypes.byref(err))
+            zptr, zlen = _buf(data), len(data)
+        self.h = self.lib.nzcb_ctx_create(zptr, zlen, device, ctypes.byref(err))
         if not self.h:
             raise NzcbError(err.code, err.msg.decode(errors="replace"))
+        verr = _Err()
+        _check(self.lib.nzcb_vk_from_zkey(zptr, zlen, vk, ctypes.byref(verr)), verr)
+        self.vk = bytes(vk)  # binary verification key (nzcb.verify / vk_to_json)
         info = (c_uint32 * 5)()
         self.lib.nzcb_ctx_info(self.h, info)
         self.domain_size, self.n_public, self.n_vars, self.n_additions, self.n_constraints = list(info)

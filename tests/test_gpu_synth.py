@@ -29,3 +29,21 @@ def test_synth_setup_proves_and_verifies():
     p = plonk.proof_from_bytes(proof)
     pubv = [int.from_bytes(pub[i:i + 32], "little") for i in range(0, len(pub), 32)]
     assert plonk.verify_with_trapdoor(zk, pubv, p, tau)
+
+
+def test_full_pipeline_proofs_verify_with_pairing():
+    """Larger synthetic circuit (2^14): random-blinding proofs from a 2-lane batch are
+    accepted by the pairing verifier; a tampered one is rejected (size-independent
+    parity check used by bench.py at 2^21)."""
+    import nzcb
+    ctx, wtns = nzcb.synth_context(14, 3, 40, seed=5, tau=0x1234567)
+    nwit = (len(wtns) - 76) // 32
+    wit = wtns[76:76 + 32 * nwit]
+    ctx.set_lanes(2)
+    res = ctx.prove_batch_raw([wit] * 3, blindings=[nzcb.random_blinding() for _ in range(3)])
+    assert len({p for p, _ in res}) == 3
+    for proof, pub in res:
+        assert nzcb.verify(ctx.vk, proof, pub)
+    bad = bytearray(res[0][0])
+    bad[-1] ^= 1
+    assert not nzcb.verify(ctx.vk, bytes(bad), res[0][1])
