@@ -225,6 +225,7 @@ async function exportSolidityCallData(proof, publicSignals) {
 module.exports = {
   plonk: { prove, fullProve, verify, exportSolidityCallData },
   zKey: { exportVerificationKey },
+  nzcp: require('./nzcp.js'),
   wtns: { calculate: wtnsCalculate },
   version: addon.version,
   deviceCount: addon.deviceCount,

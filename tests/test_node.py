@@ -91,3 +91,48 @@ def test_cli_plonk_prove_verifies(tmp_path):
     pt.update({k: int(proof[k]) for k in plonk.PROOF_EVALS})
     zk = binfmt.read_zkey(open(os.path.join(GOLD, "p8.zkey"), "rb").read())
     assert plonk.verify_with_trapdoor(zk, pub, pt, meta["tau"])
+
+
+EXAMPLE_PASS_URI = (  # /root/reference/test/nzcp.js:71 (MoH example pass)
+    "NZCP:/1/2KCEVIQEIVVWK6JNGEASNICZAEP2KALYDZSGSZB2O5SWEOTOPJRXALTDN53GSZBRHEXGQZLBNR2GQLTOPICRUYMBTIFAIGTUKBAA"
+    "UYTWMOSGQQDDN5XHIZLYOSBHQJTIOR2HA4Z2F4XXO53XFZ3TGLTPOJTS6MRQGE4C6Y3SMVSGK3TUNFQWY4ZPOYYXQKTIOR2HA4Z2F4XW46"
+    "TDOAXGG33WNFSDCOJONBSWC3DUNAXG46RPMNXW45DFPB2HGL3WGFTXMZLSONUW63TFGEXDALRQMR2HS4DFQJ2FMZLSNFTGSYLCNRSUG4TF"
+    "MRSW45DJMFWG6UDVMJWGSY2DN53GSZCQMFZXG4LDOJSWIZLOORUWC3CTOVRGUZLDOSRWSZ3JOZSW4TTBNVSWISTBMNVWUZTBNVUWY6KO"
+    "MFWWKZ2TOBQXE4TPO5RWI33CNIYTSNRQFUYDILJRGYDVAYFE6VGU4MCDGK7DHLLYWHVPUS2YIDJOA6Y524TD3AZRM263WTY2BE4DPKIF"
+    "27WKF3UDNNVSVWRDYIYVJ65IRJJJ6Z25M2DO4YZLBHWFQGVQR5ZLIWEQJOZTS3IQ7JTNCFDX")
+
+
+@needs_node
+def test_nzcp_input_preparation_kats():
+    """pass URI -> ToBeSigned -> circuit input / expected public
+    signals, pinned by the reference test's KATs (test/utils.js:16-20 SHA-256 chunks of
+    the example ToBeSigned, test/nzcp.js:18,36 nullifier and data) and SURVEY.md §8c."""
+    import hashlib
+    script = f"""
+const z = require('./').nzcp;
+const uri = '{EXAMPLE_PASS_URI}';
+const data = Buffer.from([...Array(20).keys()].map((i) => i + 1));
+const inp = z.circuitInput(uri, data, z.EXAMPLE_TOBESIGNED_MAX);
+console.log(JSON.stringify({{tbs: z.toBeSigned(uri).toString('hex'), claims: z.claims(uri),
+  pub: z.expectedPublicSignals(uri, data), inp}}));
+"""
+    d = json.loads(run_node(script))
+    tbs = bytes.fromhex(d["tbs"])
+    assert len(tbs) == 314
+    # reference KAT: sha256(ToBeSigned) as two LSB-first chunks of 248 bits (test/utils.js:11-19)
+    chunks = [366677313775235426412199931337625106565467678080892143469223808086055532772, 119]
+    bits = [(c >> j) & 1 for c in chunks for j in range(248)]
+    kat = bytes(sum(bits[8 * i + t] << (7 - t) for t in range(8)) for i in range(32))
+    assert hashlib.sha256(tbs).digest() == kat
+    assert d["claims"]["exp"] == 1951416330
+    assert f"{d['claims']['givenName']},{d['claims']['familyName']},{d['claims']['dob']}" == "Jack,Sparrow,1960-04-16"
+    assert d["pub"] == [
+        "8464235439336389695359576364537904521787463454426143836621154307990710930",
+        "334204042160295982690797293769892102755483197293558786265320143920457223185",
+        "430989588176824417852954207888075491695208395262355815151652761069951123456"]
+    inp = d["inp"]
+    assert inp["toBeSignedLen"] == 314 and len(inp["toBeSigned"]) == 314 * 8 and len(inp["data"]) == 160
+    assert bytes(sum(inp["toBeSigned"][8 * i + t] << (7 - t) for t in range(8)) for i in range(314)) == tbs
+    # data: bytes reversed, bits reversed within each byte (EVM rearrangement)
+    dbytes = bytes(sum(inp["data"][8 * i + t] << (7 - t) for t in range(8)) for i in range(20))
+    assert dbytes == bytes(int(f"{b:08b}"[::-1], 2) for b in reversed(range(1, 21)))
