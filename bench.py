@@ -28,6 +28,12 @@ import os
 import sys
 import time
 
+# HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default);
+# 4 lanes x 4 streams on 4 queues falsely serialise kernels of independent proofs.
+# 24 queues measured +12-16 % over 4 (DESIGN.md §4 "Concurrency"); set before HIP initialises.
+if os.environ.get("GPU_MAX_HW_QUEUES", "4") == "4":  # unset or HIP's default (the box exports 4)
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "nzcb-circom_amd"))
 
@@ -80,10 +86,10 @@ def cpu_baseline_sample(power: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--power", type=int, default=21, help="log2 PLONK domain (nzcp_live: 21)")
-    ap.add_argument("--lanes", type=int, default=2, help="proofs in flight per GPU")
+    ap.add_argument("--lanes", type=int, default=4, help="proofs in flight per GPU")
     ap.add_argument("--batch", type=int, default=0,
                     help="fixed total batch sharded over the ranks (configs[3]: 512); default: --steps per rank")
     ap.add_argument("--msm-devices", default="",
@@ -95,17 +101,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (not used by the driver): gloo instead of RCCL, and every rank on
+    # one device, to run the multi-rank flow on a one-GPU box
+    backend = os.environ.get("NZCB_DIST_BACKEND", "nccl")
+    device = int(os.environ.get("NZCB_BENCH_DEVICE", local))
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     import nzcb
     n = 1 << args.power
     t_setup = time.time()
-    ctx, wtns = nzcb.synth_context(args.power, 3, NZCP_INPUTS, SEED, 0, TAU, device=local)
+    ctx, wtns = nzcb.synth_context(args.power, 3, NZCP_INPUTS, SEED, 0, TAU, device=device)
     setup_s = time.time() - t_setup
     nwit = (len(wtns) - 76) // 32
     dev_w = nzcb.dev_alloc(nwit * 32)
@@ -114,7 +127,7 @@ def main():
     def barrier():
         if dist is not None:
             import torch
-            torch.cuda.synchronize(local)
+            torch.cuda.synchronize(device)
             dist.barrier()
 
     # single-proof latency (one lane) and the PCIe-inclusive rate (host witness) for
@@ -133,7 +146,7 @@ def main():
         args.lanes = 1
     ctx.set_lanes(args.lanes)
     if args.warmup:
-        nw = max(args.warmup, args.lanes)
+        nw = max(args.warmup, 2 * args.lanes)  # every lane proves at least once before timing
         ctx.prove_batch_raw([dev_w] * nw, n_witness=nwit, blindings=[blinding_for(1000 + i) for i in range(nw)],
                             on_device=True)
     ctx.kernel_stats(1)
@@ -150,7 +163,7 @@ def main():
     # first and last proof of the timed batch (host, outside the timed region)
     verified = all(nzcb.verify(ctx.vk, proofs[i][0], proofs[i][1]) for i in {0, len(proofs) - 1})
     kms, klaunch, kpoints, kentries = ctx.kernel_stats(0)
-    elapsed = max_over_ranks(elapsed, dist, f"cuda:{local}")
+    elapsed = max_over_ranks(elapsed, dist, f"cuda:{device}" if backend == "nccl" else "cpu")
     total_proofs = args.batch if args.batch else args.steps * world
     steps = len(shard(args.batch, 0, world)) if args.batch else args.steps
     value = total_proofs / elapsed

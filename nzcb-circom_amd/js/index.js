@@ -13,6 +13,9 @@ const fs = require('fs');
 const path = require('path');
 const crypto = require('crypto');
 
+// proof streams need more than HIP's default 4 hardware queues per process (kernels of
+// independent streams sharing a queue serialise); read when HIP initialises
+if ((process.env.GPU_MAX_HW_QUEUES || '4') === '4') process.env.GPU_MAX_HW_QUEUES = '24';
 const addon = require(path.join(__dirname, 'build', 'nzcb.node'));
 
 const R = BigInt('21888242871839275222246405745257275088548364400416034343698204186575808495617');

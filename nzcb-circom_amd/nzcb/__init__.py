@@ -66,6 +66,11 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
+    # proof lanes and commitment streams need more than HIP's default 4 hardware queues
+    # per process (kernels of independent streams sharing a queue serialise); only
+    # effective when the HIP runtime has not been initialised yet in this process
+    if os.environ.get("GPU_MAX_HW_QUEUES", "4") == "4":  # unset or HIP's default
+        os.environ["GPU_MAX_HW_QUEUES"] = "24"
     lib = ctypes.CDLL(path or LIB_PATH)
     u8p = POINTER(c_uint8)
     sigs = {
