@@ -196,4 +196,56 @@ NZ_HD Xyzz29 mdbl29(const F29& x, const F29& y) {
   return r;
 }
 
+NZ_HD bool is_inf29(const Xyzz29& a) {
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) z |= a.ZZ.v[i];
+  return z == 0;
+}
+
+// dbl-2008-s-1 (a = 0) of a finite XYZZ point (its Y is never 0 mod p on BN254 G1)
+NZ_HD Xyzz29 dbl29(const Xyzz29& p) {
+  Xyzz29 r;
+  F29 U;
+#pragma unroll
+  for (int i = 0; i < 9; i++) U.v[i] = p.Y.v[i] << 1;  // < 8p, limbs < 2^30
+  const F29 V = mul29(U, U);
+  const F29 W = mul29(U, V);
+  const F29 S = mul29(p.X, V);
+  const F29 xx = mul29(p.X, p.X);
+  F29 M;
+#pragma unroll
+  for (int i = 0; i < 9; i++) M.v[i] = xx.v[i] * 3u;  // < 6p
+  norm29(M);
+  r.X = sub29(mul29(M, M), add29(S, S), Fq29::K4);   // < 6p
+  r.Y = sub29(mul29(M, sub29(S, r.X, Fq29::K8)), mul29(W, p.Y), Fq29::K2);  // < 4p
+  r.ZZ = mul29(V, p.ZZ);
+  r.ZZZ = mul29(W, p.ZZZ);
+  return r;
+}
+
+// add-2008-s: XYZZ + XYZZ (infinity = ZZ stored as 0), 12 products + 2 squares
+NZ_HD Xyzz29 add29(const Xyzz29& p, const Xyzz29& q) {
+  if (is_inf29(p)) return q;
+  if (is_inf29(q)) return p;
+  const F29 U1 = mul29(p.X, q.ZZ), U2 = mul29(q.X, p.ZZ);
+  const F29 S1 = mul29(p.Y, q.ZZZ), S2 = mul29(q.Y, p.ZZZ);
+  const F29 P = sub29(U2, U1, Fq29::K2);  // < 4p
+  const F29 R = sub29(S2, S1, Fq29::K2);  // < 4p
+  const F29 PP = mul29(P, P), PPP = mul29(P, PP), Q = mul29(U1, PP), RR = mul29(R, R);
+  Xyzz29 r;
+  r.ZZ = mul29(mul29(p.ZZ, q.ZZ), PP);
+  if (is0p29(r.ZZ)) {  // same abscissa
+    if (is0p29(RR)) return dbl29(p);
+    Xyzz29 inf = r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) inf.ZZ.v[i] = 0;
+    return inf;
+  }
+  r.X = sub29(RR, add2x29(PPP, Q), Fq29::K6);                                    // < 8p
+  r.Y = sub29(mul29(R, sub29(Q, r.X, Fq29::K8)), mul29(S1, PPP), Fq29::K2);        // < 4p
+  r.ZZZ = mul29(mul29(p.ZZZ, q.ZZZ), PPP);
+  return r;
+}
+
 }  // namespace nzcb

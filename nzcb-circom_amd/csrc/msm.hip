@@ -336,6 +336,21 @@ msm_accumulate29_kernel(const G1Affine* __restrict__ bases, const uint32_t* __re
 
 // Buckets whose entries span several accumulation chunks: owner chunk's carry plus
 // the continuation carries of the chunks the bucket spills into (thread per bucket).
+// sum of a bucket's carries: the owner chunk's and the continuations c0+1..c1
+__device__ __forceinline__ G1xyzz sum_run(const G1xyzz* carry_own, const G1xyzz* carry_cont, uint32_t c0,
+                                          uint32_t c1) {
+  G1xyzz v = carry_own[c0];
+  for (uint32_t u = c0 + 1; u <= c1; u++) v = xyzz_add(v, carry_cont[u]);
+  return v;
+}
+// radix-2^29 carries are summed in that radix (no per-carry conversion), converted once
+__device__ __forceinline__ G1xyzz sum_run(const Xyzz29* carry_own, const Xyzz29* carry_cont, uint32_t c0,
+                                          uint32_t c1) {
+  Xyzz29 v = carry_own[c0];
+  for (uint32_t u = c0 + 1; u <= c1; u++) v = add29(v, carry_cont[u]);
+  return load_point(v);
+}
+
 // P = G1xyzz: the generic accumulation already wrote single-chunk buckets in place;
 // P = Xyzz29: every bucket is converted here (single-chunk ones from `single`).
 template <class P>
@@ -356,9 +371,7 @@ msm_bucket_finalize_kernel(const uint32_t* __restrict__ offsets, uint32_t nkeys,
     large[1 + atomicAdd(&large[0], 1u)] = (uint32_t)k;
     return;
   }
-  G1xyzz v = load_point(carry_own[c0]);
-  for (uint32_t u = c0 + 1; u <= c1; u++) v = xyzz_add(v, load_point(carry_cont[u]));
-  buckets[k] = v;
+  buckets[k] = sum_run(carry_own, carry_cont, c0, c1);
 }
 
 // thread per (set, L-bucket segment): run = sum_j B_j, tot = sum_j (j+1) B_j
