@@ -16,10 +16,24 @@ struct NttTables {
   void init(int max_log, hipStream_t st);
 };
 
+// Optional fused prologue / epilogue (coset NTTs of zero-padded polynomials):
+//   input  j: in[j] * in_lo[j & 4095] * in_hi[j >> 12] for j < in_len, 0 beyond (not read)
+//   output j: out[j] * out_lo[j & 4095] * out_hi[j >> 12]; sets *out_flags if an output
+//             at j >= out_limit is nonzero
+struct NttIo {
+  size_t in_len = ~size_t(0);
+  const Fr* in_lo = nullptr;
+  const Fr* in_hi = nullptr;
+  const Fr* out_lo = nullptr;
+  const Fr* out_hi = nullptr;
+  size_t out_limit = ~size_t(0);
+  uint32_t* out_flags = nullptr;
+};
+
 // out = NTT(in) (inverse: out = (1/N) * iNTT(in)), N = 2^log_n <= 2^max_log.
 // Natural order in and out; in != out required (first pass gathers in bit-reversed order).
 // scale (optional, Montgomery) multiplies every input element on load.
 void ntt(const NttTables& t, const Fr* in, Fr* out, int log_n, bool inverse, hipStream_t st,
-         const Fr* scale = nullptr);
+         const Fr* scale = nullptr, const NttIo* io = nullptr);
 
 }  // namespace nzcb

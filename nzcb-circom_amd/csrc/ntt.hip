@@ -92,7 +92,7 @@ void NttTables::init(int L, hipStream_t st) {
 // One pass: stages [s, s+q) on tiles of (2^q rows) x (2^logC columns).
 __global__ void __launch_bounds__(kNttThreads)
 ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int s, int q, int logC, int first, Fr scale,
-                int do_scale) {
+                int do_scale, int last, NttIo io) {
   extern __shared__ Fr tile[];
   const int C = 1 << logC;
   const int rows = 1 << q;
@@ -105,8 +105,12 @@ ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int s, 
     for (int e = tid; e < n_el; e += kNttThreads) {
       int j = e >> logC, c = e & (C - 1);
       size_t src = ((size_t)bit_rev((uint32_t)j, q) << (L - q)) + c0 + c;
-      Fr v = in[src];
-      if (do_scale) v = v * scale;
+      Fr v = Fr::zero();
+      if (src < io.in_len) {
+        v = in[src];
+        if (io.in_lo) v = v * (io.in_lo[src & 4095] * io.in_hi[src >> 12]);
+        if (do_scale) v = v * scale;
+      }
       tile[e] = v;
     }
   } else {
@@ -176,21 +180,31 @@ ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int s, 
     }
     __syncthreads();
   }
+  // final store, with the optional epilogue on the transform's last pass
+  auto store = [&](size_t dst, Fr v) {
+    if (last) {
+      if (io.out_lo) v = v * (io.out_lo[dst & 4095] * io.out_hi[dst >> 12]);
+      if (io.out_flags && dst >= io.out_limit && !v.is_zero()) atomicOr(io.out_flags, 1u);
+    }
+    out[dst] = v;
+  };
   if (first) {
     for (int e = tid; e < n_el; e += kNttThreads) {
       int j = e & (rows - 1), c = e >> q;
       size_t dst = ((size_t)bit_rev((uint32_t)(c0 + c), L - q) << q) + j;
-      out[dst] = tile[(j << logC) + c];
+      store(dst, tile[(j << logC) + c]);
     }
   } else {
     for (int e = tid; e < n_el; e += kNttThreads) {
       int j = e >> logC, c = e & (C - 1);
-      out[base + ((size_t)j << s) + c] = tile[e];
+      store(base + ((size_t)j << s) + c, tile[e]);
     }
   }
 }
 
-void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hipStream_t st, const Fr* scale) {
+void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hipStream_t st, const Fr* scale,
+         const NttIo* iop) {
+  const NttIo io = iop ? *iop : NttIo();
   if (L > t.max_log) throw Error(NZCB_ERR_ARG, "ntt size exceeds table");
   if (in == out) throw Error(NZCB_ERR_ARG, "ntt requires in != out");
   const Fr* tw = inverse_dir ? t.inv.p : t.fwd.p;
@@ -207,7 +221,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   }
   if (L == 0) {
     hipLaunchKernelGGL(ntt_pass_kernel, dim3(1), dim3(kNttThreads), sizeof(Fr), st, in, out, tw, 0, 0, 0, 0, 1, sc,
-                       do_scale);
+                       do_scale, 1, io);
     NZ_HIP(hipGetLastError());
     return;
   }
@@ -218,7 +232,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   size_t tiles = (size_t)cols >> logC1;
   size_t lds = (size_t(1) << (q1 + logC1)) * sizeof(Fr);
   hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)tiles), dim3(kNttThreads), lds, st, in, out, tw, L, 0, q1, logC1,
-                     1, sc, do_scale);
+                     1, sc, do_scale, q1 == L ? 1 : 0, io);
   NZ_HIP(hipGetLastError());
   int s = q1;
   while (s < L) {
@@ -228,7 +242,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
     size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
     size_t lds2 = (size_t(1) << (q + logC)) * sizeof(Fr);
     hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)ntiles), dim3(kNttThreads), lds2, st, out, out, tw, L, s, q,
-                       logC, 0, sc, 0);
+                       logC, 0, sc, 0, s + q == L ? 1 : 0, io);
     NZ_HIP(hipGetLastError());
     s += q;
   }

@@ -65,7 +65,7 @@ struct Prover {
   DevBuf<Fr> wtns_in;             // raw witness upload (normal form)
   DevBuf<Fr> A, B, C, Z;          // n
   DevBuf<Fr> pol_a, pol_b, pol_c, pol_z;  // n+2 / n+3
-  DevBuf<Fr> A4, B4, C4, Z4, T, Tz, t, pad4;  // 4n (A4..Z4: coset evaluations)
+  DevBuf<Fr> A4, B4, C4, Z4, T, Tz, t;  // 4n (A4..Z4: coset evaluations)
   DevBuf<Fr> pol_r, pol_wxi, pol_wxiw;    // n+3, n+6, n+3
   DevBuf<Fr> blind;               // 12 (index 0 unused)
   DevBuf<Fr> scan_tmp;            // recursive scan levels

@@ -243,24 +243,6 @@ k_quotient_coset(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* _
   T[i] = (gate + q.alpha * (num - den) + e4) * q.zhinv[i & 3];
 }
 
-// dst[j] = src[j] * g^j for j < len, 0 up to n4 (coefficients of p(g X), zero-padded)
-__global__ void k_coset_pad(const Fr* __restrict__ src, size_t len, Fr* __restrict__ dst, size_t n4,
-                            const Fr* __restrict__ glo, const Fr* __restrict__ ghi) {
-  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n4) return;
-  dst[j] = j < len ? src[j] * (glo[j & 4095] * ghi[j >> 12]) : Fr::zero();
-}
-
-// t[j] *= g^-j (back from the coset); "T Polynomial is not divisible" unless t[j] = 0 for j >= limit
-__global__ void k_coset_unscale(Fr* __restrict__ t, size_t n4, const Fr* __restrict__ gilo,
-                                const Fr* __restrict__ gihi, size_t limit, uint32_t* flags) {
-  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n4) return;
-  Fr v = t[j] * (gilo[j & 4095] * gihi[j >> 12]);
-  t[j] = v;
-  if (j >= limit && !v.is_zero()) atomicOr(flags, 1u);
-}
-
 // chunked Horner: partial[block] = sum over the block's chunks of p(chunk) * x^(chunk start)
 __global__ void __launch_bounds__(kT)
 k_eval(const Fr* __restrict__ p, size_t len, Fr x, Fr xK, Fr* __restrict__ partial) {
@@ -539,9 +521,11 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     cs.alloc((size_t)3 * n4);
     cl.alloc((size_t)nl * n4);
     auto coset_eval = [&](const Fr* coefs, Fr* out) {
-      hipLaunchKernelGGL(k_coset_pad, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, coefs, (size_t)n, pad4.p,
-                         (size_t)n4, g_lo.p, g_hi.p);
-      ntt(eng->ntt_tables, pad4.p, out, power + 2, false, s);
+      NttIo io;  // coset shift g^j and the zero padding fused into the NTT's first pass
+      io.in_len = n;
+      io.in_lo = g_lo.p;
+      io.in_hi = g_hi.p;
+      ntt(eng->ntt_tables, coefs, out, power + 2, false, s, nullptr, &io);
     };
     const DevBuf<Fr>* qs[5] = {&qm, &ql, &qr, &qo, &qc};
     for (int k = 0; k < 5; k++) coset_eval(qs[k]->p, cq.p + (size_t)k * n4);
@@ -568,7 +552,7 @@ void Prover::alloc_workspace() {
   A.alloc(n); B.alloc(n); C.alloc(n); Z.alloc(n);
   pol_a.alloc(n + 2); pol_b.alloc(n + 2); pol_c.alloc(n + 2); pol_z.alloc(n + 3);
   A4.alloc(n4); B4.alloc(n4); C4.alloc(n4); Z4.alloc(n4);
-  T.alloc(n4); Tz.alloc(n4); t.alloc(n4); pad4.alloc(n4);
+  T.alloc(n4); Tz.alloc(n4); t.alloc(n4);
   pol_r.alloc(n + 3); pol_wxi.alloc(n + 6); pol_wxiw.alloc(n + 3);
   blind.alloc(12);
   size_t lv = 0, m = n4;
@@ -617,9 +601,11 @@ void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int n
   for (int k = 0; k < nb; k++) bi.idx[k] = bidx[k];
   hipLaunchKernelGGL(k_blind, dim3(1), dim3(64), 0, s, coefs, (size_t)n, blind.p, bi);
   // evaluations of the *blinded* polynomial on the coset g*<w4> (round-3 quotient input)
-  hipLaunchKernelGGL(k_coset_pad, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, coefs, (size_t)n + nb, pad4.p,
-                     (size_t)n4, g_lo.p, g_hi.p);
-  ntt(eng->ntt_tables, pad4.p, evals4, power + 2, false, s);
+  NttIo io;  // coset shift g^j and the zero padding fused into the NTT's first pass
+  io.in_len = (size_t)n + nb;
+  io.in_lo = g_lo.p;
+  io.in_hi = g_hi.p;
+  ntt(eng->ntt_tables, coefs, evals4, power + 2, false, s, nullptr, &io);
   NZ_HIP(hipGetLastError());
   ntt_ms += ms_since(t0);  // host enqueue time only (kernels run asynchronously)
 }
@@ -846,9 +832,12 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     hipLaunchKernelGGL(k_quotient_coset, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, A4.p, B4.p, C4.p, Z4.p,
                        cq.p, cs.p, cl.p, nPublic, A.p, (size_t)n, x_lo.p, root_hi.p, q, T.p);
     NZ_HIP(hipGetLastError());
-    ntt(eng->ntt_tables, T.p, t.p, power + 2, true, s);
-    hipLaunchKernelGGL(k_coset_unscale, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, t.p, (size_t)n4, gi_lo.p,
-                       gi_hi.p, (size_t)3 * n + 6, flags.p);
+    NttIo io;  // coset unscale g^-j and the degree check fused into the iNTT's last pass
+    io.out_lo = gi_lo.p;
+    io.out_hi = gi_hi.p;
+    io.out_limit = (size_t)3 * n + 6;
+    io.out_flags = flags.p;
+    ntt(eng->ntt_tables, T.p, t.p, power + 2, true, s, nullptr, &io);
     NZ_HIP(hipGetLastError());
     uint32_t f = 0;
     NZ_HIP(hipMemcpyAsync(&f, flags.p, 4, hipMemcpyDeviceToHost, s));
