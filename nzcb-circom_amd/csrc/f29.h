@@ -82,6 +82,77 @@ NZ_HD F29 mul29(const F29& a, const F29& b) {
   return r;
 }
 
+// a^2 * 2^-261 mod p: the cross products a_j a_k (j < k) once, against 2 a_k
+// (45 instead of 81 product terms; same bounds as mul29, products < 2^59 for
+// normalized limbs, so a column stays < 2^64)
+NZ_HD F29 sqr29(const F29& a) {
+  using Q = Fq29;
+  uint32_t a2[9], m[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) a2[i] = a.v[i] << 1;
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+#pragma unroll
+    for (int j = 0; 2 * j < i; j++) acc += (uint64_t)a.v[j] * a2[i - j];
+    if (!(i & 1)) acc += (uint64_t)a.v[i >> 1] * a.v[i >> 1];
+#pragma unroll
+    for (int j = 0; j < i; j++) acc += (uint64_t)m[j] * Q::P[i - j];
+    m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
+    acc += (uint64_t)m[i] * Q::P[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int i = 9; i < 17; i++) {
+#pragma unroll
+    for (int j = i - 8; 2 * j < i; j++) acc += (uint64_t)a.v[j] * a2[i - j];
+    if (!(i & 1)) acc += (uint64_t)a.v[i >> 1] * a.v[i >> 1];
+#pragma unroll
+    for (int j = i - 8; j < 9; j++) acc += (uint64_t)m[j] * Q::P[i - j];
+    r.v[i - 9] = (uint32_t)acc & Q::MASK;
+    acc >>= 29;
+  }
+  r.v[8] = (uint32_t)acc;
+  return r;
+}
+
+// (a b + c d) * 2^-261 mod p with one Montgomery reduction. Needs every limb < 2^29
+// (normalized or product outputs: a column is <= 27 terms < 2^58) and a, b, c, d < 2^257
+// with a b + c d < 2^515; result < 2p for the operand sizes used (see msm.hip)
+NZ_HD F29 mul2sum29(const F29& a, const F29& b, const F29& c, const F29& d) {
+  using Q = Fq29;
+  uint32_t m[9];
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+#pragma unroll
+    for (int j = 0; j <= i; j++) {
+      acc += (uint64_t)a.v[j] * b.v[i - j];
+      acc += (uint64_t)c.v[j] * d.v[i - j];
+    }
+#pragma unroll
+    for (int j = 0; j < i; j++) acc += (uint64_t)m[j] * Q::P[i - j];
+    m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
+    acc += (uint64_t)m[i] * Q::P[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int i = 9; i < 17; i++) {
+#pragma unroll
+    for (int j = i - 8; j < 9; j++) {
+      acc += (uint64_t)a.v[j] * b.v[i - j];
+      acc += (uint64_t)c.v[j] * d.v[i - j];
+      acc += (uint64_t)m[j] * Q::P[i - j];
+    }
+    r.v[i - 9] = (uint32_t)acc & Q::MASK;
+    acc >>= 29;
+  }
+  r.v[8] = (uint32_t)acc;
+  return r;
+}
+
 NZ_HD void norm29(F29& r) {
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -111,6 +182,15 @@ NZ_HD F29 add2x29(const F29& a, const F29& b) {  // a + 2b
   F29 r;
 #pragma unroll
   for (int i = 0; i < 9; i++) r.v[i] = a.v[i] + (b.v[i] << 1);
+  norm29(r);
+  return r;
+}
+
+// 4p - y for y < 4p (K4 borrowed form), normalized
+NZ_HD F29 neg4p29(const F29& y) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = Fq29::K4[i] - y.v[i];
   norm29(r);
   return r;
 }
@@ -179,16 +259,16 @@ NZ_HD Xyzz29 mdbl29(const F29& x, const F29& y) {
   F29 U;
 #pragma unroll
   for (int i = 0; i < 9; i++) U.v[i] = y.v[i] << 1;  // < 2p, limbs < 2^30
-  const F29 V = mul29(U, U);
+  const F29 V = sqr29(U);
   const F29 W = mul29(U, V);
   const F29 S = mul29(x, V);
-  const F29 xx = mul29(x, x);
+  const F29 xx = sqr29(x);
   F29 M;
 #pragma unroll
   for (int i = 0; i < 9; i++) M.v[i] = xx.v[i] * 3u;  // < 6p
   norm29(M);
   const F29 t = add29(S, S);                                      // < 4p
-  r.X = sub29(mul29(M, M), t, Fq29::K4);                          // < 6p
+  r.X = sub29(sqr29(M), t, Fq29::K4);                          // < 6p
   const F29 d = sub29(S, r.X, Fq29::K8);                          // < 10p
   r.Y = sub29(mul29(M, d), mul29(W, y), Fq29::K2);                // < 4p
   r.ZZ = V;
@@ -209,15 +289,15 @@ NZ_HD Xyzz29 dbl29(const Xyzz29& p) {
   F29 U;
 #pragma unroll
   for (int i = 0; i < 9; i++) U.v[i] = p.Y.v[i] << 1;  // < 8p, limbs < 2^30
-  const F29 V = mul29(U, U);
+  const F29 V = sqr29(U);
   const F29 W = mul29(U, V);
   const F29 S = mul29(p.X, V);
-  const F29 xx = mul29(p.X, p.X);
+  const F29 xx = sqr29(p.X);
   F29 M;
 #pragma unroll
   for (int i = 0; i < 9; i++) M.v[i] = xx.v[i] * 3u;  // < 6p
   norm29(M);
-  r.X = sub29(mul29(M, M), add29(S, S), Fq29::K4);   // < 6p
+  r.X = sub29(sqr29(M), add29(S, S), Fq29::K4);   // < 6p
   r.Y = sub29(mul29(M, sub29(S, r.X, Fq29::K8)), mul29(W, p.Y), Fq29::K2);  // < 4p
   r.ZZ = mul29(V, p.ZZ);
   r.ZZZ = mul29(W, p.ZZZ);
@@ -232,7 +312,7 @@ NZ_HD Xyzz29 add29(const Xyzz29& p, const Xyzz29& q) {
   const F29 S1 = mul29(p.Y, q.ZZZ), S2 = mul29(q.Y, p.ZZZ);
   const F29 P = sub29(U2, U1, Fq29::K2);  // < 4p
   const F29 R = sub29(S2, S1, Fq29::K2);  // < 4p
-  const F29 PP = mul29(P, P), PPP = mul29(P, PP), Q = mul29(U1, PP), RR = mul29(R, R);
+  const F29 PP = sqr29(P), PPP = mul29(P, PP), Q = mul29(U1, PP), RR = sqr29(R);
   Xyzz29 r;
   r.ZZ = mul29(mul29(p.ZZ, q.ZZ), PP);
   if (is0p29(r.ZZ)) {  // same abscissa

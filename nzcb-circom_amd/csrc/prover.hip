@@ -631,6 +631,8 @@ void Prover::commit_start(int slot, const Fr* coefs, size_t len) {
     len = std::min(len, own_hi);
   }
   msm_enqueue(*msc[slot], ptau.p, coefs, len, true, aux[slot], &ptab);
+  static const bool serial = std::getenv("NZCB_SERIAL") != nullptr;  // profiling: one kernel at a time
+  if (serial) NZ_HIP(hipStreamSynchronize(aux[slot]));
 }
 
 G1Affine Prover::commit_finish(int slot) {
