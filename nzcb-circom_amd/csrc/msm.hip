@@ -683,14 +683,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   auto mark = [&](int i) {
     if (phases) NZ_HIP(hipEventRecord(sc.ev[i], st));
   };
-  static const int exp_skip = [] {
-    const char* e = std::getenv("NZCB_EXP_SKIP");
-    return e ? std::atoi(e) : 0;
-  }();
-  static int exp_calls = 0;
-  const bool warm = ++exp_calls > 64;
   mark(0);
-  if (!(warm && (exp_skip & 1)))
   keys_dispatch(p.c, scalars, n, mont ? 1 : 0, table, sc, st);
   mark(1);
   size_t tmp = sc.sort_tmp_bytes;
@@ -698,7 +691,6 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   if (table && p.nkeys <= 65536) {  // 16-bit keys, no sentinel (see msm_keys_kernel)
     int end_bit = 0;
     while ((1u << end_bit) < p.nkeys) end_bit++;
-    if (!(warm && (exp_skip & 2)))
     radix_sort(sc.sort_tmp.p, tmp, (const uint16_t*)sc.keys_in.p, (uint16_t*)sc.keys_out.p, sc.vals_in.p,
                sc.sorted.p, p.entries, end_bit, st);
     mark(2);
@@ -722,7 +714,6 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   const dim3 agrid(grid_for(nthreads, kMsmThreads, 1u << 30));
   if (table) {
     if (!sc.buckets29.p) throw Error(NZCB_ERR_ARG, "msm scratch was not sized for the fixed-base schedule");
-    if (!(warm && (exp_skip & 4)))
     hipLaunchKernelGGL(acc_waves >= 4 ? msm_accumulate29_kernel<4> : msm_accumulate29_kernel<3>, agrid,
                        dim3(kMsmThreads), 0, st, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads,
                        sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
@@ -734,8 +725,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[4], st));
   NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
-  if (table && warm && (exp_skip & 8)) {
-  } else if (table) {
+  if (table) {
     hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, sc.offsets.p, p.nkeys,
                        (const Xyzz29*)sc.buckets29.p, (const Xyzz29*)sc.carry_own29.p,
                        (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p, sc.large.p);
@@ -752,13 +742,11 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   }
   NZ_HIP(hipGetLastError());
   mark(5);
-  if (!(table && warm && (exp_skip & 16)))
   hipLaunchKernelGGL(msm_bucket_reduce_kernel, dim3(grid_for((size_t)p.nsets * p.nseg, kMsmThreads, 1u << 30)),
                      dim3(kMsmThreads), 0, st, sc.buckets.p, sc.offsets.p, (int)p.nb, p.seglen, p.nseg, p.nsets,
                      sc.seg_tot.p, sc.seg_run.p);
   NZ_HIP(hipGetLastError());
   mark(6);
-  if (!(table && warm && (exp_skip & 32)))
   hipLaunchKernelGGL(msm_sums_kernel, dim3(p.nsets * p.nslots * p.nparts), dim3(kSumThreads), 0, st, sc.seg_tot.p,
                      sc.seg_run.p, p.nseg, p.nslots, p.nparts, sc.parts.p);
   NZ_HIP(hipGetLastError());
