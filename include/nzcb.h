@@ -147,6 +147,66 @@ int nzcb_verify(const uint8_t* vk, const uint8_t* proof, const uint8_t* pub, int
  * "0x<proof hex>,[\"0x<pub>\",...]"; returns 0, or the needed size if cap is short. */
 int nzcb_proof_to_calldata(const uint8_t* proof, const uint8_t* pub, int n_public, char* out, size_t cap);
 
+/* ---- nzcp witness -----------------------------------
+ * The semantic signals and public outputs of NZCPPubIdentity
+ * (/root/reference/circuits/nzcptpl.circom:444-655, cbortpl.circom, quinSelector.circom)
+ * for a batch of passes, one GPU workgroup per pass. Replaces, for the signals the
+ * proof's public inputs depend on, circom_runtime's
+ *   WitnessCalculator.calculateWitness(input, sanityCheck)   [EXT] circom_runtime 0.1.17
+ * as called by snarkjs plonk.fullProve (wtns_calculate) and by the reference tests
+ * (test/nzcp.js:42 `cir.calculateWitness(input, true)`).
+ * Inputs per pass: the main's input signals in declaration order, each a 32-byte LE
+ * field element (values >= r are reduced): toBeSigned[8*max_tbs_bytes] (bits, MSB
+ * first per byte, test/helpers/utils.js:2-10), toBeSignedLen, data[160]
+ * (nzcb_nzcp_input_signals() elements). Status codes mirror the circuit's failing
+ * constraint or assert (the first one in template order); oracle/nzcp_circuit.py
+ * is the CPU restatement with the same codes. */
+enum {
+  NZCB_NZCP_OK = 0,
+  NZCB_NZCP_ERR_BIT = 1,        /* toBeSigned[i] * (toBeSigned[i] - 1) === 0 (detail = i) */
+  NZCB_NZCP_ERR_LEN = 2,        /* toBeSignedLen < MaxToBeSignedBytes + 1 */
+  NZCB_NZCP_ERR_RANGE = 3,      /* a LessThan / Num2Bits operand outside its bit range */
+  NZCB_NZCP_ERR_SELECT = 4,     /* QuinSelector index >= choices (detail = index) */
+  NZCB_NZCP_ERR_NOT_MAP = 5,    /* ReadMapLength: CBOR type is not a map */
+  NZCB_NZCP_ERR_UINT23 = 6,     /* DecodeUint23: map length > 23 */
+  NZCB_NZCP_ERR_NOT_STRING = 7, /* ReadStringLength: CBOR type is not a string */
+  NZCB_NZCP_ERR_UNPINNED = 8    /* negative toBeSignedLen: Sha256Var behaviour not on disk */
+};
+
+/* NZCPPubIdentity(IsLive, MaxToBeSignedBytes, MaxCborArrayLenVC, MaxCborMapLenVC, ...):
+ * nzcp_live = {1, 351, 0, 4}, nzcp_example = {0, 314, 0, 4} (circuits/nzcp_*.circom). */
+typedef struct nzcb_nzcp_params {
+  int32_t is_live;          /* CWT claims map at byte 30 (live) or 27 (example) */
+  int32_t max_tbs_bytes;    /* 1..512 */
+  int32_t max_array_len_vc; /* 0..8 */
+  int32_t max_map_len_vc;   /* 0..32 */
+} nzcb_nzcp_params;
+
+/* One pass's result. On status != OK every other field except detail is zero. */
+typedef struct nzcb_nzcp_record {
+  int32_t status;
+  int32_t detail;
+  uint32_t exp;             /* CWT claim 4 */
+  int32_t vc_pos;           /* FindCWTClaims.vcPos */
+  int32_t given_len, family_len, dob_len, nullifier_len;
+  uint8_t tbs_sha256[32];   /* SHA-256(ToBeSigned) */
+  uint8_t nullifier_sha512[64];
+  uint8_t nullifier[64];    /* "given,family,dob" zero-padded (ConstructNullifier.result) */
+  uint8_t pub[3][32];       /* out[0..2] = witness[1..3], 32-byte LE normal-form Fr */
+} nzcb_nzcp_record;
+
+size_t nzcb_nzcp_input_signals(const nzcb_nzcp_params* prm);
+/* Host buffers: inputs count x nzcb_nzcp_input_signals() x 32 B; records: count. */
+int nzcb_nzcp_witness(int device, const nzcb_nzcp_params* prm, const uint8_t* inputs, int count,
+                      nzcb_nzcp_record* records, nzcb_err* err);
+/* Device buffers, asynchronous on `stream` (a hipStream_t, NULL = default stream).
+ * dev_records may be NULL. When dev_witness is not NULL, pass i's out[0..2] are also
+ * written as witness[1..3] of the witness at dev_witness + i * witness_stride (bytes),
+ * so the prover's public inputs come straight from the pass (fullProve on device). */
+int nzcb_nzcp_witness_dev(int device, const nzcb_nzcp_params* prm, const void* dev_inputs, int count,
+                          void* dev_records, void* dev_witness, size_t witness_stride, void* stream,
+                          nzcb_err* err);
+
 /* ---- Synthetic circuit + setup ------- */
 /* Builds the seeded synthetic circuit of oracle/synth.py and its snarkjs-0.4
  * PLONK zkey with trapdoor tau (32-byte LE normal) on `device`. Buffers are

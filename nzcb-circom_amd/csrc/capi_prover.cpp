@@ -10,7 +10,6 @@
 #include "prover.h"
 
 namespace nzcb {
-void set_err(nzcb_err* err, int code, const char* msg);
 
 // decimal string of a 32-byte little-endian integer (snarkjs stringifyBigInts)
 std::string dec_le32(const uint8_t* le32) {

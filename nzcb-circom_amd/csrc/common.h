@@ -17,7 +17,8 @@ struct Error : std::runtime_error {
   Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 
-// Error codes: NZCB_* from include/nzcb.h.
+// Error codes: NZCB_* from include/nzcb.h. Fills `err` (may be NULL); capi_engine.hip.
+void set_err(nzcb_err* err, int code, const char* msg);
 
 
 #define NZ_HIP(call)                                                                  \

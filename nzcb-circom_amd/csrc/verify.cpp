@@ -27,7 +27,6 @@
 #include "zkey.h"
 
 namespace nzcb {
-void set_err(nzcb_err* err, int code, const char* msg);
 
 namespace {
 

@@ -41,7 +41,8 @@ EXPORTED_SYMBOLS = [
     "nzcb_engine_time_ntt", "nzcb_engine_fr_mul", "nzcb_engine_random_fr", "nzcb_engine_fixed_base",
     "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_to_json", "nzcb_verify",
-    "nzcb_proof_to_calldata", "nzcb_ctx_set_msm_devices",
+    "nzcb_proof_to_calldata", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
+    "nzcb_nzcp_witness_dev",
 ]
 
 
@@ -55,6 +56,24 @@ class NzcbError(RuntimeError):
 class _Err(ctypes.Structure):
     _fields_ = [("code", c_int), ("msg", c_char * 256)]
 
+
+class NzcpParams(ctypes.Structure):
+    """NZCPPubIdentity(IsLive, MaxToBeSignedBytes, MaxCborArrayLenVC, MaxCborMapLenVC, ...)."""
+    _fields_ = [("is_live", ctypes.c_int32), ("max_tbs_bytes", ctypes.c_int32),
+                ("max_array_len_vc", ctypes.c_int32), ("max_map_len_vc", ctypes.c_int32)]
+
+
+class NzcpRecord(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("detail", ctypes.c_int32), ("exp", ctypes.c_uint32),
+                ("vc_pos", ctypes.c_int32), ("given_len", ctypes.c_int32), ("family_len", ctypes.c_int32),
+                ("dob_len", ctypes.c_int32), ("nullifier_len", ctypes.c_int32),
+                ("tbs_sha256", c_uint8 * 32), ("nullifier_sha512", c_uint8 * 64), ("nullifier", c_uint8 * 64),
+                ("pub", (c_uint8 * 32) * 3)]
+
+
+# circuits/nzcp_live.circom / nzcp_example.circom mains
+NZCP_LIVE = dict(is_live=1, max_tbs_bytes=351, max_array_len_vc=0, max_map_len_vc=4)
+NZCP_EXAMPLE = dict(is_live=0, max_tbs_bytes=314, max_array_len_vc=0, max_map_len_vc=4)
 
 LOG_FN = ctypes.CFUNCTYPE(None, c_void_p, ctypes.c_char_p)
 
@@ -120,6 +139,10 @@ def load(path: str | None = None):
                                          POINTER(c_double), POINTER(_Err)]),
         "nzcb_engine_msm_fixed_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_int, u8p,
                                               POINTER(_Err)]),
+        "nzcb_nzcp_input_signals": (c_size_t, [POINTER(NzcpParams)]),
+        "nzcb_nzcp_witness": (c_int, [c_int, POINTER(NzcpParams), u8p, c_int, POINTER(NzcpRecord), POINTER(_Err)]),
+        "nzcb_nzcp_witness_dev": (c_int, [c_int, POINTER(NzcpParams), c_void_p, c_int, c_void_p, c_void_p, c_size_t,
+                                          c_void_p, POINTER(_Err)]),
         "nzcb_engine_time_msm2": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_int,
                                           POINTER(c_double), POINTER(_Err)]),
     }
@@ -155,6 +178,51 @@ def version() -> str:
 
 def device_count() -> int:
     return load().nzcb_device_count()
+
+
+def nzcp_input_signals(params: dict) -> int:
+    """Input signals per pass: toBeSigned[8*MaxToBeSignedBytes], toBeSignedLen, data[160]."""
+    return load().nzcb_nzcp_input_signals(ctypes.byref(NzcpParams(**params)))
+
+
+def _record_dict(r: NzcpRecord) -> dict:
+    return {
+        "status": r.status, "detail": r.detail, "exp": r.exp, "vc_pos": r.vc_pos, "given_len": r.given_len,
+        "family_len": r.family_len, "dob_len": r.dob_len, "nullifier_len": r.nullifier_len,
+        "tbs_sha256": bytes(r.tbs_sha256), "nullifier_sha512": bytes(r.nullifier_sha512),
+        "nullifier": bytes(r.nullifier), "out": [int.from_bytes(bytes(r.pub[k]), "little") for k in range(3)],
+    }
+
+
+def nzcp_witness(inputs: bytes, count: int, params: dict = NZCP_LIVE, device: int = 0) -> list:
+    """NZCPPubIdentity witness on the GPU for `count` passes (include/nzcb.h
+    nzcb_nzcp_witness). `inputs`: count x nzcp_input_signals(params) x 32-byte LE field
+    elements. Returns one dict per pass (status, detail, exp, vc_pos, lengths,
+    tbs_sha256, nullifier_sha512, nullifier, out = the 3 public signals as ints)."""
+    lib = load()
+    prm = NzcpParams(**params)
+    need = lib.nzcb_nzcp_input_signals(ctypes.byref(prm)) * 32 * count
+    if len(inputs) != need:
+        raise ValueError(f"nzcp inputs are {len(inputs)} bytes, expected {need}")
+    recs = (NzcpRecord * max(count, 1))()
+    err = _Err()
+    _check(lib.nzcb_nzcp_witness(device, ctypes.byref(prm), _buf(inputs), count, recs, ctypes.byref(err)), err)
+    return [_record_dict(recs[i]) for i in range(count)]
+
+
+def nzcp_witness_dev(dev_inputs: int, count: int, params: dict = NZCP_LIVE, device: int = 0,
+                     dev_records: int | None = None, dev_witness: int | None = None, witness_stride: int = 0,
+                     stream: int | None = None):
+    """Device-pointer variant (asynchronous on `stream`); see nzcb_nzcp_witness_dev."""
+    lib = load()
+    err = _Err()
+    _check(lib.nzcb_nzcp_witness_dev(device, ctypes.byref(NzcpParams(**params)), dev_inputs, count, dev_records,
+                                     dev_witness, witness_stride, stream, ctypes.byref(err)), err)
+
+
+def nzcp_records_from_bytes(raw: bytes, count: int) -> list:
+    size = ctypes.sizeof(NzcpRecord)
+    return [_record_dict(NzcpRecord.from_buffer_copy(raw[i * size:(i + 1) * size])) for i in range(count)]
 
 
 class Engine:
