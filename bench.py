@@ -5,9 +5,12 @@ Metric and config come from BASELINE.json: "PLONK proofs/sec for nzcp_live
 (~2^21 constraints) at 1/2/4/8 MI355X"; workload = configs[2] (single nzcp_live
 proof on one GPU), batch-sharded with no collective across ranks (configs[3]).
 
-A "step" is one full proof (snarkjs plonk_prove rounds 1-5) of one
-witness whose values are already resident in HBM when the timed region starts;
-the 800-byte proof and the public signals are copied back to the host inside it.
+A "step" is one plonk.fullProve of one NZ COVID Pass: the GPU nzcp witness kernel
+computes the pass's public signals (NZCPPubIdentity outputs)
+into that proof's HBM witness, then the full proof runs (snarkjs plonk_prove
+rounds 1-5, a3-a12). The passes' input signals and the rest of the witness are
+resident in HBM when the timed region starts; the 800-byte proofs and the public
+signals are copied back to the host inside it.
 The K timed proofs are one nzcb_prove_batch call: --lanes proofs are in flight
 on each GPU (lanes share the HBM-resident proving key; SURVEY.md §8e batch mode),
 so one proof's latency-bound phases overlap another's compute.
@@ -77,6 +80,15 @@ def max_over_ranks(x: float, dist, device) -> float:
     return float(t.item())
 
 
+def pass_inputs(indices) -> bytes:
+    """nzcp_live input signals of distinct live-shaped passes: one ToBeSigned, the 20
+    pass-through data bytes derived from the proof index."""
+    from nzcb import nzcp
+    tbs = nzcp.pass_tbs(live=True)
+    return b"".join(nzcp.input_signals(nzcp.circuit_input(
+        tbs, hashlib.sha256(b"nzcb-pass" + i.to_bytes(4, "little")).digest()[:20])) for i in indices)
+
+
 def cpu_baseline_sample(power: int):
     """Time the CPU port (oracle) on a bounded sample; rank 0, N=1 only."""
     from oracle import cbind
@@ -118,11 +130,14 @@ def main():
     import nzcb
     n = 1 << args.power
     t_setup = time.time()
-    ctx, wtns = nzcb.synth_context(args.power, 3, NZCP_INPUTS, SEED, 0, TAU, device=device)
+    # public signals on their public-input gates only, so each pass's nzcp outputs can
+    # be written into witness[1..3] (NZCB_SYNTH_FREE_PUBLIC)
+    ctx, wtns = nzcb.synth_context(args.power, 3, NZCP_INPUTS, SEED, 0, TAU, device=device, free_public=True)
     setup_s = time.time() - t_setup
     nwit = (len(wtns) - 76) // 32
     dev_w = nzcb.dev_alloc(nwit * 32)
     nzcb.h2d(dev_w, wtns[76:76 + nwit * 32])
+    prover = nzcb.NzcpProver(ctx, wtns[76:76 + nwit * 32], nzcb.NZCP_LIVE)
 
     def barrier():
         if dist is not None:
@@ -145,24 +160,32 @@ def main():
         ctx.set_msm_devices(msm_devices)
         args.lanes = 1
     ctx.set_lanes(args.lanes)
-    if args.warmup:
-        nw = max(args.warmup, 2 * args.lanes)  # every lane proves at least once before timing
-        ctx.prove_batch_raw([dev_w] * nw, n_witness=nwit, blindings=[blinding_for(1000 + i) for i in range(nw)],
-                            on_device=True)
-    ctx.kernel_stats(1)
     mine = list(shard(args.batch, rank, world)) if args.batch else list(range(rank * args.steps,
                                                                               (rank + 1) * args.steps))
+    if args.warmup:
+        nw = max(args.warmup, 2 * args.lanes)  # every lane proves at least once before timing
+        prover.upload_inputs(pass_inputs(range(100000, 100000 + nw)))
+        prover.full_prove_staged(nw, [blinding_for(1000 + i) for i in range(nw)])
+    ctx.kernel_stats(1)
     blinds = [blinding_for(i) for i in mine]
+    prover.upload_inputs(pass_inputs(mine))      # the passes' input signals, resident in HBM
+    prover.witness_buffers(len(mine))
     barrier()
     t0 = time.perf_counter()
-    proofs = ctx.prove_batch_raw([dev_w] * len(mine), n_witness=nwit, blindings=blinds, on_device=True)
+    proofs, records = prover.full_prove_staged(len(mine), blinds)
     barrier()
     elapsed = time.perf_counter() - t0
-    assert len({p for p, _ in proofs}) == len(mine)  # distinct blindings -> distinct proofs
-    # full-size parity by a size-independent property: the pairing verifier accepts the
-    # first and last proof of the timed batch (host, outside the timed region)
-    verified = all(nzcb.verify(ctx.vk, proofs[i][0], proofs[i][1]) for i in {0, len(proofs) - 1})
     kms, klaunch, kpoints, kentries = ctx.kernel_stats(0)
+    assert len({p for p, _ in proofs}) == len(mine)  # distinct passes -> distinct proofs
+    # every proof's public signals are its pass's nzcp outputs; full-size parity by a
+    # size-independent property: the pairing verifier accepts the first and last proof
+    # of the timed batch (host, outside the timed region)
+    pubs_ok = all([int.from_bytes(pub[32 * k:32 * k + 32], "little") for k in range(3)] == r["out"]
+                  for (_, pub), r in zip(proofs, records))
+    verified = pubs_ok and all(nzcb.verify(ctx.vk, proofs[i][0], proofs[i][1]) for i in {0, len(proofs) - 1})
+    t_w = time.perf_counter()
+    prover.witness_staged(len(mine))
+    nzcp_ms = (time.perf_counter() - t_w) * 1e3
     elapsed = max_over_ranks(elapsed, dist, f"cuda:{device}" if backend == "nccl" else "cpu")
     total_proofs = args.batch if args.batch else args.steps * world
     steps = len(shard(args.batch, 0, world)) if args.batch else args.steps
@@ -200,9 +223,12 @@ def main():
             "scaling": "strong" if args.batch else "weak",
             "vs_baseline": None,
             "dtype": "u32x8 Montgomery (BN254 Fr/Fq)",
-            "data": "synthetic: seeded satisfied PLONK circuit, snarkjs-0.4 zkey with trapdoor tau (SURVEY §8d cfg 3)",
+            "data": "synthetic: seeded satisfied PLONK circuit with free public wires, snarkjs-0.4 zkey with trapdoor "
+                    "tau (SURVEY §8d cfg 3); public signals = nzcp witness kernel outputs of distinct live-shaped "
+                    "passes (data bytes vary per proof)",
             "config": {
-                "workload": f"nzcp_live single PLONK proof, n=2^{args.power}, nPublic=3, {NZCP_INPUTS} inputs",
+                "workload": f"nzcp_live fullProve (GPU nzcp witness -> witness[1..3], PLONK proof), "
+                            f"n=2^{args.power}, nPublic=3, {NZCP_INPUTS} inputs",
                 "domain_size": n,
                 "n_public": 3,
                 "n_constraints": ctx.n_constraints,
@@ -237,6 +263,7 @@ def main():
                 "frac": round(proof_gbs / HBM_PEAK_GBS, 5),
             },
             "proofs_verified": verified,
+            "nzcp_witness_ms_per_batch": round(nzcp_ms, 3),
             "single_proof_latency_ms": round(latency_ms, 3),
             "phase_ms_single_proof": {k: round(v, 3) for k, v in single_timings.items()},
             "pcie_inclusive_ms": round(pcie_ms, 3),

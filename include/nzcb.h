@@ -214,6 +214,13 @@ int nzcb_nzcp_witness_dev(int device, const nzcb_nzcp_params* prm, const void* d
 int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints,
                      const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len, uint8_t** wtns_out,
                      size_t* wtns_len, nzcb_err* err);
+/* Same with flags: NZCB_SYNTH_FREE_PUBLIC keeps the public signals off every gate but
+ * their public-input gate, so any public values satisfy the circuit. The bench's
+ * fullProve pipeline writes the nzcp outputs of each pass there (nzcb_nzcp_witness_dev). */
+#define NZCB_SYNTH_FREE_PUBLIC 1u
+int nzcb_synth_setup_ex(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints, uint32_t flags,
+                        const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len, uint8_t** wtns_out,
+                        size_t* wtns_len, nzcb_err* err);
 void nzcb_free(void* p);
 
 /* ---- Kernel-level entry points (tests / microbench) */
@@ -231,6 +238,7 @@ void* nzcb_dev_alloc(size_t bytes);
 void nzcb_dev_free(void* p);
 int nzcb_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int nzcb_memcpy_d2h(void* dst, const void* src, size_t bytes);
+int nzcb_memcpy_d2d(void* dst, const void* src, size_t bytes);
 int nzcb_engine_ntt_dev(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, nzcb_err* err);
 int nzcb_engine_msm_dev(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
                         uint8_t* out_affine, nzcb_err* err);

@@ -179,7 +179,8 @@ struct Circuit {
 };
 
 // Bit-exact restatement of oracle/synth.py::synth_circuit
-Circuit build_circuit(int power, uint32_t n_public, uint32_t n_inputs, uint64_t seed, uint32_t n_cons) {
+Circuit build_circuit(int power, uint32_t n_public, uint32_t n_inputs, uint64_t seed, uint32_t n_cons,
+                      uint32_t flags) {
   Circuit c;
   c.n = 1u << power;
   c.n_public = n_public;
@@ -190,7 +191,10 @@ Circuit build_circuit(int power, uint32_t n_public, uint32_t n_inputs, uint64_t 
   std::vector<Fr> internal;
   for (uint32_t i = 0; i < n_public + n_inputs; i++) c.wit.push_back(to_mont(rng.fr()));
   std::vector<uint32_t> pool;
-  for (uint32_t i = 1; i <= n_public + n_inputs; i++) pool.push_back(i);
+  // NZCB_SYNTH_FREE_PUBLIC: public signals sit on their public-input gate only, so any
+  // values satisfy the circuit (the nzcp outputs computed per pass, nzcp.hip)
+  for (uint32_t i = (flags & NZCB_SYNTH_FREE_PUBLIC) ? 1 + n_public : 1; i <= n_public + n_inputs; i++)
+    pool.push_back(i);
   uint32_t unused_next = 1 + n_public, unused_end = 1 + n_public + n_inputs;
   auto pick = [&]() -> uint32_t {
     if (unused_next < unused_end) return unused_next++;
@@ -279,10 +283,11 @@ void launch_fixed_base(const Fr* scalars_mont, size_t n, G1Affine* out, hipStrea
 }
 
 // The whole setup; returns (zkey, wtns) as malloc'ed buffers.
-static void synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_cons, const uint8_t* tau_le,
-                        int device, uint8_t** zk_out, size_t* zk_len, uint8_t** wt_out, size_t* wt_len) {
+static void synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_cons, uint32_t flags,
+                        const uint8_t* tau_le, int device, uint8_t** zk_out, size_t* zk_len, uint8_t** wt_out, size_t* wt_len) {
   if (power < 1 || power > 24 || n_public < 0 || n_inputs < 0) throw Error(NZCB_ERR_ARG, "bad setup arguments");
-  Circuit c = build_circuit(power, (uint32_t)n_public, (uint32_t)n_inputs, seed, n_cons);
+  if (flags & ~(uint32_t)NZCB_SYNTH_FREE_PUBLIC) throw Error(NZCB_ERR_ARG, "unknown synth flags");
+  Circuit c = build_circuit(power, (uint32_t)n_public, (uint32_t)n_inputs, seed, n_cons, flags);
   const uint32_t n = c.n, n4 = 4 * n;
   const uint32_t nc = (uint32_t)c.sa.size();
   Engine eng(device, power + 2, n);
@@ -471,9 +476,9 @@ static void synth_setup(int power, int n_public, int n_inputs, uint64_t seed, ui
 
 }  // namespace nzcb
 
-extern "C" int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints,
-                                const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len,
-                                uint8_t** wtns_out, size_t* wtns_len, nzcb_err* err) {
+extern "C" int nzcb_synth_setup_ex(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints,
+                                   uint32_t flags, const uint8_t* tau, int device, uint8_t** zkey_out,
+                                   size_t* zkey_len, uint8_t** wtns_out, size_t* wtns_len, nzcb_err* err) {
   using namespace nzcb;
   if (!tau || !zkey_out || !zkey_len || !wtns_out || !wtns_len) {
     set_err(err, NZCB_ERR_ARG, "null argument");
@@ -481,7 +486,8 @@ extern "C" int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t 
   }
   try {
     NZ_HIP(hipSetDevice(device));
-    synth_setup(power, n_public, n_inputs, seed, n_constraints, tau, device, zkey_out, zkey_len, wtns_out, wtns_len);
+    synth_setup(power, n_public, n_inputs, seed, n_constraints, flags, tau, device, zkey_out, zkey_len, wtns_out,
+                wtns_len);
     return 0;
   } catch (const Error& e) {
     set_err(err, e.code, e.what());
@@ -490,4 +496,11 @@ extern "C" int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t 
     set_err(err, NZCB_ERR_INTERNAL, e.what());
     return NZCB_ERR_INTERNAL;
   }
+}
+
+extern "C" int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints,
+                                const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len,
+                                uint8_t** wtns_out, size_t* wtns_len, nzcb_err* err) {
+  return nzcb_synth_setup_ex(power, n_public, n_inputs, seed, n_constraints, 0, tau, device, zkey_out, zkey_len,
+                             wtns_out, wtns_len, err);
 }

@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_to_json", "nzcb_verify",
     "nzcb_proof_to_calldata", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
-    "nzcb_nzcp_witness_dev",
+    "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d",
 ]
 
 
@@ -119,6 +119,9 @@ def load(path: str | None = None):
         "nzcb_synth_setup": (c_int, [c_int, c_int, c_int, c_uint64, c_uint32, u8p, c_int,
                                      POINTER(POINTER(c_uint8)), POINTER(c_size_t),
                                      POINTER(POINTER(c_uint8)), POINTER(c_size_t), POINTER(_Err)]),
+        "nzcb_synth_setup_ex": (c_int, [c_int, c_int, c_int, c_uint64, c_uint32, c_uint32, u8p, c_int,
+                                        POINTER(POINTER(c_uint8)), POINTER(c_size_t),
+                                        POINTER(POINTER(c_uint8)), POINTER(c_size_t), POINTER(_Err)]),
         "nzcb_free": (None, [c_void_p]),
         "nzcb_engine_create": (c_void_p, [c_int, c_int, c_size_t, POINTER(_Err)]),
         "nzcb_engine_destroy": (None, [c_void_p]),
@@ -128,6 +131,7 @@ def load(path: str | None = None):
         "nzcb_dev_free": (None, [c_void_p]),
         "nzcb_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_size_t]),
         "nzcb_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_size_t]),
+        "nzcb_memcpy_d2d": (c_int, [c_void_p, c_void_p, c_size_t]),
         "nzcb_engine_ntt_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, POINTER(_Err)]),
         "nzcb_engine_msm_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, u8p, POINTER(_Err)]),
         "nzcb_engine_time_ntt": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, POINTER(c_double),
@@ -337,6 +341,11 @@ def h2d(dst: int, data: bytes):
         raise NzcbError(rc, "h2d failed")
 
 
+def d2d(dst: int, src: int, nbytes: int):
+    if load().nzcb_memcpy_d2d(dst, src, nbytes) != 0:
+        raise NzcbError(10, "hipMemcpy D2D failed")
+
+
 def d2h(src: int, nbytes: int) -> bytes:
     buf = ctypes.create_string_buffer(nbytes)
     rc = load().nzcb_memcpy_d2h(buf, src, nbytes)
@@ -360,6 +369,7 @@ class ProverContext:
 
     def __init__(self, zkey, device: int = 0, logger=None, transcript_public: bool = True, _raw=None):
         self.lib = load()
+        self.device = device
         err = _Err()
         vk = _out(VK_BYTES)
         if _raw is not None:            # (pointer, length) owned by the caller: no host copy
@@ -488,6 +498,94 @@ class ProverContext:
         return dict(zip(names[:k], list(ms)[:k]))
 
 
+class NzcpProver:
+    """fullProve for nzcp passes on one GPU: the nzcp witness kernel computes each pass's
+    public signals (NZCPPubIdentity out[0..2], include/nzcb.h nzcb_nzcp_witness_dev)
+    straight into that proof's HBM witness, then nzcb_prove_batch proves them.
+
+    The circuit is a zkey whose public signals are witness[1..3] (snarkjs convention:
+    main's outputs first). The rest of each witness is `base_witness` (the nzcp_live
+    stand-in of SURVEY.md §8d: a synthetic circuit built with free_public=True, since
+    the real r1cs/wasm cannot be built offline). A pass whose witness calculation
+    fails raises like circom_runtime's calculateWitness does."""
+
+    def __init__(self, ctx: ProverContext, base_witness: bytes, params: dict = NZCP_LIVE):
+        if ctx.n_public != 3:
+            raise ValueError("nzcp circuits have 3 public signals")
+        self.ctx, self.params = ctx, dict(params)
+        self.device = ctx.device
+        self.n_witness = len(base_witness) // 32
+        self.n_inputs = nzcp_input_signals(self.params)
+        self._base = dev_alloc(len(base_witness))
+        h2d(self._base, base_witness)
+        self._block, self._block_count = None, 0   # per-proof device witnesses, grown on demand
+        self._rec = None                          # device records of the same passes
+        self._inputs, self._inputs_cap = None, 0
+
+    def close(self):
+        for p in (self._block, self._rec, self._base, self._inputs):
+            if p:
+                dev_free(p)
+        self._block = self._rec = self._base = self._inputs = None
+
+    def witness_buffers(self, count: int):
+        """Device pointers of `count` witnesses, one contiguous block (stride n_witness x 32 B),
+        each initialised from the base witness."""
+        stride = self.n_witness * 32
+        if count > self._block_count:
+            if self._block:
+                dev_free(self._block)
+                dev_free(self._rec)
+            self._block = dev_alloc(stride * count)
+            self._rec = dev_alloc(ctypes.sizeof(NzcpRecord) * count)
+            for i in range(count):
+                d2d(self._block + i * stride, self._base, stride)
+            self._block_count = count
+        return [self._block + i * stride for i in range(count)]
+
+    def upload_inputs(self, inputs: bytes) -> int:
+        """Stage count x n_inputs x 32 B of input signals in HBM; returns the pass count."""
+        per = self.n_inputs * 32
+        if len(inputs) % per:
+            raise ValueError("inputs are not a whole number of passes")
+        if len(inputs) > self._inputs_cap:
+            if self._inputs:
+                dev_free(self._inputs)
+            self._inputs, self._inputs_cap = dev_alloc(len(inputs)), len(inputs)
+        h2d(self._inputs, inputs)
+        return len(inputs) // per
+
+    def witness_staged(self, count: int) -> list:
+        """nzcp witness of the staged passes: public signals into witness[1..3] of each
+        proof's HBM witness; returns the records. Raises on a failed pass."""
+        bufs = self.witness_buffers(count)
+        rec_size = ctypes.sizeof(NzcpRecord)
+        nzcp_witness_dev(self._inputs, count, self.params, self.device, self._rec, bufs[0], self.n_witness * 32)
+        recs = nzcp_records_from_bytes(d2h(self._rec, rec_size * count), count)
+        for i, r in enumerate(recs):
+            if r["status"] != 0:
+                raise NzcbError(r["status"], f"nzcp witness of pass {i} failed: "
+                                             f"{NZCP_STATUS.get(r['status'], r['status'])} (detail {r['detail']})")
+        return recs
+
+    def full_prove_staged(self, count: int, blindings=None):
+        """Witness + proof for the `count` passes staged by upload_inputs (all in HBM).
+        Returns ([(proof, public)], records)."""
+        recs = self.witness_staged(count)
+        res = self.ctx.prove_batch_raw(self.witness_buffers(count), n_witness=self.n_witness, blindings=blindings,
+                                       on_device=True)
+        return res, recs
+
+    def full_prove(self, inputs: bytes, blindings=None):
+        return self.full_prove_staged(self.upload_inputs(inputs), blindings)
+
+
+NZCP_STATUS = {0: "ok", 1: "toBeSigned bit check", 2: "toBeSignedLen > MaxToBeSignedBytes",
+               3: "LessThan operands out of range", 4: "QuinSelector index out of range",
+               5: "CBOR type is not a map", 6: "CBOR map length > 23", 7: "CBOR type is not a string",
+               8: "negative toBeSignedLen (unpinned)"}
+
+
 def proof_to_json(proof: bytes) -> dict:
     lib = load()
     cap = 8192
@@ -598,10 +696,10 @@ def random_blinding() -> bytes:
     return b"".join((secrets.randbelow(r)).to_bytes(32, "little") for _ in range(11))
 
 
-def synth_context(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,
-                  n_constraints: int = 0, tau: int = 0x6E7A6362746175, device: int = 0):
-    """Build the synthetic circuit's zkey on `device` and upload it straight into a
-    ProverContext without copying the (multi-GB) zkey through Python. Returns (ctx, wtns bytes)."""
+SYNTH_FREE_PUBLIC = 1
+
+
+def _synth_raw(power, n_public, n_inputs, seed, n_constraints, tau, device, free_public):
     lib = load()
     zp = POINTER(c_uint8)()
     wp = POINTER(c_uint8)()
@@ -609,11 +707,23 @@ def synth_context(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 
     wl = c_size_t()
     err = _Err()
     taub = _buf(int(tau).to_bytes(32, "little"))
-    _check(lib.nzcb_synth_setup(power, n_public, n_inputs, seed, n_constraints, taub, device, ctypes.byref(zp),
-                                ctypes.byref(zl), ctypes.byref(wp), ctypes.byref(wl), ctypes.byref(err)), err)
+    flags = SYNTH_FREE_PUBLIC if free_public else 0
+    _check(lib.nzcb_synth_setup_ex(power, n_public, n_inputs, seed, n_constraints, flags, taub, device,
+                                   ctypes.byref(zp), ctypes.byref(zl), ctypes.byref(wp), ctypes.byref(wl),
+                                   ctypes.byref(err)), err)
+    return zp, zl.value, wp, wl.value
+
+
+def synth_context(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,
+                  n_constraints: int = 0, tau: int = 0x6E7A6362746175, device: int = 0, free_public: bool = False):
+    """Build the synthetic circuit's zkey on `device` and upload it straight into a
+    ProverContext without copying the (multi-GB) zkey through Python. Returns (ctx, wtns bytes).
+    free_public: public signals on their public-input gate only (NZCB_SYNTH_FREE_PUBLIC)."""
+    lib = load()
+    zp, zl, wp, wl = _synth_raw(power, n_public, n_inputs, seed, n_constraints, tau, device, free_public)
     try:
-        ctx = ProverContext(None, device=device, _raw=(zp, zl.value))
-        wtns = ctypes.string_at(wp, wl.value)
+        ctx = ProverContext(None, device=device, _raw=(zp, zl))
+        wtns = ctypes.string_at(wp, wl)
     finally:
         lib.nzcb_free(ctypes.cast(zp, c_void_p))
         lib.nzcb_free(ctypes.cast(wp, c_void_p))
@@ -621,21 +731,13 @@ def synth_context(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 
 
 
 def synth_setup(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,
-                n_constraints: int = 0, tau: int = 0x6E7A6362746175, device: int = 0):
-    """Seeded synthetic circuit + zkey built on the GPU (``nzcb_synth_setup``). Returns (zkey, wtns) bytes."""
+                n_constraints: int = 0, tau: int = 0x6E7A6362746175, device: int = 0, free_public: bool = False):
+    """Seeded synthetic circuit + zkey built on the GPU (``nzcb_synth_setup_ex``). Returns (zkey, wtns) bytes."""
     lib = load()
-    zp = POINTER(c_uint8)()
-    wp = POINTER(c_uint8)()
-    zl = c_size_t()
-    wl = c_size_t()
-    err = _Err()
-    taub = _buf(int(tau).to_bytes(32, "little"))
-    rc = lib.nzcb_synth_setup(power, n_public, n_inputs, seed, n_constraints, taub, device, ctypes.byref(zp),
-                              ctypes.byref(zl), ctypes.byref(wp), ctypes.byref(wl), ctypes.byref(err))
-    _check(rc, err)
+    zp, zl, wp, wl = _synth_raw(power, n_public, n_inputs, seed, n_constraints, tau, device, free_public)
     try:
-        zkey = ctypes.string_at(zp, zl.value)
-        wtns = ctypes.string_at(wp, wl.value)
+        zkey = ctypes.string_at(zp, zl)
+        wtns = ctypes.string_at(wp, wl)
     finally:
         lib.nzcb_free(ctypes.cast(zp, c_void_p))
         lib.nzcb_free(ctypes.cast(wp, c_void_p))
@@ -643,19 +745,11 @@ def synth_setup(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x
 
 
 def synth_setup_raw(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,
-                    n_constraints: int = 0, tau: int = 0x6E7A6362746175, device: int = 0):
+                    n_constraints: int = 0, tau: int = 0x6E7A6362746175, device: int = 0, free_public: bool = False):
     """Like synth_setup but returns library-owned host buffers (zkey_ptr, zkey_len, wtns_ptr, wtns_len)
     without copying them into Python; release with free_raw()."""
-    lib = load()
-    zp = POINTER(c_uint8)()
-    wp = POINTER(c_uint8)()
-    zl = c_size_t()
-    wl = c_size_t()
-    err = _Err()
-    taub = _buf(int(tau).to_bytes(32, "little"))
-    _check(lib.nzcb_synth_setup(power, n_public, n_inputs, seed, n_constraints, taub, device, ctypes.byref(zp),
-                                ctypes.byref(zl), ctypes.byref(wp), ctypes.byref(wl), ctypes.byref(err)), err)
-    return (ctypes.cast(zp, c_void_p).value, zl.value, ctypes.cast(wp, c_void_p).value, wl.value)
+    zp, zl, wp, wl = _synth_raw(power, n_public, n_inputs, seed, n_constraints, tau, device, free_public)
+    return (ctypes.cast(zp, c_void_p).value, zl, ctypes.cast(wp, c_void_p).value, wl)
 
 
 def free_raw(raw):

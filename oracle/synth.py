@@ -71,12 +71,14 @@ def default_n_constraints(power: int) -> int:
 
 
 def synth_circuit(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,
-                  n_constraints: int | None = None):
+                  n_constraints: int | None = None, free_public: bool = False):
     """Return a dict describing a satisfied circuit plus its full witness.
 
     Keys: ``constraints`` (list of (sa, sb, sc, qm, ql, qr, qo, qc)),
     ``additions`` (ai, bi, ac, bc), ``witness`` (file witness, w[0] = 1),
-    ``nVars``, ``nAdditions``, ``nPublic``.
+    ``nVars``, ``nAdditions``, ``nPublic``. With ``free_public`` the public signals
+    are left out of the wire pool (NZCB_SYNTH_FREE_PUBLIC), so they sit on their
+    public-input gate only and any public values keep the circuit satisfied.
     """
     n = 1 << power
     if n_constraints is None:
@@ -93,7 +95,7 @@ def synth_circuit(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 
         wit.append(v)
     internal = []
     additions = []
-    pool = list(range(1, 1 + n_public + n_inputs))
+    pool = list(range(1 + n_public if free_public else 1, 1 + n_public + n_inputs))
     unused = list(range(1 + n_public, 1 + n_public + n_inputs))
     unused_pos = 0
 

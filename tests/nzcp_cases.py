@@ -11,78 +11,20 @@ from __future__ import annotations
 
 import random
 
+import nzcb.nzcp  # noqa: F401  (input preparation: pass builders, CBOR codec)
 from oracle import nzcp_circuit as nz
 from oracle.bn254 import R_MOD
 
-EXAMPLE_JTI = bytes.fromhex("60a4f54d4e304332be33ad78b1eafa4b")
-EXAMPLE_KID = b"key-1"
-LIVE_KID = b"z12Kf7UQ"
-EXAMPLE_ISS = "did:web:nzcp.covid19.health.nz"
-LIVE_ISS = "did:web:nzcp.identity.health.nz"
-EXAMPLE_NBF = 1635883530
-EXAMPLE_EXP = 1951416330
+from nzcb.nzcp import (EXAMPLE_EXP, EXAMPLE_ISS, EXAMPLE_JTI, EXAMPLE_KID, EXAMPLE_NBF, LIVE_ISS,  # noqa: F401
+                       LIVE_KID, Raw, claims, credential_subject, sig_structure)
+from nzcb.nzcp import cbor_encode as cbor
+from nzcb.nzcp import cbor_head as _head
+
 DATA_1_20 = bytes(range(1, 21))   # test/nzcp.js:36
 
 
-class Raw(bytes):
-    """Pre-encoded CBOR item."""
-
-
-def _head(major: int, n: int) -> bytes:
-    if n < 24:
-        return bytes([major << 5 | n])
-    if n < 256:
-        return bytes([major << 5 | 24, n])
-    if n < 65536:
-        return bytes([major << 5 | 25]) + n.to_bytes(2, "big")
-    if n < 1 << 32:
-        return bytes([major << 5 | 26]) + n.to_bytes(4, "big")
-    return bytes([major << 5 | 27]) + n.to_bytes(8, "big")
-
-
-def cbor(x) -> bytes:
-    """Minimal CBOR encoder (RFC 7049 definite lengths); dicts keep insertion order."""
-    if isinstance(x, Raw):
-        return bytes(x)
-    if isinstance(x, bool):
-        return b"\xf5" if x else b"\xf4"
-    if isinstance(x, int):
-        return _head(0, x) if x >= 0 else _head(1, -1 - x)
-    if isinstance(x, bytes):
-        return _head(2, len(x)) + x
-    if isinstance(x, str):
-        b = x.encode()
-        return _head(3, len(b)) + b
-    if isinstance(x, list):
-        return _head(4, len(x)) + b"".join(cbor(v) for v in x)
-    if isinstance(x, dict):
-        return _head(5, len(x)) + b"".join(cbor(k) + cbor(v) for k, v in x.items())
-    raise TypeError(type(x))
-
-
-def credential_subject(given="Jack", family="Sparrow", dob="1960-04-16", order=("givenName", "familyName", "dob")):
-    vals = {"givenName": given, "familyName": family, "dob": dob}
-    return {k: vals[k] for k in order}
-
-
-def vc(subject: dict) -> dict:
-    return {
-        "@context": ["https://www.w3.org/2018/credentials/v1", "https://nzcp.covid19.health.nz/contexts/v1"],
-        "version": "1.0.0",
-        "type": ["VerifiableCredential", "PublicCovidPass"],
-        "credentialSubject": subject,
-    }
-
-
-def claims(iss=EXAMPLE_ISS, nbf=EXAMPLE_NBF, exp=EXAMPLE_EXP, subject=None, jti=EXAMPLE_JTI, order=(1, 5, 4, "vc", 7)):
-    vals = {1: iss, 5: nbf, 4: exp, "vc": vc(subject or credential_subject()), 7: jti}
-    return {k: vals[k] for k in order}
-
-
 def to_be_signed(payload: bytes, kid: bytes = EXAMPLE_KID) -> bytes:
-    """COSE Sig_structure ["Signature1", protected, h'', payload] (RFC 8152 §4.4)."""
-    protected = cbor({4: kid, 1: -7})
-    return cbor(["Signature1", protected, b"", payload])
+    return sig_structure(cbor({4: kid, 1: -7}), payload)
 
 
 def example_tbs() -> bytes:

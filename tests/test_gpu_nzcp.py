@@ -109,3 +109,46 @@ def test_device_path_writes_witness_publics(nzcb_mod):
 def test_bad_params_rejected(nzcb_mod):
     with pytest.raises(nzcb_mod.NzcbError):
         nzcb_mod.nzcp_witness(b"", 0, dict(is_live=1, max_tbs_bytes=600, max_array_len_vc=0, max_map_len_vc=4))
+
+
+@pytest.mark.parametrize("power,nin,seed", [(6, 4, 21), (8, 8, 22)])
+def test_free_public_synth_bytes(nzcb_mod, power, nin, seed):
+    from oracle import binfmt, plonk, synth
+    zkey, wtns = nzcb_mod.synth_setup(power, 3, nin, seed, 0, 555, free_public=True)
+    c = synth.synth_circuit(power, 3, nin, seed=seed, free_public=True)
+    assert wtns == binfmt.write_wtns(c["witness"])
+    assert zkey == binfmt.write_zkey(plonk.setup(c, 555))
+
+
+def test_full_prove_pipeline_bit_exact(nzcb_mod):
+    """fullProve on device: nzcp witness kernel -> witness[1..3] in HBM -> prove_batch.
+    Proofs bit-exact against the C oracle prover on the same witness (publics replaced
+    by the CPU restatement's outputs), publics equal the restatement's, pairing-verified."""
+    from oracle import cbind, synth
+    nzcb = nzcb_mod
+    zkey, wtns = nzcb.synth_setup(12, 3, 2970, 0x6E7A6362, 0, 0x6E7A6362746175, free_public=True)
+    nwit = (len(wtns) - 76) // 32
+    base = wtns[76:76 + 32 * nwit]
+    ctx = nzcb.ProverContext(zkey)
+    ctx.set_lanes(2)
+    prover = nzcb.NzcpProver(ctx, base)
+    cases = [C.case(f"p{i}", nz.LIVE_PARAMS, C.live_tbs(subject=C.credential_subject(g, f, "1960-04-16")),
+                    data=bytes([i + 1]) * 20)
+             for i, (g, f) in enumerate((("Jack", "Sparrow"), ("Jo", "Bloggs"), ("Ana", "Te Whare")))]
+    bl = b"".join(x.to_bytes(32, "little") for x in synth.fixed_blindings())
+    try:
+        res, recs = prover.full_prove(b"".join(C.case_input_bytes(c) for c in cases), [bl] * 3)
+        with pytest.raises(nzcb.NzcbError):
+            prover.full_prove(C.case_input_bytes(C.case("bad", nz.LIVE_PARAMS, C.live_tbs(), length=360)))
+    finally:
+        prover.close()
+        ctx.close()
+    for c, (proof, pub), r in zip(cases, res, recs):
+        exp = [int(v) for v in C.oracle_record(c)["out"]]
+        assert [int.from_bytes(pub[32 * k:32 * k + 32], "little") for k in range(3)] == exp == r["out"]
+        assert nzcb.verify(ctx.vk, proof, pub)
+        w = bytearray(wtns)
+        for k in range(3):
+            w[76 + 32 * (1 + k):76 + 32 * (2 + k)] = exp[k].to_bytes(32, "little")
+        ref_proof, ref_pub, _ = cbind.prove(zkey, bytes(w), bl, npub=3)
+        assert proof == ref_proof and pub == ref_pub[:96]

@@ -190,3 +190,38 @@ def test_golden_fixture_is_current():
     statuses = {r["status"] for r in gold["expected"]}
     assert statuses >= {nz.OK, nz.ERR_BIT, nz.ERR_LEN, nz.ERR_RANGE, nz.ERR_SELECT, nz.ERR_NOT_MAP,
                         nz.ERR_UINT23, nz.ERR_NOT_STRING, nz.ERR_UNPINNED}
+
+
+def test_free_public_synth_accepts_any_public_values():
+    """NZCB_SYNTH_FREE_PUBLIC circuits stay satisfied when witness[1..3] are replaced
+    by nzcp outputs (the fullProve stand-in of bench.py): oracle prove + trapdoor verify."""
+    from oracle import plonk, synth
+    c = synth.synth_circuit(6, 3, 5, seed=11, free_public=True)
+    zk = plonk.setup(c, 4321)
+    bits, ln, data = nz.circuit_input(C.live_tbs(), C.DATA_1_20, 351)
+    out = nz.nzcp_pub_identity(bits, ln, data, **nz.LIVE_PARAMS).out
+    wit = list(c["witness"])
+    wit[1:4] = out
+    proof, pub = plonk.prove(zk, wit, synth.fixed_blindings())
+    assert pub == out
+    assert plonk.verify_with_trapdoor(zk, pub, proof, 4321)
+    # the default family wires the public signals into later gates: replacing them breaks it
+    c2 = synth.synth_circuit(6, 3, 5, seed=11)
+    assert any(s in (1, 2, 3) for g in c2["constraints"][3:] for s in g[:3])
+    assert not any(s in (1, 2, 3) for g in c["constraints"][3:] for s in g[:3])
+
+
+def test_bench_passes_are_valid_and_distinct():
+    """bench.py's per-proof passes: the restatement accepts them with distinct outputs."""
+    import bench
+    from oracle.bn254 import R_MOD  # noqa: F401
+    raw = bench.pass_inputs(range(3))
+    per = (351 * 8 + 161) * 32
+    assert len(raw) == 3 * per
+    outs = []
+    for i in range(3):
+        sig = [int.from_bytes(raw[i * per + 32 * k:i * per + 32 * k + 32], "little") for k in range(351 * 8 + 161)]
+        w = nz.nzcp_pub_identity(sig[:2808], sig[2808], sig[2809:], **nz.LIVE_PARAMS)
+        assert w.status == nz.OK and w.vc_pos == 80
+        outs.append(tuple(w.out))
+    assert len(set(outs)) == 3
