@@ -303,6 +303,43 @@ napi_value Calldata(napi_env env, napi_callback_info info) {
   return json_string(env, s);
 }
 
+// nzcpWitness(inputs: Buffer, count: number, params: [isLive, maxTbsBytes, maxArrayLenVC,
+// maxMapLenVC], device: number) -> Buffer of count nzcb_nzcp_record (include/nzcb.h).
+// Synchronous: one launch of the nzcp witness kernel, well under a millisecond.
+napi_value NzcpWitness(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  void* data = nullptr;
+  size_t len = 0;
+  CHECK(napi_get_buffer_info(env, argv[0], &data, &len));
+  int32_t count = 0, device = 0;
+  CHECK(napi_get_value_int32(env, argv[1], &count));
+  nzcb_nzcp_params prm{};
+  int32_t* fields[4] = {&prm.is_live, &prm.max_tbs_bytes, &prm.max_array_len_vc, &prm.max_map_len_vc};
+  for (uint32_t i = 0; i < 4; i++) {
+    napi_value v;
+    CHECK(napi_get_element(env, argv[2], i, &v));
+    CHECK(napi_get_value_int32(env, v, fields[i]));
+  }
+  if (argc > 3) napi_get_value_int32(env, argv[3], &device);
+  if (count < 0 || len != nzcb_nzcp_input_signals(&prm) * 32 * (size_t)count) {
+    napi_throw_error(env, nullptr, "nzcpWitness: inputs must be count x input signals x 32 bytes");
+    return nullptr;
+  }
+  void* out_data = nullptr;
+  napi_value out;
+  CHECK(napi_create_buffer(env, sizeof(nzcb_nzcp_record) * (size_t)(count ? count : 1), &out_data, &out));
+  nzcb_err err{};
+  int rc = nzcb_nzcp_witness(device, &prm, static_cast<const uint8_t*>(data), count,
+                             static_cast<nzcb_nzcp_record*>(out_data), &err);
+  if (rc) {
+    napi_throw(env, make_error(env, err.code, err.msg));
+    return nullptr;
+  }
+  return out;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"createContext", nullptr, CreateContext, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -314,6 +351,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"vkToJson", nullptr, VkToJson, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"verify", nullptr, Verify, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"calldata", nullptr, Calldata, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"nzcpWitness", nullptr, NzcpWitness, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

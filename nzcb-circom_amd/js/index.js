@@ -225,10 +225,61 @@ async function exportSolidityCallData(proof, publicSignals) {
   return addon.calldata(proofBuf(proof), pubBuf(publicSignals));
 }
 
+// nzcp witness on the GPU (include/nzcb.h nzcb_nzcp_witness): the NZCPPubIdentity
+// public signals and semantic signals of one or more circuit inputs (the object
+// plonk.fullProve takes, test/nzcp.js:41). Throws like calculateWitness when a pass
+// fails one of the circuit's constraints.
+const NZCP_PARAMS = { live: [1, 351, 0, 4], example: [0, 314, 0, 4] };
+const NZCP_STATUS = ['ok', 'toBeSigned bit check', 'toBeSignedLen > MaxToBeSignedBytes',
+  'LessThan operands out of range', 'QuinSelector index out of range', 'CBOR type is not a map',
+  'CBOR map length > 23', 'CBOR type is not a string', 'negative toBeSignedLen (unpinned)'];
+const NZCP_RECORD_BYTES = 288;
+
+function fieldLE(v) {
+  let x = BigInt(v) % R;
+  if (x < BigInt(0)) x += R;
+  return le32(x.toString());
+}
+
+function nzcpWitness(inputs, options) {
+  options = options || {};
+  const list = Array.isArray(inputs) ? inputs : [inputs];
+  const params = options.params || NZCP_PARAMS[options.circuit || 'live'];
+  const bufs = [];
+  for (const inp of list) {
+    if (inp.toBeSigned.length !== 8 * params[1] || inp.data.length !== 160) {
+      throw new Error(`nzcp input: toBeSigned must have ${8 * params[1]} bits and data 160`);
+    }
+    for (const b of inp.toBeSigned) bufs.push(fieldLE(b));
+    bufs.push(fieldLE(inp.toBeSignedLen));
+    for (const b of inp.data) bufs.push(fieldLE(b));
+  }
+  const raw = addon.nzcpWitness(Buffer.concat(bufs), list.length, params, options.device || 0);
+  const out = [];
+  for (let i = 0; i < list.length; i++) {
+    const r = raw.subarray(i * NZCP_RECORD_BYTES, (i + 1) * NZCP_RECORD_BYTES);
+    const status = r.readInt32LE(0);
+    if (status !== 0) {
+      throw new Error(`Assert Failed (nzcp pass ${i}): ${NZCP_STATUS[status] || status} (detail ${r.readInt32LE(4)})`);
+    }
+    const nullifier = r.subarray(128, 192);
+    out.push({
+      publicSignals: [0, 1, 2].map((k) => BigInt('0x' + Buffer.from(r.subarray(192 + 32 * k, 224 + 32 * k))
+        .reverse().toString('hex')).toString()),
+      exp: r.readUInt32LE(8),
+      vcPos: r.readInt32LE(12),
+      nullifier: nullifier.subarray(0, Math.max(0, Math.min(64, r.readInt32LE(28)))).toString('latin1'),
+      toBeSignedHash: r.subarray(32, 64).toString('hex'),
+      nullifierHash: r.subarray(64, 128).toString('hex'),
+    });
+  }
+  return Array.isArray(inputs) ? out : out[0];
+}
+
 module.exports = {
   plonk: { prove, fullProve, verify, exportSolidityCallData },
   zKey: { exportVerificationKey },
-  nzcp: require('./nzcp.js'),
+  nzcp: Object.assign({}, require('./nzcp.js'), { witness: nzcpWitness }),
   wtns: { calculate: wtnsCalculate },
   version: addon.version,
   deviceCount: addon.deviceCount,

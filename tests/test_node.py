@@ -136,3 +136,26 @@ console.log(JSON.stringify({{tbs: z.toBeSigned(uri).toString('hex'), claims: z.c
     # data: bytes reversed, bits reversed within each byte (EVM rearrangement)
     dbytes = bytes(sum(inp["data"][8 * i + t] << (7 - t) for t in range(8)) for i in range(20))
     assert dbytes == bytes(int(f"{b:08b}"[::-1], 2) for b in reversed(range(1, 21)))
+
+
+@needs_node
+@pytest.mark.gpu
+def test_node_nzcp_witness_on_gpu():
+    """Node nzcp.witness (addon.nzcpWitness -> nzcb_nzcp_witness): the example pass in the
+    example circuit gives the reference test's public signals; a pass in
+    the wrong circuit throws like calculateWitness."""
+    script = f"""
+const n = require('./');
+const z = n.nzcp;
+const uri = '{EXAMPLE_PASS_URI}';
+const data = Buffer.from([...Array(20).keys()].map((i) => i + 1));
+const r = z.witness(z.circuitInput(uri, data, z.EXAMPLE_TOBESIGNED_MAX), {{circuit: 'example'}});
+let threw = '';
+try {{ z.witness(z.circuitInput(uri, data, z.LIVE_TOBESIGNED_MAX)); }} catch (e) {{ threw = e.message; }}
+console.log(JSON.stringify({{r, expected: z.expectedPublicSignals(uri, data), threw}}));
+"""
+    d = json.loads(run_node(script))
+    assert d["r"]["publicSignals"] == d["expected"]
+    assert d["r"]["vcPos"] == 76 and d["r"]["nullifier"] == "Jack,Sparrow,1960-04-16"
+    assert d["r"]["toBeSignedHash"] == "271ce33d671a2d3b816d788135f4343e14bc66802f8cd841faac939e8c11f3ee"
+    assert "CBOR type is not a map" in d["threw"]
