@@ -43,6 +43,15 @@ struct Fq29 {
                                        0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0x000e0a77u};  // 2^256 mod p
 };
 
+// BN254 Fr in the same radix (the NTT's twiddle products, ntt.hip). r = 1 + 2^28 t,
+// so -r^-1 mod 2^29 = 2^28 - 1.
+struct Fr29 {
+  static constexpr uint32_t MASK = (1u << 29) - 1;
+  static constexpr uint32_t INV = 0x0fffffffu;
+  static constexpr uint32_t P[9] = {0x10000001u, 0x1f0fac9fu, 0x0e5c2450u, 0x07d090f3u, 0x1585d283u,
+                                    0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
+};
+
 NZ_HD F29 f29_const(const uint32_t (&c)[9]) {
   F29 r;
 #pragma unroll
@@ -50,9 +59,9 @@ NZ_HD F29 f29_const(const uint32_t (&c)[9]) {
   return r;
 }
 
-// a * b * 2^-261 mod p (see the invariants above)
+// a * b * 2^-261 mod p (see the invariants above); Q = Fq29 or Fr29
+template <class Q = Fq29>
 NZ_HD F29 mul29(const F29& a, const F29& b) {
-  using Q = Fq29;
   uint32_t m[9];
   F29 r;
   uint64_t acc = 0;
@@ -218,7 +227,8 @@ NZ_HD bool is0p29(const F29& x) {
 }
 
 // radix change of the same integer (< 2^256, no Montgomery change)
-NZ_HD F29 split29(const Fq& x) {
+template <class Par>
+NZ_HD F29 split29(const Fe<Par>& x) {
   F29 r;
 #pragma unroll
   for (int i = 0; i < 9; i++) {
@@ -241,6 +251,24 @@ NZ_HD Fq join29(const F29& x) {  // x normalized, < 2^256
     if (limb + 1 < 8) r.v[limb + 1] |= (uint32_t)(w >> 32);
   }
   return r;
+}
+
+// a * w for a canonical Montgomery-256 Fr and a twiddle w given as split29 of its
+// Montgomery-261 form (w * 2^261 mod r): one 9x29 product instead of the 8x32 mac
+// chain of field.h, canonical Montgomery-256 result
+NZ_HD Fr mul_fr29(const Fr& a, const F29& w29) {
+  const F29 t = mul29<Fr29>(split29(a), w29);  // < 2r, limbs < 2^29
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int bit = 29 * i, limb = bit >> 5, sh = bit & 31;
+    const uint64_t w = (uint64_t)t.v[i] << sh;
+    r.v[limb] |= (uint32_t)w;
+    if (limb + 1 < 8) r.v[limb + 1] |= (uint32_t)(w >> 32);
+  }
+  return reduce_once(r);
 }
 
 // Montgomery-261 value (any F29 < 2^257) -> canonical Montgomery-256 Fq (csrc/field.h)

@@ -1,5 +1,6 @@
 // Fr radix-2 NTT / iNTT over natural-order data.
 #pragma once
+#include "f29.h"
 #include "common.h"
 
 namespace nzcb {
@@ -13,6 +14,9 @@ struct NttTables {
   // k < 2^g, stored contiguously at offset 2^g - 1, so the twiddles of consecutive
   // butterflies of a stage are consecutive in memory (coalesced 32-byte loads).
   DevBuf<Fr> fwd, inv;  // 2^max_log - 1 entries each
+  // The same twiddles as split29 of their Montgomery-261 form (w * 2^261 mod r), the
+  // operand of mul_fr29 (f29.h) in the butterflies
+  DevBuf<F29> fwd29, inv29;
   void init(int max_log, hipStream_t st);
 };
 

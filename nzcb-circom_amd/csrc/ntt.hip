@@ -60,12 +60,24 @@ ntt_stage_table_kernel(Fr* __restrict__ out, const Fr* __restrict__ full, int L,
   out[i] = full[k << (L - g - 1)];
 }
 
+// out[i] = split29(tw[i] * 2^5): Montgomery-256 -> Montgomery-261 twiddles
+__global__ void __launch_bounds__(256) ntt_tw29_kernel(F29* __restrict__ out, const Fr* __restrict__ tw, size_t count) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  Fr w = tw[i];
+#pragma unroll
+  for (int k = 0; k < 5; k++) w = w + w;
+  out[i] = split29(w);
+}
+
 void NttTables::init(int L, hipStream_t st) {
   max_log = L;
   const size_t half = L >= 1 ? (size_t(1) << (L - 1)) : 1;
   const size_t total = (size_t(1) << L) - 1;
   fwd.alloc(total ? total : 1);
   inv.alloc(total ? total : 1);
+  fwd29.alloc(total ? total : 1);
+  inv29.alloc(total ? total : 1);
   DevBuf<Fr> full(half);
   for (int dir = 0; dir < 2; dir++) {
     Fr w = fr_root_of_unity(L);
@@ -81,9 +93,12 @@ void NttTables::init(int L, hipStream_t st) {
     NZ_HIP(hipMemcpyAsync(dhi.p, hi.data(), nhi * sizeof(Fr), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(ntt_table_kernel, dim3(grid_for(half, 256, 1u << 30)), dim3(256), 0, st, full.p, dlo.p, dhi.p,
                        half);
-    if (total)
+    if (total) {
       hipLaunchKernelGGL(ntt_stage_table_kernel, dim3(grid_for(total, 256, 1u << 30)), dim3(256), 0, st,
                          dir ? inv.p : fwd.p, full.p, L, total);
+      hipLaunchKernelGGL(ntt_tw29_kernel, dim3(grid_for(total, 256, 1u << 30)), dim3(256), 0, st,
+                         dir ? inv29.p : fwd29.p, dir ? inv.p : fwd.p, total);
+    }
     NZ_HIP(hipGetLastError());
     NZ_HIP(hipStreamSynchronize(st));
   }
@@ -91,7 +106,7 @@ void NttTables::init(int L, hipStream_t st) {
 
 // One pass: stages [s, s+q) on tiles of (2^q rows) x (2^logC columns).
 __global__ void __launch_bounds__(kNttThreads)
-ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int s, int q, int logC, int first, Fr scale,
+ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s, int q, int logC, int first, Fr scale,
                 int do_scale, int last, NttIo io) {
   extern __shared__ Fr tile[];
   const int C = 1 << logC;
@@ -125,11 +140,10 @@ ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int s, 
   }
   __syncthreads();
   const int nbf = n_el >> 1;
-  const Fr one = Fr::one();
   int st = 0;
   if (q & 1) {  // odd stage count: one radix-2 stage, then radix-4 pairs of stages
     const int g = s;
-    const Fr* __restrict__ twg = tw + (((size_t)1 << g) - 1);
+    const F29* __restrict__ twg = tw + (((size_t)1 << g) - 1);
 #pragma unroll
     for (int u = 0; u < kBfPerThread; u++) {
       const int b = tid + u * kNttThreads;
@@ -139,7 +153,7 @@ ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int s, 
       const int i0 = ((2 * j0) << logC) + c, i1 = ((2 * j0 + 1) << logC) + c;
       const size_t k = first ? 0 : (lo0 + c);
       const Fr x0 = tile[i0];
-      const Fr x1 = g ? tile[i1] * twg[k] : tile[i1];
+      const Fr x1 = g ? mul_fr29(tile[i1], twg[k]) : tile[i1];
       tile[i0] = x0 + x1;
       tile[i1] = x0 - x1;
     }
@@ -153,8 +167,8 @@ ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int s, 
   for (; st < q; st += 2) {
     const int h = 1 << st;
     const int g = s + st;
-    const Fr* __restrict__ twa = tw + (((size_t)1 << g) - 1);
-    const Fr* __restrict__ twb = tw + (((size_t)1 << (g + 1)) - 1);
+    const F29* __restrict__ twa = tw + (((size_t)1 << g) - 1);
+    const F29* __restrict__ twb = tw + (((size_t)1 << (g + 1)) - 1);
     const int b = tid;
     if (b < ngroups) {
       const int c = b & (C - 1);
@@ -163,16 +177,19 @@ ntt_pass_kernel(const Fr* in, Fr* out, const Fr* __restrict__ tw, int L, int s, 
       const int j = ((pr >> st) << (st + 2)) | low;
       const size_t ka = first ? (size_t)low : (((size_t)low << s) + lo0 + c);
       const size_t kc = first ? (size_t)(low + h) : (((size_t)(low + h) << s) + lo0 + c);
-      const Fr wa = g ? twa[ka] : one;
-      const Fr wb = twb[ka];
-      const Fr wc = twb[kc];
+      const F29 wb = twb[ka];
+      const F29 wc = twb[kc];
       const int i0 = (j << logC) + c, i1 = ((j + h) << logC) + c, i2 = ((j + 2 * h) << logC) + c,
                 i3 = ((j + 3 * h) << logC) + c;
       const Fr x0 = tile[i0], x1 = tile[i1], x2 = tile[i2], x3 = tile[i3];
-      const Fr t1 = g ? x1 * wa : x1;
-      const Fr t3 = g ? x3 * wa : x3;
+      Fr t1 = x1, t3 = x3;
+      if (g) {
+        const F29 wa = twa[ka];
+        t1 = mul_fr29(x1, wa);
+        t3 = mul_fr29(x3, wa);
+      }
       const Fr y0 = x0 + t1, y1 = x0 - t1, y2 = x2 + t3, y3 = x2 - t3;
-      const Fr u2 = y2 * wb, u3 = y3 * wc;
+      const Fr u2 = mul_fr29(y2, wb), u3 = mul_fr29(y3, wc);
       tile[i0] = y0 + u2;
       tile[i2] = y0 - u2;
       tile[i1] = y1 + u3;
@@ -207,7 +224,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   const NttIo io = iop ? *iop : NttIo();
   if (L > t.max_log) throw Error(NZCB_ERR_ARG, "ntt size exceeds table");
   if (in == out) throw Error(NZCB_ERR_ARG, "ntt requires in != out");
-  const Fr* tw = inverse_dir ? t.inv.p : t.fwd.p;
+  const F29* tw = inverse_dir ? t.inv29.p : t.fwd29.p;
   Fr sc = Fr::one();
   int do_scale = 0;
   if (inverse_dir) {

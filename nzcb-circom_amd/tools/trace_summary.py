@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 --kernel-trace CSV: per-kernel time and the GPU busy fraction
+"""Summarise a rocprofv3 --kernel-trace CSV (or rocpd .db): per-kernel time and the GPU busy fraction
 (union of kernel intervals) over the trace's last `--window` seconds."""
 import argparse
 import csv
@@ -15,9 +15,14 @@ def main():
                     help="window from the COUNT-th last launch of a kernel whose name contains KERNEL to its last")
     a = ap.parse_args()
     rows = []
-    with open(a.trace) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    if a.trace.endswith(".db"):  # rocprofv3 >= 7 default output (rocpd SQLite)
+        import sqlite3
+        con = sqlite3.connect(a.trace)
+        rows = [(int(s), int(e), n) for s, e, n in con.execute("select start, end, name from kernels")]
+    else:
+        with open(a.trace) as f:
+            for r in csv.DictReader(f):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
     t_end = max(e for _, e, _ in rows)
     if a.last:
