@@ -48,10 +48,17 @@ static constexpr int kMsmThreads = 256;
 
 // Onesweep with a chosen digit width: the generic path's 20-bit keys take 2 passes of
 // 10 bits instead of 3 with the library's 8-bit default for gfx950.
+#ifndef NZ_SORT_BLOCK
+#define NZ_SORT_BLOCK 1024
+#endif
+#ifndef NZ_SORT_ITEMS
+#define NZ_SORT_ITEMS 16
+#endif
 template <unsigned Bits>
 using SortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, Bits,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<NZ_SORT_BLOCK, NZ_SORT_ITEMS>,
+                                        rocprim::kernel_config<NZ_SORT_BLOCK, NZ_SORT_ITEMS>, Bits,
                                         rocprim::block_radix_rank_algorithm::match>>;
 
 // digit bits per onesweep pass: 8 for 16-bit keys, 10 for the <= 20-bit 32-bit keys
