@@ -24,7 +24,8 @@
 //  2. sort:       rocPRIM onesweep radix sort of (key, base index|sign), 2 passes of
 //                 <= 10 key bits (16-bit keys for the fixed-base c <= 17)
 //  3. offsets:    bucket start positions by binary search in the sorted keys
-//  4. accumulate: thread per fixed 32-entry chunk of the sorted stream (load balance
+//  4. accumulate: thread per fixed 32-entry chunk of the sorted stream (doubled past
+//                 2^25 entries, chunk_for; load balance
 //                 independent of the digit distribution): XYZZ mixed adds of the
 //                 gathered affine bases; bucket runs inside one chunk are written
 //                 directly, runs crossing a chunk edge go to per-chunk carries
@@ -86,7 +87,16 @@ static void radix_sort(void* tmp, size_t& tmp_bytes, const K* kin, K* kout, cons
       NZ_HIP(rocprim::radix_sort_pairs<SortConfig<10>>(tmp, tmp_bytes, kin, kout, vin, vout, m, 0, end_bit, st));
   }
 }
-static constexpr uint32_t kChunk = 32;
+static constexpr uint32_t kChunk = 32;  // entries per accumulation thread, up to 2^25 entries
+
+// Entries per accumulation thread: kChunk up to 2^25 entries, then doubled so the grid
+// stays ~2^20 threads and a bucket spans ~15 chunks at every size (at 2^24 points a
+// 32-entry chunk left ~120 carries per bucket and the finalize took 360 ms).
+static uint32_t chunk_for(size_t entries) {
+  uint32_t c = kChunk;
+  while (entries / c > (size_t(1) << 20)) c *= 2;
+  return c;
+}
 static constexpr int kSegLen = 8;
 static constexpr int kSumThreads = 256;  // level-1 sums: block size
 static constexpr int kSumPer = 4;        // level-1 sums: sequential adds per thread
@@ -204,16 +214,16 @@ __device__ __forceinline__ uint32_t find_key(const uint32_t* __restrict__ offset
 }
 
 __global__ void __launch_bounds__(kMsmThreads)
-msm_accumulate_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
+msm_accumulate_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
                       const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
                       G1xyzz* __restrict__ buckets, G1xyzz* __restrict__ carry_own,
                       G1xyzz* __restrict__ carry_cont) {
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nthreads) return;
   const uint32_t M = offsets[nkeys];
-  const uint32_t s = (uint32_t)t * kChunk;
+  const uint32_t s = (uint32_t)t * chunk;
   if (s >= M) return;
-  const uint32_t e = (s + kChunk < M) ? s + kChunk : M;
+  const uint32_t e = (s + chunk < M) ? s + chunk : M;
   uint32_t k = find_key(offsets, nkeys, s);
   uint32_t kstart = offsets[k], kend = offsets[k + 1];
   G1xyzz acc = G1xyzz::inf();
@@ -264,16 +274,16 @@ __device__ __forceinline__ G1xyzz load_point(const Xyzz29& a) {
 
 template <int WAVES>
 __global__ void __launch_bounds__(kMsmThreads) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
-msm_accumulate29_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
+msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
                         const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
                         Xyzz29* __restrict__ buckets, Xyzz29* __restrict__ carry_own,
                         Xyzz29* __restrict__ carry_cont) {
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nthreads) return;
   const uint32_t M = offsets[nkeys];
-  const uint32_t s = (uint32_t)t * kChunk;
+  const uint32_t s = (uint32_t)t * chunk;
   if (s >= M) return;
-  const uint32_t e = (s + kChunk < M) ? s + kChunk : M;
+  const uint32_t e = (s + chunk < M) ? s + chunk : M;
   uint32_t k = find_key(offsets, nkeys, s);
   uint32_t kstart = offsets[k], kend = offsets[k + 1];
   Xyzz29 acc;
@@ -360,14 +370,15 @@ __device__ __forceinline__ G1xyzz sum_run(const Xyzz29* carry_own, const Xyzz29*
 // P = Xyzz29: every bucket is converted here (single-chunk ones from `single`).
 template <class P>
 __global__ void __launch_bounds__(kMsmThreads)
-msm_bucket_finalize_kernel(const uint32_t* __restrict__ offsets, uint32_t nkeys, const P* __restrict__ single,
+msm_bucket_finalize_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys,
+                           const P* __restrict__ single,
                            const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
                            G1xyzz* __restrict__ buckets, uint32_t* __restrict__ large) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nkeys) return;
   const uint32_t s = offsets[k], e = offsets[k + 1];
   if (e == s) return;
-  const uint32_t c0 = s / kChunk, c1 = (e - 1) / kChunk;
+  const uint32_t c0 = s / chunk, c1 = (e - 1) / chunk;
   if (c0 == c1) {  // stored by the accumulation
     if (single) buckets[k] = load_point(single[k]);
     return;
@@ -448,14 +459,14 @@ __device__ __forceinline__ G1xyzz block_sum(int per, G1xyzz* sh, Load&& load) {
 // digits): one workgroup per bucket, kSumThreads-way partial sums + LDS tree.
 template <class P>
 __global__ void __launch_bounds__(kSumThreads)
-msm_bucket_large_kernel(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
+msm_bucket_large_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
                         const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
                         G1xyzz* __restrict__ buckets) {
   __shared__ G1xyzz sh[kSumThreads];
   const uint32_t count = large[0];
   for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
     const uint32_t k = large[1 + i];
-    const uint32_t c0 = offsets[k] / kChunk, c1 = (offsets[k + 1] - 1) / kChunk;
+    const uint32_t c0 = offsets[k] / chunk, c1 = (offsets[k + 1] - 1) / chunk;
     const uint32_t span = c1 - c0 + 1;
     const int per = (int)((span + kSumThreads - 1) / kSumThreads);
     const G1xyzz r = block_sum<kSumThreads>(per, sh, [&](int step, G1xyzz& rhs) {
@@ -712,7 +723,8 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                        p.nkeys, sc.offsets.p);
   }
   NZ_HIP(hipGetLastError());
-  const size_t nthreads = (p.entries + kChunk - 1) / kChunk;
+  const uint32_t chunk = chunk_for(p.entries);
+  const size_t nthreads = (p.entries + chunk - 1) / chunk;
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[3], st));
   static const int acc_waves = [] {
     const char* e = std::getenv("NZCB_ACC29_WAVES");
@@ -722,10 +734,10 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   if (table) {
     if (!sc.buckets29.p) throw Error(NZCB_ERR_ARG, "msm scratch was not sized for the fixed-base schedule");
     hipLaunchKernelGGL(acc_waves >= 4 ? msm_accumulate29_kernel<4> : msm_accumulate29_kernel<3>, agrid,
-                       dim3(kMsmThreads), 0, st, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads,
+                       dim3(kMsmThreads), 0, st, chunk, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads,
                        sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
   } else {
-    hipLaunchKernelGGL(msm_accumulate_kernel, agrid, dim3(kMsmThreads), 0, st, gather, sc.sorted.p, sc.offsets.p,
+    hipLaunchKernelGGL(msm_accumulate_kernel, agrid, dim3(kMsmThreads), 0, st, chunk, gather, sc.sorted.p, sc.offsets.p,
                        p.nkeys, nthreads, sc.buckets.p, sc.carry_own.p, sc.carry_cont.p);
   }
   NZ_HIP(hipGetLastError());
@@ -733,18 +745,20 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
   if (table) {
-    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, sc.offsets.p, p.nkeys,
+    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
                        (const Xyzz29*)sc.buckets29.p, (const Xyzz29*)sc.carry_own29.p,
                        (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p, sc.large.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_bucket_large_kernel<Xyzz29>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, sc.offsets.p,
+    hipLaunchKernelGGL(msm_bucket_large_kernel<Xyzz29>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, chunk,
+                       sc.offsets.p,
                        sc.large.p, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p);
   } else {
-    hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, sc.offsets.p, p.nkeys,
+    hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
                        (const G1xyzz*)nullptr, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p,
                        sc.buckets.p, sc.large.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_bucket_large_kernel<G1xyzz>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, sc.offsets.p,
+    hipLaunchKernelGGL(msm_bucket_large_kernel<G1xyzz>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, chunk,
+                       sc.offsets.p,
                        sc.large.p, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p, sc.buckets.p);
   }
   NZ_HIP(hipGetLastError());

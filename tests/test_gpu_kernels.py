@@ -167,3 +167,28 @@ def test_msm_long_carry_runs(engine, fixed):
         bases = b"".join(bn.g1_to_lem(p) for p in pts)
         got = _affine(engine.msm(bases, b"".join(bn.to_le(s) for s in sc), False))
         assert got == want
+
+
+def test_msm_large_chunks_schedules_agree_and_split_linearly():
+    """2^22 points (about 63-67 M bucket entries): the accumulation chunk doubles past
+    2^25 entries (msm.hip chunk_for). The generic schedule (c = 16 windows) and the
+    fixed-base table schedule (c = 17, 29-bit radix) are independent code paths and
+    must agree, and MSM(P, s) = MSM(P[:h], s[:h]) + MSM(P[h:], s[h:]) (size-independent)."""
+    import nzcb
+    n, h = 1 << 22, 1 << 21
+    eng = nzcb.Engine(0, max_log_ntt=-1, max_msm_points=n + 8)
+    sc, bases = nzcb.dev_alloc(n * 32), nzcb.dev_alloc(n * 64)
+    try:
+        eng.random_fr(sc, n, 0x6E7A6362)
+        eng.fixed_base(sc, n, bases)          # bases_i = [s_i] G1, affine LEM
+        eng.random_fr(sc, n, 0x5EED)          # fresh scalars (Montgomery)
+        generic = _affine(eng.msm_dev(bases, sc, n, True))
+        fixed = _affine(eng.msm_fixed_dev(bases, n, sc, n, True))
+        lo = _affine(eng.msm_fixed_dev(bases, h, sc, h, True))
+        hi = _affine(eng.msm_fixed_dev(bases + h * 64, n - h, sc + h * 32, n - h, True))
+    finally:
+        nzcb.dev_free(sc)
+        nzcb.dev_free(bases)
+        eng.close()
+    assert generic is not None and generic == fixed
+    assert bn.g1_add(lo, hi) == fixed
