@@ -241,7 +241,7 @@ def main():
                 "msm_devices": msm_devices or None,
             },
             "roofline": {
-                "kernel": "msm_accumulate_kernel (Pippenger bucket accumulation)",
+                "kernel": "msm_accumulate29_kernel (fixed-base Pippenger bucket accumulation)",
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
