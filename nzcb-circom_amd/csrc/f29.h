@@ -50,6 +50,9 @@ struct Fr29 {
   static constexpr uint32_t INV = 0x0fffffffu;
   static constexpr uint32_t P[9] = {0x10000001u, 0x1f0fac9fu, 0x0e5c2450u, 0x07d090f3u, 0x1585d283u,
                                     0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
+  // 2r in borrowed form (every limb >= 2^29 - 1), for sub29
+  static constexpr uint32_t K2[9] = {0x20000002u, 0x3e1f593eu, 0x3cb848a0u, 0x2fa121e5u, 0x2b0ba505u,
+                                     0x25b68180u, 0x214dc281u, 0x3cb84c67u, 0x0060c89bu};
 };
 
 NZ_HD F29 f29_const(const uint32_t (&c)[9]) {
@@ -162,6 +165,41 @@ NZ_HD F29 mul2sum29(const F29& a, const F29& b, const F29& c, const F29& d) {
   return r;
 }
 
+// sum_k a[k] b[k] * 2^-261 mod q with one Montgomery reduction (K <= 6 keeps a column
+// of 9K + 9 terms < 2^58 below 2^64). Needs normalized limbs (< 2^29); for inputs
+// below 4q the result is below (0.1 K + 1) q < 2q for K <= 6 (q ~ 2^253.6).
+template <class Q, int K>
+NZ_HD F29 mulsum29(const F29 (&a)[K], const F29 (&b)[K]) {
+  uint32_t m[9];
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+#pragma unroll
+    for (int k = 0; k < K; k++)
+#pragma unroll
+      for (int j = 0; j <= i; j++) acc += (uint64_t)a[k].v[j] * b[k].v[i - j];
+#pragma unroll
+    for (int j = 0; j < i; j++) acc += (uint64_t)m[j] * Q::P[i - j];
+    m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
+    acc += (uint64_t)m[i] * Q::P[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int i = 9; i < 17; i++) {
+#pragma unroll
+    for (int j = i - 8; j < 9; j++) {
+#pragma unroll
+      for (int k = 0; k < K; k++) acc += (uint64_t)a[k].v[j] * b[k].v[i - j];
+      acc += (uint64_t)m[j] * Q::P[i - j];
+    }
+    r.v[i - 9] = (uint32_t)acc & Q::MASK;
+    acc >>= 29;
+  }
+  r.v[8] = (uint32_t)acc;
+  return r;
+}
+
 NZ_HD void norm29(F29& r) {
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -256,8 +294,8 @@ NZ_HD Fq join29(const F29& x) {  // x normalized, < 2^256
 // a * w for a canonical Montgomery-256 Fr and a twiddle w given as split29 of its
 // Montgomery-261 form (w * 2^261 mod r): one 9x29 product instead of the 8x32 mac
 // chain of field.h, canonical Montgomery-256 result
-NZ_HD Fr mul_fr29(const Fr& a, const F29& w29) {
-  const F29 t = mul29<Fr29>(split29(a), w29);  // < 2r, limbs < 2^29
+// normalized F29 below 2r -> canonical Fr (same integer mod r, no Montgomery change)
+NZ_HD Fr join_fr29(const F29& t) {
   Fr r;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.v[i] = 0;
@@ -269,6 +307,9 @@ NZ_HD Fr mul_fr29(const Fr& a, const F29& w29) {
     if (limb + 1 < 8) r.v[limb + 1] |= (uint32_t)(w >> 32);
   }
   return reduce_once(r);
+}
+NZ_HD Fr mul_fr29(const Fr& a, const F29& w29) {
+  return join_fr29(mul29<Fr29>(split29(a), w29));  // product < 2r, limbs < 2^29
 }
 
 // Montgomery-261 value (any F29 < 2^257) -> canonical Montgomery-256 Fq (csrc/field.h)

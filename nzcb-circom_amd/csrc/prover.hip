@@ -243,6 +243,91 @@ k_quotient_coset(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* _
   T[i] = (gate + q.alpha * (num - den) + e4) * q.zhinv[i & 3];
 }
 
+// The same quotient in the 9x29-bit radix (f29.h, Fr29). Every summand is kept at the
+// Montgomery exponent 2^256: a mul29 of exponents e1, e2 gives e1 + e2 - 261, so the
+// per-context coset arrays are stored pre-scaled (qm * 2^10, ql / qr / qo / L_j * 2^5,
+// x_lo * 2^5; kQ29Scale) and the scalars come in the exponent their product needs
+// (QArgs29). Bounds: loaded values < r, products < 2r, mulsum29 of <= 4 terms < 2r,
+// the final sum S < 9r < 2^257 (mul29's input limit), so T is canonical after one
+// conditional subtraction. Used for nPublic <= 8 (two PI chunks at most).
+constexpr uint32_t kQ29MaxPub = 8;
+struct QArgs29 {
+  F29 beta, bk1, bk2, alpha2, zhinv[4];  // exponent 261
+  F29 gamma, negone;                     // exponent 256 (negone = r - 1)
+  F29 alpha;                             // exponent 276 (multiplies the exponent-241 permutation term)
+};
+
+template <int K>
+__device__ __forceinline__ F29 q29_pi_chunk(const Fr* __restrict__ cl, const Fr* __restrict__ Apub, uint32_t j0,
+                                            size_t n4, size_t i) {
+  F29 pa[K], pb[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    pa[k] = split29(cl[(size_t)(j0 + k) * n4 + i]);  // L_j * 2^5
+    pb[k] = split29(neg(Apub[j0 + k]));             // -Apub_j
+  }
+  return mulsum29<Fr29, K>(pa, pb);
+}
+
+__device__ __forceinline__ F29 q29_pi(const Fr* __restrict__ cl, const Fr* __restrict__ Apub, uint32_t j0,
+                                      uint32_t cnt, size_t n4, size_t i) {
+  switch (cnt) {
+    case 1: return q29_pi_chunk<1>(cl, Apub, j0, n4, i);
+    case 2: return q29_pi_chunk<2>(cl, Apub, j0, n4, i);
+    case 3: return q29_pi_chunk<3>(cl, Apub, j0, n4, i);
+    default: return q29_pi_chunk<4>(cl, Apub, j0, n4, i);
+  }
+}
+
+__global__ void __launch_bounds__(kT)
+k_quotient_coset29(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
+                   const Fr* __restrict__ Z, const Fr* __restrict__ cq, const Fr* __restrict__ cs,
+                   const Fr* __restrict__ cl, uint32_t npub, const Fr* __restrict__ Apub, size_t n,
+                   const Fr* __restrict__ xlo, const Fr* __restrict__ xhi, QArgs29 q, Fr* __restrict__ T) {
+  const size_t n4 = 4 * n;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const F29 a = split29(A[i]), b = split29(B[i]), c = split29(C[i]), z = split29(Z[i]);
+  // gate: qm a b + ql a + qr b + qo c + qc - sum_j L_j Apub_j
+  F29 gate;
+  {
+    const F29 ga[4] = {mul29<Fr29>(a, b), a, b, c};
+    const F29 gb[4] = {split29(cq[i]), split29(cq[n4 + i]), split29(cq[2 * n4 + i]), split29(cq[3 * n4 + i])};
+    gate = add29(mulsum29<Fr29, 4>(ga, gb), split29(cq[4 * n4 + i]));  // < 3r
+  }
+  if (npub > 0) gate = add29(gate, q29_pi(cl, Apub, 0, npub < 4 ? npub : 4, n4, i));
+  if (npub > 4) gate = add29(gate, q29_pi(cl, Apub, 4, npub - 4, n4, i));  // < 7r
+  // permutation: (a + b x + g)(b + b k1 x + g)(c + b k2 x + g) z - (a + b s1 + g)(..)(..) z(w x)
+  const F29 x = mul29<Fr29>(split29(xlo[i & 4095]), split29(xhi[i >> 12]));
+  const F29 f1 = add29(add29(a, mul29<Fr29>(q.beta, x)), q.gamma);  // < 4r
+  const F29 f2 = add29(add29(b, mul29<Fr29>(q.bk1, x)), q.gamma);
+  const F29 f3 = add29(add29(c, mul29<Fr29>(q.bk2, x)), q.gamma);
+  const F29 num = mul29<Fr29>(mul29<Fr29>(mul29<Fr29>(f1, f2), f3), z);  // exponent 241
+  const F29 g1 = add29(add29(a, mul29<Fr29>(q.beta, split29(cs[i]))), q.gamma);
+  const F29 g2 = add29(add29(b, mul29<Fr29>(q.beta, split29(cs[n4 + i]))), q.gamma);
+  const F29 g3 = add29(add29(c, mul29<Fr29>(q.beta, split29(cs[2 * n4 + i]))), q.gamma);
+  const F29 den = mul29<Fr29>(mul29<Fr29>(mul29<Fr29>(g1, g2), g3), split29(Z[(i + 4) & (n4 - 1)]));
+  // alpha (num - den) + alpha^2 (z - 1) L1, one reduction
+  const F29 pa[2] = {q.alpha, q.alpha2};
+  const F29 pb[2] = {sub29(num, den, Fr29::K2), mul29<Fr29>(add29(z, q.negone), split29(cl[i]))};
+  const F29 S = add29(gate, mulsum29<Fr29, 2>(pa, pb));  // < 9r
+  T[i] = join_fr29(mul29<Fr29>(S, q.zhinv[i & 3]));
+}
+
+// x <- x * 2^e (mod r), canonical in and out: the exponent pre-scaling of kQ29
+__global__ void k_dbl_pow(Fr* __restrict__ x, size_t m, int e) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  Fr v = x[i];
+  for (int k = 0; k < e; k++) v = v + v;
+  x[i] = v;
+}
+
+static F29 f29_exp(Fr v, int extra) {  // split29 of v * 2^extra (host)
+  for (int k = 0; k < extra; k++) v = v + v;
+  return split29(v);
+}
+
 // chunked Horner: partial[block] = sum over the block's chunks of p(chunk) * x^(chunk start)
 __global__ void __launch_bounds__(kT)
 k_eval(const Fr* __restrict__ p, size_t len, Fr x, Fr xK, Fr* __restrict__ partial) {
@@ -532,6 +617,16 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     for (int k = 0; k < 3; k++) coset_eval(sigma.p + (size_t)k * 5 * n, cs.p + (size_t)k * n4);
     for (uint32_t j = 0; j < nl; j++) coset_eval(lagrange.p + (size_t)j * 5 * n, cl.p + (size_t)j * n4);
     NZ_HIP(hipGetLastError());
+    if (nPublic <= kQ29MaxPub) {  // exponent pre-scaling of the 29-bit quotient (k_quotient_coset29)
+      auto scale = [&](Fr* p, size_t m, int e) {
+        hipLaunchKernelGGL(k_dbl_pow, dim3(grid_for(m, kT, 1u << 30)), dim3(kT), 0, s, p, m, e);
+      };
+      scale(cq.p, n4, 10);                      // qm
+      scale(cq.p + n4, 3 * n4, 5);              // ql, qr, qo
+      scale(cl.p, (size_t)nl * n4, 5);          // L_j
+      scale(x_lo.p, nlo, 5);                    // g w4^j
+      NZ_HIP(hipGetLastError());
+    }
   }
   NZ_HIP(hipStreamSynchronize(s));
 }
@@ -831,8 +926,22 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     q.bk2 = beta * k2;
     for (int k = 0; k < 4; k++) q.zhinv[k] = zh_inv[k];
     auto tq = std::chrono::steady_clock::now();
-    hipLaunchKernelGGL(k_quotient_coset, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, A4.p, B4.p, C4.p, Z4.p,
-                       cq.p, cs.p, cl.p, nPublic, A.p, (size_t)n, x_lo.p, root_hi.p, q, T.p);
+    if (nPublic <= kQ29MaxPub) {
+      QArgs29 q29;
+      q29.beta = f29_exp(beta, 5);
+      q29.bk1 = f29_exp(q.bk1, 5);
+      q29.bk2 = f29_exp(q.bk2, 5);
+      q29.alpha2 = f29_exp(q.alpha2, 5);
+      for (int k = 0; k < 4; k++) q29.zhinv[k] = f29_exp(zh_inv[k], 5);
+      q29.gamma = f29_exp(gamma, 0);
+      q29.negone = f29_exp(neg(Fr::one()), 0);
+      q29.alpha = f29_exp(alpha, 20);
+      hipLaunchKernelGGL(k_quotient_coset29, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, A4.p, B4.p, C4.p,
+                         Z4.p, cq.p, cs.p, cl.p, nPublic, A.p, (size_t)n, x_lo.p, root_hi.p, q29, T.p);
+    } else {
+      hipLaunchKernelGGL(k_quotient_coset, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, A4.p, B4.p, C4.p,
+                         Z4.p, cq.p, cs.p, cl.p, nPublic, A.p, (size_t)n, x_lo.p, root_hi.p, q, T.p);
+    }
     NZ_HIP(hipGetLastError());
     NttIo io;  // coset unscale g^-j and the degree check fused into the iNTT's last pass
     io.out_lo = gi_lo.p;

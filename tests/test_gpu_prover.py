@@ -54,7 +54,8 @@ def test_repeat_proofs_same_context():
         assert proof.hex() == exp["proof_bin"]
 
 
-@pytest.mark.parametrize("power,seed,npub,nin", [(4, 11, 1, 2), (6, 12, 3, 5), (10, 13, 3, 8), (11, 14, 5, 16)])
+@pytest.mark.parametrize("power,seed,npub,nin", [(4, 11, 1, 2), (6, 12, 3, 5), (10, 13, 3, 8), (11, 14, 5, 16),
+                                                 (7, 16, 8, 10), (7, 17, 10, 12)])
 def test_live_oracle(power, seed, npub, nin):
     c = synth.synth_circuit(power, npub, nin, seed=seed)
     tau = 1000003 + seed
