@@ -55,6 +55,22 @@ struct Fr29 {
                                      0x25b68180u, 0x214dc281u, 0x3cb84c67u, 0x0060c89bu};
 };
 
+// acc + x * y as one v_mad_u64_u32 with acc as its addend. Written as asm so the
+// compiler keeps each column one accumulation chain: left to itself it restarts every
+// column at 0 and adds the previous column's carry with an extra 64-bit add (about
+// 150 v_lshl_add_u64 per XYZZ addition). mad29c takes y from an SGPR (modulus limbs).
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void mad29(uint64_t& acc, uint32_t x, uint32_t y) {
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(x), "v"(y) : "vcc");
+}
+__device__ __forceinline__ void mad29c(uint64_t& acc, uint32_t x, uint32_t y) {
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(x), "s"(y) : "vcc");
+}
+#else
+NZ_HD void mad29(uint64_t& acc, uint32_t x, uint32_t y) { acc += (uint64_t)x * y; }
+NZ_HD void mad29c(uint64_t& acc, uint32_t x, uint32_t y) { acc += (uint64_t)x * y; }
+#endif
+
 NZ_HD F29 f29_const(const uint32_t (&c)[9]) {
   F29 r;
 #pragma unroll
@@ -72,20 +88,20 @@ NZ_HD F29 mul29(const F29& a, const F29& b) {
   for (int i = 0; i < 9; i++) {
 #pragma unroll
     for (int j = 0; j < i; j++) {
-      acc += (uint64_t)a.v[j] * b.v[i - j];
-      acc += (uint64_t)m[j] * Q::P[i - j];
+      mad29(acc, a.v[j], b.v[i - j]);
+      mad29c(acc, m[j], Q::P[i - j]);
     }
-    acc += (uint64_t)a.v[i] * b.v[0];
+    mad29(acc, a.v[i], b.v[0]);
     m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
-    acc += (uint64_t)m[i] * Q::P[0];
+    mad29c(acc, m[i], Q::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int i = 9; i < 17; i++) {
 #pragma unroll
     for (int j = i - 8; j < 9; j++) {
-      acc += (uint64_t)a.v[j] * b.v[i - j];
-      acc += (uint64_t)m[j] * Q::P[i - j];
+      mad29(acc, a.v[j], b.v[i - j]);
+      mad29c(acc, m[j], Q::P[i - j]);
     }
     r.v[i - 9] = (uint32_t)acc & Q::MASK;
     acc >>= 29;
@@ -107,21 +123,21 @@ NZ_HD F29 sqr29(const F29& a) {
 #pragma unroll
   for (int i = 0; i < 9; i++) {
 #pragma unroll
-    for (int j = 0; 2 * j < i; j++) acc += (uint64_t)a.v[j] * a2[i - j];
-    if (!(i & 1)) acc += (uint64_t)a.v[i >> 1] * a.v[i >> 1];
+    for (int j = 0; 2 * j < i; j++) mad29(acc, a.v[j], a2[i - j]);
+    if (!(i & 1)) mad29(acc, a.v[i >> 1], a.v[i >> 1]);
 #pragma unroll
-    for (int j = 0; j < i; j++) acc += (uint64_t)m[j] * Q::P[i - j];
+    for (int j = 0; j < i; j++) mad29c(acc, m[j], Q::P[i - j]);
     m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
-    acc += (uint64_t)m[i] * Q::P[0];
+    mad29c(acc, m[i], Q::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int i = 9; i < 17; i++) {
 #pragma unroll
-    for (int j = i - 8; 2 * j < i; j++) acc += (uint64_t)a.v[j] * a2[i - j];
-    if (!(i & 1)) acc += (uint64_t)a.v[i >> 1] * a.v[i >> 1];
+    for (int j = i - 8; 2 * j < i; j++) mad29(acc, a.v[j], a2[i - j]);
+    if (!(i & 1)) mad29(acc, a.v[i >> 1], a.v[i >> 1]);
 #pragma unroll
-    for (int j = i - 8; j < 9; j++) acc += (uint64_t)m[j] * Q::P[i - j];
+    for (int j = i - 8; j < 9; j++) mad29c(acc, m[j], Q::P[i - j]);
     r.v[i - 9] = (uint32_t)acc & Q::MASK;
     acc >>= 29;
   }
@@ -141,22 +157,22 @@ NZ_HD F29 mul2sum29(const F29& a, const F29& b, const F29& c, const F29& d) {
   for (int i = 0; i < 9; i++) {
 #pragma unroll
     for (int j = 0; j <= i; j++) {
-      acc += (uint64_t)a.v[j] * b.v[i - j];
-      acc += (uint64_t)c.v[j] * d.v[i - j];
+      mad29(acc, a.v[j], b.v[i - j]);
+      mad29(acc, c.v[j], d.v[i - j]);
     }
 #pragma unroll
-    for (int j = 0; j < i; j++) acc += (uint64_t)m[j] * Q::P[i - j];
+    for (int j = 0; j < i; j++) mad29c(acc, m[j], Q::P[i - j]);
     m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
-    acc += (uint64_t)m[i] * Q::P[0];
+    mad29c(acc, m[i], Q::P[0]);
     acc >>= 29;
   }
 #pragma unroll
   for (int i = 9; i < 17; i++) {
 #pragma unroll
     for (int j = i - 8; j < 9; j++) {
-      acc += (uint64_t)a.v[j] * b.v[i - j];
-      acc += (uint64_t)c.v[j] * d.v[i - j];
-      acc += (uint64_t)m[j] * Q::P[i - j];
+      mad29(acc, a.v[j], b.v[i - j]);
+      mad29(acc, c.v[j], d.v[i - j]);
+      mad29c(acc, m[j], Q::P[i - j]);
     }
     r.v[i - 9] = (uint32_t)acc & Q::MASK;
     acc >>= 29;
@@ -178,11 +194,11 @@ NZ_HD F29 mulsum29(const F29 (&a)[K], const F29 (&b)[K]) {
 #pragma unroll
     for (int k = 0; k < K; k++)
 #pragma unroll
-      for (int j = 0; j <= i; j++) acc += (uint64_t)a[k].v[j] * b[k].v[i - j];
+      for (int j = 0; j <= i; j++) mad29(acc, a[k].v[j], b[k].v[i - j]);
 #pragma unroll
-    for (int j = 0; j < i; j++) acc += (uint64_t)m[j] * Q::P[i - j];
+    for (int j = 0; j < i; j++) mad29c(acc, m[j], Q::P[i - j]);
     m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
-    acc += (uint64_t)m[i] * Q::P[0];
+    mad29c(acc, m[i], Q::P[0]);
     acc >>= 29;
   }
 #pragma unroll
@@ -190,8 +206,8 @@ NZ_HD F29 mulsum29(const F29 (&a)[K], const F29 (&b)[K]) {
 #pragma unroll
     for (int j = i - 8; j < 9; j++) {
 #pragma unroll
-      for (int k = 0; k < K; k++) acc += (uint64_t)a[k].v[j] * b[k].v[i - j];
-      acc += (uint64_t)m[j] * Q::P[i - j];
+      for (int k = 0; k < K; k++) mad29(acc, a[k].v[j], b[k].v[i - j]);
+      mad29c(acc, m[j], Q::P[i - j]);
     }
     r.v[i - 9] = (uint32_t)acc & Q::MASK;
     acc >>= 29;
