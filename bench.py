@@ -168,8 +168,9 @@ def main():
         prover.full_prove_staged(nw, [blinding_for(1000 + i) for i in range(nw)])
     ctx.kernel_stats(1)
     blinds = [blinding_for(i) for i in mine]
-    prover.upload_inputs(pass_inputs(mine))      # the passes' input signals, resident in HBM
-    prover.witness_buffers(len(mine))
+    if mine:  # a rank can hold no proofs when --batch is smaller than the world
+        prover.upload_inputs(pass_inputs(mine))  # the passes' input signals, resident in HBM
+        prover.witness_buffers(len(mine))
     barrier()
     t0 = time.perf_counter()
     proofs, records = prover.full_prove_staged(len(mine), blinds)
@@ -182,7 +183,8 @@ def main():
     # of the timed batch (host, outside the timed region)
     pubs_ok = all([int.from_bytes(pub[32 * k:32 * k + 32], "little") for k in range(3)] == r["out"]
                   for (_, pub), r in zip(proofs, records))
-    verified = pubs_ok and all(nzcb.verify(ctx.vk, proofs[i][0], proofs[i][1]) for i in {0, len(proofs) - 1})
+    verified = pubs_ok and all(nzcb.verify(ctx.vk, proofs[i][0], proofs[i][1])
+                               for i in ({0, len(proofs) - 1} if proofs else ()))
     t_w = time.perf_counter()
     prover.witness_staged(len(mine))
     nzcp_ms = (time.perf_counter() - t_w) * 1e3

@@ -558,6 +558,8 @@ class NzcpProver:
     def witness_staged(self, count: int) -> list:
         """nzcp witness of the staged passes: public signals into witness[1..3] of each
         proof's HBM witness; returns the records. Raises on a failed pass."""
+        if count == 0:
+            return []
         bufs = self.witness_buffers(count)
         rec_size = ctypes.sizeof(NzcpRecord)
         nzcp_witness_dev(self._inputs, count, self.params, self.device, self._rec, bufs[0], self.n_witness * 32)
