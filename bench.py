@@ -47,10 +47,11 @@ PROOF_BYTES_PER_N = 7104       # algorithmic bytes per proof = 7
 NZCP_INPUTS = 2970             # nzcp_live input signals (toBeSigned bits + len + data)
 SEED = 0x6E7A6362
 TAU = 0x6E7A6362746175
-# Product-scanning Montgomery product: 128 (v_mad_u64_u32 + v_addc_co_u32) pairs per
-# 8x32-bit product, 4 SIMD-cycles per wave64 instruction (profiles/r1_isa_bench.txt),
-# 1024 SIMDs at ~2.0 GHz under load: 1024 * 2.0e9 * 64 / (256 * 4) = 128 G products/s.
-VALU_MULT_BOUND_GS = 128.0
+# The accumulation's Fq products are 9x29-bit Montgomery products: an XYZZ mixed
+# addition (10 products) issues 1467 v_mad_u64_u32 (ISA count of the common path,
+# 146.7 per product) at 4.9 SIMD-cycles each (profiles/r1_isa_bench.txt); 1024 SIMDs
+# at ~2.0 GHz under load: 1024 * 2.0e9 * 64 / (146.7 * 4.9) = 182 G products/s.
+VALU_MULT_BOUND_GS = 182.0
 
 
 def blinding_for(step: int) -> bytes:
@@ -101,7 +102,7 @@ def main():
     ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--power", type=int, default=21, help="log2 PLONK domain (nzcp_live: 21)")
-    ap.add_argument("--lanes", type=int, default=4, help="proofs in flight per GPU")
+    ap.add_argument("--lanes", type=int, default=5, help="proofs in flight per GPU")
     ap.add_argument("--batch", type=int, default=0,
                     help="fixed total batch sharded over the ranks (configs[3]: 512); default: --steps per rank")
     ap.add_argument("--msm-devices", default="",
@@ -256,7 +257,7 @@ def main():
                 "bytes_per_point": MSM_BYTES_PER_POINT,
                 "bucket_entries_per_launch": int(ent_per_launch),
                 "valu": {"fq_mont_mul_per_s": round(mults_per_s / 1e9, 2), "unit": "G/s",
-                         "bound_mad_addc": VALU_MULT_BOUND_GS,
+                         "bound_mad_f29": VALU_MULT_BOUND_GS,
                          "frac": round(mults_per_s / 1e9 / VALU_MULT_BOUND_GS, 4)},
             },
             "proof_roofline": {
