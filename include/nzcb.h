@@ -259,6 +259,11 @@ int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars,
  * One-shot (table and scratch freed on return); for parity tests. */
 int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
                               int scalars_mont, uint8_t* out_affine, nzcb_err* err);
+/* Batch-affine pairing rounds ahead of the fixed-base bucket accumulation (each halves
+ * every bucket's run): rounds >= 0 forces that many (at most 6; 0 = XYZZ accumulation
+ * only), rounds < 0 restores the automatic choice (NZCB_PAIR_ROUNDS, default 0, while
+ * the average run is >= 8 entries). Process-wide; for tests and tuning. */
+int nzcb_msm_set_pair_rounds(int rounds);
 /* Per-phase MSM timing (HIP events, average over reps after one warm-up):
  * out[0] wall ms, out[1..7] keys, sort, offsets, accumulate, finalize, reduce, sums,
  * out[8] table build ms (fixed_base only). */

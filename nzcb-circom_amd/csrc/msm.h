@@ -35,6 +35,11 @@ struct MsmScratch {
   // fixed-base schedule: the accumulation stores its results unconverted (radix 2^29,
   // Montgomery-261); the finalize kernel converts them into buckets
   DevBuf<Xyzz29> buckets29, carry_own29, carry_cont29;
+  // fixed-base pairing rounds (msm.hip msm_pair29_kernel): ping-pong affine sums and
+  // bucket offsets, and the exclusive prefix products of the slope denominators
+  DevBuf<G1Affine> pair_pts[2];
+  DevBuf<uint32_t> pair_off[2];
+  DevBuf<uint32_t> pair_pre;
   DevBuf<uint32_t> large;     // [count, bucket ids...] of buckets with long carry runs
   DevBuf<G1xyzz> seg_tot;     // per (bucket set, segment): sum_j (j+1) * bucket_j
   DevBuf<G1xyzz> seg_run;     // per (bucket set, segment): sum_j bucket_j
@@ -56,6 +61,10 @@ struct MsmScratch {
   void init(size_t max_points, bool fixed_base = false);
   ~MsmScratch();
 };
+
+// Batch-affine pairing rounds before the fixed-base accumulation: r >= 0 forces r rounds
+// (at most 6), r < 0 restores the automatic choice. Process-wide.
+void msm_set_pair_rounds(int r);
 
 // Window size of the generic (variable-base) MSM of n points.
 int msm_window_bits(size_t n);

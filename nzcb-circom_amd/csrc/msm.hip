@@ -40,6 +40,7 @@
 
 #include "f29.h"
 
+#include <atomic>
 #include <cstdlib>
 #include <rocprim/rocprim.hpp>
 
@@ -97,6 +98,9 @@ static uint32_t chunk_for(size_t entries) {
   while (entries / c > (size_t(1) << 20)) c *= 2;
   return c;
 }
+static constexpr int kPairThreads = 256;  // pairing rounds: workgroup (one inversion each)
+static constexpr int kPairPer = 64;       // pairing rounds: pair slots per thread
+static constexpr int kMaxPairRounds = 6;
 static constexpr int kSegLen = 8;
 static constexpr int kSumThreads = 256;  // level-1 sums: block size
 static constexpr int kSumPer = 4;        // level-1 sums: sequential adds per thread
@@ -111,6 +115,33 @@ int fixed_base_window() {
     return (v >= 16 && v <= 20) ? v : 17;
   }();
   return c;
+}
+
+// Pairing rounds (msm_pair29_kernel) before the fixed-base accumulation: -1 = automatic
+// (NZCB_PAIR_ROUNDS rounds while the average bucket run is >= 8 entries; default 0, see
+// at 2^21 one round costs 2.9 ms against 2.35 ms for the whole XYZZ
+// accumulation), >= 0 = exactly that many (nzcb_msm_set_pair_rounds, tests).
+static std::atomic<int> g_pair_rounds{-1};
+void msm_set_pair_rounds(int r) { g_pair_rounds.store(r < 0 ? -1 : (r > kMaxPairRounds ? kMaxPairRounds : r)); }
+
+static int pair_rounds_for(size_t entries, uint32_t nkeys) {
+  const int forced = g_pair_rounds.load();
+  if (forced >= 0) return forced;
+  static const int dflt = [] {
+    const char* e = std::getenv("NZCB_PAIR_ROUNDS");
+    const int v = e ? std::atoi(e) : 0;
+    return v < 0 ? 0 : (v > kMaxPairRounds ? kMaxPairRounds : v);
+  }();
+  int r = 0;
+  while (r < dflt && (entries >> r) >= (size_t)8 * nkeys) r++;
+  return r;
+}
+
+// upper bound of the entries left after a pairing round: sum_k ceil(L_k / 2)
+static size_t pair_bound(size_t entries, uint32_t nkeys) { return std::min(entries, (entries + nkeys) / 2); }
+static size_t pair_grid(size_t slots) {
+  const size_t per = (size_t)kPairThreads * kPairPer;
+  return std::max<size_t>(1, (slots + per - 1) / per);
 }
 
 int msm_window_bits(size_t n) {
@@ -272,7 +303,9 @@ __device__ __forceinline__ G1xyzz load_point(const Xyzz29& a) {
   return r;
 }
 
-template <int WAVES>
+// kDirect: entries are the pairing rounds' affine sums (msm_pair29_kernel), read in
+// place (position = entry), instead of signed table indices in `sorted`.
+template <int WAVES, bool kDirect = false>
 __global__ void __launch_bounds__(kMsmThreads) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
                         const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
@@ -289,8 +322,8 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
   Xyzz29 acc;
   bool inf = true;
   for (uint32_t pos = s; pos < e;) {
-    const uint32_t ent = sorted[pos];
-    const G1Affine P = bases[ent & 0x7fffffffu];
+    const uint32_t ent = kDirect ? 0u : sorted[pos];
+    const G1Affine P = bases[kDirect ? pos : ent & 0x7fffffffu];
     if (!P.is_inf()) {
       const F29 x = split29(P.x);
       F29 y = split29(P.y);
@@ -342,6 +375,206 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
         kend = offsets[k + 1];
       }
     }
+  }
+}
+
+// ---- Batch-affine pairing rounds (fixed-base schedule) ---------------------------
+// Before the XYZZ accumulation, R rounds halve every bucket's run in place of the
+// sequential mixed additions: entries 2j and 2j+1 of a bucket's run become one affine
+// point. An affine addition needs 1/(x2 - x1); the workgroup shares ONE Fermat
+// inversion among all its pairs (Montgomery's trick: a prefix product per thread, a
+// product tree over the workgroup's threads in LDS, then the prefixes unwound), so a
+// pair costs 5 products + 1 square (3 for the trick, lambda, lambda^2, y3) against the
+// 8 products + 2 squares of the XYZZ mixed addition (madd-2008-s), plus the tree and
+// inversion shared by kPairThreads * kPairPer pairs. The exclusive prefixes go to a
+// scratch array laid out [slot][limb][thread] (coalesced). Round 1 gathers the signed
+// table entries through `sorted`; later rounds read the previous round's output.
+// Pair slot p of bucket k (noff[k] <= p < noff[k+1], noff = exclusive scan of
+// ceil(run/2), msm_pair_offsets_kernel) adds source positions off[k] + 2(p - noff[k])
+// and the one after it, or copies the last entry of an odd run. Coordinates stay
+// canonical Montgomery-261 (so the table's x == x' test finds doublings and P + (-P));
+// infinity is (0, 0) as in the table.
+
+enum : uint32_t { kPairAdd = 0, kPairDbl = 1, kPairCopyA = 2, kPairCopyB = 3, kPairInf = 4 };
+
+template <bool kGather>
+__device__ __forceinline__ G1Affine pair_point(const G1Affine* __restrict__ src, const uint32_t* __restrict__ sorted,
+                                               uint32_t pos) {
+  if (!kGather) return src[pos];
+  const uint32_t ent = sorted[pos];
+  G1Affine P = src[ent & 0x7fffffffu];
+  if ((ent >> 31) && !P.is_inf()) P.y = neg(P.y);
+  return P;
+}
+
+__device__ __forceinline__ uint32_t pair_kind(const G1Affine& a, const G1Affine& b) {
+  if (a.is_inf()) return kPairCopyB;
+  if (b.is_inf()) return kPairCopyA;
+  if (a.x == b.x) return a.y == b.y ? kPairDbl : kPairInf;
+  return kPairAdd;
+}
+
+// denominator of the slope: x2 - x1, or 2 y1 for a doubling (y1 != 0 on BN254 G1)
+__device__ __forceinline__ F29 pair_den(const G1Affine& a, const G1Affine& b, uint32_t kind) {
+  return split29(kind == kPairAdd ? b.x - a.x : a.y + a.y);
+}
+
+// numerator of a doubling's slope, 3 x^2 (rare: kept out of line)
+__device__ __noinline__ F29 pair_dbl_num(const Fq x) {
+  const Fq xx = reduce_once(join29(sqr29(split29(x))));
+  return split29(xx + xx + xx);
+}
+
+__device__ __forceinline__ uint32_t pm2_limb(int i) {  // limb i (radix 2^29) of p - 2
+  switch (i) {
+    case 0: return Fq29::P[0] - 2u;
+    case 1: return Fq29::P[1];
+    case 2: return Fq29::P[2];
+    case 3: return Fq29::P[3];
+    case 4: return Fq29::P[4];
+    case 5: return Fq29::P[5];
+    case 6: return Fq29::P[6];
+    case 7: return Fq29::P[7];
+    default: return Fq29::P[8];
+  }
+}
+
+// a^(p-2) = a^-1 (Montgomery-261 in and out; a != 0 mod p), left-to-right binary powering
+__device__ __noinline__ F29 inv29(const F29 a) {
+  F29 r = f29_const(Fq29::ONE);
+  for (int i = 8; i >= 0; i--) {
+    const uint32_t e = pm2_limb(i);
+    for (int b = (i == 8 ? 21 : 28); b >= 0; b--) {
+      r = sqr29(r);
+      if ((e >> b) & 1u) r = mul29(r, a);
+    }
+  }
+  return r;
+}
+
+// noff[k] = sum_{j<k} ceil((off[j+1] - off[j]) / 2), noff[nkeys] = total (one workgroup)
+__global__ void __launch_bounds__(1024)
+msm_pair_offsets_kernel(const uint32_t* __restrict__ off, uint32_t nkeys, uint32_t* __restrict__ noff) {
+  __shared__ uint32_t sh[1024];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (nkeys + 1023u) / 1024u;
+  const uint32_t k0 = tid * per < nkeys ? tid * per : nkeys;
+  const uint32_t k1 = k0 + per < nkeys ? k0 + per : nkeys;
+  uint32_t sum = 0;
+  for (uint32_t k = k0; k < k1; k++) sum += (off[k + 1] - off[k] + 1u) >> 1;
+  sh[tid] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint32_t v = tid >= d ? sh[tid - d] : 0u;
+    __syncthreads();
+    sh[tid] += v;
+    __syncthreads();
+  }
+  uint32_t base = sh[tid] - sum;
+  for (uint32_t k = k0; k < k1; k++) {
+    noff[k] = base;
+    base += (off[k + 1] - off[k] + 1u) >> 1;
+  }
+  if (tid == 1023) noff[nkeys] = sh[1023];
+}
+
+template <bool kGather>
+__global__ void __launch_bounds__(kPairThreads)
+msm_pair29_kernel(const G1Affine* __restrict__ src, const uint32_t* __restrict__ sorted,
+                  const uint32_t* __restrict__ off, const uint32_t* __restrict__ noff, uint32_t nkeys,
+                  uint32_t* __restrict__ pre, G1Affine* __restrict__ dst) {
+  __shared__ F29 tree[2 * kPairThreads];
+  const uint32_t total = noff[nkeys];
+  if ((size_t)blockIdx.x * kPairThreads * kPairPer >= total) return;  // whole workgroup idle
+  const uint32_t tid = threadIdx.x;
+  const size_t nthr = (size_t)gridDim.x * kPairThreads;
+  const size_t t = (size_t)blockIdx.x * kPairThreads + tid;
+  const uint32_t p0 = (uint32_t)(t * kPairPer);
+  const uint32_t p1 = p0 >= total ? p0 : (p0 + kPairPer < total ? p0 + kPairPer : total);
+  uint32_t k = 0, ds = 0, de = 0, ss = 0, se = 0;  // bucket k: slots [ds, de), sources [ss, se)
+  if (p0 < p1) {
+    k = find_key(noff, nkeys, p0);
+    ds = noff[k];
+    de = noff[k + 1];
+    ss = off[k];
+    se = off[k + 1];
+  }
+  // forward: exclusive prefix products of the denominators
+  F29 c = f29_const(Fq29::ONE);
+  for (uint32_t p = p0; p < p1; p++) {
+    while (p >= de) {
+      k++;
+      ds = de;
+      de = noff[k + 1];
+      ss = se;
+      se = off[k + 1];
+    }
+    const uint32_t s = ss + 2u * (p - ds);
+    if (s + 1u < se) {
+      const G1Affine a = pair_point<kGather>(src, sorted, s), b = pair_point<kGather>(src, sorted, s + 1u);
+      const uint32_t kind = pair_kind(a, b);
+      if (kind <= kPairDbl) {
+        uint32_t* q = pre + (size_t)(p - p0) * 9u * nthr + t;
+#pragma unroll
+        for (int l = 0; l < 9; l++) q[(size_t)l * nthr] = c.v[l];
+        c = mul29(c, pair_den(a, b, kind));
+      }
+    }
+  }
+  // one inversion for the workgroup: product tree over the threads' totals
+  tree[kPairThreads + tid] = c;
+  __syncthreads();
+  for (uint32_t w = kPairThreads / 2; w >= 1; w >>= 1) {
+    if (tid < w) tree[w + tid] = mul29(tree[2 * (w + tid)], tree[2 * (w + tid) + 1]);
+    __syncthreads();
+  }
+  if (tid == 0) tree[1] = inv29(tree[1]);
+  __syncthreads();
+  for (uint32_t w = 1; w < kPairThreads; w <<= 1) {
+    if (tid < w) {
+      const uint32_t nd = w + tid;
+      const F29 iv = tree[nd], l = tree[2 * nd], r = tree[2 * nd + 1];
+      tree[2 * nd] = mul29(iv, r);
+      tree[2 * nd + 1] = mul29(iv, l);
+    }
+    __syncthreads();
+  }
+  F29 ic = tree[kPairThreads + tid];  // 1 / (product of this thread's denominators)
+  // backward: unwind the prefixes, add the pairs
+  for (uint32_t p = p1; p-- > p0;) {
+    while (p < ds) {
+      k--;
+      de = ds;
+      ds = noff[k];
+      se = ss;
+      ss = off[k];
+    }
+    const uint32_t s = ss + 2u * (p - ds);
+    const G1Affine a = pair_point<kGather>(src, sorted, s);
+    G1Affine out = a;
+    if (s + 1u < se) {
+      const G1Affine b = pair_point<kGather>(src, sorted, s + 1u);
+      const uint32_t kind = pair_kind(a, b);
+      if (kind <= kPairDbl) {
+        const uint32_t* q = pre + (size_t)(p - p0) * 9u * nthr + t;
+        F29 e;
+#pragma unroll
+        for (int l = 0; l < 9; l++) e.v[l] = q[(size_t)l * nthr];
+        const F29 id = mul29(ic, e);  // 1 / den
+        ic = mul29(ic, pair_den(a, b, kind));
+        const F29 num = kind == kPairAdd ? split29(b.y - a.y) : pair_dbl_num(a.x);
+        const F29 lam = mul29(num, id);
+        const Fq x2 = kind == kPairAdd ? b.x : a.x;
+        out.x = reduce_once(join29(sqr29(lam))) - a.x - x2;
+        out.y = reduce_once(join29(mul29(lam, split29(a.x - out.x)))) - a.y;
+      } else if (kind == kPairCopyB) {
+        out = b;
+      } else if (kind == kPairInf) {
+        out.x = Fq::zero();
+        out.y = Fq::zero();
+      }
+    }
+    dst[p] = out;
   }
 }
 
@@ -619,6 +852,15 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
   carry_own.alloc(nthreads);
   large.alloc(max_keys + 1);
   if (fixed_base) {
+    MsmBaseTable t;
+    t.c = fixed_base_window();
+    const MsmPlan fp = make_plan(maxp, &t);
+    const size_t b1 = pair_bound(fp.entries, fp.nkeys), b2 = pair_bound(b1, fp.nkeys);
+    pair_pts[0].alloc(b1 ? b1 : 1);
+    pair_pts[1].alloc(b2 ? b2 : 1);
+    pair_off[0].alloc((size_t)fp.nkeys + 1);
+    pair_off[1].alloc((size_t)fp.nkeys + 1);
+    pair_pre.alloc(pair_grid(b1) * kPairThreads * kPairPer * 9);
     buckets29.alloc(max_keys);
     carry_own29.alloc(nthreads);
     carry_cont29.alloc(nthreads);
@@ -723,9 +965,35 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                        p.nkeys, sc.offsets.p);
   }
   NZ_HIP(hipGetLastError());
-  const uint32_t chunk = chunk_for(p.entries);
-  const size_t nthreads = (p.entries + chunk - 1) / chunk;
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[3], st));
+  // pairing rounds (fixed base): each halves every bucket's run of entries
+  const int rounds = table ? pair_rounds_for(p.entries, p.nkeys) : 0;
+  const uint32_t* acc_off = sc.offsets.p;
+  const G1Affine* acc_src = gather;
+  size_t acc_entries = p.entries;
+  for (int r = 0; r < rounds; r++) {
+    uint32_t* noff = sc.pair_off[r & 1].p;
+    G1Affine* dst = sc.pair_pts[r & 1].p;
+    const size_t bound = pair_bound(acc_entries, p.nkeys);
+    if (!noff || bound > sc.pair_pts[r & 1].n || pair_grid(bound) * kPairThreads * kPairPer * 9 > sc.pair_pre.n ||
+        p.nkeys + 1 > sc.pair_off[r & 1].n)
+      throw Error(NZCB_ERR_ARG, "msm scratch was not sized for the pairing rounds");
+    hipLaunchKernelGGL(msm_pair_offsets_kernel, dim3(1), dim3(1024), 0, st, acc_off, p.nkeys, noff);
+    NZ_HIP(hipGetLastError());
+    const dim3 pgrid((uint32_t)pair_grid(bound));
+    if (r == 0)
+      hipLaunchKernelGGL(msm_pair29_kernel<true>, pgrid, dim3(kPairThreads), 0, st, acc_src, sc.sorted.p, acc_off,
+                         noff, p.nkeys, sc.pair_pre.p, dst);
+    else
+      hipLaunchKernelGGL(msm_pair29_kernel<false>, pgrid, dim3(kPairThreads), 0, st, acc_src, sc.sorted.p, acc_off,
+                         noff, p.nkeys, sc.pair_pre.p, dst);
+    NZ_HIP(hipGetLastError());
+    acc_off = noff;
+    acc_src = dst;
+    acc_entries = bound;
+  }
+  const uint32_t chunk = chunk_for(acc_entries);
+  const size_t nthreads = (acc_entries + chunk - 1) / chunk;
   static const int acc_waves = [] {
     const char* e = std::getenv("NZCB_ACC29_WAVES");
     return e ? std::atoi(e) : 4;
@@ -733,9 +1001,14 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   const dim3 agrid(grid_for(nthreads, kMsmThreads, 1u << 30));
   if (table) {
     if (!sc.buckets29.p) throw Error(NZCB_ERR_ARG, "msm scratch was not sized for the fixed-base schedule");
-    hipLaunchKernelGGL(acc_waves >= 4 ? msm_accumulate29_kernel<4> : msm_accumulate29_kernel<3>, agrid,
-                       dim3(kMsmThreads), 0, st, chunk, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads,
-                       sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
+    if (rounds)
+      hipLaunchKernelGGL((msm_accumulate29_kernel<4, true>), agrid, dim3(kMsmThreads), 0, st, chunk, acc_src,
+                         sc.sorted.p, acc_off, p.nkeys, nthreads, sc.buckets29.p, sc.carry_own29.p,
+                         sc.carry_cont29.p);
+    else
+      hipLaunchKernelGGL(acc_waves >= 4 ? msm_accumulate29_kernel<4> : msm_accumulate29_kernel<3>, agrid,
+                         dim3(kMsmThreads), 0, st, chunk, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads,
+                         sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
   } else {
     hipLaunchKernelGGL(msm_accumulate_kernel, agrid, dim3(kMsmThreads), 0, st, chunk, gather, sc.sorted.p, sc.offsets.p,
                        p.nkeys, nthreads, sc.buckets.p, sc.carry_own.p, sc.carry_cont.p);
@@ -745,12 +1018,12 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
   if (table) {
-    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
+    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, acc_off, p.nkeys,
                        (const Xyzz29*)sc.buckets29.p, (const Xyzz29*)sc.carry_own29.p,
                        (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p, sc.large.p);
     NZ_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_bucket_large_kernel<Xyzz29>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, chunk,
-                       sc.offsets.p,
+                       acc_off,
                        sc.large.p, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p);
   } else {
     hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,

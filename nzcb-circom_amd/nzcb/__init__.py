@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_to_json", "nzcb_verify",
     "nzcb_proof_to_calldata", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
-    "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d",
+    "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d", "nzcb_msm_set_pair_rounds",
 ]
 
 
@@ -143,6 +143,7 @@ def load(path: str | None = None):
                                          POINTER(c_double), POINTER(_Err)]),
         "nzcb_engine_msm_fixed_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_int, u8p,
                                               POINTER(_Err)]),
+        "nzcb_msm_set_pair_rounds": (c_int, [c_int]),
         "nzcb_nzcp_input_signals": (c_size_t, [POINTER(NzcpParams)]),
         "nzcb_nzcp_witness": (c_int, [c_int, POINTER(NzcpParams), u8p, c_int, POINTER(NzcpRecord), POINTER(_Err)]),
         "nzcb_nzcp_witness_dev": (c_int, [c_int, POINTER(NzcpParams), c_void_p, c_int, c_void_p, c_void_p, c_size_t,
@@ -339,6 +340,11 @@ def h2d(dst: int, data: bytes):
     rc = load().nzcb_memcpy_h2d(dst, buf, len(data))
     if rc:
         raise NzcbError(rc, "h2d failed")
+
+
+def msm_set_pair_rounds(rounds: int):
+    """Force `rounds` batch-affine pairing rounds in fixed-base MSMs (< 0: automatic)."""
+    load().nzcb_msm_set_pair_rounds(int(rounds))
 
 
 def d2d(dst: int, src: int, nbytes: int):

@@ -30,6 +30,11 @@ __global__ void probe(uint64_t* out, int iters) {
           : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
           : "v"(x), "v"(y)
           : "vcc");
+    } else if (K == 29) {  // 16 dependent v_mad_u64_u32 (one accumulation chain, as in mul29)
+      asm volatile(REP16("v_mad_u64_u32 %0, vcc, %1, %2, %0\n") : "+v"(a0) : "v"(x), "v"(y) : "vcc");
+    } else if (K == 30) {  // 2 interleaved chains
+      asm volatile(REP16("v_mad_u64_u32 %0, vcc, %2, %3, %0\n v_mad_u64_u32 %1, vcc, %2, %3, %1\n")
+                   : "+v"(a0), "+v"(a1) : "v"(x), "v"(y) : "vcc");
     } else if (K == 1) {  // 16 x v_add_co_u32
       asm volatile(REP16("v_add_co_u32 %0, vcc, %0, %1\n") : "+v"(x) : "v"(y) : "vcc");
     } else if (K == 2) {  // 16 x s_nop 1
@@ -87,7 +92,7 @@ __global__ void probe(uint64_t* out, int iters) {
                          "v_addc_co_u32_e64 %4, s[20:21], %4, 0, s[20:21]\n v_addc_co_u32_e64 %5, s[22:23], %5, 0, s[22:23]\n")
                    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(x), "v"(y)
                    : "s20", "s21", "s22", "s23");
-    } else if (K >= 15 && K <= 24) {
+    } else if (K >= 15 && K <= 28) {
 #define NZ_OP8(OP) asm volatile(REP16(OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7)) \
                    : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y), "v"(x))
 #define NZ_OP8W(OP) asm volatile(REP16(OP(0) OP(1) OP(2) OP(3) OP(4) OP(5) OP(6) OP(7)) \
@@ -102,6 +107,10 @@ __global__ void probe(uint64_t* out, int iters) {
 #define LSHLADD64(i) "v_lshl_add_u64 %" #i ", %" #i ", 0, %10\n"
 #define ADD64CO(i) "v_add_co_u32 %" #i ", vcc, %" #i ", %8\n"
 #define CND(i) "v_cndmask_b32 %" #i ", %" #i ", %8, vcc\n"
+#define CND64(i) "v_cndmask_b32_e64 %" #i ", %" #i ", %8, s[20:21]\n"
+#define BFI(i) "v_bfi_b32 %" #i ", %9, %" #i ", %8\n"
+#define SUBB(i) "v_subb_co_u32 %" #i ", vcc, %" #i ", %8, vcc\n"
+#define SUBCND(i) "v_subb_co_u32 %" #i ", vcc, %" #i ", %8, vcc\n v_cndmask_b32 %" #i ", %" #i ", %8, vcc\n"
       if (K == 15) NZ_OP8(AND);
       else if (K == 16) NZ_OP8(ALIGN);
       else if (K == 17) NZ_OP8(SHR);
@@ -111,7 +120,18 @@ __global__ void probe(uint64_t* out, int iters) {
       else if (K == 21) NZ_OP8W(SHR64);
       else if (K == 22) NZ_OP8W(LSHLADD64);
       else if (K == 23) NZ_OP8(CND);
-      else NZ_OP8(ADD64CO);
+      else if (K == 24) NZ_OP8(ADD64CO);
+      else if (K == 25) { asm volatile("s_mov_b64 s[20:21], -1" ::: "s20", "s21");
+        asm volatile(REP16(CND64(0) CND64(1) CND64(2) CND64(3) CND64(4) CND64(5) CND64(6) CND64(7))
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y), "v"(x)
+                   : "s20", "s21"); }
+      else if (K == 26) NZ_OP8(BFI);
+      else if (K == 27) { asm volatile(REP16(SUBB(0) SUBB(1) SUBB(2) SUBB(3) SUBB(4) SUBB(5) SUBB(6) SUBB(7))
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y), "v"(x)
+                   : "vcc"); }
+      else { asm volatile(REP16(SUBCND(0) SUBCND(1) SUBCND(2) SUBCND(3))
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7) : "v"(y), "v"(x)
+                   : "vcc"); }
     } else if (K == 6) {  // 8 x (mad; s_nop 1; addc) as in field.h mac
       asm volatile(
           "v_mad_u64_u32 %0, s[20:21], %2, %3, %0\n s_nop 1\n v_addc_co_u32_e64 %1, s[20:21], %1, 0, s[20:21]\n"
@@ -153,13 +173,14 @@ int main() {
   const int blocks = 256 * 8, threads = 256, iters = 4000;
   uint64_t* d;
   (void)hipMalloc(&d, (size_t)blocks * threads * 8);
-  const int NK = 25;
+  const int NK = 29;
   const char* names[NK] = {"v_mad_u64_u32 x8", "v_add_co_u32 chain", "s_nop 1", "v_fma_f64 x8", "v_mul_lo_u32 chain",
                            "v_mul_hi_u32 chain", "mac(mad;nop;addc)", "v_add_u32 x8", "v_add_co_u32 x8",
                            "v_addc_co_u32 x8", "v_add3_u32 x8", "v_mad_u32_u24 x8", "v_mul_lo_u32 x8",
                            "v_fma_f32 x8", "mad,mad,addc,addc x2", "v_and_b32 x8", "v_alignbit_b32 x8",
                            "v_lshrrev_b32 x8", "v_mul_u32_u24 x8", "v_mul_hi_u32_u24 x8", "v_bfe_u32 x8",
-                           "v_lshrrev_b64 x8", "v_lshl_add_u64 x8", "v_cndmask_b32 x8", "v_add_co_u32(e32) x8"};
+                           "v_lshrrev_b64 x8", "v_lshl_add_u64 x8", "v_cndmask_b32 x8", "v_add_co_u32(e32) x8",
+                           "v_cndmask_b32_e64 sgpr x8", "v_bfi_b32 x8", "v_subb_co_u32 x8", "subb+cndmask x4"};
   double ms[NK] = {run<0>(d, blocks, threads, iters), run<1>(d, blocks, threads, iters), run<2>(d, blocks, threads, iters),
                    run<3>(d, blocks, threads, iters), run<4>(d, blocks, threads, iters), run<5>(d, blocks, threads, iters),
                    run<6>(d, blocks, threads, iters), run<7>(d, blocks, threads, iters / 8),
@@ -171,7 +192,17 @@ int main() {
                    run<18>(d, blocks, threads, iters / 8), run<19>(d, blocks, threads, iters / 8),
                    run<20>(d, blocks, threads, iters / 8), run<21>(d, blocks, threads, iters / 8),
                    run<22>(d, blocks, threads, iters / 8), run<23>(d, blocks, threads, iters / 8),
-                   run<24>(d, blocks, threads, iters / 8)};
+                   run<24>(d, blocks, threads, iters / 8), run<25>(d, blocks, threads, iters / 8),
+                   run<26>(d, blocks, threads, iters / 8), run<27>(d, blocks, threads, iters / 8),
+                   run<28>(d, blocks, threads, iters / 8)};
+  // dependent-chain latency: mad chains at 1, 2, 4, 8 waves per SIMD (256 CUs x 4 SIMDs)
+  for (int wps = 1; wps <= 8; wps *= 2) {
+    const int b = 256 * wps;  // 256-thread blocks = 4 waves = one per SIMD
+    const double m1 = run<29>(d, b, 256, iters), m2 = run<30>(d, b, 256, iters / 2);
+    const double nw = (double)b * 256 / 64 / 1024;  // waves per SIMD
+    printf("mad chain, %d wave(s)/SIMD: 1 chain %.2f, 2 chains %.2f SIMD-cycles per mad\n", wps,
+           m1 * 1e-3 * 2.4e9 / (nw * iters * 16), m2 * 1e-3 * 2.4e9 / (nw * iters / 2 * 32));
+  }
   const double waves = (double)blocks * threads / 64;
   for (int k = 0; k < NK; k++) {
     // wave-instructions per iteration (mac = one mad+nop+addc group)
