@@ -221,6 +221,12 @@ int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint3
 int nzcb_synth_setup_ex(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints, uint32_t flags,
                         const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len, uint8_t** wtns_out,
                         size_t* wtns_len, nzcb_err* err);
+/* snarkjs `plonk setup <r1cs> <ptau> <zkey>` (snarkjs 0.4.12 plonk_setup.js, run at
+ * /root/reference/Makefile:55,60): iden3 r1cs + powers-of-tau file -> snarkjs-0.4 PLONK
+ * zkey (malloc'ed, release with nzcb_free). Uses the ptau's tauG1 (section 2) and
+ * tauG2 (section 3); NTTs and commitments run on `device`. */
+int nzcb_plonk_setup(const uint8_t* r1cs, size_t r1cs_len, const uint8_t* ptau, size_t ptau_len, int device,
+                     uint8_t** zkey_out, size_t* zkey_len, nzcb_err* err);
 void nzcb_free(void* p);
 
 /* ---- Kernel-level entry points (tests / microbench) */

@@ -13,6 +13,7 @@
 // tests/test_gpu_synth.py checks the zkey/wtns bytes against the oracle.
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "../../include/nzcb.h"
@@ -282,27 +283,42 @@ void launch_fixed_base(const Fr* scalars_mont, size_t n, G1Affine* out, hipStrea
   NZ_HIP(hipGetLastError());
 }
 
-// The whole setup; returns (zkey, wtns) as malloc'ed buffers.
-static void synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_cons, uint32_t flags,
-                        const uint8_t* tau_le, int device, uint8_t** zk_out, size_t* zk_len, uint8_t** wt_out, size_t* wt_len) {
-  if (power < 1 || power > 24 || n_public < 0 || n_inputs < 0) throw Error(NZCB_ERR_ARG, "bad setup arguments");
-  if (flags & ~(uint32_t)NZCB_SYNTH_FREE_PUBLIC) throw Error(NZCB_ERR_ARG, "unknown synth flags");
-  Circuit c = build_circuit(power, (uint32_t)n_public, (uint32_t)n_inputs, seed, n_cons, flags);
+// Source of the powers of tau: a trapdoor tau (synthetic setups, tests), or the
+// tauG1 / tauG2 sections of a snarkjs .ptau file.
+struct PtauSrc {
+  const uint8_t* tau_le = nullptr;  // 32 B LE trapdoor
+  const uint8_t* g1 = nullptr;      // >= n + 6 LEM affine [tau^i]G1 (ptau section 2)
+  size_t g1_count = 0;
+  const uint8_t* x2 = nullptr;      // 128 B LEM [tau]G2 (ptau section 3, point 1)
+};
+
+// snarkjs plonk_setup's zkey for a processed circuit (sections 1-14);
+// malloc'ed buffer.
+static void setup_zkey(const Circuit& c, int power, int n_public, const PtauSrc& src, int device, uint8_t** zk_out,
+                       size_t* zk_len) {
   const uint32_t n = c.n, n4 = 4 * n;
   const uint32_t nc = (uint32_t)c.sa.size();
+  if (n != (1u << power) || nc > n) throw Error(NZCB_ERR_INTERNAL, "circuit does not fit its domain");
   Engine eng(device, power + 2, n);
   hipStream_t st = eng.stream;
 
   // PTau: [tau^i] G1, i < n + 6
-  Fr tau;
-  std::memcpy(tau.v, tau_le, 32);
-  tau = to_mont(reduce_once(reduce_once(tau)));
   const size_t nptau = (size_t)n + 6;
-  DevBuf<Fr> taupow(nptau);
   DevBuf<G1Affine> ptau(nptau);
-  hipLaunchKernelGGL(k_pow_table, dim3(grid_for(nptau, kT, 1u << 30)), dim3(kT), 0, st, taupow.p, tau, nptau);
-  hipLaunchKernelGGL(k_fixed_base, dim3(grid_for(nptau, kT, 1u << 30)), dim3(kT), 0, st, taupow.p, nptau, ptau.p);
-  NZ_HIP(hipGetLastError());
+  Fr tau = Fr::zero();
+  if (src.tau_le) {
+    std::memcpy(tau.v, src.tau_le, 32);
+    tau = to_mont(reduce_once(reduce_once(tau)));
+    DevBuf<Fr> taupow(nptau);
+    hipLaunchKernelGGL(k_pow_table, dim3(grid_for(nptau, kT, 1u << 30)), dim3(kT), 0, st, taupow.p, tau, nptau);
+    hipLaunchKernelGGL(k_fixed_base, dim3(grid_for(nptau, kT, 1u << 30)), dim3(kT), 0, st, taupow.p, nptau,
+                       ptau.p);
+    NZ_HIP(hipGetLastError());
+    NZ_HIP(hipStreamSynchronize(st));
+  } else {
+    if (!src.g1 || !src.x2 || src.g1_count < nptau) throw Error(NZCB_ERR_ARG, "powers of tau too small for the circuit");
+    NZ_HIP(hipMemcpyAsync(ptau.p, src.g1, nptau * 64, hipMemcpyHostToDevice, st));
+  }
 
   DevBuf<Fr> dcol(n), dcoef(n), dpad(n4), deval(n4);
   // writeP4 for one column on n points: returns [coefs | evals4] (LEM bytes) and the commitment
@@ -377,8 +393,8 @@ static void synth_setup(int power, int n_public, int n_inputs, uint64_t seed, ui
   std::vector<uint8_t> ptau_bytes(nptau * 64);
   NZ_HIP(hipMemcpyAsync(ptau_bytes.data(), ptau.p, nptau * 64, hipMemcpyDeviceToHost, st));
   NZ_HIP(hipStreamSynchronize(st));
-  Fr tau_n = from_mont(tau);
-  G2 x2 = g2_mul_gen(tau_n);
+  G2 x2{};
+  if (src.tau_le) x2 = g2_mul_gen(from_mont(tau));
 
   // ---- assemble the zkey ----
   static const uint32_t kQ[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
@@ -398,7 +414,9 @@ static void synth_setup(int power, int n_public, int n_inputs, uint64_t seed, ui
   put_bytes(s2, k1.v, 32);
   put_bytes(s2, k2.v, 32);
   for (int k = 0; k < 8; k++) put_bytes(s2, &com[k], 64);
-  if (x2.inf) {
+  if (!src.tau_le) {
+    put_bytes(s2, src.x2, 128);
+  } else if (x2.inf) {
     std::vector<uint8_t> z(128, 0);
     put_bytes(s2, z.data(), 128);
   } else {
@@ -441,6 +459,21 @@ static void synth_setup(int power, int n_public, int n_inputs, uint64_t seed, ui
     if (!secs[i]->empty()) std::memcpy(zk + off, secs[i]->data(), secs[i]->size());
     off += secs[i]->size();
   }
+  *zk_out = zk;
+  *zk_len = total;
+}
+
+// The whole synthetic setup; returns (zkey, wtns) as malloc'ed buffers.
+static void synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_cons, uint32_t flags,
+                        const uint8_t* tau_le, int device, uint8_t** zk_out, size_t* zk_len, uint8_t** wt_out, size_t* wt_len) {
+  if (power < 1 || power > 24 || n_public < 0 || n_inputs < 0) throw Error(NZCB_ERR_ARG, "bad setup arguments");
+  if (flags & ~(uint32_t)NZCB_SYNTH_FREE_PUBLIC) throw Error(NZCB_ERR_ARG, "unknown synth flags");
+  Circuit c = build_circuit(power, (uint32_t)n_public, (uint32_t)n_inputs, seed, n_cons, flags);
+  PtauSrc src;
+  src.tau_le = tau_le;
+  uint8_t* zk = nullptr;
+  size_t total = 0;
+  setup_zkey(c, power, n_public, src, device, &zk, &total);
   // ---- wtns ----
   size_t wtotal = 12 + 12 + 4 + 32 + 4 + 12 + (size_t)c.n_wit * 32;
   uint8_t* wt = (uint8_t*)std::malloc(wtotal);
@@ -474,6 +507,191 @@ static void synth_setup(int power, int n_public, int n_inputs, uint64_t seed, ui
   *wt_len = wtotal;
 }
 
+
+// ---- snarkjs `plonk setup <r1cs> <ptau> <zkey>` (/root/reference/Makefile:55,60) ------
+// Restates snarkjs 0.4.12 plonk_setup.js [EXT]: processConstraints
+// turns every R1CS constraint (A)(B) = (C) into one PLONK gate, after splitting each
+// linear combination with more than one signal into a binary tree of addition gates
+// (reduceCoef: first half, second half, then a new signal so = l1 a + l2 b, recorded as
+// an "addition" for calculateAdditions); the nPublic public signals get the first
+// gates. The columns, sigma, Lagrange polynomials and commitments are the synthetic
+// setup's (setup_zkey). Commitments use the coefficient form against tauG1 (section 2),
+// the same group elements snarkjs gets from the Lagrange points (section 12).
+
+struct BinSections {  // iden3 binfile: magic, u32 version, u32 count, (u32 type, u64 size, data)*
+  std::vector<std::pair<const uint8_t*, uint64_t>> sec[16];
+};
+static BinSections read_binfile(const uint8_t* d, size_t len, const char* magic, const char* what) {
+  BinSections b;
+  char msg[96];
+  if (!d || len < 12 || std::memcmp(d, magic, 4) != 0) {
+    std::snprintf(msg, sizeof msg, "%s: invalid file format", what);
+    throw Error(NZCB_ERR_FORMAT, msg);
+  }
+  uint32_t version, nsec;
+  std::memcpy(&version, d + 4, 4);
+  std::memcpy(&nsec, d + 8, 4);
+  size_t off = 12;
+  for (uint32_t i = 0; i < nsec; i++) {
+    if (off + 12 > len) throw Error(NZCB_ERR_FORMAT, "truncated section table");
+    uint32_t type;
+    uint64_t size;
+    std::memcpy(&type, d + off, 4);
+    std::memcpy(&size, d + off + 4, 8);
+    off += 12;
+    if (size > len - off) throw Error(NZCB_ERR_FORMAT, "truncated section");
+    if (type < 16) b.sec[type].push_back({d + off, size});
+    off += size;
+  }
+  return b;
+}
+
+struct ByteReader {
+  const uint8_t* p;
+  uint64_t left;
+  uint32_t u32() {
+    if (left < 4) throw Error(NZCB_ERR_FORMAT, "r1cs: truncated");
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    p += 4;
+    left -= 4;
+    return v;
+  }
+  uint64_t u64() {
+    const uint64_t lo = u32();
+    return lo | ((uint64_t)u32() << 32);
+  }
+  Fr fr_normal() {  // 32 B LE normal form -> Montgomery (ffjavascript Fr.fromRprLE)
+    if (left < 32) throw Error(NZCB_ERR_FORMAT, "r1cs: truncated");
+    Fr v;
+    std::memcpy(v.v, p, 32);
+    p += 32;
+    left -= 32;
+    if (!(reduce_once(v) == v) || v == Fr::modulus()) throw Error(NZCB_ERR_FORMAT, "r1cs: coefficient not reduced");
+    return to_mont(v);
+  }
+};
+
+struct R1csCircuit {
+  Circuit c;
+  int power = 0;
+  uint32_t n_public = 0;
+};
+
+static R1csCircuit circuit_from_r1cs(const uint8_t* d, size_t len) {
+  BinSections b = read_binfile(d, len, "r1cs", "r1cs");
+  if (b.sec[1].empty() || b.sec[2].empty()) throw Error(NZCB_ERR_FORMAT, "r1cs: missing header or constraints");
+  ByteReader h{b.sec[1][0].first, b.sec[1][0].second};
+  if (h.u32() != 32) throw Error(NZCB_ERR_FORMAT, "r1cs: field size is not 32 bytes");
+  if (h.left < 32 || std::memcmp(h.p, FrParams::P, 32) != 0)
+    throw Error(NZCB_ERR_CURVE, "r1cs curve does not match powers of tau ceremony curve");
+  h.p += 32;
+  h.left -= 32;
+  const uint32_t n_wires = h.u32(), n_out = h.u32(), n_pub_in = h.u32();
+  (void)h.u32();  // private inputs
+  (void)h.u64();  // labels
+  const uint32_t n_cons = h.u32();
+  R1csCircuit r;
+  Circuit& c = r.c;
+  r.n_public = n_out + n_pub_in;
+  if (r.n_public >= n_wires) throw Error(NZCB_ERR_FORMAT, "r1cs: more public signals than wires");
+  uint32_t nvars = n_wires;
+  auto gate = [&](uint32_t sl, uint32_t sr, uint32_t so, const Fr& qm, const Fr& ql, const Fr& qr, const Fr& qo,
+                  const Fr& qc) {
+    c.sa.push_back(sl);
+    c.sb.push_back(sr);
+    c.sc.push_back(so);
+    c.q[0].push_back(qm);
+    c.q[1].push_back(ql);
+    c.q[2].push_back(qr);
+    c.q[3].push_back(qo);
+    c.q[4].push_back(qc);
+  };
+  using Term = std::pair<uint32_t, Fr>;
+  std::function<Term(const std::vector<Term>&, size_t, size_t)> reduce = [&](const std::vector<Term>& v, size_t lo,
+                                                                              size_t hi) -> Term {
+    const size_t m = hi - lo;
+    if (m == 0) return {0u, Fr::zero()};
+    if (m == 1) return v[lo];
+    const Term t1 = reduce(v, lo, lo + (m >> 1));
+    const Term t2 = reduce(v, lo + (m >> 1), hi);
+    const uint32_t so = nvars++;
+    gate(t1.first, t2.first, so, Fr::zero(), neg(t1.second), neg(t2.second), Fr::one(), Fr::zero());
+    c.ax.push_back(t1.first);
+    c.ay.push_back(t2.first);
+    c.ac.push_back(t1.second);
+    c.bc.push_back(t2.second);
+    return {so, Fr::one()};
+  };
+  struct Lc {
+    uint32_t s;
+    Fr coef, k;
+  };
+  ByteReader cr{b.sec[2][0].first, b.sec[2][0].second};
+  auto read_lc = [&]() -> Lc {
+    Lc lc{0u, Fr::zero(), Fr::zero()};
+    std::vector<Term> terms;
+    const uint32_t nt = cr.u32();
+    for (uint32_t i = 0; i < nt; i++) {
+      const uint32_t s = cr.u32();
+      const Fr coef = cr.fr_normal();
+      if (s >= n_wires) throw Error(NZCB_ERR_FORMAT, "r1cs: signal out of range");
+      if (s == 0) lc.k = coef;
+      else terms.push_back({s, coef});
+    }
+    const Term t = reduce(terms, 0, terms.size());
+    lc.s = t.first;
+    lc.coef = t.second;
+    return lc;
+  };
+  for (uint32_t s = 1; s <= r.n_public; s++)
+    gate(s, 0, 0, Fr::zero(), Fr::one(), Fr::zero(), Fr::zero(), Fr::zero());
+  for (uint32_t i = 0; i < n_cons; i++) {
+    const Lc A = read_lc();
+    const Lc B = read_lc();
+    const Lc C = read_lc();
+    gate(A.s, B.s, C.s, A.coef * B.coef, A.coef * B.k, A.k * B.coef, neg(C.coef), A.k * B.k - C.k);
+  }
+  const size_t nc = c.sa.size();
+  int p = 0;  // snarkjs: cirPower = log2(nConstraints - 1) + 1, at least 3
+  for (size_t v = nc ? nc - 1 : 0; v > 1; v >>= 1) p++;
+  p += 1;
+  if (p < 3) p = 3;
+  r.power = p;
+  c.n = 1u << p;
+  c.n_public = r.n_public;
+  c.n_vars = nvars;
+  c.n_add = (uint32_t)c.ax.size();
+  c.n_wit = n_wires;
+  return r;
+}
+
+static void plonk_setup(const uint8_t* r1cs, size_t r1cs_len, const uint8_t* ptau, size_t ptau_len, int device,
+                        uint8_t** zk_out, size_t* zk_len) {
+  BinSections pt = read_binfile(ptau, ptau_len, "ptau", "ptau");
+  if (pt.sec[1].empty() || pt.sec[2].empty() || pt.sec[3].empty())
+    throw Error(NZCB_ERR_FORMAT, "ptau: missing header, tauG1 or tauG2");
+  ByteReader h{pt.sec[1][0].first, pt.sec[1][0].second};
+  if (h.u32() != 32 || h.left < 40 || std::memcmp(h.p, FqParams::P, 32) != 0)
+    throw Error(NZCB_ERR_FORMAT, "ptau: not a bn128 powers of tau file");
+  h.p += 32;
+  h.left -= 32;
+  const uint32_t ptau_power = h.u32();
+  R1csCircuit rc = circuit_from_r1cs(r1cs, r1cs_len);
+  if (rc.power > (int)ptau_power || rc.power > 24) {
+    char msg[128];
+    std::snprintf(msg, sizeof msg, "circuit too big for this power of tau ceremony. %zu > 2**%u", rc.c.sa.size(),
+                  ptau_power);
+    throw Error(NZCB_ERR_ARG, msg);
+  }
+  if (pt.sec[3][0].second < 256) throw Error(NZCB_ERR_FORMAT, "ptau: tauG2 section too small");
+  PtauSrc src;
+  src.g1 = pt.sec[2][0].first;
+  src.g1_count = pt.sec[2][0].second / 64;
+  src.x2 = pt.sec[3][0].first + 128;
+  setup_zkey(rc.c, rc.power, (int)rc.n_public, src, device, zk_out, zk_len);
+}
+
 }  // namespace nzcb
 
 extern "C" int nzcb_synth_setup_ex(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints,
@@ -503,4 +721,24 @@ extern "C" int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t 
                                 uint8_t** wtns_out, size_t* wtns_len, nzcb_err* err) {
   return nzcb_synth_setup_ex(power, n_public, n_inputs, seed, n_constraints, 0, tau, device, zkey_out, zkey_len,
                              wtns_out, wtns_len, err);
+}
+
+extern "C" int nzcb_plonk_setup(const uint8_t* r1cs, size_t r1cs_len, const uint8_t* ptau, size_t ptau_len,
+                                int device, uint8_t** zkey_out, size_t* zkey_len, nzcb_err* err) {
+  using namespace nzcb;
+  if (!r1cs || !ptau || !zkey_out || !zkey_len) {
+    set_err(err, NZCB_ERR_ARG, "null argument");
+    return NZCB_ERR_ARG;
+  }
+  try {
+    NZ_HIP(hipSetDevice(device));
+    plonk_setup(r1cs, r1cs_len, ptau, ptau_len, device, zkey_out, zkey_len);
+    return 0;
+  } catch (const Error& e) {
+    set_err(err, e.code, e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+    return NZCB_ERR_INTERNAL;
+  }
 }

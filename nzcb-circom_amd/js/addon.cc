@@ -340,6 +340,35 @@ napi_value NzcpWitness(napi_env env, napi_callback_info info) {
   return out;
 }
 
+// plonkSetup(r1cs: Buffer, ptau: Buffer, device: number) -> Buffer (the zkey):
+// snarkjs `plonk setup` (nzcb_plonk_setup). Synchronous: a one-off key generation.
+napi_value PlonkSetup(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  const uint8_t *r1cs, *ptau;
+  size_t rl, pl;
+  int32_t device = 0;
+  if (argc < 2 || !buf_arg(env, argv[0], &r1cs, &rl) || !buf_arg(env, argv[1], &ptau, &pl)) {
+    napi_throw_type_error(env, nullptr, "plonkSetup(r1cs: Buffer, ptau: Buffer, device?: number)");
+    return nullptr;
+  }
+  if (argc > 2) napi_get_value_int32(env, argv[2], &device);
+  uint8_t* zk = nullptr;
+  size_t zl = 0;
+  nzcb_err err{};
+  if (nzcb_plonk_setup(r1cs, rl, ptau, pl, device, &zk, &zl, &err)) {
+    napi_throw(env, make_error(env, err.code, err.msg));
+    return nullptr;
+  }
+  void* out_data = nullptr;
+  napi_value out;
+  napi_status stc = napi_create_buffer_copy(env, zl, zk, &out_data, &out);
+  nzcb_free(zk);
+  CHECK(stc);
+  return out;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"createContext", nullptr, CreateContext, nullptr, nullptr, nullptr, napi_default, nullptr},
@@ -352,6 +381,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"verify", nullptr, Verify, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"calldata", nullptr, Calldata, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"nzcpWitness", nullptr, NzcpWitness, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"plonkSetup", nullptr, PlonkSetup, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

@@ -1,6 +1,7 @@
 #!/usr/bin/env node
 'use strict';
-// `snarkjs plonk prove|fullprove` equivalent on the MI355X prover (SURVEY.md §8b):
+// `snarkjs plonk setup|prove|fullprove` equivalent on the MI355X prover (SURVEY.md §8b):
+//   node cli.js plonk setup     <circuit.r1cs> <pot.ptau> <circuit.zkey>
 //   node cli.js plonk prove     <circuit.zkey> <witness.wtns> <proof.json> <public.json>
 //   node cli.js plonk fullprove <input.json> <circuit.wasm> <circuit.zkey> <proof.json> <public.json>
 // Output JSON is written like snarkjs's CLI (stringifyBigInts, 1-space indent).
@@ -8,7 +9,8 @@ const fs = require('fs');
 const nz = require('./index.js');
 
 function usage() {
-  console.error('usage: cli.js plonk prove <zkey> <wtns> <proof.json> <public.json>\n' +
+  console.error('usage: cli.js plonk setup <r1cs> <ptau> <zkey>\n' +
+                '       cli.js plonk prove <zkey> <wtns> <proof.json> <public.json>\n' +
                 '       cli.js plonk fullprove <input.json> <wasm> <zkey> <proof.json> <public.json>');
   process.exit(1);
 }
@@ -17,6 +19,10 @@ async function main(argv) {
   if (argv[0] !== 'plonk') usage();
   const logger = process.env.NZCB_VERBOSE ? { debug: (m) => console.error(m) } : null;
   let res, out;
+  if (argv[1] === 'setup' && argv.length === 5) {
+    await nz.plonk.setup(argv[2], argv[3], argv[4], logger);
+    return;
+  }
   if (argv[1] === 'prove' && argv.length === 6) {
     res = await nz.plonk.prove(argv[2], argv[3], logger);
     out = argv.slice(4);

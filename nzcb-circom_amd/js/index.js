@@ -208,6 +208,20 @@ function vkBuf(vk) {
     .concat([le32(x2[0][0]), le32(x2[0][1]), le32(x2[1][0]), le32(x2[1][1]), le32(vk.w)]));
 }
 
+// snarkjs plonk.setup(r1csName, ptauName, zkeyName, logger) (snarkjs 0.4.12
+// plonk_setup.js, run at /root/reference/Makefile:55,60): writes the PLONK zkey.
+// Names may also be {type: "mem", data} objects; a {type: "mem"} zkeyName receives
+// the bytes in .data.
+async function setup(r1csName, ptauName, zkeyName, logger, options) {
+  options = options || {};
+  const log = loggerFn(logger);
+  const zkey = addon.plonkSetup(readBin(r1csName), readBin(ptauName), options.device || 0);
+  if (zkeyName && typeof zkeyName === 'object') zkeyName.data = new Uint8Array(zkey);
+  else fs.writeFileSync(zkeyName, zkey);
+  if (log) log(`Plonk setup: zkey of ${zkey.length} bytes`);
+  return 0;
+}
+
 async function exportVerificationKey(zkeyFileName) {
   return JSON.parse(addon.vkToJson(addon.vkFromZkey(readBin(zkeyFileName))));
 }
@@ -277,7 +291,7 @@ function nzcpWitness(inputs, options) {
 }
 
 module.exports = {
-  plonk: { prove, fullProve, verify, exportSolidityCallData },
+  plonk: { setup, prove, fullProve, verify, exportSolidityCallData },
   zKey: { exportVerificationKey },
   nzcp: Object.assign({}, require('./nzcp.js'), { witness: nzcpWitness }),
   wtns: { calculate: wtnsCalculate },

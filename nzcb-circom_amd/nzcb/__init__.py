@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_to_json", "nzcb_verify",
     "nzcb_proof_to_calldata", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d", "nzcb_msm_set_pair_rounds",
+    "nzcb_plonk_setup",
 ]
 
 
@@ -144,6 +145,8 @@ def load(path: str | None = None):
         "nzcb_engine_msm_fixed_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_int, u8p,
                                               POINTER(_Err)]),
         "nzcb_msm_set_pair_rounds": (c_int, [c_int]),
+        "nzcb_plonk_setup": (c_int, [ctypes.c_char_p, c_size_t, ctypes.c_char_p, c_size_t, c_int, POINTER(POINTER(c_uint8)),
+                                     POINTER(c_size_t), POINTER(_Err)]),
         "nzcb_nzcp_input_signals": (c_size_t, [POINTER(NzcpParams)]),
         "nzcb_nzcp_witness": (c_int, [c_int, POINTER(NzcpParams), u8p, c_int, POINTER(NzcpRecord), POINTER(_Err)]),
         "nzcb_nzcp_witness_dev": (c_int, [c_int, POINTER(NzcpParams), c_void_p, c_int, c_void_p, c_void_p, c_size_t,
@@ -750,6 +753,23 @@ def synth_setup(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x
         lib.nzcb_free(ctypes.cast(zp, c_void_p))
         lib.nzcb_free(ctypes.cast(wp, c_void_p))
     return zkey, wtns
+
+
+def plonk_setup(r1cs: bytes, ptau: bytes, device: int = 0) -> bytes:
+    """snarkjs ``plonk setup <r1cs> <ptau> <zkey>`` (snarkjs 0.4.12 plonk_setup.js, run at
+    /root/reference/Makefile:55,60): returns the PLONK zkey bytes. The NTTs and the
+    commitments run on `device`; raises NzcbError as snarkjs throws (curve mismatch,
+    "circuit too big for this power of tau ceremony", "Variable not used")."""
+    lib = load()
+    zp = POINTER(c_uint8)()
+    zl = c_size_t()
+    err = _Err()
+    _check(lib.nzcb_plonk_setup(bytes(r1cs), len(r1cs), bytes(ptau), len(ptau), device, ctypes.byref(zp),
+                                ctypes.byref(zl), ctypes.byref(err)), err)
+    try:
+        return ctypes.string_at(zp, zl.value)
+    finally:
+        lib.nzcb_free(zp)
 
 
 def synth_setup_raw(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,

@@ -159,3 +159,22 @@ console.log(JSON.stringify({{r, expected: z.expectedPublicSignals(uri, data), th
     assert d["r"]["vcPos"] == 76 and d["r"]["nullifier"] == "Jack,Sparrow,1960-04-16"
     assert d["r"]["toBeSignedHash"] == "271ce33d671a2d3b816d788135f4343e14bc66802f8cd841faac939e8c11f3ee"
     assert "CBOR type is not a map" in d["threw"]
+
+
+@needs_node
+@pytest.mark.gpu
+def test_cli_plonk_setup_matches_library(tmp_path):
+    """`node cli.js plonk setup <r1cs> <ptau> <zkey>` (/root/reference/Makefile:55,60) writes
+    the zkey nzcb_plonk_setup builds, which tests/test_r1cs_setup.py checks against the
+    oracle and proves with."""
+    import nzcb
+    from oracle import r1cs
+    data, _ = r1cs.random_r1cs(31, n_steps=30)
+    ptau = r1cs.write_ptau(0x5E7A9, 8)
+    (tmp_path / "c.r1cs").write_bytes(data)
+    (tmp_path / "p.ptau").write_bytes(ptau)
+    zf = tmp_path / "c.zkey"
+    p = subprocess.run(["node", os.path.join(JS, "cli.js"), "plonk", "setup", str(tmp_path / "c.r1cs"),
+                        str(tmp_path / "p.ptau"), str(zf)], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    assert zf.read_bytes() == nzcb.plonk_setup(data, ptau)
