@@ -41,6 +41,35 @@ def test_ntt(engine, log_n, inverse):
     assert got == want
 
 
+@pytest.mark.parametrize("log_n", [21, 23])
+def test_ntt_full_size_properties(log_n):
+    """The prover's NTT sizes (n = 2^21, 4n = 2^23), size-independent properties on
+    pseudo-random Montgomery inputs: iNTT(NTT(x)) = x bit-exactly; NTT(x)[0] = sum x;
+    NTT(x)[n/2] = alternating sum; at 2^21 also NTT(x)[1] and NTT(x)[n-1] against Horner
+    at w and w^-1 (every twiddle contributes). All linear, so the checks run on the raw
+    Montgomery values."""
+    import nzcb
+    n = 1 << log_n
+    eng = nzcb.Engine(0, max_log_ntt=log_n, max_msm_points=0)
+    dev = nzcb.dev_alloc(n * 32)
+    try:
+        eng.random_fr(dev, n, 0x4E5454 + log_n)
+        data = nzcb.d2h(dev, n * 32)
+        fwd = eng.ntt(data, log_n, False)
+        assert eng.ntt(fwd, log_n, True) == data
+    finally:
+        nzcb.dev_free(dev)
+        eng.close()
+    x = [int.from_bytes(data[i:i + 32], "little") for i in range(0, 32 * n, 32)]
+    y = [int.from_bytes(fwd[i:i + 32], "little") for i in (0, 32, 32 * (n // 2), 32 * (n - 1))]
+    assert y[0] == sum(x) % R_MOD
+    assert y[2] == (sum(x[0::2]) - sum(x[1::2])) % R_MOD
+    if log_n <= 21:
+        w = bn.FR_W[log_n]
+        assert y[1] == bn.eval_pol(x, w)
+        assert y[3] == bn.eval_pol(x, bn.fr_inv(w))
+
+
 def _affine(out):
     x = bn.from_le(out[:32])
     y = bn.from_le(out[32:])
