@@ -20,16 +20,18 @@ struct NttTables {
   void init(int max_log, hipStream_t st);
 };
 
-// Optional fused prologue / epilogue (coset NTTs of zero-padded polynomials):
-//   input  j: in[j] * in_lo[j & 4095] * in_hi[j >> 12] for j < in_len, 0 beyond (not read)
-//   output j: out[j] * out_lo[j & 4095] * out_hi[j >> 12]; sets *out_flags if an output
-//             at j >= out_limit is nonzero
+// Optional fused prologue / epilogue (coset NTTs of zero-padded polynomials). Factors
+// are split29 of their Montgomery-261 form (f * 2^261 mod r, as the twiddles), one
+// 9x29 product per element:
+//   input  j: in[j] * in_f[j] for j < in_len, 0 beyond (not read)
+//   output j: out[j] * out_f[j]; sets *out_flags if an output at j >= out_limit is
+//             nonzero. out_f_has_scale: out_f already holds the inverse transform's
+//             1/N (the first pass then skips it).
 struct NttIo {
   size_t in_len = ~size_t(0);
-  const Fr* in_lo = nullptr;
-  const Fr* in_hi = nullptr;
-  const Fr* out_lo = nullptr;
-  const Fr* out_hi = nullptr;
+  const F29* in_f = nullptr;
+  const F29* out_f = nullptr;
+  bool out_f_has_scale = false;
   size_t out_limit = ~size_t(0);
   uint32_t* out_flags = nullptr;
 };

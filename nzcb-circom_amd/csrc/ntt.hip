@@ -106,8 +106,8 @@ void NttTables::init(int L, hipStream_t st) {
 
 // One pass: stages [s, s+q) on tiles of (2^q rows) x (2^logC columns).
 __global__ void __launch_bounds__(kNttThreads)
-ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s, int q, int logC, int first, Fr scale,
-                int do_scale, int last, NttIo io) {
+ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s, int q, int logC, int first,
+                F29 scale29, int do_scale, int last, NttIo io) {
   extern __shared__ Fr tile[];
   const int C = 1 << logC;
   const int rows = 1 << q;
@@ -123,8 +123,8 @@ ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s,
       Fr v = Fr::zero();
       if (src < io.in_len) {
         v = in[src];
-        if (io.in_lo) v = v * (io.in_lo[src & 4095] * io.in_hi[src >> 12]);
-        if (do_scale) v = v * scale;
+        if (io.in_f) v = mul_fr29(v, io.in_f[src]);
+        if (do_scale) v = mul_fr29(v, scale29);
       }
       tile[e] = v;
     }
@@ -200,7 +200,7 @@ ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s,
   // final store, with the optional epilogue on the transform's last pass
   auto store = [&](size_t dst, Fr v) {
     if (last) {
-      if (io.out_lo) v = v * (io.out_lo[dst & 4095] * io.out_hi[dst >> 12]);
+      if (io.out_f) v = mul_fr29(v, io.out_f[dst]);
       if (io.out_flags && dst >= io.out_limit && !v.is_zero()) atomicOr(io.out_flags, 1u);
     }
     out[dst] = v;
@@ -227,7 +227,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   const F29* tw = inverse_dir ? t.inv29.p : t.fwd29.p;
   Fr sc = Fr::one();
   int do_scale = 0;
-  if (inverse_dir) {
+  if (inverse_dir && !io.out_f_has_scale) {
     Fr two = Fr::one() + Fr::one();
     sc = inverse(pow_u64(two, (uint64_t)L));  // N^-1
     do_scale = 1;
@@ -236,8 +236,10 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
     sc = do_scale ? sc * *scale : *scale;
     do_scale = 1;
   }
+  for (int k = 0; k < 5; k++) sc = sc + sc;  // Montgomery-261 operand of mul_fr29
+  const F29 sc29 = split29(sc);
   if (L == 0) {
-    hipLaunchKernelGGL(ntt_pass_kernel, dim3(1), dim3(kNttThreads), sizeof(Fr), st, in, out, tw, 0, 0, 0, 0, 1, sc,
+    hipLaunchKernelGGL(ntt_pass_kernel, dim3(1), dim3(kNttThreads), sizeof(Fr), st, in, out, tw, 0, 0, 0, 0, 1, sc29,
                        do_scale, 1, io);
     NZ_HIP(hipGetLastError());
     return;
@@ -249,7 +251,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   size_t tiles = (size_t)cols >> logC1;
   size_t lds = (size_t(1) << (q1 + logC1)) * sizeof(Fr);
   hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)tiles), dim3(kNttThreads), lds, st, in, out, tw, L, 0, q1, logC1,
-                     1, sc, do_scale, q1 == L ? 1 : 0, io);
+                     1, sc29, do_scale, q1 == L ? 1 : 0, io);
   NZ_HIP(hipGetLastError());
   int s = q1;
   while (s < L) {
@@ -259,7 +261,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
     size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
     size_t lds2 = (size_t(1) << (q + logC)) * sizeof(Fr);
     hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)ntiles), dim3(kNttThreads), lds2, st, out, out, tw, L, s, q,
-                       logC, 0, sc, 0, s + q == L ? 1 : 0, io);
+                       logC, 0, sc29, 0, s + q == L ? 1 : 0, io);
     NZ_HIP(hipGetLastError());
     s += q;
   }

@@ -58,6 +58,7 @@ struct Prover {
   DevBuf<Fr> root_lo, root_hi;    // w4^j, w4^(4096 k)
   DevBuf<Fr> x_lo;                // g * w4^j (coset points, with root_hi)
   DevBuf<Fr> g_lo, g_hi, gi_lo, gi_hi;  // g^j, g^-j split tables
+  DevBuf<F29> g29, gi29;                 // g^j (j < n + 8) and g^-j / 4n (j < 4n), mul_fr29 operands
   Fr zh_inv[4];
   DevBuf<Fr> cq, cs, cl;          // coset evaluations: Qm..Qc (5 x 4n), sigma1..3 (3 x 4n), L_j (nl x 4n)
   // per-proof working set

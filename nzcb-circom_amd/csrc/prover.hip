@@ -408,6 +408,18 @@ __global__ void k_root_table(Fr* __restrict__ out, Fr base, Fr scale, size_t cou
   out[i] = scale * pow_u64(base, i);
 }
 
+// out[i] = split29(lo[i & 4095] * hi[i >> 12] * scale * 2^5): the per-index factor
+// (scale * base^i) as the Montgomery-261 operand of mul_fr29 (NttIo in_f / out_f)
+__global__ void k_factor29_table(F29* __restrict__ out, const Fr* __restrict__ lo, const Fr* __restrict__ hi, Fr scale,
+                                 size_t count) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  Fr v = lo[i & 4095] * hi[i >> 12] * scale;
+#pragma unroll
+  for (int k = 0; k < 5; k++) v = v + v;
+  out[i] = split29(v);
+}
+
 // ----------------------------------------------------------------------------
 // host helpers
 // ----------------------------------------------------------------------------
@@ -591,6 +603,17 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   table(g_hi, nhi, pow_u64(g, 4096), one);
   table(gi_lo, nlo, gi, one);
   table(gi_hi, nhi, pow_u64(gi, 4096), one);
+  {  // full per-index coset factors for the NTT prologue (g^j, j < n + 8) and the
+     // quotient iNTT's epilogue (g^-j / 4n, j < 4n)
+    const Fr two = one + one;
+    g29.alloc((size_t)n + 8);
+    gi29.alloc(n4);
+    hipLaunchKernelGGL(k_factor29_table, dim3(grid_for((size_t)n + 8, kT, 1u << 30)), dim3(kT), 0, s, g29.p, g_lo.p,
+                       g_hi.p, one, (size_t)n + 8);
+    hipLaunchKernelGGL(k_factor29_table, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, gi29.p, gi_lo.p, gi_hi.p,
+                       inverse(pow_u64(two, (uint64_t)power + 2)), (size_t)n4);
+    NZ_HIP(hipGetLastError());
+  }
   {
     Fr gn = pow_u64(g, n), w4n = pow_u64(w4, n), p = gn;
     for (int k = 0; k < 4; k++) {
@@ -608,8 +631,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     auto coset_eval = [&](const Fr* coefs, Fr* out) {
       NttIo io;  // coset shift g^j and the zero padding fused into the NTT's first pass
       io.in_len = n;
-      io.in_lo = g_lo.p;
-      io.in_hi = g_hi.p;
+      io.in_f = g29.p;
       ntt(eng->ntt_tables, coefs, out, power + 2, false, s, nullptr, &io);
     };
     const DevBuf<Fr>* qs[5] = {&qm, &ql, &qr, &qo, &qc};
@@ -680,6 +702,7 @@ Prover::Prover(const Prover& pk, int) {
   amap.alias(pk.amap); bmap.alias(pk.bmap); cmap.alias(pk.cmap); adds.alias(pk.adds);
   root_lo.alias(pk.root_lo); root_hi.alias(pk.root_hi); x_lo.alias(pk.x_lo);
   g_lo.alias(pk.g_lo); g_hi.alias(pk.g_hi); gi_lo.alias(pk.gi_lo); gi_hi.alias(pk.gi_hi);
+  g29.alias(pk.g29); gi29.alias(pk.gi29);
   cq.alias(pk.cq); cs.alias(pk.cs); cl.alias(pk.cl);
   alloc_workspace();
 }
@@ -698,8 +721,7 @@ void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int n
   // evaluations of the *blinded* polynomial on the coset g*<w4> (round-3 quotient input)
   NttIo io;  // coset shift g^j and the zero padding fused into the NTT's first pass
   io.in_len = (size_t)n + nb;
-  io.in_lo = g_lo.p;
-  io.in_hi = g_hi.p;
+  io.in_f = g29.p;
   ntt(eng->ntt_tables, coefs, evals4, power + 2, false, s, nullptr, &io);
   NZ_HIP(hipGetLastError());
   ntt_ms += ms_since(t0);  // host enqueue time only (kernels run asynchronously)
@@ -943,9 +965,9 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
                          Z4.p, cq.p, cs.p, cl.p, nPublic, A.p, (size_t)n, x_lo.p, root_hi.p, q, T.p);
     }
     NZ_HIP(hipGetLastError());
-    NttIo io;  // coset unscale g^-j and the degree check fused into the iNTT's last pass
-    io.out_lo = gi_lo.p;
-    io.out_hi = gi_hi.p;
+    NttIo io;  // 1/4n, the coset unscale g^-j and the degree check fused into the iNTT's last pass
+    io.out_f = gi29.p;
+    io.out_f_has_scale = true;
     io.out_limit = (size_t)3 * n + 6;
     io.out_flags = flags.p;
     ntt(eng->ntt_tables, T.p, t.p, power + 2, true, s, nullptr, &io);
