@@ -115,6 +115,13 @@ int nzcb_ctx_set_msm_devices(nzcb_ctx* ctx, const int* devices, int ndev, nzcb_e
 int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witness, int count, int witness_on_device,
                      const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out, size_t pub_stride,
                      nzcb_err* err);
+/* As nzcb_prove_batch, but a failed proof does not stop the batch: every
+ * item is proved, status_out[i] (count ints) receives 0 or proof i's error code, and a
+ * failed item's proof and public bytes are zeroed. Returns (and reports in err) the
+ * error of the lowest failing index, 0 when all succeed. */
+int nzcb_prove_batch_status(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witness, int count,
+                            int witness_on_device, const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out,
+                            size_t pub_stride, int* status_out, nzcb_err* err);
 
 /* Wall-clock milliseconds of the last proof's phases:
  * [0] total [1] witness upload+additions+ABC [2] round1 [3] round2 [4] round3 [5] round4 [6] round5

@@ -142,9 +142,12 @@ int nzcb_ctx_set_msm_devices(nzcb_ctx* ctx, const int* devices, int ndev, nzcb_e
   }
 }
 
-int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witness, int count, int witness_on_device,
-                     const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out, size_t pub_stride,
-                     nzcb_err* err) {
+// keep_going: prove every item and report each one's code in status_out (SURVEY.md §5:
+// a failed proof is reported per item without aborting the batch); otherwise stop
+// taking items past the first failure.
+static int prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witness, int count, int witness_on_device,
+                       const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out, size_t pub_stride,
+                       bool keep_going, int* status_out, nzcb_err* err) {
   if (!ctx || count < 0 || (count && (!witnesses || !proofs_out))) return fail(err, NZCB_ERR_ARG, "null argument");
   const size_t npub = ctx->p->nPublic;
   if (npub && (!pubs_out || pub_stride < 32 * npub)) return fail(err, NZCB_ERR_ARG, "public output buffer too small");
@@ -156,7 +159,7 @@ int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witne
   auto worker = [&](Prover* pr) {
     for (;;) {
       const int i = next.fetch_add(1);
-      if (i >= count || i > first_bad.load()) return;
+      if (i >= count || (!keep_going && i > first_bad.load())) return;
       try {
         pr->prove((const uint8_t*)witnesses[i], n_witness,
                   blindings ? blindings + (size_t)i * NZCB_BLINDING_BYTES : nullptr,
@@ -170,6 +173,10 @@ int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witne
         msgs[i] = e.what();
       }
       if (codes[i]) {
+        if (keep_going) {  // no partial output for a failed item
+          std::memset(proofs_out + (size_t)i * NZCB_PROOF_BYTES, 0, NZCB_PROOF_BYTES);
+          if (npub) std::memset(pubs_out + (size_t)i * pub_stride, 0, 32 * npub);
+        }
         int cur = first_bad.load();
         while (i < cur && !first_bad.compare_exchange_weak(cur, i)) {
         }
@@ -181,6 +188,8 @@ int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witne
   for (size_t l = 1; l < nl; l++) th.emplace_back(worker, ctx->lane(l));
   worker(ctx->lane(0));
   for (auto& t : th) t.join();
+  if (status_out)
+    for (int i = 0; i < count; i++) status_out[i] = codes[i];
   const int bad = first_bad.load();
   if (bad < count) {
     std::string m = "proof " + std::to_string(bad) + ": " + msgs[bad];
@@ -188,6 +197,21 @@ int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witne
   }
   if (err) err->code = 0;
   return 0;
+}
+
+int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witness, int count, int witness_on_device,
+                     const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out, size_t pub_stride,
+                     nzcb_err* err) {
+  return prove_batch(ctx, witnesses, n_witness, count, witness_on_device, blindings, proofs_out, pubs_out, pub_stride,
+                     false, nullptr, err);
+}
+
+int nzcb_prove_batch_status(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witness, int count,
+                            int witness_on_device, const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out,
+                            size_t pub_stride, int* status_out, nzcb_err* err) {
+  if (count > 0 && !status_out) return fail(err, NZCB_ERR_ARG, "null argument");
+  return prove_batch(ctx, witnesses, n_witness, count, witness_on_device, blindings, proofs_out, pubs_out, pub_stride,
+                     true, status_out, err);
 }
 
 int nzcb_ctx_info(const nzcb_ctx* ctx, uint32_t out[5]) {

@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_to_json", "nzcb_verify",
     "nzcb_proof_to_calldata", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d", "nzcb_msm_set_pair_rounds",
-    "nzcb_plonk_setup",
+    "nzcb_plonk_setup", "nzcb_prove_batch_status",
 ]
 
 
@@ -114,6 +114,8 @@ def load(path: str | None = None):
         "nzcb_ctx_lanes": (c_int, [c_void_p]),
         "nzcb_prove_batch": (c_int, [c_void_p, POINTER(c_void_p), c_size_t, c_int, c_int, u8p, u8p, u8p, c_size_t,
                                      POINTER(_Err)]),
+        "nzcb_prove_batch_status": (c_int, [c_void_p, POINTER(c_void_p), c_size_t, c_int, c_int, u8p, u8p, u8p,
+                                            c_size_t, POINTER(c_int), POINTER(_Err)]),
         "nzcb_ctx_last_timings": (c_int, [c_void_p, POINTER(c_double), c_int]),
         "nzcb_proof_to_json": (c_int, [u8p, ctypes.c_char_p, c_size_t]),
         "nzcb_public_to_json": (c_int, [u8p, c_int, ctypes.c_char_p, c_size_t]),
@@ -461,9 +463,13 @@ class ProverContext:
     def lanes(self) -> int:
         return self.lib.nzcb_ctx_lanes(self.h)
 
-    def prove_batch_raw(self, witnesses, n_witness: int | None = None, blindings=None, on_device: bool = False):
+    def prove_batch_raw(self, witnesses, n_witness: int | None = None, blindings=None, on_device: bool = False,
+                        statuses: list | None = None):
         """Independent proofs over the lanes. witnesses: list of bytes (host) or device
-        pointers (on_device). blindings: list of 352-byte values / None. Returns [(proof, pub)]."""
+        pointers (on_device). blindings: list of 352-byte values / None. Returns [(proof, pub)].
+        With a `statuses` list, a failed proof does not stop the batch: the list receives
+        each item's error code (0 = proved; a failed item's bytes are zero) and nothing is
+        raised (nzcb_prove_batch_status)."""
         count = len(witnesses)
         keep = []
         ptrs = (c_void_p * max(count, 1))()
@@ -483,8 +489,16 @@ class ProverContext:
         stride = 32 * max(self.n_public, 1)
         pubs = _out(stride * count)
         err = _Err()
-        _check(self.lib.nzcb_prove_batch(self.h, ptrs, n_witness or 0, count, int(on_device), bl, proofs, pubs,
-                                         stride, ctypes.byref(err)), err)
+        if statuses is None:
+            _check(self.lib.nzcb_prove_batch(self.h, ptrs, n_witness or 0, count, int(on_device), bl, proofs, pubs,
+                                             stride, ctypes.byref(err)), err)
+        else:
+            st = (c_int * max(count, 1))()
+            rc = self.lib.nzcb_prove_batch_status(self.h, ptrs, n_witness or 0, count, int(on_device), bl, proofs,
+                                                  pubs, stride, st, ctypes.byref(err))
+            if rc and not any(st[i] for i in range(count)):  # argument errors, before any proof
+                _check(rc, err)
+            statuses[:] = [st[i] for i in range(count)]
         P, Q = bytes(proofs), bytes(pubs)
         return [(P[i * PROOF_BYTES:(i + 1) * PROOF_BYTES], Q[i * stride:i * stride + 32 * self.n_public])
                 for i in range(count)]

@@ -47,3 +47,26 @@ def test_full_pipeline_proofs_verify_with_pairing():
     bad = bytearray(res[0][0])
     bad[-1] ^= 1
     assert not nzcb.verify(ctx.vk, bytes(bad), res[0][1])
+
+
+def test_batch_reports_failed_proofs_per_item():
+    """in a batch, a witness that breaks the circuit fails its own proof
+    only (nzcb_prove_batch_status); the plain batch call raises snarkjs's error."""
+    import nzcb
+    ctx, wtns = nzcb.synth_context(10, 3, 8, seed=9, tau=0x1234567)
+    nwit = (len(wtns) - 76) // 32
+    wit = wtns[76:76 + 32 * nwit]
+    bad = bytearray(wit)
+    bad[32 * (nwit - 1)] ^= 1
+    bad = bytes(bad)
+    ctx.set_lanes(2)
+    st = []
+    res = ctx.prove_batch_raw([wit, bad, wit, bad, wit], blindings=[nzcb.random_blinding() for _ in range(5)],
+                              statuses=st)
+    assert [s != 0 for s in st] == [False, True, False, True, False]
+    assert st[1] == st[3] == 7  # NZCB_ERR_T_DIV
+    assert res[1][0] == bytes(nzcb.PROOF_BYTES) and res[3][1] == bytes(len(res[3][1]))
+    for i in (0, 2, 4):
+        assert nzcb.verify(ctx.vk, res[i][0], res[i][1])
+    with pytest.raises(nzcb.NzcbError, match="T Polynomial is not divisible"):
+        ctx.prove_batch_raw([wit, bad])
