@@ -14,6 +14,7 @@
 //   * Z grand product  -> chunked batch inversion + exclusive prefix-product scan
 //   * divPol1          -> suffix linear-recurrence scan y_i = x_i + d*y_{i+1}
 //   * evalPol (Horner) -> chunked Horner * x^(chunk start) + tree sum
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include "prover.h"
 #include "transcript.h"
 
@@ -819,6 +820,24 @@ void Prover::div_pol1(const Fr* src, size_t m, const Fr& d, const Fr& p0_adjust,
 // ----------------------------------------------------------------------------
 // prove
 // ----------------------------------------------------------------------------
+// roctx ranges for rocprofv3 --marker-trace (SURVEY.md §5 tracing): "plonk_prove" around
+// a proof and one range per phase inside it; exception-safe (the destructor pops).
+namespace {
+struct RoctxPhases {
+  bool open = false;
+  explicit RoctxPhases(const char* proof) { roctxRangePush(proof); }
+  void next(const char* phase) {
+    if (open) roctxRangePop();
+    roctxRangePush(phase);
+    open = true;
+  }
+  ~RoctxPhases() {
+    if (open) roctxRangePop();
+    roctxRangePop();
+  }
+};
+}  // namespace
+
 void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blinding, uint8_t* proof_out,
                    uint8_t* pub_out, bool witness_on_device) {
   if (n_witness != nWit) {
@@ -829,6 +848,8 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   NZ_HIP(hipSetDevice(eng->device));
   hipStream_t s = st();
   msm_ms = ntt_ms = 0;
+  RoctxPhases ranges("plonk_prove");
+  ranges.next("witness: calculateAdditions + buildABC");
   auto T0 = std::chrono::steady_clock::now();
   auto lg = [&](const std::string& m) { if (log) log(m); };
   // blinding scalars b1..b11 (Montgomery); index 0 unused
@@ -859,6 +880,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   tm[1] = ms_since(T0);
 
   // ---------------- round 1 ----------------
+  ranges.next("round1: to4T + commit A, B, C");
   auto t1 = std::chrono::steady_clock::now();
   G1Affine pA, pB, pC, pZ, pT1, pT2, pT3, pWxi, pWxiw;
   {
@@ -879,6 +901,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   tm[2] = ms_since(t1);
 
   // ---------------- round 2 ----------------
+  ranges.next("round2: grand product Z + commit");
   auto t2 = std::chrono::steady_clock::now();
   Fr beta, gamma;
   std::vector<Fr> Apub(nPublic);
@@ -930,6 +953,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   tm[3] = ms_since(t2);
 
   // ---------------- round 3 ----------------
+  ranges.next("round3: quotient t + commit T1, T2, T3");
   auto t3 = std::chrono::steady_clock::now();
   Fr alpha;
   {
@@ -990,6 +1014,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   tm[4] = ms_since(t3);
 
   // ---------------- round 4 ----------------
+  ranges.next("round4: evaluations");
   auto t4 = std::chrono::steady_clock::now();
   Fr xi, ea, eb, ec, es1, es2, et, ezw, er, xim;
   {
@@ -1025,6 +1050,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   tm[5] = ms_since(t4);
 
   // ---------------- round 5 ----------------
+  ranges.next("round5: Wxi, Wxiw + commit");
   auto t5 = std::chrono::steady_clock::now();
   {
     std::vector<uint8_t> tr(7 * 32);
