@@ -99,7 +99,7 @@ def cpu_baseline_sample(power: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--power", type=int, default=21, help="log2 PLONK domain (nzcp_live: 21)")
     ap.add_argument("--lanes", type=int, default=5, help="proofs in flight per GPU")
