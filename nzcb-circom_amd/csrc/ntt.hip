@@ -19,6 +19,7 @@
 // twiddles), and stage 0's unit twiddles are skipped.
 #include "ntt.h"
 
+#include <cstdlib>
 #include <vector>
 
 namespace nzcb {
@@ -107,7 +108,7 @@ void NttTables::init(int L, hipStream_t st) {
 // One pass: stages [s, s+q) on tiles of (2^q rows) x (2^logC columns).
 __global__ void __launch_bounds__(kNttThreads)
 ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s, int q, int logC, int first,
-                F29 scale29, int do_scale, int last, NttIo io) {
+                F29 scale29, int do_scale, int last, NttIo io, int sparse4) {
   extern __shared__ Fr tile[];
   const int C = 1 << logC;
   const int rows = 1 << q;
@@ -141,7 +142,17 @@ ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s,
   __syncthreads();
   const int nbf = n_el >> 1;
   int st = 0;
-  if (q & 1) {  // odd stage count: one radix-2 stage, then radix-4 pairs of stages
+  if (sparse4 && blockIdx.x != 0) {
+    // zero-padded input (only the first N/4 entries nonzero, past tile 0): of every four
+    // bit-reversed rows 4m..4m+3 only row 4m is nonzero, and stages 0-1 map (x, 0, 0, 0)
+    // to (x, x, x, x) whatever the twiddles, so the first radix-4 step is a copy
+    for (int e = tid; e < n_el; e += kNttThreads) {
+      const int j = e >> logC;
+      if (j & 3) tile[e] = tile[((j & ~3) << logC) + (e & (C - 1))];
+    }
+    __syncthreads();
+    st = 2;
+  } else if (q & 1) {  // odd stage count: one radix-2 stage, then radix-4 pairs of stages
     const int g = s;
     const F29* __restrict__ twg = tw + (((size_t)1 << g) - 1);
 #pragma unroll
@@ -240,7 +251,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   const F29 sc29 = split29(sc);
   if (L == 0) {
     hipLaunchKernelGGL(ntt_pass_kernel, dim3(1), dim3(kNttThreads), sizeof(Fr), st, in, out, tw, 0, 0, 0, 0, 1, sc29,
-                       do_scale, 1, io);
+                       do_scale, 1, io, 0);
     NZ_HIP(hipGetLastError());
     return;
   }
@@ -250,8 +261,16 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   while ((1 << (logC1 + 1)) <= cols && ((1 << (q1 + logC1 + 1)) <= kTileElems)) logC1++;
   size_t tiles = (size_t)cols >> logC1;
   size_t lds = (size_t(1) << (q1 + logC1)) * sizeof(Fr);
+  // inputs nonzero only below N/4 (+ a few in tile 0's columns: the blinding terms):
+  // tiles past the first skip stages 0-1 (a 4n coset NTT of an n+3-term polynomial)
+  static const bool sparse_ok = [] {  // NZCB_NTT_SPARSE=0 disables (A/B measurements)
+    const char* e = std::getenv("NZCB_NTT_SPARSE");
+    return !(e && e[0] == '0');
+  }();
+  const int sparse4 = sparse_ok && L >= 2 && q1 >= 2 && !(q1 & 1) &&
+                      io.in_len <= ((size_t)1 << (L - 2)) + ((size_t)1 << logC1);
   hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)tiles), dim3(kNttThreads), lds, st, in, out, tw, L, 0, q1, logC1,
-                     1, sc29, do_scale, q1 == L ? 1 : 0, io);
+                     1, sc29, do_scale, q1 == L ? 1 : 0, io, sparse4);
   NZ_HIP(hipGetLastError());
   int s = q1;
   while (s < L) {
@@ -261,7 +280,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
     size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
     size_t lds2 = (size_t(1) << (q + logC)) * sizeof(Fr);
     hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)ntiles), dim3(kNttThreads), lds2, st, out, out, tw, L, s, q,
-                       logC, 0, sc29, 0, s + q == L ? 1 : 0, io);
+                       logC, 0, sc29, 0, s + q == L ? 1 : 0, io, 0);
     NZ_HIP(hipGetLastError());
     s += q;
   }
