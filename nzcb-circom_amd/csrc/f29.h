@@ -328,6 +328,35 @@ NZ_HD Fr mul_fr29(const Fr& a, const F29& w29) {
   return join_fr29(mul29<Fr29>(split29(a), w29));  // product < 2r, limbs < 2^29
 }
 
+// a * 2^-256 mod r: Montgomery-256 Fr -> canonical normal form (the MSM's scalars), as
+// mul29<Fr29>(split29(a), 32) with the single-term product columns a_i * 32 (81
+// reduction mads instead of field.h's 8x32 product by 1)
+NZ_HD Fr from_mont_fr29(const Fr& a) {
+  using Q = Fr29;
+  const F29 x = split29(a);
+  uint32_t m[9];
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    acc += (uint64_t)x.v[i] << 5;
+#pragma unroll
+    for (int j = 0; j < i; j++) mad29c(acc, m[j], Q::P[i - j]);
+    m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
+    mad29c(acc, m[i], Q::P[0]);
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int i = 9; i < 17; i++) {
+#pragma unroll
+    for (int j = i - 8; j < 9; j++) mad29c(acc, m[j], Q::P[i - j]);
+    r.v[i - 9] = (uint32_t)acc & Q::MASK;
+    acc >>= 29;
+  }
+  r.v[8] = (uint32_t)acc;
+  return join_fr29(r);
+}
+
 // Montgomery-261 value (any F29 < 2^257) -> canonical Montgomery-256 Fq (csrc/field.h)
 NZ_HD Fq to_fq256(const F29& x) { return reduce_once(join29(mul29(x, f29_const(Fq29::C256)))); }
 

@@ -195,7 +195,7 @@ msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t strid
   constexpr uint32_t SENTINEL = K16 ? 0u : FIXED ? NB : NW * NB;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     Fr s = scalars[i];
-    if (mont) s = from_mont(s);
+    if (mont) s = from_mont_fr29(s);
     uint32_t k[NW];
     uint32_t v[NW];
 #pragma unroll
@@ -394,6 +394,8 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
 // and the one after it, or copies the last entry of an odd run. Coordinates stay
 // canonical Montgomery-261 (so the table's x == x' test finds doublings and P + (-P));
 // infinity is (0, 0) as in the table.
+// Opt-in (NZCB_PAIR_ROUNDS, nzcb_msm_set_pair_rounds): measured slower than the XYZZ
+// accumulation alone at 2^21 (tried and dropped), kept parity-tested.
 
 enum : uint32_t { kPairAdd = 0, kPairDbl = 1, kPairCopyA = 2, kPairCopyB = 3, kPairInf = 4 };
 
