@@ -121,3 +121,49 @@ def test_plonk_setup_errors():
         nzcb.plonk_setup(bytes(bad), _ptau(9))
     with pytest.raises(nzcb.NzcbError, match="invalid file format"):
         nzcb.plonk_setup(b"junk" + data[4:], _ptau(9))
+
+
+@pytest.mark.gpu
+def test_plonk_setup_larger_circuit_proves_and_verifies():
+    """A 2^15-domain r1cs (5000 constraints folded into about 18.9k PLONK gates) against a
+    2^15 ptau whose tauG1 points come from the GPU fixed-base kernel: the zkey proves
+    and the pairing verifier accepts (size-independent check of the setup's
+    commitments), and the proof equals the C oracle prover's on the same zkey."""
+    import nzcb
+    import struct
+    from oracle import bn254 as bn, cbind, synth
+    from oracle.binfmt import write_binfile
+    power = 15
+    cnt = (1 << (power + 1)) - 1
+    scal = bytearray()
+    t = 1
+    for _ in range(cnt):
+        scal += bn.to_lem(t, R_MOD)
+        t = t * TAU % R_MOD
+    eng = nzcb.Engine(0, max_log_ntt=-1, max_msm_points=0)
+    ds, dp = nzcb.dev_alloc(len(scal)), nzcb.dev_alloc(64 * cnt)
+    try:
+        nzcb.h2d(ds, bytes(scal))
+        eng.fixed_base(ds, cnt, dp)
+        g1 = nzcb.d2h(dp, 64 * cnt)
+    finally:
+        nzcb.dev_free(ds)
+        nzcb.dev_free(dp)
+        eng.close()
+    assert bn.g1_from_lem(g1[64:128]) == bn.g1_mul(bn.G1_GEN, TAU)
+    s1 = struct.pack("<I", 32) + bn.to_le(bn.P_MOD) + struct.pack("<II", power, power)
+    g2 = bn.g2_to_lem(bn.G2_GEN) + bn.g2_to_lem(bn.g2_mul(bn.G2_GEN, TAU))
+    ptau = write_binfile(b"ptau", 1, [(1, s1), (2, g1), (3, g2)])
+    data, w = r1cs.random_r1cs(77, n_out=3, n_pub_in=1, n_prv_in=6, n_steps=5000)
+    zkey = nzcb.plonk_setup(data, ptau)
+    wtns = binfmt.write_wtns(w)
+    bl = b"".join(x.to_bytes(32, "little") for x in synth.fixed_blindings())
+    ctx = nzcb.ProverContext(zkey)
+    try:
+        assert ctx.domain_size == 1 << 15
+        proof, pub = ctx.prove_raw(wtns, bl)
+        assert nzcb.verify(ctx.vk, proof, pub)
+    finally:
+        ctx.close()
+    ref_proof, ref_pub, _ = cbind.prove(zkey, wtns, bl)
+    assert proof == ref_proof and pub == ref_pub[:len(pub)]
