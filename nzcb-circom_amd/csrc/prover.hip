@@ -86,7 +86,15 @@ __device__ __forceinline__ Fr root4(const Fr* __restrict__ lo, const Fr* __restr
 
 struct PermArgs {
   Fr beta, gamma, k1, k2;
+  F29 beta29, k1beta29, k2beta29;  // beta, k1 beta, k2 beta as mul_fr29 operands
 };
+
+// c * 2^5 split into the 9x29 radix: the Montgomery-261 operand of mul_fr29 for a
+// Montgomery-256 constant c
+static F29 fr29_operand(Fr c) {
+  for (int k = 0; k < 5; k++) c = c + c;
+  return split29(c);
+}
 
 // Round 2: num_i / den_i with chunked Montgomery batch inversion.
 __global__ void __launch_bounds__(kT)
@@ -103,12 +111,11 @@ k_perm_ratio(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __res
   Fr pre = Fr::one();
   for (size_t i = s; i < e; i++) {
     Fr w = root4(rlo, rhi, 4 * i);
-    Fr bw = pa.beta * w;
     Fr a = A[i], b = B[i], c = C[i];
-    Fr num = (a + bw + pa.gamma) * (b + pa.k1 * bw + pa.gamma);
-    num = num * (c + pa.k2 * bw + pa.gamma);
-    Fr den = (a + pa.beta * s1[4 * i] + pa.gamma) * (b + pa.beta * s2[4 * i] + pa.gamma);
-    den = den * (c + pa.beta * s3[4 * i] + pa.gamma);
+    Fr num = (a + mul_fr29(w, pa.beta29) + pa.gamma) * (b + mul_fr29(w, pa.k1beta29) + pa.gamma);
+    num = num * (c + mul_fr29(w, pa.k2beta29) + pa.gamma);
+    Fr den = (a + mul_fr29(s1[4 * i], pa.beta29) + pa.gamma) * (b + mul_fr29(s2[4 * i], pa.beta29) + pa.gamma);
+    den = den * (c + mul_fr29(s3[4 * i], pa.beta29) + pa.gamma);
     ratio[i] = num;
     den_s[i] = den;
     pre = pre * den;
@@ -931,7 +938,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     lg("gamma: " + fr_dec(gamma));
   }
   {
-    PermArgs pa{beta, gamma, k1, k2};
+    PermArgs pa{beta, gamma, k1, k2, fr29_operand(beta), fr29_operand(k1 * beta), fr29_operand(k2 * beta)};
     size_t nchunks = (n + kScanChunk - 1) / kScanChunk;
     hipLaunchKernelGGL(k_perm_ratio, dim3(grid_for(nchunks, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, sigma.p,
                        (size_t)n, root_lo.p, root_hi.p, pa, Z.p, T.p, Tz.p);
