@@ -47,11 +47,17 @@ PROOF_BYTES_PER_N = 7104       # algorithmic bytes per proof = 7
 NZCP_INPUTS = 2970             # nzcp_live input signals (toBeSigned bits + len + data)
 SEED = 0x6E7A6362
 TAU = 0x6E7A6362746175
-# The accumulation's Fq products are 9x29-bit Montgomery products: an XYZZ mixed
-# addition (10 products) issues 1467 v_mad_u64_u32 (ISA count of the common path,
-# 146.7 per product) at 4.9 SIMD-cycles each (profiles/r1_isa_bench.txt); 1024 SIMDs
-# at ~2.0 GHz under load: 1024 * 2.0e9 * 64 / (146.7 * 4.9) = 182 G products/s.
-VALU_MULT_BOUND_GS = 182.0
+# The dominant kernel (fixed-base bucket accumulation) is bound by VALU integer
+# multiply issue, not by HBM (SURVEY.md §8d "Bounding roofline"). Its algorithmic
+# work is the 9x29-bit Montgomery products of one XYZZ mixed addition per bucket
+# entry: 1467 v_mad_u64_u32 per entry (ISA count of the common path).
+MADS_PER_ENTRY = 1467
+# Peak: MI355X_MICROARCH.md chip table (256 CUs x 4 SIMDs, 2400 MHz max clock; FP32
+# vector peak 157.3 TFLOPS = v_fma_f32 issuing one wave64 instruction per 2 cycles per
+# SIMD). v_mad_u64_u32 issues at 5.00 / 2.60 = 1.92x the v_fma_f32 cost in the same
+# harness (profiles/r1_isa_bench.txt), so the chip issues at most
+# 1024 * 2.4e9 / (2 * 1.923) wave-mads/s x 64 lanes = 40.9 T lane-mads/s.
+MAD_PEAK_T = 1024 * 2.4e9 / (2 * 5.00 / 2.60) * 64 / 1e12
 
 
 def blinding_for(step: int) -> bytes:
@@ -81,13 +87,38 @@ def max_over_ranks(x: float, dist, device) -> float:
     return float(t.item())
 
 
+def pass_data(i: int) -> bytes:
+    """The 20 pass-through data bytes of proof i."""
+    return hashlib.sha256(b"nzcb-pass" + i.to_bytes(4, "little")).digest()[:20]
+
+
 def pass_inputs(indices) -> bytes:
     """nzcp_live input signals of distinct live-shaped passes: one ToBeSigned, the 20
-    pass-through data bytes derived from the proof index (SURVEY.md §8d config 4)."""
+    pass-through data bytes derived from the proof index."""
     from nzcb import nzcp
     tbs = nzcp.pass_tbs(live=True)
-    return b"".join(nzcp.input_signals(nzcp.circuit_input(
-        tbs, hashlib.sha256(b"nzcb-pass" + i.to_bytes(4, "little")).digest()[:20])) for i in indices)
+    return b"".join(nzcp.input_signals(nzcp.circuit_input(tbs, pass_data(i))) for i in indices)
+
+
+def accumulate_probe(n_points: int, device: int, reps: int = 10) -> dict:
+    """The dominant kernel alone on the chip: `reps` fixed-base MSMs of the prover's size
+    (n + 6 points, random scalars, the same c = 17 table schedule) with HIP events around
+    each phase on the engine's stream (msm.hip MsmScratch::prof). Run after the timed
+    region; its accumulation launches are the last `reps` of the rocprofv3 trace."""
+    import nzcb
+    eng = nzcb.Engine(device, max_log_ntt=-1, max_msm_points=n_points + 8)
+    sc, bases = nzcb.dev_alloc(n_points * 32), nzcb.dev_alloc(n_points * 64)
+    try:
+        eng.random_fr(sc, n_points, 0x70726F6265)
+        eng.fixed_base(sc, n_points, bases)
+        eng.random_fr(sc, n_points, 0x5CA1A25)
+        eng.time_msm_phases(bases, sc, n_points, True, True, 1)   # warm (table build, code load)
+        ph = eng.time_msm_phases(bases, sc, n_points, True, True, reps)
+    finally:
+        nzcb.dev_free(sc)
+        nzcb.dev_free(bases)
+        eng.close()
+    return ph
 
 
 def cpu_baseline_sample(power: int):
@@ -109,6 +140,7 @@ def main():
                     help="configs[4] single-proof mode: split each MSM over these device ids, e.g. 0,1,2,3 "
                          "(one process; lanes forced to 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the isolated accumulation-kernel probe")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -191,6 +223,7 @@ def main():
     t_w = time.perf_counter()
     prover.witness_staged(len(mine))
     nzcp_ms = (time.perf_counter() - t_w) * 1e3
+    probe = accumulate_probe(n + 6, device) if rank == 0 and not args.no_probe else None
     elapsed = max_over_ranks(elapsed, dist, f"cuda:{device}" if backend == "nccl" else "cpu")
     total_proofs = args.batch if args.batch else args.steps * world
     steps = len(shard(args.batch, 0, world)) if args.batch else args.steps
@@ -198,12 +231,17 @@ def main():
     ms_step = elapsed / steps * 1e3
 
     if rank == 0:
-        avg_launch_ms = kms / max(klaunch, 1)
+        # the accumulation kernel over the timed region (HIP events on the MSM streams;
+        # --lanes proofs share the chip, so these launches overlap other kernels)
+        shared_ms = kms / max(klaunch, 1)
         pts_per_launch = kpoints / max(klaunch, 1)
         ent_per_launch = kentries / max(klaunch, 1)
-        achieved = MSM_BYTES_PER_POINT * pts_per_launch / (avg_launch_ms / 1e3) / 1e9 if avg_launch_ms else 0.0
-        # VALU view of the same kernel: 10 Fq Montgomery products per XYZZ mixed addition
-        mults_per_s = 10 * ent_per_launch / (avg_launch_ms / 1e3) if avg_launch_ms else 0.0
+        # the same kernel alone on the chip, same size and schedule: its duration is the
+        # roofline's launch time (profiles/: the last 10 accumulation launches of the trace)
+        iso_ms = probe["accumulate"] if probe else None
+        launch_ms = iso_ms or shared_ms
+        mads_t = MADS_PER_ENTRY * ent_per_launch / (launch_ms / 1e3) / 1e12 if launch_ms else 0.0
+        hbm_gbs = MSM_BYTES_PER_POINT * pts_per_launch / (launch_ms / 1e3) / 1e9 if launch_ms else 0.0
         traffic = None
         tf = os.environ.get("NZCB_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "accumulate_traffic.json"))
         if tf and os.path.exists(tf):
@@ -227,10 +265,11 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if args.batch else "weak",
             "vs_baseline": None,
-            "dtype": "u32x8 Montgomery (BN254 Fr/Fq)",
+            "dtype": "u32 limbs: BN254 Fr/Fq Montgomery, 8x32-bit and 9x29-bit (MSM, NTT twiddles, quotient)",
             "data": "synthetic: seeded satisfied PLONK circuit with free public wires, snarkjs-0.4 zkey with trapdoor "
                     "tau (SURVEY §8d cfg 3); public signals = nzcp witness kernel outputs of distinct live-shaped "
-                    "passes (data bytes vary per proof)",
+                    "passes (data bytes vary per proof). The synthetic circuit does not constrain its public "
+                    "signals to the pass: the host checks them against the witness records",
             "config": {
                 "workload": f"nzcp_live fullProve (GPU nzcp witness -> witness[1..3], PLONK proof), "
                             f"n=2^{args.power}, nPublic=3, {NZCP_INPUTS} inputs",
@@ -246,24 +285,28 @@ def main():
                 "msm_devices": msm_devices or None,
             },
             "roofline": {
-                "kernel": "msm_accumulate29_kernel (fixed-base Pippenger bucket accumulation)",
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "kernel": "msm_accumulate29_kernel (fixed-base Pippenger bucket accumulation, c=17, 2^21+6 points)",
+                # VALU integer-multiply issue governs this kernel; the contract's
+                # hbm/mfma vocabulary has no word for it, and there is no MFMA in modular arithmetic
+                "bound": "valu",
+                "achieved": round(mads_t, 3),
+                "peak": round(MAD_PEAK_T, 2),
+                "unit": "T v_mad_u64_u32 lane-ops/s",
+                "frac": round(mads_t / MAD_PEAK_T, 4),
                 "traffic": traffic,
-                "avg_launch_ms": round(avg_launch_ms, 4),
-                # the timed batch keeps --lanes proofs in flight, so a launch shares the chip;
-                # the same kernel during the single-proof latency run (one proof in flight):
+                "avg_launch_ms": round(launch_ms, 4),
+                "launch_ms_basis": "isolated launches (accumulate_probe, HIP events)" if iso_ms
+                                   else "timed region, shared chip (probe skipped)",
+                "timed_region_avg_launch_ms": round(shared_ms, 4),
                 "single_proof_avg_launch_ms": round(lat_kms / max(lat_klaunch, 1), 4),
-                "launches": int(klaunch),
+                "launches_timed": int(klaunch),
                 "points_per_launch": int(pts_per_launch),
-                "bytes_per_point": MSM_BYTES_PER_POINT,
                 "bucket_entries_per_launch": int(ent_per_launch),
-                "valu": {"fq_mont_mul_per_s": round(mults_per_s / 1e9, 2), "unit": "G/s",
-                         "bound_mad_f29": VALU_MULT_BOUND_GS,
-                         "frac": round(mults_per_s / 1e9 / VALU_MULT_BOUND_GS, 4)},
+                "mads_per_entry": MADS_PER_ENTRY,
+                "hbm": {"algorithmic_bytes_per_launch": int(MSM_BYTES_PER_POINT * pts_per_launch),
+                        "bytes_per_point": MSM_BYTES_PER_POINT, "achieved_GBs": round(hbm_gbs, 2),
+                        "peak_GBs": HBM_PEAK_GBS, "frac": round(hbm_gbs / HBM_PEAK_GBS, 5)},
+                "probe_phase_ms": {k: round(v, 4) for k, v in probe.items()} if probe else None,
             },
             "proof_roofline": {
                 "algorithmic_bytes": PROOF_BYTES_PER_N * n,
@@ -278,7 +321,13 @@ def main():
             "setup_s": round(setup_s, 2),
             "cpu_baseline": cpu,
         }
+        if not verified:  # never report a rate for proofs that do not verify
+            line["value"] = None
+            line["error"] = "proofs_verified is false: public signals differ from the nzcp records or a proof " \
+                            "failed the pairing check"
         print(json.dumps(line), flush=True)
+        if not verified:
+            sys.exit(3)
     nzcb.dev_free(dev_w)
     ctx.close()
     if dist is not None:

@@ -17,9 +17,10 @@
  *                 (infinity = 64 zero bytes), then 7 Fr evaluations
  *                 (eval_a,eval_b,eval_c,eval_s1,eval_s2,eval_zw,eval_r), 32 B LE each.
  *   public      : nPublic x 32-byte LE Fr (= witness[1..nPublic]).
- *   blinding    : 11 x 32-byte LE Fr (b1..b11) or NULL = all zero (deterministic).
- *                 snarkjs draws them with Fr.random(); pass random bytes for
- *                 zero-knowledge, fixed bytes for bit-exact tests.
+ *   blinding    : 11 x 32-byte LE Fr (b1..b11), or NULL = drawn uniformly from the
+ *                 OS CSPRNG per proof, as snarkjs's Fr.random() (zero-knowledge).
+ *                 Fixed bytes (352 zero bytes included) give reproducible,
+ *                 bit-exact proofs for tests; zero blinding is NOT zero-knowledge.
  */
 #ifndef NZCB_H
 #define NZCB_H

@@ -19,6 +19,7 @@
 #include "transcript.h"
 
 #include <cstring>
+#include <sys/random.h>
 
 #include "keccak.h"
 
@@ -845,6 +846,25 @@ struct RoctxPhases {
 };
 }  // namespace
 
+namespace {
+// uniform in [0, r): 254-bit draws from getrandom(2), rejected when >= r
+Fr random_fr() {
+  for (;;) {
+    uint8_t b[32];
+    size_t got = 0;
+    while (got < sizeof(b)) {
+      ssize_t k = getrandom(b + got, sizeof(b) - got, 0);
+      if (k < 0) throw Error(NZCB_ERR_ARG, "getrandom failed: no entropy for the blinding scalars");
+      got += (size_t)k;
+    }
+    b[31] &= 0x3f;
+    Fr x;
+    std::memcpy(x.v, b, 32);
+    if (reduce_once(x) == x) return to_mont(x);
+  }
+}
+}  // namespace
+
 void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blinding, uint8_t* proof_out,
                    uint8_t* pub_out, bool witness_on_device) {
   if (n_witness != nWit) {
@@ -862,7 +882,10 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   // blinding scalars b1..b11 (Montgomery); index 0 unused
   Fr bl[12];
   bl[0] = Fr::zero();
-  for (int i = 1; i <= 11; i++) bl[i] = blinding ? fr_from_le_normal(blinding + 32 * (i - 1)) : Fr::zero();
+  // NULL blinding: uniform scalars from the OS CSPRNG, as snarkjs's Fr.random() (a proof
+  // with zero blinding is not zero-knowledge); callers that want a reproducible proof pass
+  // explicit bytes (all zero included)
+  for (int i = 1; i <= 11; i++) bl[i] = blinding ? fr_from_le_normal(blinding + 32 * (i - 1)) : random_fr();
   NZ_HIP(hipMemcpyAsync(blind.p, bl, sizeof(bl), hipMemcpyHostToDevice, s));
   NZ_HIP(hipMemsetAsync(flags.p, 0, sizeof(uint32_t), s));
 

@@ -416,7 +416,9 @@ class ProverContext:
     __del__ = close
 
     def prove_raw(self, wtns, blinding: bytes | None = None):
-        """Returns (proof_bytes, public_bytes) in the C-ABI layout."""
+        """Returns (proof_bytes, public_bytes) in the C-ABI layout. blinding None draws
+        random scalars (snarkjs Fr.random(), zero-knowledge); pass fixed bytes, e.g.
+        bytes(352), only for reproducible test proofs."""
         data = _read(wtns)
         proof = _out(PROOF_BYTES)
         pub = _out(32 * self.n_public)
@@ -484,7 +486,8 @@ class ProverContext:
                     n_witness = len(w) // 32
         bl = None
         if blindings is not None:
-            bl = _buf(b"".join(x if x is not None else bytes(352) for x in blindings))
+            # an item without blinding gets fresh random scalars (snarkjs Fr.random()), never zeros
+            bl = _buf(b"".join(x if x is not None else random_blinding() for x in blindings))
         proofs = _out(PROOF_BYTES * count)
         stride = 32 * max(self.n_public, 1)
         pubs = _out(stride * count)

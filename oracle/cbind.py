@@ -39,8 +39,21 @@ def _buf(b: bytes):
 
 
 def default_threads() -> int:
-    n = os.cpu_count() or 1
-    return max(1, min(16, n))   # the GPU box's CPU share is 16 cores per GPU
+    """Every core this process may use: the CPU affinity set, capped by OMP_NUM_THREADS
+    when the host exports it (the GPU box shows the whole machine in nproc / affinity but
+    leases 16 cores per GPU and exports OMP_NUM_THREADS=16 to say so)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def threads_reason(th: int) -> str:
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) == th:
+        return f"{th} threads = the lease's CPU share (OMP_NUM_THREADS={omp})"
+    return f"{th} threads = every core in the process's CPU affinity set"
 
 
 def prove(zkey, wtns, blinding: bytes | None = None, transcript_pub: bool = True,
@@ -91,5 +104,5 @@ def timed_sample(power: int, threads: int | None = None):
         nzcb.free_raw(raw)
     wall = time.time() - t0
     return {"value": round(1.0 / wall, 5), "unit": "proofs/s", "cores": th, "kind": "port",
-            "sample": f"1 full proof, n=2^{power} synthetic nzcp_live, oracle/c/nzcb_ref.c on {th} threads "
+            "sample": f"1 full proof, n=2^{power} synthetic nzcp_live, oracle/c/nzcb_ref.c on {threads_reason(th)} "
                       f"({wall:.1f} s; msm {t['msm']:.1f} s, ntt {t['ntt']:.1f} s)"}

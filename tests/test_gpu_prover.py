@@ -33,7 +33,7 @@ def test_golden_proof_bits(name, bl):
     meta, zkey, wtns = _gold(name)
     exp = meta["proofs"][bl]
     ctx = nzcb.ProverContext(zkey)
-    blinding = bytes.fromhex(exp["blinding"]) if exp["blinding"] else None
+    blinding = bytes.fromhex(exp["blinding"]) if exp["blinding"] else bytes(352)  # explicit zero blinding
     proof, pub = ctx.prove_raw(wtns, blinding)
     assert proof.hex() == exp["proof_bin"]
     res = ctx.prove(wtns, blinding)
@@ -210,7 +210,7 @@ def test_msm_split_over_devices_bit_exact(devices):
     ctx.set_msm_devices(devices)
     for bl in ("fixed", "zero"):
         exp = meta["proofs"][bl]
-        blinding = bytes.fromhex(exp["blinding"]) if exp["blinding"] else None
+        blinding = bytes.fromhex(exp["blinding"]) if exp["blinding"] else bytes(352)  # explicit zero blinding
         proof, _ = ctx.prove_raw(wtns, blinding)
         assert proof.hex() == exp["proof_bin"]
     ctx.set_msm_devices([0])
