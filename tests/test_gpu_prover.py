@@ -168,7 +168,7 @@ def test_batch_lanes_bit_exact():
     ctx.set_lanes(3)
     assert ctx.lanes == 3
     kinds = ["fixed", "zero", "fixed", "fixed", "zero", "zero", "fixed"]
-    bls = [bytes.fromhex(meta["proofs"][k]["blinding"]) if meta["proofs"][k]["blinding"] else None for k in kinds]
+    bls = [bytes.fromhex(meta["proofs"][k]["blinding"]) if meta["proofs"][k]["blinding"] else bytes(352) for k in kinds]
     res = ctx.prove_batch_raw([wit] * len(kinds), blindings=bls)
     for k, (proof, pub) in zip(kinds, res):
         assert proof.hex() == meta["proofs"][k]["proof_bin"]
