@@ -222,6 +222,31 @@ int nzcb_nzcp_witness_dev(int device, const nzcb_nzcp_params* prm, const void* d
 int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints,
                      const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len, uint8_t** wtns_out,
                      size_t* wtns_len, nzcb_err* err);
+/* ---- Witness programs: the circom witness calculator on the GPU ------------------
+ * Replaces circom_runtime's calculateWitness / snarkjs wtns_calculate (circom_runtime
+ * 0.1.17, /root/reference/yarn.lock:2496) for circuits
+ * compiled by nzcb-circom_amd/nzcb/circuit.py (nzcp_live = NZCPPubIdentity(1, 351, 0, 4,
+ * 2, 4), nzcb/nzcpgen.py). The program (format: csrc/wvm.hip) is uploaded once; each
+ * run computes `count` full witnesses, one workgroup each.
+ *   inputs : count x (n_pub_in + n_prv_in) x 32-byte LE field elements, the main's
+ *            input signals in declaration order (as nzcb_nzcp_input_signals for nzcp)
+ *   witness: witness i at dev_witness + i * witness_stride: n_wires x 32-byte LE normal
+ *            form (wire 0 = 1, outputs, inputs, intermediate signals), the wtns order
+ *            that nzcb_prove_device / nzcb_prove_batch take
+ *   status : per witness, 0 or the failure code of the first failing check in circuit
+ *            order (nzcp: NZCB_NZCP_* codes), as circom's calculator throws */
+typedef struct nzcb_wprog nzcb_wprog;
+nzcb_wprog* nzcb_wprog_create(const uint8_t* prog, size_t len, int device, nzcb_err* err);
+void nzcb_wprog_destroy(nzcb_wprog* prog);
+/* info: n_wires, n_outputs, n_pub_inputs, n_prv_inputs, n_levels */
+int nzcb_wprog_info(const nzcb_wprog* prog, uint32_t info[5]);
+/* Device buffers; stream may be NULL; returns after the statuses are on the host. */
+int nzcb_wprog_run_dev(nzcb_wprog* prog, const void* dev_inputs, int count, void* dev_witness,
+                       size_t witness_stride, int32_t* status_out, void* stream, nzcb_err* err);
+/* Host buffers: witness_out receives count x n_wires x 32 bytes. */
+int nzcb_wprog_run(nzcb_wprog* prog, const uint8_t* inputs, int count, uint8_t* witness_out,
+                   int32_t* status_out, nzcb_err* err);
+
 /* Same with flags: NZCB_SYNTH_FREE_PUBLIC keeps the public signals off every gate but
  * their public-input gate, so any public values satisfy the circuit. The bench's
  * fullProve pipeline writes the nzcp outputs of each pass there (nzcb_nzcp_witness_dev). */
@@ -235,6 +260,11 @@ int nzcb_synth_setup_ex(int power, int n_public, int n_inputs, uint64_t seed, ui
  * tauG2 (section 3); NTTs and commitments run on `device`. */
 int nzcb_plonk_setup(const uint8_t* r1cs, size_t r1cs_len, const uint8_t* ptau, size_t ptau_len, int device,
                      uint8_t** zkey_out, size_t* zkey_len, nzcb_err* err);
+/* A powers-of-tau file (sections 1-3 of the snarkjs ptau layout: header, tauG1 =
+ * [tau^i]G1 for i < 2^(power+1) - 1, tauG2 = [1]G2, [tau]G2) for a trapdoor tau (32 B LE),
+ * built on `device`; malloc'ed, release with nzcb_free. The offline stand-in for
+ * powersOfTau28_hez_final_21.ptau (/root/reference/README.md:40, Makefile:60). */
+int nzcb_ptau_synth(int power, const uint8_t* tau, int device, uint8_t** ptau_out, size_t* ptau_len, nzcb_err* err);
 void nzcb_free(void* p);
 
 /* ---- Kernel-level entry points (tests / microbench) */

@@ -692,7 +692,89 @@ static void plonk_setup(const uint8_t* r1cs, size_t r1cs_len, const uint8_t* pta
   setup_zkey(rc.c, rc.power, (int)rc.n_public, src, device, zk_out, zk_len);
 }
 
+// A powers-of-tau file for a trapdoor tau (the layout `snarkjs powersoftau` writes,
+// sections 1-3, which is all `plonk setup` reads): header (n8, q, power, ceremonyPower),
+// tauG1 = [tau^i]G1 for i < 2^(power+1) - 1 (LEM affine, from the GPU fixed-base kernel)
+// and tauG2 = [1]G2, [tau]G2. Stands in for powersOfTau28_hez_final_21.ptau
+// (/root/reference/README.md:40), which is not on disk.
+static void ptau_synth(int power, const uint8_t* tau_le, int device, uint8_t** out, size_t* out_len) {
+  if (power < 1 || power > 24) throw Error(NZCB_ERR_ARG, "ptau: power must be in 1..24");
+  const size_t ng1 = ((size_t)2 << power) - 1;
+  Fr tau = Fr::zero();
+  std::memcpy(tau.v, tau_le, 32);
+  tau = reduce_once(reduce_once(tau));
+  const Fr tau_m = to_mont(tau);
+  hipStream_t st;
+  NZ_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  std::vector<uint8_t> g1(ng1 * 64);
+  try {
+    DevBuf<Fr> taupow(ng1);
+    DevBuf<G1Affine> pts(ng1);
+    hipLaunchKernelGGL(k_pow_table, dim3(grid_for(ng1, kT, 1u << 30)), dim3(kT), 0, st, taupow.p, tau_m, ng1);
+    hipLaunchKernelGGL(k_fixed_base, dim3(grid_for(ng1, kT, 1u << 30)), dim3(kT), 0, st, taupow.p, ng1, pts.p);
+    NZ_HIP(hipGetLastError());
+    NZ_HIP(hipMemcpyAsync(g1.data(), pts.p, ng1 * 64, hipMemcpyDeviceToHost, st));
+    NZ_HIP(hipStreamSynchronize(st));
+  } catch (...) {
+    (void)hipStreamDestroy(st);
+    throw;
+  }
+  (void)hipStreamDestroy(st);
+  std::vector<uint8_t> s1, s3;
+  put_u32(s1, 32);
+  put_bytes(s1, FqParams::P, 32);
+  put_u32(s1, (uint32_t)power);
+  put_u32(s1, (uint32_t)power);
+  Fr one_n = Fr::zero();
+  one_n.v[0] = 1;
+  for (const G2& q : {g2_mul_gen(one_n), g2_mul_gen(tau)}) {
+    put_bytes(s3, q.x.c0.v, 32);
+    put_bytes(s3, q.x.c1.v, 32);
+    put_bytes(s3, q.y.c0.v, 32);
+    put_bytes(s3, q.y.c1.v, 32);
+  }
+  const size_t total = 12 + 3 * 12 + s1.size() + g1.size() + s3.size();
+  uint8_t* buf = (uint8_t*)std::malloc(total);
+  if (!buf) throw Error(NZCB_ERR_INTERNAL, "out of host memory");
+  size_t o = 0;
+  auto w32 = [&](uint32_t v) { std::memcpy(buf + o, &v, 4); o += 4; };
+  auto w64 = [&](uint64_t v) { std::memcpy(buf + o, &v, 8); o += 8; };
+  std::memcpy(buf, "ptau", 4);
+  o = 4;
+  w32(1);
+  w32(3);
+  const std::vector<uint8_t>* secs[3] = {&s1, &g1, &s3};
+  for (int i = 0; i < 3; i++) {
+    w32((uint32_t)(i + 1));
+    w64(secs[i]->size());
+    std::memcpy(buf + o, secs[i]->data(), secs[i]->size());
+    o += secs[i]->size();
+  }
+  *out = buf;
+  *out_len = total;
+}
+
 }  // namespace nzcb
+
+extern "C" int nzcb_ptau_synth(int power, const uint8_t* tau, int device, uint8_t** ptau_out, size_t* ptau_len,
+                               nzcb_err* err) {
+  using namespace nzcb;
+  if (!tau || !ptau_out || !ptau_len) {
+    set_err(err, NZCB_ERR_ARG, "null argument");
+    return NZCB_ERR_ARG;
+  }
+  try {
+    NZ_HIP(hipSetDevice(device));
+    ptau_synth(power, tau, device, ptau_out, ptau_len);
+    return 0;
+  } catch (const Error& e) {
+    set_err(err, e.code, e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+    return NZCB_ERR_INTERNAL;
+  }
+}
 
 extern "C" int nzcb_synth_setup_ex(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints,
                                    uint32_t flags, const uint8_t* tau, int device, uint8_t** zkey_out,

@@ -1,0 +1,736 @@
+// Witness VM: runs a circuit's witness program (nzcb/circuit.py Circuit.write_program)
+// on the GPU, one workgroup per witness, in place of the circom wasm witness calculator
+// (circom_runtime 0.1.17, /root/reference/yarn.lock:2496; called by snarkjs
+// plonk.fullProve's wtns_calculate). For nzcp_live the program
+// is NZCPPubIdentity(1, 351, 0, 4, 2, 4) (nzcb/nzcpgen.py).
+//
+// Program format (little endian):
+//   "nzwp" u32 version n_wires n_out n_pub_in n_prv_in n_consts n_terms n_ops n_levels
+//   consts[n_consts] 32 B normal form | terms[n_terms] (u32 wire, u32 const) |
+//   ops[n_ops] 8 x u32 {type | err << 8 | n << 16, dst, a_off, a_n, b_off, b_n, c_off, c_n}
+//   level_start[n_levels + 1] u32 | level_macro_start[n_levels] u32
+// Ops are sorted by dependency level; inside a level the scalar ops (LIN MUL INV BITS
+// CHECK) come first and are spread over the workgroup's threads, the macro ops (QUIN,
+// SHA256, SHA512) follow and each runs on the whole workgroup. One barrier per level.
+//
+// Witness values live in HBM in normal form (what nzcb_prove_device reads). A linear
+// combination is evaluated in Montgomery form with coefficients pre-scaled by R^2:
+// mont_mul(w, c R^2) = (w c) R, so one product per term and one conversion per result.
+// Almost every value of this circuit is a bit, a byte or a small position, and the
+// heavy gadgets are macro ops that write their signals straight from integer state:
+//   QUIN   QuinSelector's 2n + m signals; IsZero inverses of the small integers i - index
+//          from a table of 1/1..1/kInvTable (Fermat only for a non-small index)
+//   SHA*   one compression computed by lane 0 in 32/64-bit integers, then every signal
+//          of the block (all in {0, 1, -1}) written by the workgroup
+// A failing BITS/CHECK does an atomicMin of (creation order << 8 | err) on the pass's
+// status word, so the host sees the first failure in template order, as circom throws.
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace nzcb {
+namespace wvm {
+
+constexpr int kThreads = 256;
+constexpr uint32_t kInvTable = 4096;
+constexpr uint32_t kNoWire = 0xFFFFFFFFu;
+enum { OP_LIN = 0, OP_MUL, OP_INV, OP_BITS, OP_CHECK, OP_QUIN, OP_SHA256, OP_SHA512 };
+
+struct Op {
+  uint32_t code, dst, a_off, a_n, b_off, b_n, c_off, c_n;
+};
+struct Term {
+  uint32_t wire, ci;
+};
+
+struct Prog {
+  const Fr* consts;   // coefficient * R^2 mod r
+  const Term* terms;
+  const Op* ops;
+  const uint32_t* starts;
+  const uint32_t* mstarts;
+  const Fr* inv_small;  // 1/i (normal form), i < kInvTable
+  uint32_t n_levels, n_wires, n_inputs, in_base;
+};
+
+// ---- SHA-2 block layout (nzcb/circuit.py sha_block_layout) --------------------------
+template <int B>
+struct Sha;
+template <>
+struct Sha<32> {
+  static constexpr int R = 64, S0a = 2, S0b = 13, S0c = 22, S1a = 6, S1b = 11, S1c = 25;
+  static constexpr int s0a = 7, s0b = 18, s0c = 3, s1a = 17, s1b = 19, s1c = 10;
+};
+template <>
+struct Sha<64> {
+  static constexpr int R = 80, S0a = 28, S0b = 34, S0c = 39, S1a = 14, S1b = 18, S1c = 41;
+  static constexpr int s0a = 1, s0b = 8, s0c = 7, s1a = 19, s1b = 61, s1c = 6;
+};
+
+__constant__ uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+__constant__ uint32_t kSha256IV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                      0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+__constant__ uint64_t kSha512K[80] = {
+    0x428a2f98d728ae22ull, 0x7137449123ef65cdull, 0xb5c0fbcfec4d3b2full, 0xe9b5dba58189dbbcull,
+    0x3956c25bf348b538ull, 0x59f111f1b605d019ull, 0x923f82a4af194f9bull, 0xab1c5ed5da6d8118ull,
+    0xd807aa98a3030242ull, 0x12835b0145706fbeull, 0x243185be4ee4b28cull, 0x550c7dc3d5ffb4e2ull,
+    0x72be5d74f27b896full, 0x80deb1fe3b1696b1ull, 0x9bdc06a725c71235ull, 0xc19bf174cf692694ull,
+    0xe49b69c19ef14ad2ull, 0xefbe4786384f25e3ull, 0x0fc19dc68b8cd5b5ull, 0x240ca1cc77ac9c65ull,
+    0x2de92c6f592b0275ull, 0x4a7484aa6ea6e483ull, 0x5cb0a9dcbd41fbd4ull, 0x76f988da831153b5ull,
+    0x983e5152ee66dfabull, 0xa831c66d2db43210ull, 0xb00327c898fb213full, 0xbf597fc7beef0ee4ull,
+    0xc6e00bf33da88fc2ull, 0xd5a79147930aa725ull, 0x06ca6351e003826full, 0x142929670a0e6e70ull,
+    0x27b70a8546d22ffcull, 0x2e1b21385c26c926ull, 0x4d2c6dfc5ac42aedull, 0x53380d139d95b3dfull,
+    0x650a73548baf63deull, 0x766a0abb3c77b2a8ull, 0x81c2c92e47edaee6ull, 0x92722c851482353bull,
+    0xa2bfe8a14cf10364ull, 0xa81a664bbc423001ull, 0xc24b8b70d0f89791ull, 0xc76c51a30654be30ull,
+    0xd192e819d6ef5218ull, 0xd69906245565a910ull, 0xf40e35855771202aull, 0x106aa07032bbd1b8ull,
+    0x19a4c116b8d2d0c8ull, 0x1e376c085141ab53ull, 0x2748774cdf8eeb99ull, 0x34b0bcb5e19b48a8ull,
+    0x391c0cb3c5c95a63ull, 0x4ed8aa4ae3418acbull, 0x5b9cca4f7763e373ull, 0x682e6ff3d6b2b8a3ull,
+    0x748f82ee5defb2fcull, 0x78a5636f43172f60ull, 0x84c87814a1f0ab72ull, 0x8cc702081a6439ecull,
+    0x90befffa23631e28ull, 0xa4506cebde82bde9ull, 0xbef9a3f7b2c67915ull, 0xc67178f2e372532bull,
+    0xca273eceea26619cull, 0xd186b8c721c0c207ull, 0xeada7dd6cde0eb1eull, 0xf57d4f7fee6ed178ull,
+    0x06f067aa72176fbaull, 0x0a637dc5a2c898a6ull, 0x113f9804bef90daeull, 0x1b710b35131c471bull,
+    0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
+    0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
+__constant__ uint64_t kSha512IV[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull,
+                                      0xa54ff53a5f1d36f1ull, 0x510e527fade682d1ull, 0x9b05688c2b3e6c1full,
+                                      0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+
+template <int B>
+struct ShaLayout {
+  static constexpr int nx0 = 2 * B - Sha<B>::s0c;  // XOR3 signals (2 each) + XOR2 (1 each)
+  static constexpr int nx1 = 2 * B - Sha<B>::s1c;
+  static constexpr int sched = nx0 + nx1 + B + 2;
+  static constexpr int round = 9 * B + 6;
+  static constexpr int n_sched = Sha<B>::R - 16;
+  static constexpr int round_base = n_sched * sched;
+  static constexpr int final_base = round_base + Sha<B>::R * round;
+  static constexpr int size = final_base + 8 * (B + 1);
+};
+
+// per-block integer state in LDS (lane 0 fills it, the workgroup reads it)
+struct ShaShared {
+  uint64_t W[80];
+  uint64_t A[84], E[84];   // A[t + 4] = a after round t; A[0..3] = d, c, b, a of the input state
+  uint64_t H[8];
+  uint8_t wc[80], ac[80], ec[80], hc[8];  // carries of the W, new-a, new-e and final sums
+  uint8_t msg[64];
+  uint32_t state_bits[8 * 64 / 32];
+};
+
+__device__ __forceinline__ Fr fr_small(int v) {  // v in {0, 1, -1}
+  Fr r = Fr::zero();
+  if (v > 0) {
+    r.v[0] = 1;
+  } else if (v < 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = FrParams::P[i];
+    r.v[0] -= 1;
+  }
+  return r;
+}
+
+__device__ __forceinline__ int bit_of(uint64_t x, int i) { return (int)((x >> i) & 1u); }
+
+// value of XOR-signal o of ROTR r1 ^ ROTR r2 ^ (SHR|ROTR) r3 of word x
+template <int B>
+__device__ int xor_value(uint64_t x, int r1, int r2, int r3, bool shr, int o) {
+  const int n3 = shr ? B - r3 : B;
+  int i, which;
+  bool x3;
+  if (o < 2 * n3) {
+    i = o >> 1;
+    which = o & 1;
+    x3 = true;
+  } else {
+    i = n3 + (o - 2 * n3);
+    which = 0;
+    x3 = false;
+  }
+  const int a = bit_of(x, (i + r1) % B), b = bit_of(x, (i + r2) % B);
+  if (!x3) return a & b;
+  const int c = shr ? bit_of(x, i + r3) : bit_of(x, (i + r3) % B);
+  const int mid = b & c;
+  if (which == 0) return mid;
+  return a ? (b == c ? 1 : -1) : 0;
+}
+
+template <int B>
+__device__ __forceinline__ uint64_t rotr(uint64_t x, int n) {
+  const uint64_t m = B == 64 ? ~0ull : 0xffffffffull;
+  return ((x >> n) | (x << (B - n))) & m;
+}
+
+template <int B>
+__device__ __forceinline__ uint64_t sig(uint64_t x, int r1, int r2, int r3, bool shr) {
+  return rotr<B>(x, r1) ^ rotr<B>(x, r2) ^ (shr ? (x >> r3) : rotr<B>(x, r3));
+}
+
+// sum of words with carry out (k words < 8, each < 2^B)
+template <int B>
+__device__ __forceinline__ uint64_t addw(uint64_t acc, uint64_t x, uint32_t& carry) {
+  if (B == 32) {
+    const uint64_t s = acc + x;
+    carry += (uint32_t)(s >> 32);
+    return s & 0xffffffffull;
+  }
+  const uint64_t s = acc + x;
+  carry += s < x;
+  return s;
+}
+
+template <int B>
+__device__ void sha_block(Fr* W, const Op& op, ShaShared& sh) {
+  using L = ShaLayout<B>;
+  using S = Sha<B>;
+  const int tid = threadIdx.x;
+  const uint64_t mask = B == 64 ? ~0ull : 0xffffffffull;
+  // message bytes from the byte-wise bit wires (LSB first)
+  for (int k = tid; k < 64; k += blockDim.x) {
+    uint32_t byte = 0;
+    for (int j = 0; j < 8; j++) byte |= (W[op.b_off + 8 * k + j].v[0] & 1u) << j;
+    sh.msg[k] = (uint8_t)byte;
+  }
+  // input state: the previous block's final sums (bits LSB first + 1 carry per word)
+  if (op.a_off != kNoWire) {
+    for (int k = tid; k < 8 * B; k += blockDim.x) {
+      const int j = k / B, i = k % B;
+      const uint32_t bit = W[op.a_off + L::final_base + j * (B + 1) + i].v[0] & 1u;
+      if (bit) atomicOr(&sh.state_bits[k >> 5], 1u << (k & 31));
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int nbw = B / 8;
+    const int nw = B == 32 ? 16 : 8;
+    for (int t = 0; t < nw; t++) {
+      uint64_t x = 0;
+      for (int q = 0; q < nbw; q++) x = (x << 8) | sh.msg[nbw * t + q];
+      sh.W[t] = x;
+    }
+    if (B == 64) {  // SHA-512 of a 64-byte message: 0x80, zeros, 128-bit length 512
+      sh.W[8] = 1ull << 63;
+      for (int t = 9; t < 15; t++) sh.W[t] = 0;
+      sh.W[15] = 512;
+    }
+    uint64_t H[8];
+    for (int j = 0; j < 8; j++) {
+      if (op.a_off == kNoWire) {
+        H[j] = B == 32 ? (uint64_t)kSha256IV[j] : kSha512IV[j];
+      } else {
+        uint64_t x = 0;
+        for (int i = 0; i < B; i++) {
+          const int k = j * B + i;
+          x |= (uint64_t)((sh.state_bits[k >> 5] >> (k & 31)) & 1u) << i;
+        }
+        H[j] = x;
+      }
+      sh.H[j] = H[j];
+    }
+    for (int t = 16; t < S::R; t++) {
+      uint32_t c = 0;
+      uint64_t s = sig<B>(sh.W[t - 2], S::s1a, S::s1b, S::s1c, true);
+      s = addw<B>(s, sh.W[t - 7], c);
+      s = addw<B>(s, sig<B>(sh.W[t - 15], S::s0a, S::s0b, S::s0c, true), c);
+      s = addw<B>(s, sh.W[t - 16], c);
+      sh.W[t] = s;
+      sh.wc[t] = (uint8_t)c;
+    }
+    // A[0..3] = d, c, b, a; E[0..3] = h, g, f, e
+    sh.A[3] = H[0]; sh.A[2] = H[1]; sh.A[1] = H[2]; sh.A[0] = H[3];
+    sh.E[3] = H[4]; sh.E[2] = H[5]; sh.E[1] = H[6]; sh.E[0] = H[7];
+    for (int t = 0; t < S::R; t++) {
+      const uint64_t a = sh.A[t + 3], b = sh.A[t + 2], c = sh.A[t + 1], d = sh.A[t];
+      const uint64_t e = sh.E[t + 3], f = sh.E[t + 2], g = sh.E[t + 1], h = sh.E[t];
+      const uint64_t S1 = sig<B>(e, S::S1a, S::S1b, S::S1c, false);
+      const uint64_t ch = (e & f) ^ (~e & g & mask);
+      const uint64_t S0 = sig<B>(a, S::S0a, S::S0b, S::S0c, false);
+      const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
+      const uint64_t k = B == 32 ? (uint64_t)kSha256K[t] : kSha512K[t];
+      uint32_t c1 = 0;  // T1 = h + S1 + ch + K + W
+      uint64_t t1 = addw<B>(h, S1, c1);
+      t1 = addw<B>(t1, ch, c1);
+      t1 = addw<B>(t1, k, c1);
+      t1 = addw<B>(t1, sh.W[t], c1);
+      uint32_t ca = c1;
+      uint64_t na = addw<B>(t1, S0, ca);
+      na = addw<B>(na, mj, ca);
+      uint32_t ce = c1;
+      const uint64_t ne = addw<B>(t1, d, ce);
+      sh.A[t + 4] = na;
+      sh.E[t + 4] = ne;
+      sh.ac[t] = (uint8_t)ca;
+      sh.ec[t] = (uint8_t)ce;
+    }
+    const int R = S::R;
+    const uint64_t V[8] = {sh.A[R + 3], sh.A[R + 2], sh.A[R + 1], sh.A[R], sh.E[R + 3], sh.E[R + 2], sh.E[R + 1],
+                           sh.E[R]};
+    for (int j = 0; j < 8; j++) {
+      uint32_t c = 0;
+      const uint64_t s = addw<B>(H[j], V[j], c);
+      sh.hc[j] = (uint8_t)c;
+      sh.H[j] = s;  // final sums (H_in no longer needed)
+    }
+  }
+  __syncthreads();
+  // every signal of the block
+  const Fr one = fr_small(1), zero = Fr::zero(), mone = fr_small(-1);
+  Fr* out = W + op.dst;
+  for (int s = tid; s < L::size; s += blockDim.x) {
+    int v;
+    if (s < L::round_base) {
+      const int t = 16 + s / L::sched;
+      int o = s % L::sched;
+      if (o < L::nx0) {
+        v = xor_value<B>(sh.W[t - 15], S::s0a, S::s0b, S::s0c, true, o);
+      } else if ((o -= L::nx0) < L::nx1) {
+        v = xor_value<B>(sh.W[t - 2], S::s1a, S::s1b, S::s1c, true, o);
+      } else {
+        o -= L::nx1;
+        v = o < B ? bit_of(sh.W[t], o) : (int)((sh.wc[t] >> (o - B)) & 1u);
+      }
+    } else if (s < L::final_base) {
+      const int q = s - L::round_base;
+      const int t = q / L::round;
+      int o = q % L::round;
+      const uint64_t a = sh.A[t + 3], b = sh.A[t + 2], c = sh.A[t + 1];
+      const uint64_t e = sh.E[t + 3], f = sh.E[t + 2], g = sh.E[t + 1];
+      if (o < 2 * B) {
+        v = xor_value<B>(e, S::S1a, S::S1b, S::S1c, false, o);
+      } else if ((o -= 2 * B) < B) {
+        v = bit_of(e, o) ? bit_of(f, o) - bit_of(g, o) : 0;
+      } else if ((o -= B) < 2 * B) {
+        v = xor_value<B>(a, S::S0a, S::S0b, S::S0c, false, o);
+      } else if ((o -= 2 * B) < 2 * B) {
+        const int i = o >> 1;
+        v = (o & 1) ? (bit_of(a, i) & (bit_of(b, i) ^ bit_of(c, i))) : (bit_of(b, i) & bit_of(c, i));
+      } else if ((o -= 2 * B) < B + 3) {
+        v = o < B ? bit_of(sh.A[t + 4], o) : (int)((sh.ac[t] >> (o - B)) & 1u);
+      } else {
+        o -= B + 3;
+        v = o < B ? bit_of(sh.E[t + 4], o) : (int)((sh.ec[t] >> (o - B)) & 1u);
+      }
+    } else {
+      const int q = s - L::final_base;
+      const int j = q / (B + 1), i = q % (B + 1);
+      v = i < B ? bit_of(sh.H[j], i) : (int)(sh.hc[j] & 1u);
+    }
+    out[s] = v == 0 ? zero : (v > 0 ? one : mone);
+  }
+  __syncthreads();
+  for (int k = tid; k < 8 * 64 / 32; k += blockDim.x) sh.state_bits[k] = 0;
+  __syncthreads();
+}
+
+__device__ __forceinline__ Fr lc_mont(const Prog& P, const Fr* W, uint32_t off, uint32_t n) {
+  Fr acc = Fr::zero();
+  for (uint32_t i = 0; i < n; i++) {
+    const Term t = P.terms[off + i];
+    acc = acc + W[t.wire] * P.consts[t.ci];
+  }
+  return acc;
+}
+
+// normal-form x as a small signed integer: 1 = non-negative (val), -1 = negative (r - val), 0 = large
+__device__ __forceinline__ int small_int(const Fr& x, uint32_t& val) {
+  uint32_t hi = 0;
+#pragma unroll
+  for (int i = 1; i < 8; i++) hi |= x.v[i];
+  if (hi == 0 && x.v[0] < 0x40000000u) {
+    val = x.v[0];
+    return 1;
+  }
+  const Fr nx = neg(x);
+  hi = 0;
+#pragma unroll
+  for (int i = 1; i < 8; i++) hi |= nx.v[i];
+  if (hi == 0 && nx.v[0] < 0x40000000u) {
+    val = nx.v[0];
+    return -1;
+  }
+  return 0;
+}
+
+__device__ Fr inv_normal(const Prog& P, const Fr& x) {
+  uint32_t m;
+  const int s = small_int(x, m);
+  if (s != 0 && m < kInvTable) {
+    if (m == 0) return Fr::zero();
+    const Fr r = P.inv_small[m];
+    return s > 0 ? r : neg(r);
+  }
+  return from_mont(inverse(to_mont(x)));
+}
+
+__device__ __forceinline__ void fail(uint32_t* status, uint32_t order, uint32_t err) {
+  atomicMin(status, (order << 8) | err);
+}
+
+__device__ void scalar_op(const Prog& P, Fr* W, const Op& op, uint32_t* status) {
+  const uint32_t typ = op.code & 0xFF, err = (op.code >> 8) & 0xFF, n = op.code >> 16;
+  switch (typ) {
+    case OP_LIN:
+      W[op.dst] = from_mont(lc_mont(P, W, op.a_off, op.a_n));
+      break;
+    case OP_MUL: {
+      const Fr a = lc_mont(P, W, op.a_off, op.a_n);
+      const Fr b = lc_mont(P, W, op.b_off, op.b_n);
+      const Fr c = lc_mont(P, W, op.c_off, op.c_n);
+      W[op.dst] = from_mont(a * b + c);
+      break;
+    }
+    case OP_INV:
+      W[op.dst] = inv_normal(P, from_mont(lc_mont(P, W, op.a_off, op.a_n)));
+      break;
+    case OP_BITS: {
+      const Fr x = from_mont(lc_mont(P, W, op.a_off, op.a_n));
+      for (uint32_t i = 0; i < n; i++) {
+        Fr b = Fr::zero();
+        b.v[0] = (x.v[i >> 5] >> (i & 31)) & 1u;
+        W[op.dst + i] = b;
+      }
+      bool big = false;
+      for (uint32_t i = n; i < 256; i++) big |= ((x.v[i >> 5] >> (i & 31)) & 1u) != 0;
+      if (big) fail(status, op.c_off, err);
+      break;
+    }
+    case OP_CHECK: {
+      Fr x = lc_mont(P, W, op.a_off, op.a_n);
+      if (op.b_n) x = x * lc_mont(P, W, op.b_off, op.b_n);
+      if (!x.is_zero()) fail(status, op.c_off, err);
+      break;
+    }
+    default:
+      fail(status, 0xFFFFFFu, 0xFE);
+  }
+}
+
+struct QuinShared {
+  int sign;
+  uint32_t mag;
+  Fr idx;
+  Fr sel;
+};
+
+__device__ void quin(const Prog& P, Fr* W, const Op& op, QuinShared& qs) {
+  const uint32_t n = op.code >> 16, m = op.b_n;
+  if (threadIdx.x == 0) {
+    const Fr idx = from_mont(lc_mont(P, W, op.a_off, op.a_n));
+    uint32_t mag = 0;
+    qs.sign = small_int(idx, mag);
+    qs.mag = mag;
+    qs.idx = idx;
+    const bool hit = qs.sign > 0 && mag < m;
+    qs.sel = hit ? W[op.b_off + mag] : Fr::zero();
+  }
+  __syncthreads();
+  const int sign = qs.sign;
+  const uint32_t mag = qs.mag;
+  const int64_t idx = sign > 0 ? (int64_t)mag : -(int64_t)mag;
+  const Fr one = fr_small(1);
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    Fr eq = Fr::zero(), inv;
+    if (sign != 0) {
+      const int64_t d = (int64_t)i - idx;
+      if (d == 0) {
+        eq = one;
+        inv = Fr::zero();
+      } else {
+        const uint64_t ad = d < 0 ? (uint64_t)(-d) : (uint64_t)d;
+        if (ad < kInvTable) {
+          inv = d < 0 ? neg(P.inv_small[ad]) : P.inv_small[ad];
+        } else {
+          Fr df = Fr::zero();
+          df.v[0] = (uint32_t)ad;
+          df.v[1] = (uint32_t)(ad >> 32);
+          inv = from_mont(inverse(to_mont(df)));
+          if (d < 0) inv = neg(inv);
+        }
+      }
+    } else {
+      Fr fi = Fr::zero();
+      fi.v[0] = i;
+      inv = from_mont(inverse(to_mont(fi - qs.idx)));
+    }
+    W[op.dst + i] = eq;
+    W[op.dst + n + i] = inv;
+  }
+  const bool hit = sign > 0 && mag < m;
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
+    W[op.dst + 2 * n + i] = (hit && i >= mag) ? qs.sel : Fr::zero();
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kThreads) wvm_kernel(Prog P, const Fr* __restrict__ inputs, Fr* witness,
+                                                        size_t stride_elems, uint32_t* status) {
+  __shared__ ShaShared sh;
+  __shared__ QuinShared qs;
+  const uint32_t pass = blockIdx.x;
+  Fr* W = witness + (size_t)pass * stride_elems;
+  const Fr* in = inputs + (size_t)pass * P.n_inputs;
+  uint32_t* st = status + pass;
+  if (threadIdx.x == 0) {
+    *st = 0xFFFFFFFFu;
+    W[0] = fr_small(1);
+  }
+  for (int k = threadIdx.x; k < 8 * 64 / 32; k += blockDim.x) sh.state_bits[k] = 0;
+  for (uint32_t i = threadIdx.x; i < P.n_inputs; i += blockDim.x) W[P.in_base + i] = in[i];
+  __syncthreads();
+  for (uint32_t lv = 0; lv < P.n_levels; lv++) {
+    const uint32_t s0 = P.starts[lv], m0 = P.mstarts[lv], e0 = P.starts[lv + 1];
+    for (uint32_t k = s0 + threadIdx.x; k < m0; k += blockDim.x) scalar_op(P, W, P.ops[k], st);
+    for (uint32_t k = m0; k < e0; k++) {
+      const Op op = P.ops[k];
+      const uint32_t typ = op.code & 0xFF;
+      if (typ == OP_QUIN)
+        quin(P, W, op, qs);
+      else if (typ == OP_SHA256)
+        sha_block<32>(W, op, sh);
+      else
+        sha_block<64>(W, op, sh);
+    }
+    __syncthreads();
+  }
+}
+
+struct Program {
+  int device = 0;
+  uint32_t n_wires = 0, n_out = 0, n_pub = 0, n_prv = 0, n_levels = 0;
+  DevBuf<Fr> consts, inv_small;
+  DevBuf<Term> terms;
+  DevBuf<Op> ops;
+  DevBuf<uint32_t> starts, mstarts;
+  DevBuf<uint32_t> status;
+  size_t status_cap = 0;
+};
+
+static uint32_t rd32(const uint8_t* p) {
+  uint32_t x;
+  std::memcpy(&x, p, 4);
+  return x;
+}
+
+template <class T>
+static void upload(DevBuf<T>& d, const void* src, size_t count) {
+  d.alloc(count ? count : 1);
+  if (count) NZ_HIP(hipMemcpy(d.p, src, count * sizeof(T), hipMemcpyHostToDevice));
+}
+
+Program* load(const uint8_t* data, size_t len, int device) {
+  if (!data || len < 40 || std::memcmp(data, "nzwp", 4) != 0)
+    throw Error(NZCB_ERR_FORMAT, "witness program: bad magic");
+  if (rd32(data + 4) != 1) throw Error(NZCB_ERR_FORMAT, "witness program: unsupported version");
+  auto P = new Program();
+  try {
+    P->device = device;
+    P->n_wires = rd32(data + 8);
+    P->n_out = rd32(data + 12);
+    P->n_pub = rd32(data + 16);
+    P->n_prv = rd32(data + 20);
+    const uint32_t nc = rd32(data + 24), nt = rd32(data + 28), no = rd32(data + 32);
+    P->n_levels = rd32(data + 36);
+    const size_t need = 40 + (size_t)nc * 32 + (size_t)nt * 8 + (size_t)no * 32 + ((size_t)P->n_levels * 2 + 1) * 4;
+    if (len != need) throw Error(NZCB_ERR_FORMAT, "witness program: truncated or oversized");
+    const uint8_t* p = data + 40;
+    // coefficients c -> c R^2 (Montgomery of Montgomery), checked < r
+    std::vector<Fr> cs(nc);
+    for (uint32_t i = 0; i < nc; i++) {
+      Fr c;
+      std::memcpy(c.v, p + 32 * (size_t)i, 32);
+      if (reduce_once(c) != c) throw Error(NZCB_ERR_FORMAT, "witness program: coefficient >= r");
+      cs[i] = to_mont(to_mont(c));
+    }
+    p += (size_t)nc * 32;
+    const Term* tm = (const Term*)p;
+    for (uint32_t i = 0; i < nt; i++)
+      if (tm[i].wire >= P->n_wires || tm[i].ci >= nc) throw Error(NZCB_ERR_FORMAT, "witness program: bad term");
+    p += (size_t)nt * 8;
+    const Op* op = (const Op*)p;
+    for (uint32_t i = 0; i < no; i++) {
+      const Op& o = op[i];
+      const uint32_t typ = o.code & 0xFF, n = o.code >> 16;
+      auto lc_ok = [&](uint32_t off, uint32_t cnt) { return (uint64_t)off + cnt <= nt; };
+      bool ok = typ <= OP_SHA512;
+      size_t width = 1;
+      if (typ == OP_QUIN) {
+        width = 2 * (size_t)n + o.b_n;
+        ok = ok && lc_ok(o.a_off, o.a_n) && o.b_n <= n && (uint64_t)o.b_off + o.b_n <= P->n_wires;
+      } else if (typ == OP_SHA256 || typ == OP_SHA512) {
+        const size_t sz = typ == OP_SHA256 ? ShaLayout<32>::size : ShaLayout<64>::size;
+        width = sz;
+        ok = ok && (o.a_off == kNoWire || (uint64_t)o.a_off + sz <= P->n_wires) &&
+             (uint64_t)o.b_off + 512 <= P->n_wires;
+      } else {
+        ok = ok && lc_ok(o.a_off, o.a_n) && lc_ok(o.b_off, o.b_n);
+        if (typ != OP_BITS && typ != OP_CHECK) ok = ok && lc_ok(o.c_off, o.c_n);
+        if (typ == OP_BITS) width = n;
+        if (typ == OP_CHECK) width = 0;
+        ok = ok && (typ != OP_BITS || (n >= 1 && n <= 254));
+      }
+      if (width) ok = ok && (uint64_t)o.dst + width <= P->n_wires;
+      if (!ok) throw Error(NZCB_ERR_FORMAT, "witness program: bad op " + std::to_string(i));
+    }
+    p += (size_t)no * 32;
+    const uint32_t* lv = (const uint32_t*)p;
+    for (uint32_t i = 0; i < P->n_levels; i++) {
+      const uint32_t s = lv[i], e = lv[i + 1], ms = lv[P->n_levels + 1 + i];
+      if (!(s <= ms && ms <= e && e <= no)) throw Error(NZCB_ERR_FORMAT, "witness program: bad level table");
+    }
+    if (P->n_levels && lv[P->n_levels] != no) throw Error(NZCB_ERR_FORMAT, "witness program: bad level table");
+    if (1 + P->n_out + P->n_pub + P->n_prv > P->n_wires) throw Error(NZCB_ERR_FORMAT, "witness program: bad counts");
+    // 1/i for the small-integer fast path: one Fermat inverse and a prefix-product pass
+    std::vector<Fr> pre(kInvTable), inv(kInvTable, Fr::zero());
+    Fr acc = Fr::one();
+    for (uint32_t i = 1; i < kInvTable; i++) {
+      Fr fi = Fr::zero();
+      fi.v[0] = i;
+      pre[i] = acc;                 // prod_{k < i} k (Montgomery)
+      acc = acc * to_mont(fi);
+    }
+    Fr ia = inverse(acc);           // 1 / prod_{k < T} k
+    for (uint32_t i = kInvTable - 1; i >= 1; i--) {
+      Fr fi = Fr::zero();
+      fi.v[0] = i;
+      inv[i] = from_mont(ia * pre[i]);
+      ia = ia * to_mont(fi);
+    }
+    NZ_HIP(hipSetDevice(device));
+    upload(P->consts, cs.data(), nc);
+    upload(P->terms, tm, nt);
+    upload(P->ops, op, no);
+    upload(P->starts, lv, P->n_levels + 1);
+    upload(P->mstarts, lv + P->n_levels + 1, P->n_levels);
+    upload(P->inv_small, inv.data(), kInvTable);
+  } catch (...) {
+    delete P;
+    throw;
+  }
+  return P;
+}
+
+void run(Program* P, const void* dev_inputs, int count, void* dev_witness, size_t stride_bytes, int32_t* status_out,
+         hipStream_t s) {
+  if (count <= 0) return;
+  if (!dev_inputs || !dev_witness || !status_out) throw Error(NZCB_ERR_ARG, "witness program: null buffer");
+  if (stride_bytes % 32 || stride_bytes < (size_t)P->n_wires * 32)
+    throw Error(NZCB_ERR_ARG, "witness program: witness stride below n_wires x 32 B");
+  NZ_HIP(hipSetDevice(P->device));
+  if ((size_t)count > P->status_cap) {
+    P->status.alloc((size_t)count);
+    P->status_cap = (size_t)count;
+  }
+  Prog g;
+  g.consts = P->consts.p;
+  g.terms = P->terms.p;
+  g.ops = P->ops.p;
+  g.starts = P->starts.p;
+  g.mstarts = P->mstarts.p;
+  g.inv_small = P->inv_small.p;
+  g.n_levels = P->n_levels;
+  g.n_wires = P->n_wires;
+  g.n_inputs = P->n_pub + P->n_prv;
+  g.in_base = 1 + P->n_out;
+  hipLaunchKernelGGL(wvm_kernel, dim3((unsigned)count), dim3(kThreads), 0, s, g, (const Fr*)dev_inputs,
+                     (Fr*)dev_witness, stride_bytes / 32, P->status.p);
+  NZ_HIP(hipGetLastError());
+  std::vector<uint32_t> st((size_t)count);
+  NZ_HIP(hipMemcpyAsync(st.data(), P->status.p, (size_t)count * 4, hipMemcpyDeviceToHost, s));
+  NZ_HIP(hipStreamSynchronize(s));
+  for (int i = 0; i < count; i++) status_out[i] = st[i] == 0xFFFFFFFFu ? 0 : (int32_t)(st[i] & 0xFF);
+}
+
+}  // namespace wvm
+}  // namespace nzcb
+
+using namespace nzcb;
+
+struct nzcb_wprog {
+  wvm::Program* p;
+};
+
+extern "C" {
+
+nzcb_wprog* nzcb_wprog_create(const uint8_t* prog, size_t len, int device, nzcb_err* err) {
+  try {
+    auto h = new nzcb_wprog();
+    try {
+      h->p = wvm::load(prog, len, device);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    return h;
+  } catch (const Error& e) {
+    set_err(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+  }
+  return nullptr;
+}
+
+void nzcb_wprog_destroy(nzcb_wprog* h) {
+  if (!h) return;
+  if (h->p) {
+    (void)hipSetDevice(h->p->device);
+    delete h->p;
+  }
+  delete h;
+}
+
+int nzcb_wprog_info(const nzcb_wprog* h, uint32_t info[5]) {
+  if (!h || !info) return NZCB_ERR_ARG;
+  info[0] = h->p->n_wires;
+  info[1] = h->p->n_out;
+  info[2] = h->p->n_pub;
+  info[3] = h->p->n_prv;
+  info[4] = h->p->n_levels;
+  return NZCB_OK;
+}
+
+int nzcb_wprog_run_dev(nzcb_wprog* h, const void* dev_inputs, int count, void* dev_witness, size_t witness_stride,
+                       int32_t* status_out, void* stream, nzcb_err* err) {
+  try {
+    if (!h) throw Error(NZCB_ERR_ARG, "witness program: null handle");
+    wvm::run(h->p, dev_inputs, count, dev_witness, witness_stride, status_out, (hipStream_t)stream);
+    return NZCB_OK;
+  } catch (const Error& e) {
+    set_err(err, e.code, e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+    return NZCB_ERR_INTERNAL;
+  }
+}
+
+int nzcb_wprog_run(nzcb_wprog* h, const uint8_t* inputs, int count, uint8_t* witness_out, int32_t* status_out,
+                   nzcb_err* err) {
+  try {
+    if (!h) throw Error(NZCB_ERR_ARG, "witness program: null handle");
+    if (count <= 0) return NZCB_OK;
+    if (!inputs || !witness_out || !status_out) throw Error(NZCB_ERR_ARG, "witness program: null buffer");
+    NZ_HIP(hipSetDevice(h->p->device));
+    const size_t nin = (size_t)(h->p->n_pub + h->p->n_prv) * 32 * count;
+    const size_t nw = (size_t)h->p->n_wires * 32;
+    DevBuf<uint8_t> din(nin ? nin : 1), dw(nw * count);
+    if (nin) NZ_HIP(hipMemcpy(din.p, inputs, nin, hipMemcpyHostToDevice));
+    wvm::run(h->p, din.p, count, dw.p, nw, status_out, nullptr);
+    NZ_HIP(hipMemcpy(witness_out, dw.p, nw * count, hipMemcpyDeviceToHost));
+    return NZCB_OK;
+  } catch (const Error& e) {
+    set_err(err, e.code, e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+    return NZCB_ERR_INTERNAL;
+  }
+}
+
+}  // extern "C"

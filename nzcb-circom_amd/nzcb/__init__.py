@@ -155,6 +155,13 @@ def load(path: str | None = None):
                                           c_void_p, POINTER(_Err)]),
         "nzcb_engine_time_msm2": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_int,
                                           POINTER(c_double), POINTER(_Err)]),
+        "nzcb_ptau_synth": (c_int, [c_int, u8p, c_int, POINTER(POINTER(c_uint8)), POINTER(c_size_t), POINTER(_Err)]),
+        "nzcb_wprog_create": (c_void_p, [ctypes.c_char_p, c_size_t, c_int, POINTER(_Err)]),
+        "nzcb_wprog_destroy": (None, [c_void_p]),
+        "nzcb_wprog_info": (c_int, [c_void_p, POINTER(c_uint32)]),
+        "nzcb_wprog_run_dev": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, POINTER(ctypes.c_int32),
+                                       c_void_p, POINTER(_Err)]),
+        "nzcb_wprog_run": (c_int, [c_void_p, ctypes.c_char_p, c_int, u8p, POINTER(ctypes.c_int32), POINTER(_Err)]),
     }
     lib.missing_symbols = []
     for name, (res, args) in sigs.items():
@@ -524,6 +531,47 @@ class ProverContext:
         return dict(zip(names[:k], list(ms)[:k]))
 
 
+class WitnessProgram:
+    """A circuit's witness calculator on the GPU (include/nzcb.h nzcb_wprog_*): the
+    program written by nzcb.circuit.Circuit.write_program (nzcp_live: nzcb.nzcpgen),
+    uploaded once, run for a batch of input vectors, one workgroup per witness."""
+
+    def __init__(self, program: bytes, device: int = 0):
+        self.lib = load()
+        self.device = device
+        err = _Err()
+        self.h = self.lib.nzcb_wprog_create(program, len(program), device, ctypes.byref(err))
+        if not self.h:
+            raise NzcbError(err.code, err.msg.decode(errors="replace"))
+        info = (c_uint32 * 5)()
+        self.lib.nzcb_wprog_info(self.h, info)
+        self.n_wires, self.n_out, self.n_pub_in, self.n_prv_in, self.n_levels = list(info)
+        self.n_inputs = self.n_pub_in + self.n_prv_in
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.nzcb_wprog_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def run(self, inputs: bytes, count: int):
+        """Host path: returns (witnesses bytes count x n_wires x 32, statuses)."""
+        out = _out(max(1, count * self.n_wires * 32))
+        st = (ctypes.c_int32 * max(count, 1))()
+        err = _Err()
+        _check(self.lib.nzcb_wprog_run(self.h, inputs, count, out, st, ctypes.byref(err)), err)
+        return bytes(out)[:count * self.n_wires * 32], [st[i] for i in range(count)]
+
+    def run_dev(self, dev_inputs: int, count: int, dev_witness: int, stride: int) -> list:
+        """Device path: witnesses written at dev_witness + i * stride; returns statuses."""
+        st = (ctypes.c_int32 * max(count, 1))()
+        err = _Err()
+        _check(self.lib.nzcb_wprog_run_dev(self.h, dev_inputs, count, dev_witness, stride, st, None,
+                                           ctypes.byref(err)), err)
+        return [st[i] for i in range(count)]
+
+
 class NzcpProver:
     """fullProve for nzcp passes on one GPU: the nzcp witness kernel computes each pass's
     public signals (NZCPPubIdentity out[0..2], include/nzcb.h nzcb_nzcp_witness_dev)
@@ -787,6 +835,21 @@ def plonk_setup(r1cs: bytes, ptau: bytes, device: int = 0) -> bytes:
         return ctypes.string_at(zp, zl.value)
     finally:
         lib.nzcb_free(zp)
+
+
+def ptau_synth(power: int, tau: int, device: int = 0) -> bytes:
+    """Powers-of-tau file (snarkjs layout, sections 1-3) for a trapdoor tau, built on the
+    GPU (include/nzcb.h nzcb_ptau_synth)."""
+    lib = load()
+    pp = POINTER(c_uint8)()
+    pl = c_size_t()
+    err = _Err()
+    _check(lib.nzcb_ptau_synth(power, _buf(int(tau).to_bytes(32, "little")), device, ctypes.byref(pp),
+                               ctypes.byref(pl), ctypes.byref(err)), err)
+    try:
+        return ctypes.string_at(pp, pl.value)
+    finally:
+        lib.nzcb_free(pp)
 
 
 def synth_setup_raw(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x6E7A6362,

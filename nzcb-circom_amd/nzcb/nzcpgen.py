@@ -1,0 +1,388 @@
+"""Arithmetization of the reference circuit ``NZCPPubIdentity`` (circuits/nzcp_live.circom:
+``NZCPPubIdentity(1, 351, 0, 4, 2, 4)``) with ``nzcb.circuit``: the r1cs that
+``snarkjs plonk setup`` turns into ``nzcp_live_final.zkey`` (/root/reference/Makefile:59-62)
+and the witness program the GPU runs in place of the circom wasm witness calculator.
+
+Every template follows its circom source statement by statement (file:line on each
+function): the same signals, the same ``<==`` / ``===`` constraints and the same
+witness rules (circomlib Num2Bits / LessThan / IsZero / IsEqual, QuinSelector,
+CalculateTotal). Short linear ``<==`` assignments are substituted, as ``circom --O2``
+does (Makefile:12-13).
+
+Two parts come from circuit libraries the reference downloads at build time and which
+are not on disk (Makefile:20-43): ``Sha256Var`` (noway/sha256-var-circom)
+and ``Sha512`` (Electron-Labs/sha512). They are written here from FIPS 180-4 with
+circomlib's gadget shapes (Xor3, Ch, Maj, bit-decomposed modular sums; outputs MSB
+first), see ``Circuit.sha_block`` and ``sha256_var``. So the signal order, and with it
+the zkey and the proof bytes, are this build's own, not circom's: **parity against
+snarkjs on the real nzcp_live.zkey stays unpinned.** What is pinned: the circuit's
+public outputs equal the CPU restatement ``oracle/nzcp_circuit.py``, which the
+reference's own test vectors pin (test/nzcp.js, test/cbor.js, test/utils.js).
+"""
+from __future__ import annotations
+
+from .circuit import (OP_SHA256, OP_SHA512, SHA256_IV, SHA256_SPEC, SHA512_IV, SHA512_SPEC, Circuit, add, lc,
+                      scale, sub, w)
+
+# witness failure codes (oracle/nzcp_circuit.py ERR_*, include/nzcb.h NZCB_NZCP_*)
+ERR_BIT, ERR_LEN, ERR_RANGE, ERR_SELECT, ERR_NOT_MAP, ERR_UINT23, ERR_NOT_STRING = 1, 2, 3, 4, 5, 6, 7
+
+MAJOR_INT, MAJOR_STRING, MAJOR_ARRAY, MAJOR_MAP = 0, 3, 4, 5
+
+LIVE = dict(is_live=1, max_tbs_bytes=351, max_array_len_vc=0, max_map_len_vc=4)      # nzcp_live.circom:4
+EXAMPLE = dict(is_live=0, max_tbs_bytes=314, max_array_len_vc=0, max_map_len_vc=4)   # nzcp_example.circom
+
+
+def log2(x: int) -> int:
+    """log2.circom:5-12 (-1 for 0)."""
+    return x.bit_length() - 1
+
+
+class Bytes:
+    """A byte array as contiguous wires (``bytes[BytesLen]`` of the cbor templates)."""
+
+    def __init__(self, base: int, n: int):
+        self.base, self.n = base, n
+
+
+# ---------------------------------------------------------------------------- cbortpl
+def get_type(c: Circuit, v):
+    """GetType (cbortpl.circom:26-52): Num2Bits(8), ShR(8, 5), Bits2Num(3)."""
+    bits = c.num2bits(v, 8, ERR_RANGE)
+    return c.lin(add(*[scale(bits[5 + i], 1 << i) for i in range(3)]))
+
+
+def get_x(c: Circuit, v):
+    """GetX (cbortpl.circom:57-72): the 5 low bits of v."""
+    bits = c.num2bits(v, 8, ERR_RANGE)
+    return c.lin(add(*[scale(bits[i], 1 << i) for i in range(5)]))
+
+
+def get_v(c: Circuit, b: Bytes, pos):
+    """GetV (cbortpl.circom:78-90): QuinSelector(BytesLen)."""
+    return c.quin(b.n, b.base, b.n, pos, ERR_RANGE, ERR_SELECT)
+
+
+def decode_uint23(c: Circuit, v):
+    """DecodeUint23 (cbortpl.circom:95-114)."""
+    x = get_x(c, v)
+    lt = c.less_than(x, 24, 8, ERR_RANGE)
+    c.check_zero(sub(lt, 1), ERR_UINT23)
+    return x
+
+
+def decode_uint(c: Circuit, v, b: Bytes, pos):
+    """DecodeUint (cbortpl.circom:120-241): every branch is evaluated. Returns (value, nextPos)."""
+    x = get_x(c, v)
+    cond23 = c.less_than(x, 24, 8, ERR_RANGE)
+    cond24 = c.is_equal(x, 24)
+    cond25 = c.is_equal(x, 25)
+    cond26 = c.is_equal(x, 26)
+    pos = lc(pos)
+    value23, next23 = x, pos
+    value24 = get_v(c, b, c.mul(cond24, pos))
+    next24 = add(pos, 1)
+    v1_25 = get_v(c, b, c.mul(cond25, pos))
+    v2_25 = get_v(c, b, c.mul(cond25, add(pos, 1)))
+    value25 = add(scale(v1_25, 256), v2_25)
+    next25 = add(pos, 2)
+    v26 = [get_v(c, b, c.mul(cond26, add(pos, j))) for j in range(4)]
+    value26 = add(scale(v26[0], 1 << 24), scale(v26[1], 1 << 16), scale(v26[2], 1 << 8), v26[3])
+    next26 = add(pos, 4)
+    value = c.lin(add(c.mul(cond23, value23), c.mul(cond24, value24), c.mul(cond25, value25),
+                      c.mul(cond26, value26)))
+    next_pos = c.lin(add(c.mul(cond23, next23), c.mul(cond24, next24), c.mul(cond25, next25),
+                         c.mul(cond26, next26)))
+    return value, next_pos
+
+
+def read_type(c: Circuit, b: Bytes, pos):
+    """ReadType (cbortpl.circom:246-261). Returns (nextPos, type, v)."""
+    v = get_v(c, b, pos)
+    typ = get_type(c, v)
+    return add(pos, 1), typ, v
+
+
+def skip_value(c: Circuit, b: Bytes, pos, max_array_len: int):
+    """SkipValue (cbortpl.circom:301-366); MaxArrayLen = 0 for nzcp_live (no array loop,
+    QuinSelector(0) outputs 0)."""
+    if max_array_len:
+        raise NotImplementedError("SkipValue with arrays is not used by NZCPPubIdentity(1, 351, 0, 4, 2, 4)")
+    nxt, typ, v = read_type(c, b, pos)
+    value, dnext = decode_uint(c, v, b, nxt)
+    is_int = c.is_equal(typ, MAJOR_INT)
+    is_string = c.is_equal(typ, MAJOR_STRING)
+    is_array = c.is_equal(typ, MAJOR_ARRAY)
+    c.mul(is_array, sub(value, 1))        # qs.index <== isArray.out * (decodeUint.value - 1)
+    return c.lin(add(c.mul(is_int, dnext), c.mul(is_string, add(dnext, value))))
+
+
+def string_equals(c: Circuit, b: Bytes, const: list, pos, length):
+    """StringEquals (cbortpl.circom:373-404)."""
+    is_same_len = c.is_equal(length, len(const))
+    cond = [is_same_len]
+    for i, ch in enumerate(const):
+        cond.append(c.is_equal(ch, get_v(c, b, add(pos, i))))
+    return c.is_zero(sub(len(const) + 1, add(*cond)))
+
+
+def read_string_length(c: Circuit, b: Bytes, pos):
+    """ReadStringLength (cbortpl.circom:410-428). Returns (len, nextPos = pos + 1)."""
+    nxt, typ, v = read_type(c, b, pos)
+    c.check_zero(sub(typ, MAJOR_STRING), ERR_NOT_STRING)
+    value, _ = decode_uint(c, v, b, nxt)
+    return value, nxt
+
+
+def read_map_length(c: Circuit, b: Bytes, pos):
+    """ReadMapLength (cbortpl.circom:434-453). Returns (len, nextPos)."""
+    nxt, typ, v = read_type(c, b, pos)
+    c.check_zero(sub(typ, MAJOR_MAP), ERR_NOT_MAP)
+    return decode_uint23(c, v), nxt
+
+
+def copy_string(c: Circuit, b: Bytes, pos, max_len: int, out_base: int | None = None):
+    """CopyString (cbortpl.circom:460-503). Returns (outbytes, nextPos, len)."""
+    length, nxt = read_string_length(c, b, pos)
+    bits = log2(max_len) + 1
+    out = []
+    for i in range(max_len):
+        v = get_v(c, b, add(nxt, i))
+        lt = c.less_than(i, length, bits, ERR_RANGE)
+        out.append(c.mul(v, lt))
+    return out, add(nxt, length), length
+
+
+# --------------------------------------------------------------------------- nzcptpl
+def find_cwt_claims(c: Circuit, b: Bytes, map_len, pos, max_array_len: int, max_map_len: int):
+    """FindCWTClaims (nzcptpl.circom:33-145). Returns (vcPos, exp)."""
+    vc = [118, 99]
+    found, exp_pos = [], []
+    for k in range(max_map_len):
+        nxt, typ, v = read_type(c, b, pos)
+        value, dnext = decode_uint(c, v, b, nxt)
+        is_string = c.is_equal(typ, MAJOR_STRING)
+        is_int = c.is_equal(typ, MAJOR_INT)
+        skip_pos = c.mul(value, is_string, dnext)
+        next_pos = skip_value(c, b, skip_pos, max_array_len)     # runs once its inputs are set
+        needle = string_equals(c, b, vc, dnext, value)
+        is4 = c.is_equal(4, value)
+        within = c.less_than(k, map_len, 8, ERR_RANGE)
+        is_needle = c.mul(is_string, needle)
+        is_exp = c.mul(is_int, is4)
+        accepted = c.mul(is_needle, within)
+        exp_accepted = c.mul(is_exp, within)
+        found.append(c.mul(accepted, add(dnext, value)))
+        exp_pos.append(c.mul(exp_accepted, dnext))
+        pos = next_pos
+    vc_pos = c.lin(add(*found))
+    epos = c.lin(add(*exp_pos))
+    nxt, _, v = read_type(c, b, epos)
+    exp, _ = decode_uint(c, v, b, nxt)
+    return vc_pos, exp
+
+
+def read_cred_subj(c: Circuit, b: Bytes, pos, max_buffer_len: int):
+    """ReadCredSubj (nzcptpl.circom:232-360). Returns ((givenName base, len), (familyName ...),
+    (dob ...)); each name is max_buffer_len / 3 contiguous signals (zeros past them)."""
+    n_map = 3
+    max_str = max_buffer_len // n_map
+    given = [103, 105, 118, 101, 110, 78, 97, 109, 101]
+    family = [102, 97, 109, 105, 108, 121, 78, 97, 109, 101]
+    dob = [100, 111, 98]
+    is_g, is_f, is_d, copies = [], [], [], []
+    for k in range(n_map):
+        length, nxt = read_string_length(c, b, pos)
+        is_g.append(string_equals(c, b, given, nxt, length))
+        is_f.append(string_equals(c, b, family, nxt, length))
+        is_d.append(string_equals(c, b, dob, nxt, length))
+        out, pos, ln = copy_string(c, b, add(nxt, length), max_str)
+        copies.append((out, ln))
+    res = []
+    for sel in (is_g, is_f, is_d):
+        base = c.alloc(max_str)
+        prods = [[c.mul(sel[i], copies[i][0][h]) for i in range(n_map)] for h in range(max_str)]
+        for h in range(max_str):
+            c.lin(add(*prods[h]), dst=base + h)
+        ln = c.lin(add(*[c.mul(sel[i], copies[i][1]) for i in range(n_map)]))
+        res.append((base, ln))
+    return res, max_str
+
+
+def construct_nullifier(c: Circuit, names, max_str: int, max_buffer_len: int):
+    """ConstructNullifier (nzcptpl.circom:364-440). Returns the result[] LCs."""
+    comma = 44
+    bits = log2(max_buffer_len) + 1
+    (gb, gl), (fb, fl), (db, dl) = names
+    result = []
+    for k in range(max_buffer_len):
+        is_given = c.less_than(k, gl, bits, ERR_RANGE)
+        under_sep1 = c.less_than(k, add(gl, 1), bits, ERR_RANGE)
+        under_family = c.less_than(k, add(gl, 1, fl), bits, ERR_RANGE)
+        under_sep2 = c.less_than(k, add(gl, 1, fl, 1), bits, ERR_RANGE)
+        g_sel = c.quin(max_buffer_len, gb, max_str, k, ERR_RANGE, ERR_SELECT)
+        f_sel = c.quin(max_buffer_len, fb, max_str, sub(sub(k, gl), 1), ERR_RANGE, ERR_SELECT)
+        d_sel = c.quin(max_buffer_len, db, max_str, sub(sub(sub(sub(k, gl), 1), fl), 1), ERR_RANGE, ERR_SELECT)
+        not_given = sub(1, is_given)
+        is_sep1 = c.mul(under_sep1, not_given)
+        is_family = c.mul(under_family, sub(1, under_sep1))
+        is_sep2 = c.mul(under_sep2, sub(1, under_family))
+        is_dob = sub(1, under_sep2)
+        given_char = c.mul(is_given, g_sel)
+        family_char = c.mul(is_family, f_sel)
+        dob_char = c.mul(is_dob, d_sel)
+        result.append(c.lin(add(given_char, scale(is_sep1, comma), family_char, scale(is_sep2, comma), dob_char),
+                            force=True))
+    return result
+
+
+def msg_word_bits(base: int, t: int, bits: int) -> list:
+    """Bit-LCs (LSB first) of message word t over byte wires with LSB-first bits
+    (wire of byte k, bit j = base + 8k + j); words are big-endian, as in FIPS 180-4."""
+    nb = bits // 8
+    out = []
+    for i in range(bits):
+        m = bits - 1 - i                 # MSB-first index inside the word
+        byte = nb * t + m // 8
+        out.append(w(base + 8 * byte + 7 - m % 8))
+    return out
+
+
+def sha256_var(c: Circuit, msg_bits_msb: list, len_bytes, block_space: int):
+    """Sha256Var(BlockSpace) (noway/sha256-var-circom, not on disk; used at
+    nzcptpl.circom:509-517): SHA-256 of the first ``len_bytes`` bytes of the input bits,
+    with the input beyond the length masked out. Written from FIPS 180-4:
+
+    * isLen[k] = IsEqual(k, len) for every byte position; lt[k] = (k < len) as a running
+      sum; Num2Bits(9) of len for the 64-bit length field (len < 512 bytes);
+    * padded byte-wise bits p (LSB first within a byte): message bit * lt[k], the 0x80
+      byte at k = len, and the length field in bytes 62..63 of the last block, selected
+      by isLast[b] = sum of isLen over [64b - 8, 64b + 56);
+    * all 2^BlockSpace compressions chained; the digest is sum_b isLast[b] * H_b
+      (a running sum, as QuinSelector's). Output bits MSB first (circomlib's order)."""
+    nblocks = 1 << block_space
+    nbytes = 64 * nblocks
+    L = lc(len_bytes)
+    lbits = c.num2bits(L, 9, ERR_RANGE)
+    is_len = [c.is_equal(k, L) for k in range(nbytes)]
+    lt_base = c.alloc(nbytes)
+    prev = 1
+    for k in range(nbytes):
+        c.lin(sub(prev, is_len[k]), dst=lt_base + k)
+        prev = w(lt_base + k)
+    last = []
+    for b in range(nblocks):
+        terms = [is_len[k] for k in range(max(0, 64 * b - 8), min(nbytes, 64 * b + 56))]
+        last.append(c.lin(add(*terms), force=True))
+    lf = [[c.mul(last[b], lbits[i]) for i in range(9)] for b in range(nblocks)]
+    pbase = c.alloc(8 * nbytes)
+    for k in range(nbytes):
+        b, off = divmod(k, 64)
+        for j in range(8):
+            extra = {}
+            if j == 7:
+                extra = add(extra, is_len[k])
+            if off == 63 and j >= 3:
+                extra = add(extra, lf[b][j - 3])
+            if off == 62 and j <= 3:
+                extra = add(extra, lf[b][5 + j])
+            src = 8 * k + 7 - j
+            bit = msg_bits_msb[src] if src < len(msg_bits_msb) else 0
+            c.mul(bit, w(lt_base + k), extra, dst=pbase + 8 * k + j)
+    state, prev_base, hs = list(SHA256_IV), None, []
+    for b in range(nblocks):
+        mb = pbase + 512 * b
+        words = [msg_word_bits(mb, t, 32) for t in range(16)]
+        base, state = c.sha_block(SHA256_SPEC, state, words, OP_SHA256, (prev_base, mb))
+        prev_base = base
+        hs.append(state)
+    out = []
+    for j in range(8):
+        for k in range(32):
+            i = 31 - k
+            acc = 0
+            for b in range(nblocks):
+                acc = c.mul(last[b], hs[b][j][i], acc)
+            out.append(acc)
+    return out
+
+
+def sha512_64(c: Circuit, byte_base: int):
+    """Sha512(512) (Electron-Labs/sha512, not on disk; used at nzcptpl.circom:577-580) for
+    a 64-byte message over byte wires with LSB-first bits: one block, constant padding
+    (0x80, zeros, 128-bit length 512). Output bits MSB first."""
+    words = [msg_word_bits(byte_base, t, 64) for t in range(8)]
+    words += [1 << 63] + [0] * 6 + [512]
+    _, H = c.sha_block(SHA512_SPEC, list(SHA512_IV), words, OP_SHA512, (None, byte_base))
+    return [H[j][63 - k] for j in range(8) for k in range(64)]
+
+
+def nzcp_pub_identity(is_live: int, max_tbs_bytes: int, max_array_len_vc: int, max_map_len_vc: int,
+                      max_array_len_cs: int = 2, max_map_len_cs: int = 4) -> Circuit:
+    """NZCPPubIdentity (nzcptpl.circom:444-655). Wires: 1, out[3], toBeSigned[8 * Max],
+    toBeSignedLen, data[160] (circom's order: outputs, then inputs as declared)."""
+    chunk_bits, byte_bits, data_len = 248, 8, 160
+    chunk_bytes = chunk_bits // byte_bits
+    claims_skip = 30 if is_live else 27
+    cred_subj_offset, null_bytes = 171, 64
+    max_bits = 8 * max_tbs_bytes
+    c = Circuit(3, 0, max_bits + 1 + data_len)
+    tbs = [w(c.in_base + i) for i in range(max_bits)]
+    tbs_len = w(c.in_base + max_bits)
+    data = [w(c.in_base + max_bits + 1 + i) for i in range(data_len)]
+    # bit checks (:493-496)
+    for i in range(max_bits):
+        c.check_quad(tbs[i], sub(tbs[i], 1), ERR_BIT)
+    # toBeSignedLen < Max + 1 (:500-505)
+    lt_max = c.less_than(tbs_len, max_tbs_bytes + 1, log2(max_tbs_bytes + 1) + 1, ERR_RANGE)
+    c.check_zero(sub(lt_max, 1), ERR_LEN)
+    # SHA-256 of ToBeSigned (:509-517)
+    sha256 = sha256_var(c, tbs, tbs_len, 3)
+    # bits -> bytes, zero past the length (:521-533)
+    tb = c.alloc(max_tbs_bytes)
+    bits = log2(max_tbs_bytes) + 1
+    for k in range(max_tbs_bytes):
+        b2n = add(*[scale(tbs[8 * k + 7 - i], 1 << i) for i in range(8)])
+        lt = c.less_than(k, tbs_len, bits, ERR_RANGE)
+        c.mul(b2n, lt, dst=tb + k)
+    tbytes = Bytes(tb, max_tbs_bytes)
+    map_len, nxt = read_map_length(c, tbytes, claims_skip)
+    vc_pos, exp = find_cwt_claims(c, tbytes, map_len, nxt, max_array_len_vc, max_map_len_vc)
+    names, max_str = read_cred_subj(c, tbytes, add(vc_pos, cred_subj_offset), null_bytes)
+    result = construct_nullifier(c, names, max_str, null_bytes)
+    nb = [c.num2bits(result[k], 8, ERR_RANGE) for k in range(null_bytes)]
+    nbase = next(iter(nb[0][0]))            # byte wires: nbase + 8k + j (LSB-first bits)
+    sha512 = sha512_64(c, nbase)
+    exp_bits = c.num2bits(exp, 32, ERR_RANGE)
+    ins = [[0] * chunk_bits for _ in range(3)]
+    for k in range(chunk_bytes):                                   # nullifier hash part (:596-601)
+        b = chunk_bytes - 1 - k
+        for i in range(byte_bits):
+            ins[0][b * byte_bits + (7 - i)] = sha512[k * byte_bits + i]
+    for k in range(8 // byte_bits):                                # (:602-607)
+        b = chunk_bytes - 1 - k
+        for i in range(byte_bits):
+            ins[1][b * byte_bits + (7 - i)] = sha512[chunk_bits + k * byte_bits + i]
+    for k in range(1, chunk_bytes):                                # ToBeSigned sha256 (:610-615)
+        b = chunk_bytes - 1 - k
+        for i in range(byte_bits):
+            ins[1][b * byte_bits + (7 - i)] = sha256[(k * byte_bits + i) - 8]
+    for k in range(16 // byte_bits):                               # (:616-621)
+        b = chunk_bytes - 1 - k
+        for i in range(byte_bits):
+            ins[2][b * byte_bits + (7 - i)] = sha256[chunk_bits + (k * byte_bits + i) - 8]
+    for idx, k in enumerate(range(2, 2 + 4)):                      # exp (:626-634)
+        b = chunk_bytes - 1 - k
+        d = 4 - 1 - idx
+        for i in range(byte_bits):
+            ins[2][b * byte_bits + i] = exp_bits[d * byte_bits + i]
+    for idx, k in enumerate(range(2 + 4, chunk_bytes)):            # pass-through data (:637-651)
+        b = chunk_bytes - 1 - k
+        for i in range(byte_bits):
+            if idx < data_len // byte_bits:
+                d = data_len // byte_bits - 1 - idx
+                ins[2][b * byte_bits + i] = data[d * byte_bits + i]
+    for j in range(3):                                             # Bits2Num(248) -> out (:653-655)
+        c.lin(add(*[scale(x, 1 << i) if isinstance(x, dict) else 0 for i, x in enumerate(ins[j])]),
+              dst=c.out_wires[j])
+    return c
