@@ -193,7 +193,8 @@ __device__ void sha_block(Fr* W, const Op& op, ShaShared& sh) {
   using S = Sha<B>;
   const int tid = threadIdx.x;
   const uint64_t mask = B == 64 ? ~0ull : 0xffffffffull;
-  // message bytes from the byte-wise bit wires (LSB first)
+  // message bytes from the byte-wise bit wires (LSB first); a wire that is not a bit
+  // (only in a witness that already failed a check) contributes its lowest bit
   for (int k = tid; k < 64; k += blockDim.x) {
     uint32_t byte = 0;
     for (int j = 0; j < 8; j++) byte |= (W[op.b_off + 8 * k + j].v[0] & 1u) << j;
@@ -482,7 +483,13 @@ __global__ void __launch_bounds__(kThreads) wvm_kernel(Prog P, const Fr* __restr
     W[0] = fr_small(1);
   }
   for (int k = threadIdx.x; k < 8 * 64 / 32; k += blockDim.x) sh.state_bits[k] = 0;
-  for (uint32_t i = threadIdx.x; i < P.n_inputs; i += blockDim.x) W[P.in_base + i] = in[i];
+  // inputs reduced mod r (a 256-bit value is below 6r), as circom reads signals
+  for (uint32_t i = threadIdx.x; i < P.n_inputs; i += blockDim.x) {
+    Fr x = in[i];
+#pragma unroll 1
+    for (int k = 0; k < 6; k++) x = reduce_once(x);
+    W[P.in_base + i] = x;
+  }
   __syncthreads();
   for (uint32_t lv = 0; lv < P.n_levels; lv++) {
     const uint32_t s0 = P.starts[lv], m0 = P.mstarts[lv], e0 = P.starts[lv + 1];

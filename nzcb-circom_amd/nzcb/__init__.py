@@ -799,7 +799,7 @@ def synth_context(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 
     zp, zl, wp, wl = _synth_raw(power, n_public, n_inputs, seed, n_constraints, tau, device, free_public)
     try:
         ctx = ProverContext(None, device=device, _raw=(zp, zl))
-        wtns = ctypes.string_at(wp, wl)
+        wtns = _take(wp, wl)
     finally:
         lib.nzcb_free(ctypes.cast(zp, c_void_p))
         lib.nzcb_free(ctypes.cast(wp, c_void_p))
@@ -812,8 +812,8 @@ def synth_setup(power: int, n_public: int = 3, n_inputs: int = 8, seed: int = 0x
     lib = load()
     zp, zl, wp, wl = _synth_raw(power, n_public, n_inputs, seed, n_constraints, tau, device, free_public)
     try:
-        zkey = ctypes.string_at(zp, zl)
-        wtns = ctypes.string_at(wp, wl)
+        zkey = _take(zp, zl)
+        wtns = _take(wp, wl)
     finally:
         lib.nzcb_free(ctypes.cast(zp, c_void_p))
         lib.nzcb_free(ctypes.cast(wp, c_void_p))
@@ -825,16 +825,33 @@ def plonk_setup(r1cs: bytes, ptau: bytes, device: int = 0) -> bytes:
     /root/reference/Makefile:55,60): returns the PLONK zkey bytes. The NTTs and the
     commitments run on `device`; raises NzcbError as snarkjs throws (curve mismatch,
     "circuit too big for this power of tau ceremony", "Variable not used")."""
+    ptr, size = plonk_setup_raw(r1cs, ptau, device)
+    try:
+        return _take(ptr, size)
+    finally:
+        load().nzcb_free(ptr)
+
+
+def plonk_setup_raw(r1cs: bytes, ptau: bytes, device: int = 0):
+    """plonk_setup returning the library-owned zkey buffer (pointer, length) without a
+    host copy (a 2^21 zkey is about 3.9 GB); release with nzcb.free_ptr."""
     lib = load()
     zp = POINTER(c_uint8)()
     zl = c_size_t()
     err = _Err()
     _check(lib.nzcb_plonk_setup(bytes(r1cs), len(r1cs), bytes(ptau), len(ptau), device, ctypes.byref(zp),
                                 ctypes.byref(zl), ctypes.byref(err)), err)
-    try:
-        return ctypes.string_at(zp, zl.value)
-    finally:
-        lib.nzcb_free(zp)
+    return ctypes.cast(zp, c_void_p).value, zl.value
+
+
+def free_ptr(ptr: int):
+    load().nzcb_free(ptr)
+
+
+def _take(ptr, size: int) -> bytes:
+    """bytes of a library buffer (ctypes.string_at takes an int size, < 2 GiB)."""
+    addr = ctypes.cast(ptr, c_void_p).value if not isinstance(ptr, int) else ptr
+    return bytes((c_uint8 * size).from_address(addr)) if size else b""
 
 
 def ptau_synth(power: int, tau: int, device: int = 0) -> bytes:
@@ -847,7 +864,7 @@ def ptau_synth(power: int, tau: int, device: int = 0) -> bytes:
     _check(lib.nzcb_ptau_synth(power, _buf(int(tau).to_bytes(32, "little")), device, ctypes.byref(pp),
                                ctypes.byref(pl), ctypes.byref(err)), err)
     try:
-        return ctypes.string_at(pp, pl.value)
+        return _take(pp, pl.value)
     finally:
         lib.nzcb_free(pp)
 

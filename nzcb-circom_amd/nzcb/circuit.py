@@ -362,7 +362,7 @@ class Circuit:
         def le(x):
             return (x % R).to_bytes(32, "little")
 
-        hdr = struct.pack("<I", 32) + le(R)
+        hdr = struct.pack("<I", 32) + R.to_bytes(32, "little")
         hdr += struct.pack("<IIIIQI", self.n_wires, self.n_out, self.n_pub_in, self.n_prv_in, self.n_wires,
                            len(self.constraints))
         parts = []

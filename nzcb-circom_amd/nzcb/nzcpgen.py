@@ -59,8 +59,10 @@ def get_x(c: Circuit, v):
 
 
 def get_v(c: Circuit, b: Bytes, pos):
-    """GetV (cbortpl.circom:78-90): QuinSelector(BytesLen)."""
-    return c.quin(b.n, b.base, b.n, pos, ERR_RANGE, ERR_SELECT)
+    """GetV (cbortpl.circom:78-90): QuinSelector(BytesLen). Both of QuinSelector's checks
+    (the LessThan's Num2Bits and ``lessThan.out === 1``) report ERR_SELECT, as the
+    restatement oracle/nzcp_circuit.py quin_selector classifies them."""
+    return c.quin(b.n, b.base, b.n, pos, ERR_SELECT, ERR_SELECT)
 
 
 def decode_uint23(c: Circuit, v):
@@ -220,9 +222,9 @@ def construct_nullifier(c: Circuit, names, max_str: int, max_buffer_len: int):
         under_sep1 = c.less_than(k, add(gl, 1), bits, ERR_RANGE)
         under_family = c.less_than(k, add(gl, 1, fl), bits, ERR_RANGE)
         under_sep2 = c.less_than(k, add(gl, 1, fl, 1), bits, ERR_RANGE)
-        g_sel = c.quin(max_buffer_len, gb, max_str, k, ERR_RANGE, ERR_SELECT)
-        f_sel = c.quin(max_buffer_len, fb, max_str, sub(sub(k, gl), 1), ERR_RANGE, ERR_SELECT)
-        d_sel = c.quin(max_buffer_len, db, max_str, sub(sub(sub(sub(k, gl), 1), fl), 1), ERR_RANGE, ERR_SELECT)
+        g_sel = c.quin(max_buffer_len, gb, max_str, k, ERR_SELECT, ERR_SELECT)
+        f_sel = c.quin(max_buffer_len, fb, max_str, sub(sub(k, gl), 1), ERR_SELECT, ERR_SELECT)
+        d_sel = c.quin(max_buffer_len, db, max_str, sub(sub(sub(sub(k, gl), 1), fl), 1), ERR_SELECT, ERR_SELECT)
         not_given = sub(1, is_given)
         is_sep1 = c.mul(under_sep1, not_given)
         is_family = c.mul(under_family, sub(1, under_sep1))

@@ -64,11 +64,25 @@ def build(params: dict = nzcpgen.LIVE, cache: bool = True):
 PTAU_POWER = 21                 # powersOfTau28_hez_final_21.ptau (/root/reference/README.md:40)
 
 
-def setup(r1cs: bytes, tau: int = TAU, device: int = 0, ptau_power: int = PTAU_POWER) -> bytes:
+def setup_raw(r1cs: bytes, tau: int = TAU, device: int = 0, ptau_power: int = PTAU_POWER):
     """PLONK zkey of the r1cs (nzcb_plonk_setup) against a seeded-tau ptau of the
-    reference's ceremony power; raises like snarkjs if the circuit does not fit."""
+    reference's ceremony power, as a library-owned (pointer, length) buffer (release with
+    nzcb.free_ptr); raises like snarkjs if the circuit does not fit."""
     import nzcb
-    return nzcb.plonk_setup(r1cs, nzcb.ptau_synth(ptau_power, tau, device), device)
+    return nzcb.plonk_setup_raw(r1cs, nzcb.ptau_synth(ptau_power, tau, device), device)
+
+
+def context(r1cs: bytes, tau: int = TAU, device: int = 0):
+    """(ProverContext on the zkey, the zkey's raw buffer) without copying the zkey through
+    Python; the caller frees the buffer with nzcb.free_ptr once it no longer needs it."""
+    import nzcb
+    raw = setup_raw(r1cs, tau, device)
+    try:
+        ctx = nzcb.ProverContext(None, device=device, _raw=raw)
+    except Exception:
+        nzcb.free_ptr(raw[0])
+        raise
+    return ctx, raw
 
 
 class NzcpLiveProver:

@@ -135,11 +135,13 @@ def sha_block_values(bits: int, state: list, msg_words: list) -> list:
 
 def _sha_final_words(bits, wit, base, size):
     fb = base + size - 8 * (bits + 1)
-    return [sum(wit[fb + j * (bits + 1) + i] << i for i in range(bits)) for j in range(8)]
+    return [sum((wit[fb + j * (bits + 1) + i] & 1) << i for i in range(bits)) for j in range(8)]
 
 
 def _msg_words(wit, byte_base, nbytes, bits):
-    data = bytes(sum(wit[byte_base + 8 * k + j] << j for j in range(8)) for k in range(nbytes))
+    # a message wire that is not a bit (only in a witness that already failed a check)
+    # contributes its lowest bit, as the GPU VM reads it
+    data = bytes(sum((wit[byte_base + 8 * k + j] & 1) << j for j in range(8)) for k in range(nbytes))
     nb = bits // 8
     return [int.from_bytes(data[nb * t:nb * t + nb], "big") for t in range(len(data) // nb)]
 

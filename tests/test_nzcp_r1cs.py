@@ -107,7 +107,7 @@ def test_r1cs_file_round_trip():
     c = Circuit(0, 0, 512)
     nzcpgen.sha512_64(c, c.in_base)
     rd = r1cs_oracle.read_r1cs(c.write_r1cs())
-    assert rd["nWires"] == c.n_wires and rd["nPrvInputs"] == 512
+    assert rd["prime"] == R and rd["nWires"] == c.n_wires and rd["nPrvInputs"] == 512
     assert len(rd["constraints"]) == len(c.constraints)
     for (A, B, Cc), (a, b, cc) in zip(c.constraints[::997], rd["constraints"][::997]):
         assert dict(a) == A and dict(b) == B and dict(cc) == Cc
