@@ -5,17 +5,20 @@ Metric and config come from BASELINE.json: "PLONK proofs/sec for nzcp_live
 (~2^21 constraints) at 1/2/4/8 MI355X"; workload = configs[2] (single nzcp_live
 proof on one GPU), batch-sharded with no collective across ranks (configs[3]).
 
-A "step" is one plonk.fullProve of one NZ COVID Pass: the GPU nzcp witness kernel
-computes the pass's public signals (NZCPPubIdentity outputs)
-into that proof's HBM witness, then the full proof runs (snarkjs plonk_prove
-rounds 1-5, a3-a12). The passes' input signals and the rest of the witness are
-resident in HBM when the timed region starts; the 800-byte proofs and the public
-signals are copied back to the host inside it.
-The K timed proofs are one nzcb_prove_batch call: --lanes proofs are in flight
-on each GPU (lanes share the HBM-resident proving key; SURVEY.md §8e batch mode),
-so one proof's latency-bound phases overlap another's compute.
-The circuit is the seeded synthetic nzcp_live stand-in:
-the real nzcp_live_final.zkey / circom witness cannot be built offline.
+The statement is the reference's circuit, NZCPPubIdentity(1, 351, 0, 4, 2, 4)
+(/root/reference/circuits/nzcp_live.circom), compiled by nzcb/nzcpgen.py to an r1cs
+(603,800 constraints, 1.79 M PLONK gates, domain 2^21) and a witness program; the
+zkey comes from nzcb_plonk_setup against a seeded-tau ptau of power 21 (the ceremony
+file powersOfTau28_hez_final_21.ptau and circom are not on disk).
+
+A "step" is one plonk.fullProve of one NZ COVID Pass: the GPU witness program
+computes all 600,560 signals of the pass's witness in HBM (nzcb_wprog_run_dev, the
+circom witness calculator's job), then the full proof runs (snarkjs plonk_prove rounds
+1-5). The passes' input signals are resident in HBM when the timed region starts;
+the 800-byte proofs and the public signals are copied back inside it. The K timed
+proofs are one witness launch plus one nzcb_prove_batch call: --lanes proofs are in
+flight on each GPU (lanes share the HBM-resident proving key; SURVEY.md §8e batch
+mode), so one proof's latency-bound phases overlap another's compute.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -46,7 +49,7 @@ MSM_BYTES_PER_POINT = 96       # 64 B affine base + 32 B scalar
 PROOF_BYTES_PER_N = 7104       # algorithmic bytes per proof = 7104 * n
 NZCP_INPUTS = 2970             # nzcp_live input signals (toBeSigned bits + len + data)
 SEED = 0x6E7A6362
-TAU = 0x6E7A6362746175
+TAU = 0x6E7A6362746175         # seeded ptau trapdoor
 # The dominant kernel (fixed-base bucket accumulation) is bound by VALU integer
 # multiply issue, not by HBM (SURVEY.md §8d "Bounding roofline"). Its algorithmic
 # work is the 9x29-bit Montgomery products of one XYZZ mixed addition per bucket
@@ -121,10 +124,12 @@ def accumulate_probe(n_points: int, device: int, reps: int = 10) -> dict:
     return ph
 
 
-def cpu_baseline_sample(power: int):
-    """Time the CPU port (oracle) on a bounded sample; rank 0, N=1 only."""
+def cpu_baseline_sample(zkey_raw, wtns: bytes, n: int):
+    """Time the CPU port (oracle) proving one proof of the same zkey and witness; rank 0,
+    N=1 only."""
     from oracle import cbind
-    return cbind.timed_sample(power)
+    return cbind.timed_prove(zkey_raw, wtns, f"1 full proof of nzcp_live (n=2^{n.bit_length() - 1}, same zkey "
+                                             f"and GPU-computed witness)")
 
 
 def main():
@@ -132,7 +137,6 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--power", type=int, default=21, help="log2 PLONK domain (nzcp_live: 21)")
     ap.add_argument("--lanes", type=int, default=5, help="proofs in flight per GPU")
     ap.add_argument("--batch", type=int, default=0,
                     help="fixed total batch sharded over the ranks (configs[3]: 512); default: --steps per rank")
@@ -161,16 +165,16 @@ def main():
             dist.init_process_group(backend)
 
     import nzcb
-    n = 1 << args.power
+    from nzcb import nzcplive
     t_setup = time.time()
-    # public signals on their public-input gates only, so each pass's nzcp outputs can
-    # be written into witness[1..3] (NZCB_SYNTH_FREE_PUBLIC)
-    ctx, wtns = nzcb.synth_context(args.power, 3, NZCP_INPUTS, SEED, 0, TAU, device=device, free_public=True)
+    # the real statement: NZCPPubIdentity(1, 351, 0, 4, 2, 4) compiled to an r1cs and a
+    # witness program (nzcb/nzcpgen.py), zkey from nzcb_plonk_setup against a seeded
+    # ptau of the reference's power 21 (Makefile:59-62)
+    r1cs, program, _ = nzcplive.build()
+    ctx, zkey_raw = nzcplive.context(r1cs, TAU, device)
     setup_s = time.time() - t_setup
-    nwit = (len(wtns) - 76) // 32
-    dev_w = nzcb.dev_alloc(nwit * 32)
-    nzcb.h2d(dev_w, wtns[76:76 + nwit * 32])
-    prover = nzcb.NzcpProver(ctx, wtns[76:76 + nwit * 32], nzcb.NZCP_LIVE)
+    n = ctx.domain_size
+    prover = nzcplive.NzcpLiveProver(ctx, program)
 
     def barrier():
         if dist is not None:
@@ -178,8 +182,14 @@ def main():
             torch.cuda.synchronize(device)
             dist.barrier()
 
-    # single-proof latency (one lane) and the PCIe-inclusive rate (host witness) for
-    # DESIGN.md; neither is the reported value
+    # one pass's witness for the single-proof latency and the PCIe-inclusive rate
+    # (neither is the reported value) and the CPU baseline's sample
+    prover.upload_inputs(pass_inputs([999]))
+    (w0,) = prover.witness_staged(1)
+    nwit = prover.n_witness
+    dev_w = nzcb.dev_alloc(nwit * 32)
+    nzcb.d2d(dev_w, w0, nwit * 32)
+    wit_host = nzcb.d2h(dev_w, nwit * 32)
     ctx.prove_device_raw(dev_w, nwit, blinding_for(998))
     ctx.kernel_stats(1)
     t_l = time.perf_counter()
@@ -188,7 +198,7 @@ def main():
     lat_kms, lat_klaunch, _, _ = ctx.kernel_stats(0)  # one proof in flight: the kernel nearly alone
     single_timings = ctx.last_timings()
     t_h = time.perf_counter()
-    ctx.prove_witness_raw(wtns[76:76 + nwit * 32], blinding_for(999))
+    ctx.prove_witness_raw(wit_host, blinding_for(999))
     pcie_ms = (time.perf_counter() - t_h) * 1e3
     msm_devices = [int(x) for x in args.msm_devices.split(",") if x.strip() != ""]
     if msm_devices:
@@ -208,21 +218,23 @@ def main():
         prover.witness_buffers(len(mine))
     barrier()
     t0 = time.perf_counter()
-    proofs, records = prover.full_prove_staged(len(mine), blinds)
+    proofs = prover.full_prove_staged(len(mine), blinds)   # GPU witness program + prove_batch
     barrier()
     elapsed = time.perf_counter() - t0
     kms, klaunch, kpoints, kentries = ctx.kernel_stats(0)
     assert len({p for p, _ in proofs}) == len(mine)  # distinct passes -> distinct proofs
-    # every proof's public signals are its pass's nzcp outputs; full-size parity by a
-    # size-independent property: the pairing verifier accepts the first and last proof
-    # of the timed batch (host, outside the timed region)
-    pubs_ok = all([int.from_bytes(pub[32 * k:32 * k + 32], "little") for k in range(3)] == r["out"]
+    # full-size checks outside the timed region: every proof's public signals equal its
+    # pass's outputs from the independent nzcp kernel (csrc/nzcp.hip, bit-exact against
+    # the restatement pinned by the reference's KATs), and the pairing verifier accepts
+    # the first and last proof of the batch
+    records = nzcb.nzcp_witness(pass_inputs(mine), len(mine), nzcb.NZCP_LIVE, device) if mine else []
+    pubs_ok = all(r["status"] == 0 and [int.from_bytes(pub[32 * k:32 * k + 32], "little") for k in range(3)] == r["out"]
                   for (_, pub), r in zip(proofs, records))
     verified = pubs_ok and all(nzcb.verify(ctx.vk, proofs[i][0], proofs[i][1])
                                for i in ({0, len(proofs) - 1} if proofs else ()))
     t_w = time.perf_counter()
     prover.witness_staged(len(mine))
-    nzcp_ms = (time.perf_counter() - t_w) * 1e3
+    witness_ms = (time.perf_counter() - t_w) * 1e3
     probe = accumulate_probe(n + 6, device) if rank == 0 and not args.no_probe else None
     elapsed = max_over_ranks(elapsed, dist, f"cuda:{device}" if backend == "nccl" else "cpu")
     total_proofs = args.batch if args.batch else args.steps * world
@@ -250,7 +262,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline_sample(args.power)
+                cpu = cpu_baseline_sample(zkey_raw, nzcplive.wtns_file(wit_host), n)
             except Exception as e:  # reported, never silently replaced
                 cpu = {"value": None, "unit": "proofs/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
         proof_gbs = PROOF_BYTES_PER_N * n / (ms_step / 1e3) / 1e9
@@ -266,13 +278,12 @@ def main():
             "scaling": "strong" if args.batch else "weak",
             "vs_baseline": None,
             "dtype": "u32 limbs: BN254 Fr/Fq Montgomery, 8x32-bit and 9x29-bit (MSM, NTT twiddles, quotient)",
-            "data": "synthetic: seeded satisfied PLONK circuit with free public wires, snarkjs-0.4 zkey with trapdoor "
-                    "tau (SURVEY §8d cfg 3); public signals = nzcp witness kernel outputs of distinct live-shaped "
-                    "passes (data bytes vary per proof). The synthetic circuit does not constrain its public "
-                    "signals to the pass: the host checks them against the witness records",
+            "data": "synthetic passes: live-shaped NZ COVID Pass ToBeSigned (live key id and issuer) with 20 "
+                    "pass-through data bytes that differ per proof; proving key from a seeded-tau ptau (SURVEY §8d)",
             "config": {
-                "workload": f"nzcp_live fullProve (GPU nzcp witness -> witness[1..3], PLONK proof), "
-                            f"n=2^{args.power}, nPublic=3, {NZCP_INPUTS} inputs",
+                "workload": f"nzcp_live fullProve: NZCPPubIdentity(1,351,0,4,2,4) witness on the GPU "
+                            f"({prover.n_witness} signals) + PLONK proof, n=2^{n.bit_length() - 1}, nPublic=3, "
+                            f"{NZCP_INPUTS} inputs",
                 "domain_size": n,
                 "n_public": 3,
                 "n_constraints": ctx.n_constraints,
@@ -314,7 +325,7 @@ def main():
                 "frac": round(proof_gbs / HBM_PEAK_GBS, 5),
             },
             "proofs_verified": verified,
-            "nzcp_witness_ms_per_batch": round(nzcp_ms, 3),
+            "witness_program_ms_per_batch": round(witness_ms, 3),
             "single_proof_latency_ms": round(latency_ms, 3),
             "phase_ms_single_proof": {k: round(v, 3) for k, v in single_timings.items()},
             "pcie_inclusive_ms": round(pcie_ms, 3),
@@ -329,7 +340,9 @@ def main():
         if not verified:
             sys.exit(3)
     nzcb.dev_free(dev_w)
+    prover.close()
     ctx.close()
+    nzcb.free_ptr(zkey_raw[0])
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

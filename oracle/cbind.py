@@ -106,3 +106,15 @@ def timed_sample(power: int, threads: int | None = None):
     return {"value": round(1.0 / wall, 5), "unit": "proofs/s", "cores": th, "kind": "port",
             "sample": f"1 full proof, n=2^{power} synthetic nzcp_live, oracle/c/nzcb_ref.c on {threads_reason(th)} "
                       f"({wall:.1f} s; msm {t['msm']:.1f} s, ntt {t['ntt']:.1f} s)"}
+
+
+def timed_prove(zkey, wtns, what: str, threads: int | None = None):
+    """bench.py cpu_baseline: one full proof of the given zkey ((pointer, length) or bytes)
+    and wtns on `threads` host cores."""
+    th = threads or default_threads()
+    t0 = time.time()
+    _, _, t = prove(zkey, wtns, bytes(352), True, th, 3)
+    wall = time.time() - t0
+    return {"value": round(1.0 / wall, 5), "unit": "proofs/s", "cores": th, "kind": "port",
+            "sample": f"{what}, oracle/c/nzcb_ref.c on {threads_reason(th)} "
+                      f"({wall:.1f} s; msm {t['msm']:.1f} s, ntt {t['ntt']:.1f} s)"}
