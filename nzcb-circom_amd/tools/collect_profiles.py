@@ -58,10 +58,10 @@ def main():
                    "--no-cpu-baseline --steps 8",
         "counters_kb_per_launch": {"FETCH_SIZE": {"launches": nf, "avg_kb_per_launch": round(fetch_kb, 1)},
                                    "WRITE_SIZE": {"launches": nw, "avg_kb_per_launch": round(write_kb, 1)}},
-        "correction": "gfx950 FETCH_SIZE counts half the bytes of 16 B/lane reads (MI355X_MICROARCH.md, HBM "
-                      "section): fetch doubled; WRITE_SIZE as reported",
+        "correction": "none: random 64-byte gathers are counted at ~1.15x their bytes, not 1/2 "
+                      "(profiles/r2_fetch_calibration.txt, tools/gather_calib.hip); FETCH_SIZE + WRITE_SIZE as reported",
         "fetch_bytes_per_launch_raw": int(fetch_raw),
-        "bytes_per_launch": int(2 * fetch_raw + write_kb * 1024),
+        "bytes_per_launch": int(fetch_raw + write_kb * 1024),
         "note": "gathers are random 64 B affine table points (16 B/lane dwordx4 loads); algorithmic bytes "
                 "96 B x 2^21 points = 201 MB; gathered table bytes 64 B x 31.5 M entries = 2.0 GB",
     }
