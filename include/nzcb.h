@@ -68,6 +68,12 @@ int nzcb_device_count(void);
 /* Parse a snarkjs 0.4 PLONK zkey and upload it to `device` (HBM-resident,
  * context-owned). Replaces the zkey read in snarkjs plonk_prove.js [EXT]. */
 nzcb_ctx* nzcb_ctx_create(const uint8_t* zkey, size_t zkey_len, int device, nzcb_err* err);
+/* SURVEY.md §8b's form: one context over a device set. Every device holds its own
+ * HBM-resident copy of the proving key; nzcb_prove_batch spreads its items over the
+ * lanes of all devices (nzcb_ctx_set_lanes sets lanes per device); single proofs run on
+ * devices[0]. nzcb_ctx_create(z, len, d, err) is this with devices = {d}. */
+nzcb_ctx* nzcb_ctx_create_devices(const uint8_t* zkey, size_t zkey_len, const int* devices, int ndev, nzcb_err* err);
+int nzcb_ctx_devices(const nzcb_ctx* ctx);
 void nzcb_ctx_destroy(nzcb_ctx* ctx);
 
 /* Optional progress logger (snarkjs `logger.debug` lines). */
@@ -108,10 +114,27 @@ int nzcb_ctx_lanes(const nzcb_ctx* ctx);
  * restores the single-device schedule. Results are bit-identical either way. */
 int nzcb_ctx_set_msm_devices(nzcb_ctx* ctx, const int* devices, int ndev, nzcb_err* err);
 
+/* The same split across processes, one rank per GPU (scalars by
+ * RCCL broadcast, one 64-byte partial per rank back by all-gather; the collectives live in
+ * the host runtime, e.g. torch.distributed, see nzcb/msmsplit.py). The context (rank 0)
+ * computes PTau points [0, own_points) of every commitment of lane 0 and calls
+ *   send(user, slot, dev_scalars, count): the commitment's `count` scalars (32-byte
+ *       Montgomery Fr, HBM of the context's device) are ready; the other ranks take the
+ *       points [own_points, count) of it; called when the commitment starts
+ *   gather(user, slot, own_partial, partials_out): returns world x 64 bytes, every rank's
+ *       partial sum (affine x || y, 32-byte LE normal form, infinity = zeros) in rank
+ *       order (own_partial at index 0); called when the commitment is needed
+ * Up to 3 commitments (slot 0..2) are in flight at once. A callback returning non-zero
+ * fails the proof. world = 1 or NULL callbacks restore the local schedule. */
+typedef int (*nzcb_msm_send_fn)(void* user, int slot, const void* dev_scalars, size_t count);
+typedef int (*nzcb_msm_gather_fn)(void* user, int slot, const uint8_t* own_partial, uint8_t* partials_out);
+int nzcb_ctx_set_msm_split(nzcb_ctx* ctx, int world, size_t own_points, nzcb_msm_send_fn send,
+                           nzcb_msm_gather_fn gather, void* user, nzcb_err* err);
+
 /* `count` independent proofs over the context's lanes (SURVEY.md §8b nzcb_prove_batch,
  * §8e batch mode). witnesses[i]: nWitness x 32-byte LE normal-form values, host memory,
  * or device pointers when witness_on_device. blindings: count x NZCB_BLINDING_BYTES or
- * NULL (all zero). proofs_out: count x NZCB_PROOF_BYTES. pubs_out: count x pub_stride
+ * NULL (random per proof, see `blinding` above). proofs_out: count x NZCB_PROOF_BYTES. pubs_out: count x pub_stride
  * (pub_stride >= 32 * nPublic). Returns the error of the lowest failing index. */
 int nzcb_prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_witness, int count, int witness_on_device,
                      const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out, size_t pub_stride,
@@ -301,6 +324,16 @@ int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars,
 /* Fixed-base schedule (the prover's): builds the shifted-base table of the first
  * n_table bases (2^(20w) multiples, 13 rows), then runs the MSM of the first n.
  * One-shot (table and scratch freed on return); for parity tests. */
+/* A resident fixed-base MSM table over n device bases (affine LEM, e.g. a PTau range),
+ * the prover's c = 17 shifted-base schedule: the serving ranks of nzcb_ctx_set_msm_split
+ * keep one and answer every commitment with one run. out_affine: 64 bytes, x || y normal
+ * form LE (infinity = zeros); scalars: `count` <= n 32-byte values in HBM, Montgomery
+ * form when scalars_mont (the prover's coefficients). */
+typedef struct nzcb_msm_table nzcb_msm_table;
+nzcb_msm_table* nzcb_msm_table_create(int device, const void* dev_bases, size_t n, nzcb_err* err);
+int nzcb_msm_table_run(nzcb_msm_table* t, const void* dev_scalars, size_t count, int scalars_mont,
+                       uint8_t* out_affine, nzcb_err* err);
+void nzcb_msm_table_destroy(nzcb_msm_table* t);
 int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
                               int scalars_mont, uint8_t* out_affine, nzcb_err* err);
 /* Batch-affine pairing rounds ahead of the fixed-base bucket accumulation (each halves

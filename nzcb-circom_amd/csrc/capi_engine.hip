@@ -315,4 +315,57 @@ int nzcb_engine_fr_mul(nzcb_engine* e, const uint8_t* a_lem, const uint8_t* b_le
   NZ_GUARD_END(err)
 }
 
+// ---- resident fixed-base MSM tables (the serving ranks of nzcb_ctx_set_msm_split) ----
+struct nzcb_msm_table {
+  int device = 0;
+  size_t n = 0;
+  MsmBaseTable table;
+  MsmScratch sc;
+  hipStream_t st = nullptr;
+  ~nzcb_msm_table() {
+    (void)hipSetDevice(device);
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
+nzcb_msm_table* nzcb_msm_table_create(int device, const void* dev_bases, size_t n, nzcb_err* err) {
+  try {
+    if (!dev_bases || n == 0) throw Error(NZCB_ERR_ARG, "msm table: no bases");
+    NZ_HIP(hipSetDevice(device));
+    auto t = new nzcb_msm_table();
+    try {
+      t->device = device;
+      t->n = n;
+      NZ_HIP(hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking));
+      t->table.build((const G1Affine*)dev_bases, n, fixed_base_window(), t->st);
+      t->sc.init(n, true);
+      NZ_HIP(hipStreamSynchronize(t->st));
+    } catch (...) {
+      delete t;
+      throw;
+    }
+    return t;
+  } catch (const Error& e) {
+    set_err(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+  }
+  return nullptr;
+}
+
+int nzcb_msm_table_run(nzcb_msm_table* t, const void* dev_scalars, size_t count, int scalars_mont,
+                       uint8_t* out_affine, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  if (!t || !out_affine || (count && !dev_scalars)) throw Error(NZCB_ERR_ARG, "msm table: null argument");
+  if (count > t->n) throw Error(NZCB_ERR_ARG, "msm larger than its base table");
+  NZ_HIP(hipSetDevice(t->device));
+  G1xyzz r = count ? msm(t->sc, nullptr, (const Fr*)dev_scalars, count, scalars_mont != 0, t->st, &t->table)
+                   : G1xyzz::inf();
+  affine_out(r, out_affine);
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+void nzcb_msm_table_destroy(nzcb_msm_table* t) { delete t; }
+
 }  // extern "C"

@@ -35,13 +35,27 @@ std::string dec_le32(const uint8_t* le32) {
 using namespace nzcb;
 
 struct nzcb_ctx {
-  std::unique_ptr<Prover> p;                   // lane 0: owns the HBM-resident proving key
-  std::vector<std::unique_ptr<Prover>> extra;  // lanes 1..: share it (nzcb_ctx_set_lanes)
+  std::unique_ptr<Prover> p;                   // device 0, lane 0: owns that device's proving key
+  std::vector<std::unique_ptr<Prover>> extra;  // device 0, lanes 1..: share it (nzcb_ctx_set_lanes)
+  // devices 1.. of a device-set context (nzcb_ctx_create_devices): each holds its own
+  // HBM-resident copy of the proving key in its lane 0 and the same number of lanes
+  std::vector<std::unique_ptr<Prover>> dev_p;
+  std::vector<std::vector<std::unique_ptr<Prover>>> dev_extra;
   nzcb_log_fn log_fn = nullptr;
   void* log_user = nullptr;
   std::mutex mu;  // calls on one context are serialized (SURVEY.md §8b "Threading")
   Prover* lane(size_t i) { return i == 0 ? p.get() : extra[i - 1].get(); }
-  size_t lanes() const { return 1 + extra.size(); }
+  size_t lanes() const { return 1 + extra.size(); }  // per device
+  // every lane of every device (batch workers), device-interleaved so that a short batch
+  // spreads over the devices first
+  std::vector<Prover*> all() {
+    std::vector<Prover*> v;
+    for (size_t l = 0; l < lanes(); l++) {
+      v.push_back(lane(l));
+      for (size_t d = 0; d < dev_p.size(); d++) v.push_back(l == 0 ? dev_p[d].get() : dev_extra[d][l - 1].get());
+    }
+    return v;
+  }
 };
 
 namespace {
@@ -86,6 +100,38 @@ nzcb_ctx* nzcb_ctx_create(const uint8_t* zkey, size_t zkey_len, int device, nzcb
   return nullptr;
 }
 
+nzcb_ctx* nzcb_ctx_create_devices(const uint8_t* zkey, size_t zkey_len, const int* devices, int ndev, nzcb_err* err) {
+  if (!devices || ndev < 1 || ndev > 64) {
+    set_err(err, NZCB_ERR_ARG, "devices: 1..64 ids");
+    return nullptr;
+  }
+  for (int i = 0; i < ndev; i++)
+    for (int j = 0; j < i; j++)
+      if (devices[i] == devices[j]) {
+        set_err(err, NZCB_ERR_ARG, "devices: an id appears twice");
+        return nullptr;
+      }
+  nzcb_ctx* c = nzcb_ctx_create(zkey, zkey_len, devices[0], err);
+  if (!c) return nullptr;
+  try {
+    for (int i = 1; i < ndev; i++) {
+      c->dev_p.emplace_back(new Prover(zkey, zkey_len, devices[i]));
+      c->dev_extra.emplace_back();
+    }
+    NZ_HIP(hipSetDevice(devices[0]));
+    if (err) err->code = 0;
+    return c;
+  } catch (const Error& e) {
+    set_err(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+  }
+  delete c;
+  return nullptr;
+}
+
+int nzcb_ctx_devices(const nzcb_ctx* ctx) { return ctx ? 1 + (int)ctx->dev_p.size() : 0; }
+
 void nzcb_ctx_destroy(nzcb_ctx* ctx) { delete ctx; }
 
 void nzcb_ctx_set_logger(nzcb_ctx* ctx, nzcb_log_fn fn, void* user) {
@@ -93,30 +139,38 @@ void nzcb_ctx_set_logger(nzcb_ctx* ctx, nzcb_log_fn fn, void* user) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->log_fn = fn;
   ctx->log_user = user;
-  for (size_t i = 0; i < ctx->lanes(); i++) {
+  for (Prover* q : ctx->all()) {
     if (fn)
-      ctx->lane(i)->log = [ctx](const std::string& m) { ctx->log_fn(ctx->log_user, m.c_str()); };
+      q->log = [ctx](const std::string& m) { ctx->log_fn(ctx->log_user, m.c_str()); };
     else
-      ctx->lane(i)->log = nullptr;
+      q->log = nullptr;
   }
 }
 
 void nzcb_ctx_set_transcript_public(nzcb_ctx* ctx, int on) {
   if (!ctx) return;
   std::lock_guard<std::mutex> lk(ctx->mu);
-  for (size_t i = 0; i < ctx->lanes(); i++) ctx->lane(i)->transcript_public = on != 0;
+  for (Prover* q : ctx->all()) q->transcript_public = on != 0;
 }
 
 int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err) {
   if (!ctx || lanes < 1 || lanes > 16) return fail(err, NZCB_ERR_ARG, "lanes must be in 1..16");
   try {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    while (ctx->lanes() > (size_t)lanes) ctx->extra.pop_back();
-    while (ctx->lanes() < (size_t)lanes) {
-      ctx->extra.emplace_back(new Prover(*ctx->p, (int)ctx->lanes()));
-      Prover* q = ctx->extra.back().get();
-      q->log = ctx->p->log;
+    while (ctx->lanes() > (size_t)lanes) {
+      ctx->extra.pop_back();
+      for (auto& de : ctx->dev_extra) de.pop_back();
     }
+    while (ctx->lanes() < (size_t)lanes) {
+      const int l = (int)ctx->lanes();
+      ctx->extra.emplace_back(new Prover(*ctx->p, l));
+      ctx->extra.back()->log = ctx->p->log;
+      for (size_t d = 0; d < ctx->dev_p.size(); d++) {
+        ctx->dev_extra[d].emplace_back(new Prover(*ctx->dev_p[d], l));
+        ctx->dev_extra[d].back()->log = ctx->p->log;
+      }
+    }
+    NZ_HIP(hipSetDevice(ctx->p->eng->device));
     if (err) err->code = 0;
     return 0;
   } catch (const Error& e) {
@@ -133,6 +187,21 @@ int nzcb_ctx_set_msm_devices(nzcb_ctx* ctx, const int* devices, int ndev, nzcb_e
   try {
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->p->set_msm_devices(std::vector<int>(devices, devices + ndev));
+    if (err) err->code = 0;
+    return 0;
+  } catch (const Error& e) {
+    return fail(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    return fail(err, NZCB_ERR_INTERNAL, e.what());
+  }
+}
+
+int nzcb_ctx_set_msm_split(nzcb_ctx* ctx, int world, size_t own_points, nzcb_msm_send_fn send,
+                           nzcb_msm_gather_fn gather, void* user, nzcb_err* err) {
+  if (!ctx || world < 1 || world > 1024) return fail(err, NZCB_ERR_ARG, "msm split: world must be in 1..1024");
+  try {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->p->set_msm_split(world, own_points, send, gather, user);
     if (err) err->code = 0;
     return 0;
   } catch (const Error& e) {
@@ -183,10 +252,14 @@ static int prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_wit
       }
     }
   };
-  const size_t nl = std::min(ctx->lanes(), (size_t)(count > 0 ? count : 1));
+  // lane 0 of device 0 is the only lane whose commitments a split (nzcb_ctx_set_msm_devices /
+  // nzcb_ctx_set_msm_split) covers, so a split context proves its batch on lane 0 alone
+  std::vector<Prover*> ws = ctx->p->split_send || !ctx->p->shards.empty() ? std::vector<Prover*>{ctx->p.get()}
+                                                                         : ctx->all();
+  const size_t nl = std::min(ws.size(), (size_t)(count > 0 ? count : 1));
   std::vector<std::thread> th;
-  for (size_t l = 1; l < nl; l++) th.emplace_back(worker, ctx->lane(l));
-  worker(ctx->lane(0));
+  for (size_t l = 1; l < nl; l++) th.emplace_back(worker, ws[l]);
+  worker(ws[0]);
   for (auto& t : th) t.join();
   if (status_out)
     for (int i = 0; i < count; i++) status_out[i] = codes[i];
@@ -283,8 +356,8 @@ int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
   if (!ctx) return NZCB_ERR_ARG;
   if (out) {
     for (int i = 0; i < 4; i++) out[i] = 0;
-    for (size_t l = 0; l < ctx->lanes(); l++)
-      for (auto& m : ctx->lane(l)->msc) {
+    for (Prover* q : ctx->all())
+      for (auto& m : q->msc) {
         out[0] += m->prof_ms;
         out[1] += (double)m->prof_launches;
         out[2] += (double)m->prof_points;
@@ -292,8 +365,8 @@ int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
       }
   }
   if (enable >= 0) {
-    for (size_t l = 0; l < ctx->lanes(); l++)
-      for (auto& m : ctx->lane(l)->msc) {
+    for (Prover* q : ctx->all())
+      for (auto& m : q->msc) {
         m->prof = enable != 0;
         m->prof_ms = 0;
         m->prof_launches = m->prof_points = m->prof_entries = 0;

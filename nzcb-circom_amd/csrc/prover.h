@@ -83,6 +83,17 @@ struct Prover {
   void set_msm_devices(const std::vector<int>& devices);
   std::vector<std::unique_ptr<MsmShard>> shards;
   size_t own_hi = 0;  // this device's MSM point range is [0, own_hi) when shards exist
+  // SURVEY.md §8e config 5 across processes (one rank per GPU, RCCL over xGMI): this
+  // prover computes the points [0, split_own) of every commitment; `split_send` hands the
+  // commitment's scalars (HBM) to the other ranks as soon as they are ready and
+  // `split_gather` returns every rank's 64-byte affine partial (rank order), which are
+  // added here. Both are caller callbacks (the collectives live in the host runtime).
+  nzcb_msm_send_fn split_send = nullptr;
+  nzcb_msm_gather_fn split_gather = nullptr;
+  void* split_user = nullptr;
+  int split_world = 1;
+  size_t split_own = 0;
+  void set_msm_split(int world, size_t own_points, nzcb_msm_send_fn send, nzcb_msm_gather_fn gather, void* user);
   // witness: nWit x 32-byte LE normal-form values; blinding: 11 x 32-byte LE or null
   // witness_on_device: `witness` is a device pointer (HBM-resident input, no PCIe copy)
   void prove(const uint8_t* witness, size_t n_witness, const uint8_t* blinding, uint8_t* proof_out,

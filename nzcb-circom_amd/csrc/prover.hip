@@ -756,10 +756,38 @@ void Prover::commit_start(int slot, const Fr* coefs, size_t len) {
     NZ_HIP(hipSetDevice(eng->device));
     len = std::min(len, own_hi);
   }
+  if (split_send) {  // other ranks take [split_own, len): hand them the scalars once ready
+    NZ_HIP(hipEventSynchronize(ready[slot]));
+    if (split_send(split_user, slot, coefs, len) != 0)
+      throw Error(NZCB_ERR_INTERNAL, "msm split: sending the scalars to the other ranks failed");
+    len = std::min(len, split_own);
+  }
   msm_enqueue(*msc[slot], ptau.p, coefs, len, true, aux[slot], &ptab);
   static const bool serial = std::getenv("NZCB_SERIAL") != nullptr;  // profiling: one kernel at a time
   if (serial) NZ_HIP(hipStreamSynchronize(aux[slot]));
 }
+
+namespace {
+// 64-byte affine point, x || y as normal-form LE (infinity = zeros): the partials' wire format
+void affine_to_le(const G1Affine& a, uint8_t* out) {
+  const Fq x = a.is_inf() ? Fq::zero() : from_mont(a.x);
+  const Fq y = a.is_inf() ? Fq::zero() : from_mont(a.y);
+  std::memcpy(out, x.v, 32);
+  std::memcpy(out + 32, y.v, 32);
+}
+
+G1xyzz xyzz_from_le(const uint8_t* in) {
+  G1Affine a;
+  Fq x, y;
+  std::memcpy(x.v, in, 32);
+  std::memcpy(y.v, in + 32, 32);
+  if (x.is_zero() && y.is_zero()) return G1xyzz::inf();
+  if (reduce_once(x) != x || reduce_once(y) != y) throw Error(NZCB_ERR_ARG, "msm split: partial not reduced");
+  a.x = to_mont(x);
+  a.y = to_mont(y);
+  return xyzz_from_affine(a);
+}
+}  // namespace
 
 G1Affine Prover::commit_finish(int slot) {
   auto t0 = std::chrono::steady_clock::now();
@@ -769,8 +797,35 @@ G1Affine Prover::commit_finish(int slot) {
     r = xyzz_add(r, msm_finish(*sh->sc[slot], sh->st[slot]));
   }
   if (!shards.empty()) NZ_HIP(hipSetDevice(eng->device));
+  if (split_gather) {  // every rank's partial (ours included), added in rank order
+    const G1Affine own = xyzz_to_affine(r);
+    uint8_t own_le[64];
+    affine_to_le(own, own_le);
+    std::vector<uint8_t> parts((size_t)split_world * 64);
+    if (split_gather(split_user, slot, own_le, parts.data()) != 0)
+      throw Error(NZCB_ERR_INTERNAL, "msm split: gathering the partial sums failed");
+    r = G1xyzz::inf();
+    for (int k = 0; k < split_world; k++) r = xyzz_add(r, xyzz_from_le(parts.data() + 64 * (size_t)k));
+  }
   msm_ms += ms_since(t0);
   return xyzz_to_affine(r);
+}
+
+void Prover::set_msm_split(int world, size_t own_points, nzcb_msm_send_fn send, nzcb_msm_gather_fn gather,
+                           void* user) {
+  if (world <= 1 || !send || !gather) {
+    split_send = nullptr;
+    split_gather = nullptr;
+    split_world = 1;
+    return;
+  }
+  if (!shards.empty()) throw Error(NZCB_ERR_ARG, "msm split: a context splits over devices or over ranks, not both");
+  if (own_points == 0 || own_points > ptau.n) throw Error(NZCB_ERR_ARG, "msm split: bad own point count");
+  split_send = send;
+  split_gather = gather;
+  split_user = user;
+  split_world = world;
+  split_own = own_points;
 }
 
 Fr Prover::eval_poly(const Fr* p, size_t len, const Fr& x) {
@@ -894,6 +949,14 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   if (!witness_on_device) {
     NZ_HIP(hipMemcpyAsync(wtns_in.p, witness, (size_t)nWit * 32, hipMemcpyHostToDevice, s));
     wsrc = wtns_in.p;
+  } else {
+    // a witness in another GPU's HBM (device-set contexts prove one batch on every
+    // device): one copy over xGMI into this lane's upload buffer
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, witness) == hipSuccess && at.device != eng->device) {
+      NZ_HIP(hipMemcpyPeerAsync(wtns_in.p, eng->device, witness, at.device, (size_t)nWit * 32, s));
+      wsrc = wtns_in.p;
+    }
   }
   hipLaunchKernelGGL(k_wit_to_mont, dim3(grid_for(nWit, kT, 1u << 30)), dim3(kT), 0, s, wsrc, wit.p,
                      (size_t)nWit);

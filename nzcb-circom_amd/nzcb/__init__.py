@@ -77,6 +77,9 @@ NZCP_LIVE = dict(is_live=1, max_tbs_bytes=351, max_array_len_vc=0, max_map_len_v
 NZCP_EXAMPLE = dict(is_live=0, max_tbs_bytes=314, max_array_len_vc=0, max_map_len_vc=4)
 
 LOG_FN = ctypes.CFUNCTYPE(None, c_void_p, ctypes.c_char_p)
+# nzcb_ctx_set_msm_split callbacks (include/nzcb.h)
+MSM_SEND_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, c_void_p, c_size_t)
+MSM_GATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, POINTER(c_uint8), POINTER(c_uint8))
 
 _lib = None
 
@@ -155,6 +158,13 @@ def load(path: str | None = None):
                                           c_void_p, POINTER(_Err)]),
         "nzcb_engine_time_msm2": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_int, c_int,
                                           POINTER(c_double), POINTER(_Err)]),
+        "nzcb_ctx_create_devices": (c_void_p, [u8p, c_size_t, POINTER(c_int), c_int, POINTER(_Err)]),
+        "nzcb_ctx_devices": (c_int, [c_void_p]),
+        "nzcb_ctx_set_msm_split": (c_int, [c_void_p, c_int, c_size_t, MSM_SEND_FN, MSM_GATHER_FN, c_void_p,
+                                           POINTER(_Err)]),
+        "nzcb_msm_table_create": (c_void_p, [c_int, c_void_p, c_size_t, POINTER(_Err)]),
+        "nzcb_msm_table_run": (c_int, [c_void_p, c_void_p, c_size_t, c_int, u8p, POINTER(_Err)]),
+        "nzcb_msm_table_destroy": (None, [c_void_p]),
         "nzcb_ptau_synth": (c_int, [c_int, u8p, c_int, POINTER(POINTER(c_uint8)), POINTER(c_size_t), POINTER(_Err)]),
         "nzcb_wprog_create": (c_void_p, [ctypes.c_char_p, c_size_t, c_int, POINTER(_Err)]),
         "nzcb_wprog_destroy": (None, [c_void_p]),
@@ -385,9 +395,13 @@ def _read(x) -> bytes:
 class ProverContext:
     """A zkey uploaded once to one GPU (``nzcb_ctx_create``); prove many witnesses against it."""
 
-    def __init__(self, zkey, device: int = 0, logger=None, transcript_public: bool = True, _raw=None):
+    def __init__(self, zkey, device: int = 0, logger=None, transcript_public: bool = True, _raw=None,
+                 devices=None):
+        """devices: a device set (nzcb_ctx_create_devices): batches spread over all of them,
+        single proofs run on devices[0]."""
         self.lib = load()
-        self.device = device
+        self.devices = list(devices) if devices else [device]
+        self.device = self.devices[0]
         err = _Err()
         vk = _out(VK_BYTES)
         if _raw is not None:            # (pointer, length) owned by the caller: no host copy
@@ -395,7 +409,11 @@ class ProverContext:
         else:
             data = _read(zkey)
             zptr, zlen = _buf(data), len(data)
-        self.h = self.lib.nzcb_ctx_create(zptr, zlen, device, ctypes.byref(err))
+        if len(self.devices) > 1:
+            devs = (c_int * len(self.devices))(*self.devices)
+            self.h = self.lib.nzcb_ctx_create_devices(zptr, zlen, devs, len(self.devices), ctypes.byref(err))
+        else:
+            self.h = self.lib.nzcb_ctx_create(zptr, zlen, self.device, ctypes.byref(err))
         if not self.h:
             raise NzcbError(err.code, err.msg.decode(errors="replace"))
         verr = _Err()
@@ -468,6 +486,42 @@ class ProverContext:
         err = _Err()
         _check(self.lib.nzcb_ctx_set_msm_devices(self.h, arr, len(devices), ctypes.byref(err)), err)
 
+    def set_msm_split(self, world: int, own_points: int, send, gather):
+        """Split every commitment MSM across ranks (nzcb_ctx_set_msm_split; nzcb.msmsplit
+        builds the callbacks). send(slot, dev_ptr, count) -> None; gather(slot, own64) ->
+        world x 64 bytes. world = 1 restores the local schedule."""
+        if world <= 1:
+            self._split_cbs = None
+            _check(self.lib.nzcb_ctx_set_msm_split(self.h, 1, 0, MSM_SEND_FN(), MSM_GATHER_FN(), None,
+                                                   ctypes.byref(_Err())), _Err())
+            return
+
+        def _send(_u, slot, ptr, count):
+            try:
+                send(slot, ptr, count)
+                return 0
+            except Exception:  # reported through the proof's error
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        def _gather(_u, slot, own, out):
+            try:
+                parts = gather(slot, ctypes.string_at(own, 64))
+                if len(parts) != 64 * world:
+                    return 1
+                ctypes.memmove(out, parts, len(parts))
+                return 0
+            except Exception:
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._split_cbs = (MSM_SEND_FN(_send), MSM_GATHER_FN(_gather))  # keep alive
+        err = _Err()
+        _check(self.lib.nzcb_ctx_set_msm_split(self.h, world, own_points, self._split_cbs[0], self._split_cbs[1],
+                                               None, ctypes.byref(err)), err)
+
     @property
     def lanes(self) -> int:
         return self.lib.nzcb_ctx_lanes(self.h)
@@ -529,6 +583,31 @@ class ProverContext:
         k = self.lib.nzcb_ctx_last_timings(self.h, ms, 9)
         names = ["total", "witness", "round1", "round2", "round3", "round4", "round5", "msm", "ntt"]
         return dict(zip(names[:k], list(ms)[:k]))
+
+
+class MsmTable:
+    """Resident fixed-base MSM table over device bases (include/nzcb.h nzcb_msm_table_*)."""
+
+    def __init__(self, dev_bases: int, n: int, device: int = 0):
+        self.lib = load()
+        err = _Err()
+        self.n = n
+        self.h = self.lib.nzcb_msm_table_create(device, dev_bases, n, ctypes.byref(err))
+        if not self.h:
+            raise NzcbError(err.code, err.msg.decode(errors="replace"))
+
+    def run(self, dev_scalars: int, count: int, scalars_mont: bool = True) -> bytes:
+        out = _out(64)
+        err = _Err()
+        _check(self.lib.nzcb_msm_table_run(self.h, dev_scalars, count, int(scalars_mont), out, ctypes.byref(err)), err)
+        return bytes(out)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.nzcb_msm_table_destroy(self.h)
+            self.h = None
+
+    __del__ = close
 
 
 class WitnessProgram:

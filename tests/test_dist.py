@@ -52,3 +52,89 @@ def test_shard_edge_cases():
     assert [list(bench.shard(3, r, 8)) for r in range(8)] == [[0], [1], [2], [], [], [], [], []]
     assert list(bench.shard(0, 0, 1)) == []
     assert sum(len(bench.shard(512, r, 8)) for r in range(8)) == 512
+
+
+# ---- single-proof MSM split across ranks (nzcb/msmsplit.py, configs[4]) ---------------
+def _split_points(n):
+    from oracle import bn254 as bn
+    tau = 0x6E7A6362746175
+    pts, t = [], 1
+    for _ in range(n):
+        pts.append(bn.g1_to_lem(bn.g1_mul(bn.G1_GEN, t)))
+        t = t * tau % bn.R_MOD
+    return pts
+
+
+def _split_worker(rank, world, port, n, jobs, out):
+    """Rank 0 drives the protocol as the prover does (sends of up to three commitments in
+    flight, then gathers); ranks 1.. serve with the CPU port's MSM over their range."""
+    import torch.distributed as dist
+    from nzcb import msmsplit
+    from oracle import cbind
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    comm = msmsplit.Comm(dist, "cpu")
+    pts = _split_points(n)
+    ranges = msmsplit.point_ranges(n, world)
+    lo, hi = ranges[rank]
+
+    def cpu_partial(scalars: bytes, count):
+        cnt = max(0, min(count, hi) - lo)
+        if cnt == 0:
+            return bytes(64)
+        return cbind.msm(b"".join(pts[lo:lo + cnt]), scalars[32 * lo:32 * (lo + cnt)], threads=1)
+
+    if rank == 0:
+        def source(src, count, t):
+            import torch
+            t.copy_(torch.frombuffer(bytearray(src), dtype=torch.uint8))
+
+        root = msmsplit.SplitRoot(comm, n, scalar_source=source)
+        assert root.own_points == hi
+        folded = []
+        for batch in jobs:                    # up to 3 commitments in flight, as the prover
+            owns = {}
+            for slot, sc in enumerate(batch):
+                count = len(sc) // 32
+                root.send(slot, sc, count)
+                owns[slot] = cpu_partial(sc, count)
+            for slot in range(len(batch)):
+                folded.append(root.gather(slot, owns[slot]))
+        root.stop()
+        out[0] = folded
+    else:
+        out[rank] = msmsplit.serve(comm, lambda slot, t, count: cpu_partial(bytes(t.tolist()), count))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_msm_split_across_ranks_gloo(world):
+    """Every commitment's folded partials equal the unsplit MSM (C port), for MSM lengths
+    shorter than, equal to and crossing the rank boundaries (the prover's n+2 .. n+6)."""
+    import random
+    from oracle import bn254 as bn
+    from oracle import cbind
+    n = 70                                    # a 2^6 domain's n + 6 PTau points
+    rng = random.Random(world)
+
+    def scal(count):
+        return b"".join(bn.to_lem(rng.randrange(bn.R_MOD), bn.R_MOD) for _ in range(count))
+
+    jobs = [[scal(66), scal(66), scal(66)], [scal(67)], [scal(64), scal(64), scal(70)], [scal(1), scal(0)]]
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_split_worker, args=(world, _free_port(), n, jobs, out), nprocs=world, join=True)
+        res = dict(out)
+    pts = _split_points(n)
+    flat = [sc for batch in jobs for sc in batch]
+    assert [res[r] for r in range(1, world)] == [len(flat)] * (world - 1)
+    for sc, parts in zip(flat, res[0]):
+        count = len(sc) // 32
+        acc = None
+        for r in range(world):
+            p = parts[64 * r:64 * r + 64]
+            x, y = bn.from_le(p[:32]), bn.from_le(p[32:])
+            acc = bn.g1_add(acc, None if x == 0 and y == 0 else (x, y))
+        want = cbind.msm(b"".join(pts[:count]), sc, threads=1) if count else bytes(64)
+        wx, wy = bn.from_le(want[:32]), bn.from_le(want[32:])
+        assert acc == (None if wx == 0 and wy == 0 else (wx, wy))
