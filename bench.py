@@ -143,6 +143,9 @@ def main():
     ap.add_argument("--msm-devices", default="",
                     help="configs[4] single-proof mode: split each MSM over these device ids, e.g. 0,1,2,3 "
                          "(one process; lanes forced to 1)")
+    ap.add_argument("--msm-split", action="store_true",
+                    help="configs[4] across ranks: rank 0 proves --steps proofs one at a time, every commitment "
+                         "MSM split by point range over all ranks (RCCL broadcast + all-gather)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the isolated accumulation-kernel probe")
     args = ap.parse_args()
@@ -204,13 +207,47 @@ def main():
     if msm_devices:
         ctx.set_msm_devices(msm_devices)
         args.lanes = 1
+    split = args.msm_split and world > 1
+    root = backend_range = comm = None
+    if split:
+        # configs[4]: rank 0 proves one proof at a time, every commitment MSM split by PTau
+        # range over all ranks (scalars by broadcast, partials by all-gather; nzcb/msmsplit.py)
+        from nzcb import msmsplit
+        comm = msmsplit.Comm(dist, f"cuda:{device}" if backend == "nccl" else "cpu")
+        args.lanes = 1
+        if rank == 0:
+            root = msmsplit.SplitRoot(comm, n + 6)
+            root.install(ctx)
+        else:
+            addr, size = msmsplit.zkey_section(zkey_raw[0], zkey_raw[1], 14)   # PTau [tau^i]G1
+            dev_ptau = nzcb.dev_alloc(size)
+            nzcb.memcpy_h2d_ptr(dev_ptau, addr, size)
+            lo, hi = msmsplit.point_ranges(n + 6, world)[rank]
+            backend_range = (msmsplit.GpuRange(dev_ptau, lo, hi, device), dev_ptau)
     ctx.set_lanes(args.lanes)
-    mine = list(shard(args.batch, rank, world)) if args.batch else list(range(rank * args.steps,
-                                                                              (rank + 1) * args.steps))
+    if split:
+        mine = list(range(args.steps)) if rank == 0 else []
+    else:
+        mine = list(shard(args.batch, rank, world)) if args.batch else list(range(rank * args.steps,
+                                                                                  (rank + 1) * args.steps))
+
+    def run_proofs(count_or_none, blindings):
+        """The step loop of this rank: proofs (and, in split mode, the STOP that ends the
+        servers' loop), or serving rank 0's commitments."""
+        if split and rank != 0:
+            msmsplit.serve(comm, backend_range[0])
+            return []
+        res = prover.full_prove_staged(count_or_none, blindings) if count_or_none else []
+        if root is not None:
+            root.stop()
+        return res
+
     if args.warmup:
         nw = max(args.warmup, 2 * args.lanes)  # every lane proves at least once before timing
-        prover.upload_inputs(pass_inputs(range(100000, 100000 + nw)))
-        prover.full_prove_staged(nw, [blinding_for(1000 + i) for i in range(nw)])
+        if not split or rank == 0:
+            prover.upload_inputs(pass_inputs(range(100000, 100000 + nw)))
+        barrier()
+        run_proofs(nw, [blinding_for(1000 + i) for i in range(nw)])
     ctx.kernel_stats(1)
     blinds = [blinding_for(i) for i in mine]
     if mine:  # a rank can hold no proofs when --batch is smaller than the world
@@ -218,10 +255,15 @@ def main():
         prover.witness_buffers(len(mine))
     barrier()
     t0 = time.perf_counter()
-    proofs = prover.full_prove_staged(len(mine), blinds)   # GPU witness program + prove_batch
+    proofs = run_proofs(len(mine), blinds)   # GPU witness program + prove_batch
     barrier()
     elapsed = time.perf_counter() - t0
     kms, klaunch, kpoints, kentries = ctx.kernel_stats(0)
+    if root is not None:
+        ctx.set_msm_split(1, 0, None, None)
+    if backend_range is not None:
+        backend_range[0].close()
+        nzcb.dev_free(backend_range[1])
     assert len({p for p, _ in proofs}) == len(mine)  # distinct passes -> distinct proofs
     # full-size checks outside the timed region: every proof's public signals equal its
     # pass's outputs from the independent nzcp kernel (csrc/nzcp.hip, bit-exact against
@@ -237,8 +279,8 @@ def main():
     witness_ms = (time.perf_counter() - t_w) * 1e3
     probe = accumulate_probe(n + 6, device) if rank == 0 and not args.no_probe else None
     elapsed = max_over_ranks(elapsed, dist, f"cuda:{device}" if backend == "nccl" else "cpu")
-    total_proofs = args.batch if args.batch else args.steps * world
-    steps = len(shard(args.batch, 0, world)) if args.batch else args.steps
+    total_proofs = args.steps if split else (args.batch if args.batch else args.steps * world)
+    steps = len(shard(args.batch, 0, world)) if args.batch and not split else args.steps
     value = total_proofs / elapsed
     ms_step = elapsed / steps * 1e3
 
@@ -275,7 +317,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "strong" if args.batch else "weak",
+            "scaling": "strong" if (args.batch or split) else "weak",
             "vs_baseline": None,
             "dtype": "u32 limbs: BN254 Fr/Fq Montgomery, 8x32-bit and 9x29-bit (MSM, NTT twiddles, quotient)",
             "data": "synthetic passes: live-shaped NZ COVID Pass ToBeSigned (live key id and issuer) with 20 "
@@ -291,7 +333,8 @@ def main():
                 "n_additions": ctx.n_additions,
                 "proofs_per_gpu": steps,
                 "total_proofs": total_proofs,
-                "parallelism": f"batch-shard x{world} (no collective)",
+                "parallelism": (f"single-proof MSM split x{world} (RCCL broadcast of scalars + all-gather of "
+                                f"64-byte partials)" if split else f"batch-shard x{world} (no collective)"),
                 "proofs_in_flight_per_gpu": args.lanes,
                 "msm_devices": msm_devices or None,
             },

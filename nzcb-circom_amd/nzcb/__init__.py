@@ -364,6 +364,13 @@ def h2d(dst: int, data: bytes):
         raise NzcbError(rc, "h2d failed")
 
 
+def memcpy_h2d_ptr(dst: int, src_addr: int, nbytes: int):
+    """Host memory at a raw address (e.g. inside a library-owned zkey buffer) -> device."""
+    rc = load().nzcb_memcpy_h2d(dst, src_addr, nbytes)
+    if rc:
+        raise NzcbError(rc, "h2d failed")
+
+
 def msm_set_pair_rounds(rounds: int):
     """Force `rounds` batch-affine pairing rounds in fixed-base MSMs (< 0: automatic)."""
     load().nzcb_msm_set_pair_rounds(int(rounds))
