@@ -129,15 +129,28 @@ class GpuRange:
 
     def __init__(self, dev_ptau: int, lo: int, hi: int, device: int):
         import nzcb
+        self.nzcb = nzcb
         self.lo, self.hi = lo, hi
         self.table = nzcb.MsmTable(dev_ptau + 64 * lo, hi - lo, device)
+        self.staging = None   # HBM copy of this range's scalars when they arrive in host tensors (gloo)
 
     def __call__(self, slot: int, t, count: int) -> bytes:
         cnt = max(0, min(count, self.hi) - self.lo)
-        return self.table.run(t.data_ptr() + 32 * self.lo, cnt, True) if cnt else bytes(64)
+        if not cnt:
+            return bytes(64)
+        src = t.data_ptr() + 32 * self.lo
+        if not getattr(t, "is_cuda", True):
+            if self.staging is None:
+                self.staging = self.nzcb.dev_alloc(32 * (self.hi - self.lo))
+            self.nzcb.memcpy_h2d_ptr(self.staging, src, 32 * cnt)
+            src = self.staging
+        return self.table.run(src, cnt, True)
 
     def close(self):
         self.table.close()
+        if self.staging:
+            self.nzcb.dev_free(self.staging)
+            self.staging = None
 
 
 def zkey_section(ptr: int, size: int, sid: int) -> tuple:
