@@ -73,6 +73,9 @@ nzcb_ctx* nzcb_ctx_create(const uint8_t* zkey, size_t zkey_len, int device, nzcb
  * lanes of all devices (nzcb_ctx_set_lanes sets lanes per device); single proofs run on
  * devices[0]. nzcb_ctx_create(z, len, d, err) is this with devices = {d}. */
 nzcb_ctx* nzcb_ctx_create_devices(const uint8_t* zkey, size_t zkey_len, const int* devices, int ndev, nzcb_err* err);
+/* The same from a zkey file (memory-mapped, nothing retained after the call): zkeys of
+ * nzcp_live size (~3.9 GB) exceed what a Node.js Buffer holds. devices NULL = device 0. */
+nzcb_ctx* nzcb_ctx_create_file(const char* zkey_path, const int* devices, int ndev, nzcb_err* err);
 int nzcb_ctx_devices(const nzcb_ctx* ctx);
 void nzcb_ctx_destroy(nzcb_ctx* ctx);
 

@@ -1,4 +1,9 @@
 // C-ABI: prover context, proofs and snarkjs-format JSON (include/nzcb.h).
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <cstring>
 #include <mutex>
@@ -128,6 +133,36 @@ nzcb_ctx* nzcb_ctx_create_devices(const uint8_t* zkey, size_t zkey_len, const in
   }
   delete c;
   return nullptr;
+}
+
+nzcb_ctx* nzcb_ctx_create_file(const char* zkey_path, const int* devices, int ndev, nzcb_err* err) {
+  if (!zkey_path) {
+    set_err(err, NZCB_ERR_ARG, "null zkey path");
+    return nullptr;
+  }
+  const int fd = open(zkey_path, O_RDONLY);
+  if (fd < 0) {
+    set_err(err, NZCB_ERR_ARG, (std::string("cannot open ") + zkey_path).c_str());
+    return nullptr;
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0 || st.st_size <= 0) {
+    close(fd);
+    set_err(err, NZCB_ERR_FORMAT, "zkey file is empty");
+    return nullptr;
+  }
+  void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) {
+    set_err(err, NZCB_ERR_INTERNAL, "mmap of the zkey failed");
+    return nullptr;
+  }
+  int dev0 = 0;
+  nzcb_ctx* c = devices && ndev > 0
+                    ? nzcb_ctx_create_devices(static_cast<const uint8_t*>(m), (size_t)st.st_size, devices, ndev, err)
+                    : nzcb_ctx_create(static_cast<const uint8_t*>(m), (size_t)st.st_size, dev0, err);
+  munmap(m, (size_t)st.st_size);
+  return c;
 }
 
 int nzcb_ctx_devices(const nzcb_ctx* ctx) { return ctx ? 1 + (int)ctx->dev_p.size() : 0; }

@@ -8,7 +8,8 @@
 //   "nzwp" u32 version n_wires n_out n_pub_in n_prv_in n_consts n_terms n_ops n_levels
 //   consts[n_consts] 32 B normal form | terms[n_terms] (u32 wire, u32 const) |
 //   ops[n_ops] 8 x u32 {type | err << 8 | n << 16, dst, a_off, a_n, b_off, b_n, c_off, c_n}
-//   level_start[n_levels + 1] u32 | level_macro_start[n_levels] u32
+//   level_start[n_levels + 1] u32 | level_macro_start[n_levels] u32 |
+//   u32 n_names, then per main input: u32 len, name bytes, u32 size (declaration order)
 // Ops are sorted by dependency level; inside a level the scalar ops (LIN MUL INV BITS
 // CHECK) come first and are spread over the workgroup's threads, the macro ops (QUIN,
 // SHA256, SHA512) follow and each runs on the whole workgroup. One barrier per level.
@@ -534,7 +535,7 @@ static void upload(DevBuf<T>& d, const void* src, size_t count) {
 Program* load(const uint8_t* data, size_t len, int device) {
   if (!data || len < 40 || std::memcmp(data, "nzwp", 4) != 0)
     throw Error(NZCB_ERR_FORMAT, "witness program: bad magic");
-  if (rd32(data + 4) != 1) throw Error(NZCB_ERR_FORMAT, "witness program: unsupported version");
+  if (rd32(data + 4) != 2) throw Error(NZCB_ERR_FORMAT, "witness program: unsupported version");
   auto P = new Program();
   try {
     P->device = device;
@@ -545,7 +546,24 @@ Program* load(const uint8_t* data, size_t len, int device) {
     const uint32_t nc = rd32(data + 24), nt = rd32(data + 28), no = rd32(data + 32);
     P->n_levels = rd32(data + 36);
     const size_t need = 40 + (size_t)nc * 32 + (size_t)nt * 8 + (size_t)no * 32 + ((size_t)P->n_levels * 2 + 1) * 4;
-    if (len != need) throw Error(NZCB_ERR_FORMAT, "witness program: truncated or oversized");
+    if (len < need + 4) throw Error(NZCB_ERR_FORMAT, "witness program: truncated");
+    {  // input names (host-side mapping of input objects; checked here, not used on the GPU)
+      size_t o = need;
+      const uint32_t nn = rd32(data + o);
+      o += 4;
+      uint64_t total = 0;
+      for (uint32_t i = 0; i < nn; i++) {
+        if (o + 4 > len) throw Error(NZCB_ERR_FORMAT, "witness program: truncated input names");
+        const uint32_t ln = rd32(data + o);
+        o += 4 + (size_t)ln;
+        if (o + 4 > len) throw Error(NZCB_ERR_FORMAT, "witness program: truncated input names");
+        total += rd32(data + o);
+        o += 4;
+      }
+      if (o != len) throw Error(NZCB_ERR_FORMAT, "witness program: oversized");
+      if (nn && total != (uint64_t)rd32(data + 16) + rd32(data + 20))
+        throw Error(NZCB_ERR_FORMAT, "witness program: input names do not cover the inputs");
+    }
     const uint8_t* p = data + 40;
     // coefficients c -> c R^2 (Montgomery of Montgomery), checked < r
     std::vector<Fr> cs(nc);

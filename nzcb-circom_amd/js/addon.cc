@@ -11,7 +11,9 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/nzcb.h"
 
@@ -27,6 +29,9 @@ namespace {
 
 struct Ctx {
   nzcb_ctx* ctx = nullptr;
+  // held across set_logger + prove + clear, so two in-flight prove() promises on one
+  // context never swap or drop each other's logger
+  std::mutex prove_mu;
 };
 
 void ctx_finalize(napi_env, void* data, void*) {
@@ -56,6 +61,32 @@ napi_value CreateContext(napi_env env, napi_callback_info info) {
   if (argc > 1) napi_get_value_int32(env, argv[1], &device);
   nzcb_err err{};
   nzcb_ctx* ctx = nzcb_ctx_create(static_cast<const uint8_t*>(data), len, device, &err);
+  if (!ctx) {
+    napi_throw(env, make_error(env, err.code, err.msg));
+    return nullptr;
+  }
+  Ctx* c = new Ctx();
+  c->ctx = ctx;
+  napi_value ext;
+  CHECK(napi_create_external(env, c, ctx_finalize, nullptr, &ext));
+  return ext;
+}
+
+// createContextFile(path: string, device: number) -> external (zkeys larger than a Buffer)
+napi_value CreateContextFile(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  size_t plen = 0;
+  CHECK(napi_get_value_string_utf8(env, argv[0], nullptr, 0, &plen));
+  std::string path(plen + 1, '\0');
+  CHECK(napi_get_value_string_utf8(env, argv[0], &path[0], path.size(), &plen));
+  path.resize(plen);
+  int32_t device = 0;
+  if (argc > 1) napi_get_value_int32(env, argv[1], &device);
+  nzcb_err err{};
+  const int devs[1] = {device};
+  nzcb_ctx* ctx = nzcb_ctx_create_file(path.c_str(), devs, 1, &err);
   if (!ctx) {
     napi_throw(env, make_error(env, err.code, err.msg));
     return nullptr;
@@ -112,6 +143,7 @@ void prove_execute(napi_env, void* data) {
     std::snprintf(w->err.msg, sizeof(w->err.msg), "too many public signals for the addon buffer");
     return;
   }
+  std::lock_guard<std::mutex> lk(w->c->prove_mu);
   nzcb_ctx_set_logger(w->c->ctx, w->tsfn ? log_trampoline : nullptr, w);
   w->rc = nzcb_prove(w->c->ctx, w->wtns, w->wtns_len, w->has_blinding ? w->blinding : nullptr, w->proof, w->pub,
                      sizeof(w->pub), &w->err);
@@ -173,6 +205,107 @@ napi_value Prove(napi_env env, napi_callback_info info) {
   napi_create_string_utf8(env, "nzcb-prove", NAPI_AUTO_LENGTH, &rname);
   CHECK(napi_create_async_work(env, nullptr, rname, prove_execute, prove_complete, w, &w->work));
   CHECK(napi_queue_async_work(env, w->work));
+  return promise;
+}
+
+// ---- witness programs (nzcb_wprog_*): circom's witness calculator on the GPU ----------
+struct Wprog {
+  nzcb_wprog* p = nullptr;
+};
+
+void wprog_finalize(napi_env, void* data, void*) {
+  Wprog* w = static_cast<Wprog*>(data);
+  if (w->p) nzcb_wprog_destroy(w->p);
+  delete w;
+}
+
+// createWitnessProgram(program: Buffer, device: number) -> external
+napi_value CreateWitnessProgram(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  void* data = nullptr;
+  size_t len = 0;
+  CHECK(napi_get_buffer_info(env, argv[0], &data, &len));
+  int32_t device = 0;
+  if (argc > 1) napi_get_value_int32(env, argv[1], &device);
+  nzcb_err err{};
+  nzcb_wprog* p = nzcb_wprog_create(static_cast<const uint8_t*>(data), len, device, &err);
+  if (!p) {
+    napi_throw(env, make_error(env, err.code, err.msg));
+    return nullptr;
+  }
+  Wprog* w = new Wprog();
+  w->p = p;
+  napi_value ext;
+  CHECK(napi_create_external(env, w, wprog_finalize, nullptr, &ext));
+  return ext;
+}
+
+struct WitnessWork {
+  napi_async_work work = nullptr;
+  napi_deferred deferred = nullptr;
+  napi_ref prog_ref = nullptr, in_ref = nullptr;
+  Wprog* w = nullptr;
+  const uint8_t* inputs = nullptr;
+  size_t in_len = 0;
+  std::vector<uint8_t> out;
+  int32_t status = 0;
+  int rc = 0;
+  nzcb_err err{};
+};
+
+void witness_execute(napi_env, void* data) {
+  WitnessWork* k = static_cast<WitnessWork*>(data);
+  uint32_t info[5];
+  nzcb_wprog_info(k->w->p, info);
+  const size_t nin = (size_t)info[2] + info[3];
+  if (k->in_len != nin * 32) {
+    k->rc = NZCB_ERR_ARG;
+    std::snprintf(k->err.msg, sizeof(k->err.msg), "expected %zu input signals", nin);
+    return;
+  }
+  k->out.resize((size_t)info[0] * 32);
+  k->rc = nzcb_wprog_run(k->w->p, k->inputs, 1, k->out.data(), &k->status, &k->err);
+}
+
+void witness_complete(napi_env env, napi_status, void* data) {
+  WitnessWork* k = static_cast<WitnessWork*>(data);
+  if (k->rc) {
+    napi_reject_deferred(env, k->deferred, make_error(env, k->rc, k->err.msg));
+  } else if (k->status) {
+    napi_reject_deferred(env, k->deferred, make_error(env, k->status, "Assert Failed (witness calculation)"));
+  } else {
+    napi_value buf;
+    void* dst = nullptr;
+    if (napi_create_buffer_copy(env, k->out.size(), k->out.data(), &dst, &buf) == napi_ok)
+      napi_resolve_deferred(env, k->deferred, buf);
+    else
+      napi_reject_deferred(env, k->deferred, make_error(env, NZCB_ERR_INTERNAL, "buffer allocation failed"));
+  }
+  napi_delete_reference(env, k->prog_ref);
+  napi_delete_reference(env, k->in_ref);
+  napi_delete_async_work(env, k->work);
+  delete k;
+}
+
+// calculateWitness(prog, inputs: Buffer (n_inputs x 32 B LE)) -> Promise<Buffer (n_wires x 32 B LE)>
+napi_value CalculateWitness(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  WitnessWork* k = new WitnessWork();
+  CHECK(napi_get_value_external(env, argv[0], reinterpret_cast<void**>(&k->w)));
+  void* d = nullptr;
+  CHECK(napi_get_buffer_info(env, argv[1], &d, &k->in_len));
+  k->inputs = static_cast<const uint8_t*>(d);
+  CHECK(napi_create_reference(env, argv[0], 1, &k->prog_ref));
+  CHECK(napi_create_reference(env, argv[1], 1, &k->in_ref));
+  napi_value promise, rname;
+  CHECK(napi_create_promise(env, &k->deferred, &promise));
+  napi_create_string_utf8(env, "nzcb-witness", NAPI_AUTO_LENGTH, &rname);
+  CHECK(napi_create_async_work(env, nullptr, rname, witness_execute, witness_complete, k, &k->work));
+  CHECK(napi_queue_async_work(env, k->work));
   return promise;
 }
 
@@ -382,6 +515,9 @@ napi_value Init(napi_env env, napi_value exports) {
       {"calldata", nullptr, Calldata, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"nzcpWitness", nullptr, NzcpWitness, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"plonkSetup", nullptr, PlonkSetup, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"createContextFile", nullptr, CreateContextFile, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"createWitnessProgram", nullptr, CreateWitnessProgram, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"calculateWitness", nullptr, CalculateWitness, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

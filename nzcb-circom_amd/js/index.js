@@ -44,13 +44,21 @@ function randomBlinding() {
   return out;
 }
 
-// One HBM-resident context per (zkey content, device): the zkey is uploaded once.
+// One HBM-resident context per (zkey, device): the zkey is uploaded once. A file name is
+// memory-mapped by the library (nzcb_ctx_create_file), so zkeys of nzcp_live size
+// (~3.9 GB, beyond a Node Buffer) work; buffers are keyed by content.
 const contexts = new Map();
-function contextFor(zkeyBuf, device) {
-  const key = crypto.createHash('sha256').update(zkeyBuf).digest('hex') + ':' + device;
+function contextFor(zkey, device) {
+  let key;
+  if (typeof zkey === 'string') {
+    const st = fs.statSync(zkey);
+    key = `file:${path.resolve(zkey)}:${st.size}:${st.mtimeMs}:${device}`;
+  } else {
+    key = crypto.createHash('sha256').update(readBin(zkey)).digest('hex') + ':' + device;
+  }
   let ctx = contexts.get(key);
   if (!ctx) {
-    ctx = addon.createContext(zkeyBuf, device);
+    ctx = typeof zkey === 'string' ? addon.createContextFile(zkey, device) : addon.createContext(readBin(zkey), device);
     contexts.set(key, ctx);
   }
   return ctx;
@@ -65,9 +73,8 @@ function loggerFn(logger) {
 
 async function prove(zkeyFileName, witnessFileName, logger, options) {
   options = options || {};
-  const zkey = readBin(zkeyFileName);
   const wtns = readBin(witnessFileName);
-  const ctx = contextFor(zkey, options.device || 0);
+  const ctx = contextFor(zkeyFileName, options.device || 0);
   const blinding = options.blinding ? Buffer.from(options.blinding) : randomBlinding();
   if (blinding.length !== BLINDING_BYTES) throw new Error('blinding must be 11 x 32 bytes');
   const res = await addon.prove(ctx, wtns, blinding, loggerFn(logger));
@@ -99,7 +106,7 @@ function flatArray(a) {
 }
 
 async function wtnsCalculate(input, wasmFile) {
-  const code = readBin(wasmFile);
+  const code = Buffer.isBuffer(wasmFile) ? wasmFile : readBin(wasmFile);
   let instance;
   let errStr = '';
   const getMessage = () => {
@@ -175,8 +182,82 @@ async function wtnsCalculate(input, wasmFile) {
   return out;
 }
 
+// ---------------------------------------------------------------------------
+// Witness calculation on the GPU from a witness program (nzcb/circuit.py write_program:
+// nzcp_live = NZCPPubIdentity(1, 351, 0, 4, 2, 4) compiled by nzcb/nzcpgen.py), the
+// MI355X replacement of the circom wasm for circuits this build compiles. The program
+// carries the main's input names and sizes; inputs are mapped by name, as circom does.
+// ---------------------------------------------------------------------------
+function programInputs(prog) {
+  const u32 = (o) => prog.readUInt32LE(o);
+  const nc = u32(24), nt = u32(28), no = u32(32), nlev = u32(36);
+  let o = 40 + nc * 32 + nt * 8 + no * 32 + (2 * nlev + 1) * 4;
+  const n = u32(o); o += 4;
+  const names = [];
+  for (let i = 0; i < n; i++) {
+    const len = u32(o); o += 4;
+    const name = prog.toString('utf8', o, o + len); o += len;
+    names.push([name, u32(o)]); o += 4;
+  }
+  return { nWires: u32(8), names };
+}
+
+const programs = new Map();
+function programFor(progBuf, device) {
+  const key = crypto.createHash('sha256').update(progBuf).digest('hex') + ':' + device;
+  let p = programs.get(key);
+  if (!p) {
+    p = { handle: addon.createWitnessProgram(progBuf, device), meta: programInputs(progBuf) };
+    programs.set(key, p);
+  }
+  return p;
+}
+
+async function wtnsCalculateGpu(input, progBuf, device) {
+  const { handle, meta } = programFor(progBuf, device);
+  const vals = [];
+  for (const [name, size] of meta.names) {
+    if (!(name in input)) throw new Error(`Signal ${name} not found\n`);
+    const flat = flatArray(input[name]);
+    if (flat.length < size) throw new Error(`Not enough values for input signal ${name}\n`);
+    if (flat.length > size) throw new Error(`Too many values for input signal ${name}\n`);
+    vals.push(...flat);
+  }
+  for (const k of Object.keys(input)) {
+    if (!meta.names.some(([n]) => n === k)) throw new Error(`Signal ${k} not found\n`);
+  }
+  const buf = Buffer.alloc(32 * vals.length);
+  vals.forEach((x, i) => {
+    let v = BigInt(x) % R;
+    if (v < BigInt(0)) v += R;
+    for (let j = 0; j < 32; j++) { buf[32 * i + j] = Number(v & BigInt(255)); v >>= BigInt(8); }
+  });
+  const wit = await addon.calculateWitness(handle, buf);
+  const hdr = Buffer.alloc(12 + 12 + 4 + 32 + 4 + 12);
+  let o = 0;
+  hdr.write('wtns', 0, 'latin1'); o = 4;
+  hdr.writeUInt32LE(2, o); o += 4;
+  hdr.writeUInt32LE(2, o); o += 4;
+  hdr.writeUInt32LE(1, o); o += 4;
+  hdr.writeUInt32LE(40, o); hdr.writeUInt32LE(0, o + 4); o += 8;
+  hdr.writeUInt32LE(32, o); o += 4;
+  let r = R;
+  for (let j = 0; j < 32; j++) { hdr[o + j] = Number(r & BigInt(255)); r >>= BigInt(8); }
+  o += 32;
+  hdr.writeUInt32LE(meta.nWires, o); o += 4;
+  hdr.writeUInt32LE(2, o); o += 4;
+  hdr.writeUInt32LE(wit.length % 0x100000000, o); hdr.writeUInt32LE(Math.floor(wit.length / 0x100000000), o + 4);
+  return Buffer.concat([hdr, wit]);
+}
+
+// wasmFile: a circom 2.0.x witness .wasm (run on the host CPU, as snarkjs does) or a
+// witness program ("nzwp", run on the GPU)
 async function fullProve(input, wasmFile, zkeyFileName, logger, options) {
-  const wtns = await wtnsCalculate(input, wasmFile);
+  options = options || {};
+  const code = readBin(wasmFile);
+  const wtns = code.slice(0, 4).toString('latin1') === 'nzwp'
+    ? await wtnsCalculateGpu(input, code, options.device || 0)
+    : await wtnsCalculate(input, code);
   return prove(zkeyFileName, { type: 'mem', data: wtns }, logger, options);
 }
 

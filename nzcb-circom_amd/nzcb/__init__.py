@@ -778,11 +778,16 @@ def _json_text(fn, *args) -> str:
 
 
 def vk_from_zkey(zkey) -> bytes:
-    """Binary verification key (include/nzcb.h NZCB_VK_BYTES) of a zkey (bytes or path)."""
-    data = open(zkey, "rb").read() if isinstance(zkey, str) else zkey
+    """Binary verification key (include/nzcb.h NZCB_VK_BYTES) of a zkey: bytes, a path, or
+    a (pointer, length) library buffer (nzcb.plonk_setup_raw)."""
     out = _out(VK_BYTES)
     err = _Err()
-    _check(load().nzcb_vk_from_zkey(_buf(data), len(data), out, ctypes.byref(err)), err)
+    if isinstance(zkey, tuple):
+        ptr, size = ctypes.cast(zkey[0], POINTER(c_uint8)), zkey[1]
+    else:
+        data = open(zkey, "rb").read() if isinstance(zkey, str) else zkey
+        ptr, size = _buf(data), len(data)
+    _check(load().nzcb_vk_from_zkey(ptr, size, out, ctypes.byref(err)), err)
     return bytes(out)
 
 

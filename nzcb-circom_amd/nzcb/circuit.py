@@ -45,7 +45,7 @@ OP_LIN, OP_MUL, OP_INV, OP_BITS, OP_CHECK, OP_QUIN, OP_SHA256, OP_SHA512 = range
 MACRO_OPS = (OP_QUIN, OP_SHA256, OP_SHA512)
 NO_WIRE = 0xFFFFFFFF
 PROGRAM_MAGIC = b"nzwp"
-PROGRAM_VERSION = 1
+PROGRAM_VERSION = 2
 
 
 def lc(x) -> dict:
@@ -164,8 +164,14 @@ SHA512_IV = [0x6a09e667f3bcc908, 0xbb67ae8584caa73b, 0x3c6ef372fe94f82b, 0xa54ff
 class Circuit:
     """Signals, constraints and witness operations of one circuit (see module docstring)."""
 
-    def __init__(self, n_out: int, n_pub_in: int, n_prv_in: int):
+    def __init__(self, n_out: int, n_pub_in: int, n_prv_in: int, input_names=None):
+        """input_names: [(name, size)] of the main's inputs in declaration order (sizes add
+        up to n_pub_in + n_prv_in); written into the program so a caller can map an input
+        object ({name: value | array}) onto the input signals, as circom's calculator does."""
         self.n_out, self.n_pub_in, self.n_prv_in = n_out, n_pub_in, n_prv_in
+        self.input_names = list(input_names or [])
+        if self.input_names and sum(k for _, k in self.input_names) != n_pub_in + n_prv_in:
+            raise ValueError("input names do not cover the inputs")
         self.n_wires = 1 + n_out + n_pub_in + n_prv_in
         self.constraints = []          # (A, B, C)
         self.ops = []                  # (type, err, n, dst, A, B, C, extra) in creation order
@@ -450,6 +456,11 @@ class Circuit:
         out.append(b"".join(struct.pack("<8I", *recs[i]) for i in idx))
         out.append(struct.pack(f"<{nlev + 1}I", *starts))
         out.append(struct.pack(f"<{nlev}I", *macro_starts))
+        # input names: u32 count, then per input u32 name length, utf-8 name, u32 size
+        out.append(struct.pack("<I", len(self.input_names)))
+        for name, size in self.input_names:
+            nb = name.encode()
+            out.append(struct.pack("<I", len(nb)) + nb + struct.pack("<I", size))
         return b"".join(out)
 
 

@@ -328,7 +328,8 @@ def nzcp_pub_identity(is_live: int, max_tbs_bytes: int, max_array_len_vc: int, m
     claims_skip = 30 if is_live else 27
     cred_subj_offset, null_bytes = 171, 64
     max_bits = 8 * max_tbs_bytes
-    c = Circuit(3, 0, max_bits + 1 + data_len)
+    c = Circuit(3, 0, max_bits + 1 + data_len,
+                input_names=[("toBeSigned", max_bits), ("toBeSignedLen", 1), ("data", data_len)])
     tbs = [w(c.in_base + i) for i in range(max_bits)]
     tbs_len = w(c.in_base + max_bits)
     data = [w(c.in_base + max_bits + 1 + i) for i in range(data_len)]

@@ -37,6 +37,8 @@ def parse(prog: bytes) -> dict:
     ops = [struct.unpack_from("<8I", prog, o + 32 * i) for i in range(n_ops)]
     o += 32 * n_ops
     starts = struct.unpack_from(f"<{n_lev + 1}I", prog, o)
+    if ver != 2:
+        raise ValueError("unsupported witness program version")
     return dict(n_wires=n_wires, n_out=n_out, n_pub=n_pub, n_prv=n_prv, consts=consts, terms=terms, ops=ops,
                 levels=starts)
 

@@ -178,3 +178,82 @@ def test_cli_plonk_setup_matches_library(tmp_path):
                         str(tmp_path / "p.ptau"), str(zf)], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr
     assert zf.read_bytes() == nzcb.plonk_setup(data, ptau)
+
+
+@needs_node
+@pytest.mark.gpu
+def test_node_full_prove_wasm_and_witness_program(tmp_path):
+    """plonk.fullProve end to end (configs[0]'s plumbing): a circom-2.0.x-ABI witness .wasm
+    (tests/wasm_tiny.py, `c <== a * b`) on the host, and the same circuit's witness program
+    on the GPU, give the same witness, hence the same proof under the same blinding; the
+    proof verifies and publicSignals = ["33"]. Parity with circom/snarkjs: unpinned."""
+    import nzcb
+    import wasm_tiny
+    r1cs, prog = wasm_tiny.mul_circuit()
+    zkey = nzcb.plonk_setup(r1cs, nzcb.ptau_synth(4, 0x1234567))
+    (tmp_path / "mul.zkey").write_bytes(zkey)
+    (tmp_path / "mul.wasm").write_bytes(wasm_tiny.build_mul_wasm())
+    (tmp_path / "mul.wprog").write_bytes(prog)
+    bl = "".join(f"{(7 * i + 3):064x}"[::-1] for i in range(11))  # any fixed 32-byte LE values < r
+    bl = bytes(int(bl[64 * i:64 * i + 64][::-1], 16).to_bytes(32, "little") for i in range(11)).hex()
+    script = f"""
+const m = require('./');
+(async () => {{
+  const bl = Buffer.from('{bl}', 'hex');
+  const z = '{tmp_path}/mul.zkey';
+  const a = await m.plonk.fullProve({{a: 3, b: 11}}, '{tmp_path}/mul.wasm', z, null, {{blinding: bl}});
+  const g = await m.plonk.fullProve({{b: 11, a: 3}}, '{tmp_path}/mul.wprog', z, null, {{blinding: bl}});
+  const vk = await m.zKey.exportVerificationKey(z);
+  const ok = await m.plonk.verify(vk, g.publicSignals, g.proof);
+  let err = '';
+  try {{ await m.plonk.fullProve({{a: 3}}, '{tmp_path}/mul.wprog', z); }} catch (e) {{ err = e.message; }}
+  console.log(JSON.stringify({{a, g, ok, err}}));
+}})().catch((e) => {{ console.error(e); process.exit(1); }});
+"""
+    d = json.loads(run_node(script))
+    assert d["a"]["publicSignals"] == ["33"] == d["g"]["publicSignals"]
+    assert d["a"]["proof"] == d["g"]["proof"]
+    assert d["ok"] is True
+    assert d["err"].startswith("Signal b not found")
+
+
+@needs_node
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_node_full_prove_nzcp_live(tmp_path):
+    """plonk.fullProve of the real nzcp_live circuit from Node: the test/nzcp.js-shaped input
+    object, the GPU witness program, a 3.9 GB zkey read by file name (memory-mapped by the
+    library). publicSignals equal the CPU restatement's outputs; the proof verifies."""
+    import ctypes
+    import nzcb
+    import nzcp_cases as C
+    from nzcb import nzcp, nzcplive
+    from oracle import nzcp_circuit as nz
+    r1cs, prog, _ = nzcplive.build()
+    zp, zl = nzcplive.setup_raw(r1cs)
+    try:
+        with open(tmp_path / "live.zkey", "wb") as f:
+            f.write((ctypes.c_uint8 * zl).from_address(zp))
+        vk = nzcb.vk_to_json(nzcb.vk_from_zkey((zp, zl)))
+    finally:
+        nzcb.free_ptr(zp)
+    (tmp_path / "live.wprog").write_bytes(prog)
+    (tmp_path / "vk.json").write_text(json.dumps(vk))
+    tbs = nzcp.pass_tbs(live=True)
+    inp = nzcp.circuit_input(tbs, bytes(range(1, 21)))
+    (tmp_path / "input.json").write_text(json.dumps(inp))
+    want = C.oracle_record(C.case("live", nz.LIVE_PARAMS, tbs, data=bytes(range(1, 21))))["out"]
+    script = f"""
+const m = require('./');
+const fs = require('fs');
+(async () => {{
+  const input = JSON.parse(fs.readFileSync('{tmp_path}/input.json'));
+  const r = await m.plonk.fullProve(input, '{tmp_path}/live.wprog', '{tmp_path}/live.zkey');
+  const vk = JSON.parse(fs.readFileSync('{tmp_path}/vk.json'));
+  const ok = await m.plonk.verify(vk, r.publicSignals, r.proof);
+  console.log(JSON.stringify({{pub: r.publicSignals, ok}}));
+}})().catch((e) => {{ console.error(e); process.exit(1); }});
+"""
+    d = json.loads(run_node(script, timeout=600))
+    assert d["pub"] == [str(v) for v in want]
+    assert d["ok"] is True
