@@ -194,8 +194,7 @@ def test_node_full_prove_wasm_and_witness_program(tmp_path):
     (tmp_path / "mul.zkey").write_bytes(zkey)
     (tmp_path / "mul.wasm").write_bytes(wasm_tiny.build_mul_wasm())
     (tmp_path / "mul.wprog").write_bytes(prog)
-    bl = "".join(f"{(7 * i + 3):064x}"[::-1] for i in range(11))  # any fixed 32-byte LE values < r
-    bl = bytes(int(bl[64 * i:64 * i + 64][::-1], 16).to_bytes(32, "little") for i in range(11)).hex()
+    bl = b"".join((7 * i + 3 + (i << 200)).to_bytes(32, "little") for i in range(11)).hex()  # fixed, < r
     script = f"""
 const m = require('./');
 (async () => {{
