@@ -29,6 +29,9 @@ struct MsmScratch {
   DevBuf<uint32_t> keys_in, keys_out, vals_in;
   DevBuf<uint8_t> sort_tmp;
   size_t sort_tmp_bytes = 0;
+  // fixed-base bucketing (msm.hip msm_keys_hist_kernel): per (high key byte, tile)
+  // counts, scanned in place, and the values grouped by high byte
+  DevBuf<uint32_t> bin_counts, vals_mid;
   DevBuf<G1xyzz> buckets;     // buckets whose entries lie in one accumulation chunk
   DevBuf<G1xyzz> carry_own;   // per chunk: partial sum of a bucket that starts in the chunk and spills over
   DevBuf<G1xyzz> carry_cont;  // per chunk: partial sum of a bucket that began in an earlier chunk

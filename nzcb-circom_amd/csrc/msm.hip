@@ -220,6 +220,145 @@ msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t strid
   }
 }
 
+// ---- fixed-base bucketing (16-bit keys), replacing the library radix sort ------------
+// Entries (one per scalar and window) are grouped by bucket in two counting passes over
+// the key's high and low byte, reduce-then-scan, with every counter in LDS or fully
+// written (no look-back spinning, no memsets):
+//   1. msm_keys_hist_kernel  keys + values, and per tile of 2048 scalars the histogram of
+//                            the keys' high byte -> counts[hi][tile]
+//   2. msm_bin_scan_kernel   exclusive scan of counts in (hi, tile) order, one workgroup
+//   3. msm_scatter_hi_kernel each tile scatters its entries to their high-byte region
+//   4. msm_bucket_lo_kernel  one workgroup per high byte: low-byte histogram of its region,
+//                            local scan -> the 256 bucket offsets, scatter of the values
+// Order inside a bucket is whatever the LDS atomics give: the accumulation adds the
+// bucket's points in any order and the sum is the same point.
+static constexpr int kBinThreads = 256;
+static constexpr int kBinPer = 8;                                   // scalars per thread and tile
+static constexpr uint32_t kTileScalars = kBinThreads * kBinPer;     // 2048
+static constexpr int kLoThreads = 1024;
+
+template <int C>
+__global__ void __launch_bounds__(kBinThreads)
+msm_keys_hist_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t stride, uint32_t skip_val,
+                     uint16_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t* __restrict__ counts,
+                     uint32_t ntiles) {
+  constexpr int NW = (255 + C - 1) / C;
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  for (int k = 0; k < kBinPer; k++) {
+    const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)k * kBinThreads + threadIdx.x;
+    if (i >= n) break;
+    Fr s = scalars[i];
+    if (mont) s = from_mont_fr29(s);
+    uint32_t kk[NW], vv[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      kk[w] = 0;
+      vv[w] = skip_val;
+    }
+    for_each_digit<C>(s, [&](int w, uint32_t b, uint32_t sign) {
+      kk[w] = b;
+      vv[w] = (uint32_t)((size_t)w * stride + i) | (sign << 31);
+    });
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      keys[(size_t)w * n + i] = (uint16_t)kk[w];
+      vals[(size_t)w * n + i] = vv[w];
+      atomicAdd(&h[kk[w] >> 8], 1u);
+    }
+  }
+  __syncthreads();
+  counts[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// in-place exclusive scan of counts[0..total) by one workgroup
+__global__ void __launch_bounds__(1024) msm_bin_scan_kernel(uint32_t* __restrict__ counts, size_t total) {
+  __shared__ uint32_t part[1024];
+  const size_t per = (total + 1023) / 1024;
+  const size_t lo = (size_t)threadIdx.x * per, hi = lo + per < total ? lo + per : total;
+  uint32_t s = 0;
+  for (size_t j = lo; j < hi; j++) s += counts[j];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+  for (size_t j = lo; j < hi; j++) {
+    const uint32_t c = counts[j];
+    counts[j] = run;
+    run += c;
+  }
+}
+
+template <int C>
+__global__ void __launch_bounds__(kBinThreads)
+msm_scatter_hi_kernel(const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t n,
+                      const uint32_t* __restrict__ offs, uint32_t ntiles, uint16_t* __restrict__ keys2,
+                      uint32_t* __restrict__ vals2) {
+  constexpr int NW = (255 + C - 1) / C;
+  __shared__ uint32_t base[256];
+  base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + blockIdx.x];
+  __syncthreads();
+  for (int k = 0; k < kBinPer; k++) {
+    const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)k * kBinThreads + threadIdx.x;
+    if (i >= n) break;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      const size_t e = (size_t)w * n + i;
+      const uint32_t key = keys[e];
+      const uint32_t pos = atomicAdd(&base[key >> 8], 1u);
+      keys2[pos] = (uint16_t)key;
+      vals2[pos] = vals[e];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kLoThreads)
+msm_bucket_lo_kernel(const uint16_t* __restrict__ keys2, const uint32_t* __restrict__ vals2,
+                     const uint32_t* __restrict__ offs, uint32_t ntiles, uint32_t m, uint32_t nkeys,
+                     uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted) {
+  __shared__ uint32_t h[256];
+  const uint32_t hb = blockIdx.x;
+  const uint32_t s = offs[(size_t)hb * ntiles];
+  const uint32_t e = hb == 255 ? m : offs[(size_t)(hb + 1) * ntiles];
+  if (threadIdx.x < 256) h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t p = s + threadIdx.x; p < e; p += kLoThreads) atomicAdd(&h[keys2[p] & 255u], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // exclusive scan of the 256 low-byte counts
+    uint32_t run = s;
+    for (int k = 0; k < 256; k++) {
+      const uint32_t c = h[k];
+      h[k] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    const uint32_t key = (hb << 8) | threadIdx.x;
+    if (key < nkeys) offsets[key] = h[threadIdx.x];
+  }
+  if (hb == 0 && threadIdx.x == 0) offsets[nkeys] = m;
+  __syncthreads();
+  for (uint32_t p = s + threadIdx.x; p < e; p += kLoThreads) {
+    const uint32_t pos = atomicAdd(&h[keys2[p] & 255u], 1u);
+    sorted[pos] = vals2[p];
+  }
+}
+
+static bool use_library_sort() {
+  static const bool v = [] {
+    const char* e = std::getenv("NZCB_ROCPRIM_SORT");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
 // offsets[k] = first position of a key >= k in the sorted key array (k = 0..nkeys)
 template <class K>
 __global__ void __launch_bounds__(kMsmThreads)
@@ -866,6 +1005,8 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
     buckets29.alloc(max_keys);
     carry_own29.alloc(nthreads);
     carry_cont29.alloc(nthreads);
+    bin_counts.alloc((size_t)256 * ((maxp + kTileScalars - 1) / kTileScalars));
+    vals_mid.alloc(max_entries);
   }
   carry_cont.alloc(nthreads);
   seg_tot.alloc(max_seg);
@@ -946,11 +1087,41 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     if (phases) NZ_HIP(hipEventRecord(sc.ev[i], st));
   };
   mark(0);
-  keys_dispatch(p.c, scalars, n, mont ? 1 : 0, table, sc, st);
-  mark(1);
+  const bool bins = table && (p.c == 16 || p.c == 17) && !use_library_sort() && sc.bin_counts.p;
+  if (bins) {  // hand-written bucketing (see msm_keys_hist_kernel)
+    const uint32_t ntiles = (uint32_t)((n + kTileScalars - 1) / kTileScalars);
+    const uint32_t inf_idx = (uint32_t)((size_t)table->nw * table->stride);
+    uint16_t* k16 = (uint16_t*)sc.keys_in.p;
+    uint16_t* k16b = (uint16_t*)sc.keys_out.p;
+    if (p.c == 17)
+      hipLaunchKernelGGL(msm_keys_hist_kernel<17>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, mont ? 1 : 0,
+                         table->stride, inf_idx, k16, sc.vals_in.p, sc.bin_counts.p, ntiles);
+    else
+      hipLaunchKernelGGL(msm_keys_hist_kernel<16>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, mont ? 1 : 0,
+                         table->stride, inf_idx, k16, sc.vals_in.p, sc.bin_counts.p, ntiles);
+    NZ_HIP(hipGetLastError());
+    mark(1);
+    hipLaunchKernelGGL(msm_bin_scan_kernel, dim3(1), dim3(1024), 0, st, sc.bin_counts.p, (size_t)256 * ntiles);
+    if (p.c == 17)
+      hipLaunchKernelGGL(msm_scatter_hi_kernel<17>, dim3(ntiles), dim3(kBinThreads), 0, st, k16, sc.vals_in.p, n,
+                         sc.bin_counts.p, ntiles, k16b, sc.vals_mid.p);
+    else
+      hipLaunchKernelGGL(msm_scatter_hi_kernel<16>, dim3(ntiles), dim3(kBinThreads), 0, st, k16, sc.vals_in.p, n,
+                         sc.bin_counts.p, ntiles, k16b, sc.vals_mid.p);
+    NZ_HIP(hipGetLastError());
+    mark(2);
+    hipLaunchKernelGGL(msm_bucket_lo_kernel, dim3(256), dim3(kLoThreads), 0, st, k16b, sc.vals_mid.p,
+                       sc.bin_counts.p, ntiles, (uint32_t)p.entries, p.nkeys, sc.offsets.p, sc.sorted.p);
+    NZ_HIP(hipGetLastError());
+  } else {
+    keys_dispatch(p.c, scalars, n, mont ? 1 : 0, table, sc, st);
+    mark(1);
+  }
   size_t tmp = sc.sort_tmp_bytes;
   const dim3 ogrid(grid_for((size_t)p.nkeys + 1, kMsmThreads, 1u << 30));
-  if (table && p.nkeys <= 65536) {  // 16-bit keys, no sentinel (see msm_keys_kernel)
+  if (bins) {
+    // offsets written by msm_bucket_lo_kernel
+  } else if (table && p.nkeys <= 65536) {  // 16-bit keys, no sentinel (see msm_keys_kernel)
     int end_bit = 0;
     while ((1u << end_bit) < p.nkeys) end_bit++;
     radix_sort(sc.sort_tmp.p, tmp, (const uint16_t*)sc.keys_in.p, (uint16_t*)sc.keys_out.p, sc.vals_in.p,
