@@ -122,8 +122,11 @@ int nzcb_memcpy_h2d(void* dst, const void* src, size_t bytes) {
 int nzcb_memcpy_d2h(void* dst, const void* src, size_t bytes) {
   return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : NZCB_ERR_HIP;
 }
+// Complete on return: a device-to-device hipMemcpy may return before the copy is done,
+// and callers hand the destination to work on non-blocking streams next (msmsplit).
 int nzcb_memcpy_d2d(void* dst, const void* src, size_t bytes) {
-  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice) == hipSuccess ? 0 : NZCB_ERR_HIP;
+  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, nullptr) != hipSuccess) return NZCB_ERR_HIP;
+  return hipStreamSynchronize(nullptr) == hipSuccess ? 0 : NZCB_ERR_HIP;
 }
 
 int nzcb_engine_ntt_dev(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, nzcb_err* err) {
