@@ -221,133 +221,263 @@ msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t strid
 }
 
 // ---- fixed-base bucketing (16-bit keys), replacing the library radix sort ------------
-// Entries (one per scalar and window) are grouped by bucket in two counting passes over
-// the key's high and low byte, reduce-then-scan, with every counter in LDS or fully
-// written (no look-back spinning, no memsets):
-//   1. msm_keys_hist_kernel  keys + values, and per tile of 2048 scalars the histogram of
-//                            the keys' high byte -> counts[hi][tile]
-//   2. msm_bin_scan_kernel   exclusive scan of counts in (hi, tile) order, one workgroup
-//   3. msm_scatter_hi_kernel each tile scatters its entries to their high-byte region
-//   4. msm_bucket_lo_kernel  one workgroup per high byte: low-byte histogram of its region,
-//                            local scan -> the 256 bucket offsets, scatter of the values
+// Entries (one per scalar and window) are grouped by bucket in two counting passes, over
+// the key's high byte and then its low byte, reduce-then-scan, with every counter in LDS
+// or fully written (no look-back spinning, no fills):
+//   1. msm_bin_hist_kernel    per tile of 1024 scalars: the digits, and the histogram of
+//                             the keys' high byte -> counts[hi][tile]
+//   2. msm_bin_rowscan/starts per high byte: exclusive scan over the tiles and the row
+//                             total, then the regions' starts (scan of the 256 totals)
+//   3. msm_bin_scatter_kernel per tile: the digits again (32 B read per scalar instead of
+//                             the 15 entries), ranked in LDS by high byte, then written
+//                             out run by run (coalesced) into the high-byte regions: the
+//                             value and the key's low byte
+//   4. msm_bucket_lo_kernel   one workgroup per high byte: low-byte histogram of its
+//                             region, local scan -> the 256 bucket offsets, scatter
 // Order inside a bucket is whatever the LDS atomics give: the accumulation adds the
 // bucket's points in any order and the sum is the same point.
-static constexpr int kBinThreads = 256;
-static constexpr int kBinPer = 8;                                   // scalars per thread and tile
-static constexpr uint32_t kTileScalars = kBinThreads * kBinPer;     // 2048
+static constexpr int kBinThreads = 1024;
+static constexpr uint32_t kTileScalars = kBinThreads;   // one scalar per thread and tile
 static constexpr int kLoThreads = 1024;
 
+// the (key, value) of every window of scalar i: zero digits -> key 0 and the table's
+// infinity entry, which the accumulation skips
+template <int C, int NW>
+__device__ __forceinline__ void bin_entries(const Fr* __restrict__ scalars, size_t i, int mont, size_t stride,
+                                            uint32_t skip_val, uint32_t (&kk)[NW], uint32_t (&vv)[NW]) {
+  Fr s = scalars[i];
+  if (mont) s = from_mont_fr29(s);
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    kk[w] = 0;
+    vv[w] = skip_val;
+  }
+  for_each_digit<C>(s, [&](int w, uint32_t b, uint32_t sign) {
+    kk[w] = b;
+    vv[w] = (uint32_t)((size_t)w * stride + i) | (sign << 31);
+  });
+}
+
 template <int C>
 __global__ void __launch_bounds__(kBinThreads)
-msm_keys_hist_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t stride, uint32_t skip_val,
-                     uint16_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t* __restrict__ counts,
-                     uint32_t ntiles) {
+msm_bin_hist_kernel(const Fr* __restrict__ scalars, size_t n, int mont, uint32_t* __restrict__ counts,
+                    uint32_t ntiles) {
   constexpr int NW = (255 + C - 1) / C;
   __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
+  if (threadIdx.x < 256) h[threadIdx.x] = 0;
   __syncthreads();
-  for (int k = 0; k < kBinPer; k++) {
-    const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)k * kBinThreads + threadIdx.x;
-    if (i >= n) break;
-    Fr s = scalars[i];
-    if (mont) s = from_mont_fr29(s);
+  const size_t i = (size_t)blockIdx.x * kTileScalars + threadIdx.x;
+  if (i < n) {
     uint32_t kk[NW], vv[NW];
+    bin_entries<C, NW>(scalars, i, mont, 0, 0, kk, vv);
 #pragma unroll
-    for (int w = 0; w < NW; w++) {
-      kk[w] = 0;
-      vv[w] = skip_val;
-    }
-    for_each_digit<C>(s, [&](int w, uint32_t b, uint32_t sign) {
-      kk[w] = b;
-      vv[w] = (uint32_t)((size_t)w * stride + i) | (sign << 31);
-    });
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-      keys[(size_t)w * n + i] = (uint16_t)kk[w];
-      vals[(size_t)w * n + i] = vv[w];
-      atomicAdd(&h[kk[w] >> 8], 1u);
-    }
+    for (int w = 0; w < NW; w++) atomicAdd(&h[kk[w] >> 8], 1u);
   }
   __syncthreads();
-  counts[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+  if (threadIdx.x < 256) counts[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
-// in-place exclusive scan of counts[0..total) by one workgroup
-__global__ void __launch_bounds__(1024) msm_bin_scan_kernel(uint32_t* __restrict__ counts, size_t total) {
-  __shared__ uint32_t part[1024];
-  const size_t per = (total + 1023) / 1024;
-  const size_t lo = (size_t)threadIdx.x * per, hi = lo + per < total ? lo + per : total;
-  uint32_t s = 0;
-  for (size_t j = lo; j < hi; j++) s += counts[j];
-  part[threadIdx.x] = s;
+// wave64 inclusive scan
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(v, off, 64);
+    if (lane >= off) v += u;
+  }
+  return v;
+}
+
+// one workgroup per high byte hb: exclusive scan of counts[hb][0..ntiles) in place
+// (coalesced 1024-wide chunks with a running carry), row total -> tail[hb]
+__global__ void __launch_bounds__(1024)
+msm_bin_rowscan_kernel(uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* __restrict__ tail) {
+  __shared__ uint32_t wsum[16];
+  uint32_t* row = counts + (size_t)blockIdx.x * ntiles;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < ntiles; c0 += 1024) {
+    const uint32_t t = c0 + threadIdx.x;
+    const uint32_t v = t < ntiles ? row[t] : 0u;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    if (wave == 0) {
+      const uint32_t w = lane < 16 ? wsum[lane] : 0u;
+      const uint32_t wi = wave_incl_scan(w);
+      if (lane < 16) wsum[lane] = wi - w;  // exclusive wave offsets
+    }
+    __syncthreads();
+    const uint32_t ex = carry + wsum[wave] + inc - v;
+    if (t < ntiles) row[t] = ex;
+    const uint32_t chunk_total = __shfl(inc, 63, 64) + wsum[wave];  // valid in the last wave
+    __syncthreads();
+    if (threadIdx.x == 1023) wsum[0] = chunk_total;
+    __syncthreads();
+    carry += wsum[0];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tail[blockIdx.x] = carry;
+}
+
+// tail[256 + hb] = sum of the row totals tail[0..hb): the start of high byte hb's region
+__global__ void __launch_bounds__(256) msm_bin_starts_kernel(uint32_t* __restrict__ tail) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t v = tail[threadIdx.x];
+  const uint32_t inc = wave_incl_scan(v);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) wsum[wave] = inc;
   __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-    const uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
-  for (size_t j = lo; j < hi; j++) {
-    const uint32_t c = counts[j];
-    counts[j] = run;
-    run += c;
-  }
+  uint32_t off = 0;
+  for (int w = 0; w < wave; w++) off += wsum[w];
+  tail[256 + threadIdx.x] = off + inc - v;
 }
 
 template <int C>
 __global__ void __launch_bounds__(kBinThreads)
-msm_scatter_hi_kernel(const uint16_t* __restrict__ keys, const uint32_t* __restrict__ vals, size_t n,
-                      const uint32_t* __restrict__ offs, uint32_t ntiles, uint16_t* __restrict__ keys2,
-                      uint32_t* __restrict__ vals2) {
+msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t stride, uint32_t skip_val,
+                       const uint32_t* __restrict__ counts, uint32_t ntiles, uint8_t* __restrict__ lo2,
+                       uint32_t* __restrict__ vals2) {
   constexpr int NW = (255 + C - 1) / C;
-  __shared__ uint32_t base[256];
-  base[threadIdx.x] = offs[(size_t)threadIdx.x * ntiles + blockIdx.x];
+  constexpr int TE = kTileScalars * NW;  // entries per tile
+  __shared__ uint32_t lcount[256], lstart[256], gbase[256];
+  __shared__ uint32_t lval[TE];
+  __shared__ uint16_t lkey[TE];
+  __shared__ uint32_t wsum[4];
+  if (threadIdx.x < 256) {
+    lcount[threadIdx.x] = 0;
+    const uint32_t* starts = counts + (size_t)256 * ntiles + 256;
+    gbase[threadIdx.x] = starts[threadIdx.x] + counts[(size_t)threadIdx.x * ntiles + blockIdx.x];
+  }
   __syncthreads();
-  for (int k = 0; k < kBinPer; k++) {
-    const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)k * kBinThreads + threadIdx.x;
-    if (i >= n) break;
+  const size_t i = (size_t)blockIdx.x * kTileScalars + threadIdx.x;
+  uint32_t kk[NW], vv[NW], rk[NW];
+  const bool live = i < n;
+  if (live) {
+    bin_entries<C, NW>(scalars, i, mont, stride, skip_val, kk, vv);
+#pragma unroll
+    for (int w = 0; w < NW; w++) rk[w] = atomicAdd(&lcount[kk[w] >> 8], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 256) {  // exclusive scan of the tile's 256 high-byte counts
+    const uint32_t v = lcount[threadIdx.x];
+    const uint32_t inc = wave_incl_scan(v);
+    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
+    lstart[threadIdx.x] = inc - v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    uint32_t off = 0;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) off += wsum[w];
+    lstart[threadIdx.x] += off;
+  }
+  __syncthreads();
+  if (live) {
 #pragma unroll
     for (int w = 0; w < NW; w++) {
-      const size_t e = (size_t)w * n + i;
-      const uint32_t key = keys[e];
-      const uint32_t pos = atomicAdd(&base[key >> 8], 1u);
-      keys2[pos] = (uint16_t)key;
-      vals2[pos] = vals[e];
+      const uint32_t q = lstart[kk[w] >> 8] + rk[w];
+      lkey[q] = (uint16_t)kk[w];
+      lval[q] = vv[w];
     }
+  }
+  __syncthreads();
+  const uint32_t total = n - (size_t)blockIdx.x * kTileScalars < kTileScalars
+                             ? (uint32_t)(n - (size_t)blockIdx.x * kTileScalars) * NW : (uint32_t)TE;
+  for (uint32_t q = threadIdx.x; q < total; q += kBinThreads) {  // runs of one high byte: coalesced
+    const uint32_t key = lkey[q], hb = key >> 8;
+    const uint32_t pos = gbase[hb] + (q - lstart[hb]);
+    lo2[pos] = (uint8_t)key;
+    vals2[pos] = lval[q];
   }
 }
 
 __global__ void __launch_bounds__(kLoThreads)
-msm_bucket_lo_kernel(const uint16_t* __restrict__ keys2, const uint32_t* __restrict__ vals2,
-                     const uint32_t* __restrict__ offs, uint32_t ntiles, uint32_t m, uint32_t nkeys,
-                     uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted) {
-  __shared__ uint32_t h[256];
+msm_bucket_lo_kernel(const uint8_t* __restrict__ lo2, const uint32_t* __restrict__ vals2,
+                     const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t m, uint32_t nkeys,
+                     uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted, uint32_t* __restrict__ large) {
+  constexpr uint32_t U = 8;
+  __shared__ uint32_t h[256], lcnt[256], lst[256];
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t lv[U * kLoThreads];
+  __shared__ uint8_t lk[U * kLoThreads];
   const uint32_t hb = blockIdx.x;
-  const uint32_t s = offs[(size_t)hb * ntiles];
-  const uint32_t e = hb == 255 ? m : offs[(size_t)(hb + 1) * ntiles];
+  const uint32_t* tail = counts + (size_t)256 * ntiles;  // row totals, then region starts
+  const uint32_t s = tail[256 + hb];
+  const uint32_t e = s + tail[hb];
   if (threadIdx.x < 256) h[threadIdx.x] = 0;
   __syncthreads();
-  for (uint32_t p = s + threadIdx.x; p < e; p += kLoThreads) atomicAdd(&h[keys2[p] & 255u], 1u);
-  __syncthreads();
-  if (threadIdx.x == 0) {  // exclusive scan of the 256 low-byte counts
-    uint32_t run = s;
-    for (int k = 0; k < 256; k++) {
-      const uint32_t c = h[k];
-      h[k] = run;
-      run += c;
+  // 8 independent loads in flight per thread before their atomics (the loop is
+  // latency-bound otherwise: one workgroup per CU walks ~n*15/256 entries)
+  for (uint32_t p0 = s; p0 < e; p0 += U * kLoThreads) {
+    uint32_t k8[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t p = p0 + u * kLoThreads + threadIdx.x;
+      k8[u] = p < e ? (uint32_t)lo2[p] : 256u;
     }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (k8[u] < 256u) atomicAdd(&h[k8[u]], 1u);
   }
+  __syncthreads();
+  // exclusive scan of the 256 low-byte counts -> bucket offsets (waves 0-3)
+  const uint32_t v = threadIdx.x < 256 ? h[threadIdx.x] : 0u;
+  const uint32_t inc = wave_incl_scan(v);
+  if (threadIdx.x < 256 && (threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
   __syncthreads();
   if (threadIdx.x < 256) {
+    uint32_t off = s;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) off += wsum[w];
+    h[threadIdx.x] = off + inc - v;
     const uint32_t key = (hb << 8) | threadIdx.x;
-    if (key < nkeys) offsets[key] = h[threadIdx.x];
+    if (key < nkeys) offsets[key] = off + inc - v;
   }
-  if (hb == 0 && threadIdx.x == 0) offsets[nkeys] = m;
+  if (hb == 0 && threadIdx.x == 0) {
+    offsets[nkeys] = m;
+    large[0] = 0;  // the finalize's count of long bucket runs (no fill kernel)
+  }
   __syncthreads();
-  for (uint32_t p = s + threadIdx.x; p < e; p += kLoThreads) {
-    const uint32_t pos = atomicAdd(&h[keys2[p] & 255u], 1u);
-    sorted[pos] = vals2[p];
+  // scatter in chunks of U * 1024 entries, each ranked by low byte in LDS first and
+  // written out run by run (coalesced)
+  for (uint32_t p0 = s; p0 < e; p0 += U * kLoThreads) {
+    uint32_t k8[U], v8[U], r8[U];
+    if (threadIdx.x < 256) lcnt[threadIdx.x] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t p = p0 + u * kLoThreads + threadIdx.x;
+      k8[u] = p < e ? (uint32_t)lo2[p] : 256u;
+      v8[u] = p < e ? vals2[p] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (k8[u] < 256u) r8[u] = atomicAdd(&lcnt[k8[u]], 1u);
+    __syncthreads();
+    const uint32_t c = threadIdx.x < 256 ? lcnt[threadIdx.x] : 0u;
+    const uint32_t ci = wave_incl_scan(c);
+    if (threadIdx.x < 256 && (threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = ci;
+    __syncthreads();
+    if (threadIdx.x < 256) {
+      uint32_t off = 0;
+      for (int w = 0; w < (int)(threadIdx.x >> 6); w++) off += wsum[w];
+      lst[threadIdx.x] = off + ci - c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (k8[u] < 256u) {
+        const uint32_t q = lst[k8[u]] + r8[u];
+        lk[q] = (uint8_t)k8[u];
+        lv[q] = v8[u];
+      }
+    __syncthreads();
+    const uint32_t cnt = e - p0 < U * kLoThreads ? e - p0 : U * kLoThreads;
+    for (uint32_t q = threadIdx.x; q < cnt; q += kLoThreads) {
+      const uint32_t k = lk[q];
+      sorted[h[k] + (q - lst[k])] = lv[q];
+    }
+    __syncthreads();
+    if (threadIdx.x < 256) h[threadIdx.x] += c;
   }
 }
 
@@ -1005,7 +1135,7 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
     buckets29.alloc(max_keys);
     carry_own29.alloc(nthreads);
     carry_cont29.alloc(nthreads);
-    bin_counts.alloc((size_t)256 * ((maxp + kTileScalars - 1) / kTileScalars));
+    bin_counts.alloc((size_t)256 * ((maxp + kTileScalars - 1) / kTileScalars) + 512);  // + totals, starts
     vals_mid.alloc(max_entries);
   }
   carry_cont.alloc(nthreads);
@@ -1088,30 +1218,33 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   };
   mark(0);
   const bool bins = table && (p.c == 16 || p.c == 17) && !use_library_sort() && sc.bin_counts.p;
-  if (bins) {  // hand-written bucketing (see msm_keys_hist_kernel)
+  if (bins) {  // hand-written bucketing (see msm_bin_hist_kernel)
     const uint32_t ntiles = (uint32_t)((n + kTileScalars - 1) / kTileScalars);
     const uint32_t inf_idx = (uint32_t)((size_t)table->nw * table->stride);
-    uint16_t* k16 = (uint16_t*)sc.keys_in.p;
-    uint16_t* k16b = (uint16_t*)sc.keys_out.p;
+    uint8_t* lo2 = (uint8_t*)sc.keys_out.p;
+    uint32_t* tail = sc.bin_counts.p + (size_t)256 * ntiles;
+    const int m = mont ? 1 : 0;
     if (p.c == 17)
-      hipLaunchKernelGGL(msm_keys_hist_kernel<17>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, mont ? 1 : 0,
-                         table->stride, inf_idx, k16, sc.vals_in.p, sc.bin_counts.p, ntiles);
+      hipLaunchKernelGGL(msm_bin_hist_kernel<17>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
+                         sc.bin_counts.p, ntiles);
     else
-      hipLaunchKernelGGL(msm_keys_hist_kernel<16>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, mont ? 1 : 0,
-                         table->stride, inf_idx, k16, sc.vals_in.p, sc.bin_counts.p, ntiles);
+      hipLaunchKernelGGL(msm_bin_hist_kernel<16>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
+                         sc.bin_counts.p, ntiles);
     NZ_HIP(hipGetLastError());
     mark(1);
-    hipLaunchKernelGGL(msm_bin_scan_kernel, dim3(1), dim3(1024), 0, st, sc.bin_counts.p, (size_t)256 * ntiles);
+    hipLaunchKernelGGL(msm_bin_rowscan_kernel, dim3(256), dim3(1024), 0, st, sc.bin_counts.p, ntiles, tail);
+    hipLaunchKernelGGL(msm_bin_starts_kernel, dim3(1), dim3(256), 0, st, tail);
     if (p.c == 17)
-      hipLaunchKernelGGL(msm_scatter_hi_kernel<17>, dim3(ntiles), dim3(kBinThreads), 0, st, k16, sc.vals_in.p, n,
-                         sc.bin_counts.p, ntiles, k16b, sc.vals_mid.p);
+      hipLaunchKernelGGL(msm_bin_scatter_kernel<17>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
+                         table->stride, inf_idx, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
     else
-      hipLaunchKernelGGL(msm_scatter_hi_kernel<16>, dim3(ntiles), dim3(kBinThreads), 0, st, k16, sc.vals_in.p, n,
-                         sc.bin_counts.p, ntiles, k16b, sc.vals_mid.p);
+      hipLaunchKernelGGL(msm_bin_scatter_kernel<16>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
+                         table->stride, inf_idx, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
     NZ_HIP(hipGetLastError());
     mark(2);
-    hipLaunchKernelGGL(msm_bucket_lo_kernel, dim3(256), dim3(kLoThreads), 0, st, k16b, sc.vals_mid.p,
-                       sc.bin_counts.p, ntiles, (uint32_t)p.entries, p.nkeys, sc.offsets.p, sc.sorted.p);
+    hipLaunchKernelGGL(msm_bucket_lo_kernel, dim3(256), dim3(kLoThreads), 0, st, lo2, sc.vals_mid.p,
+                       sc.bin_counts.p, ntiles, (uint32_t)p.entries, p.nkeys, sc.offsets.p, sc.sorted.p,
+                       sc.large.p);
     NZ_HIP(hipGetLastError());
   } else {
     keys_dispatch(p.c, scalars, n, mont ? 1 : 0, table, sc, st);
@@ -1188,7 +1321,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   }
   NZ_HIP(hipGetLastError());
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[4], st));
-  NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));
+  if (!bins) NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));  // bins: zeroed by msm_bucket_lo_kernel
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
   if (table) {
     hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, acc_off, p.nkeys,

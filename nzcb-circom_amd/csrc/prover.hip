@@ -680,14 +680,16 @@ void Prover::alloc_workspace() {
   A4.alloc(n4); B4.alloc(n4); C4.alloc(n4); Z4.alloc(n4);
   T.alloc(n4); Tz.alloc(n4); t.alloc(n4);
   pol_r.alloc(n + 3); pol_wxi.alloc(n + 6); pol_wxiw.alloc(n + 3);
-  blind.alloc(12);
+  blind.alloc(13);  // b1..b11 (index 0 unused), then the 32-bit check flags in slot 12
   size_t lv = 0, m = n4;
   while (m > 1024) { m = (m + kScanChunk - 1) / kScanChunk; lv += m; }
   scan_tmp.alloc(lv + 2048);
   size_t nblocks = ((size_t)3 * n + 6 + (size_t)kT * kEvalChunk - 1) / ((size_t)kT * kEvalChunk) + 1;
   eval_part.alloc(nblocks);
   host_part.resize(nblocks);
-  flags.alloc(1);
+  flags.p = (uint32_t*)(blind.p + 12);  // a view: the blinding upload also clears the flags
+  flags.n = 1;
+  flags.owned = false;
 }
 
 // An extra proof lane on the primary's device: shares the HBM-resident proving key
@@ -935,14 +937,14 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   auto T0 = std::chrono::steady_clock::now();
   auto lg = [&](const std::string& m) { if (log) log(m); };
   // blinding scalars b1..b11 (Montgomery); index 0 unused
-  Fr bl[12];
+  Fr bl[13];
   bl[0] = Fr::zero();
+  bl[12] = Fr::zero();  // the check flags (one upload, no fill kernel)
   // NULL blinding: uniform scalars from the OS CSPRNG, as snarkjs's Fr.random() (a proof
   // with zero blinding is not zero-knowledge); callers that want a reproducible proof pass
   // explicit bytes (all zero included)
   for (int i = 1; i <= 11; i++) bl[i] = blinding ? fr_from_le_normal(blinding + 32 * (i - 1)) : random_fr();
   NZ_HIP(hipMemcpyAsync(blind.p, bl, sizeof(bl), hipMemcpyHostToDevice, s));
-  NZ_HIP(hipMemsetAsync(flags.p, 0, sizeof(uint32_t), s));
 
   lg("Reading Wtns");
   const Fr* wsrc = (const Fr*)witness;
