@@ -33,7 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--prefix", default="r1")
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
-    ap.add_argument("--prof", default="prof_r1")
+    ap.add_argument("--prof", default="prof")
     a = ap.parse_args()
     out = os.path.join(ROOT, "profiles")
     src = a.src
@@ -43,12 +43,19 @@ def main():
     bench = json.loads(line)
     with open(os.path.join(out, f"{a.prefix}_bench_line.txt"), "w") as f:
         f.write("# rocprofv3 --kernel-trace --stats -- python3 bench.py   (defaults)\n" + line)
-    launches = bench["roofline"]["launches"]
-    summ = subprocess.run([sys.executable, os.path.join(HERE, "trace_summary.py"),
-                           os.path.join(prof, "run_kernel_trace.csv"), "--last", KERNEL, str(launches), "--top", "30"],
-                          check=True, capture_output=True, text=True).stdout
+    launches = bench["roofline"]["launches_timed"]
+    probe = 10   # bench.py accumulate_probe: 1 warm + 10 timed launches, the last of the run
+    ts = os.path.join(HERE, "trace_summary.py")
+    trace = os.path.join(prof, "run_kernel_trace.csv")
+    psumm = subprocess.run([sys.executable, ts, trace, "--last", KERNEL, str(probe), "--durations", "--top", "12"],
+                           check=True, capture_output=True, text=True).stdout
+    summ = subprocess.run([sys.executable, ts, trace, "--last", KERNEL, str(launches), "--skip-last", str(probe + 1),
+                           "--durations", "--top", "30"], check=True, capture_output=True, text=True).stdout
     with open(os.path.join(out, f"{a.prefix}_bench_trace_summary.txt"), "w") as f:
-        f.write(f"# timed window: the last {launches} {KERNEL} launches of the profiled bench.py run\n" + summ)
+        f.write(f"# isolated probe: the last {probe} {KERNEL} launches of the profiled bench.py run "
+                f"(bench.py accumulate_probe; roofline.avg_launch_ms = {bench['roofline']['avg_launch_ms']} ms "
+                f"from its HIP events)\n" + psumm +
+                f"\n# timed window: the {launches} {KERNEL} launches before the probe (40 proofs x 9 MSMs)\n" + summ)
     nf, fetch_kb = pmc_avg(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     nw, write_kb = pmc_avg(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     fetch_raw = fetch_kb * 1024
@@ -68,10 +75,10 @@ def main():
     with open(os.path.join(out, "accumulate_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
         f.write("\n")
-    mb = os.path.join(src, "microbench_r1.log")
+    mb = os.path.join(src, "microbench.log")
     if os.path.exists(mb):
         shutil.copy(mb, os.path.join(out, f"{a.prefix}_microbench.txt"))
-    print(summ)
+    print(psumm + summ)
 
 
 if __name__ == "__main__":

@@ -13,6 +13,10 @@ def main():
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--last", nargs=2, metavar=("KERNEL", "COUNT"),
                     help="window from the COUNT-th last launch of a kernel whose name contains KERNEL to its last")
+    ap.add_argument("--skip-last", type=int, default=0,
+                    help="with --last: end the window before the kernel's last SKIP launches (e.g. a probe)")
+    ap.add_argument("--durations", action="store_true",
+                    help="with --last: also print the average duration of the KERNEL launches in the window")
     a = ap.parse_args()
     rows = []
     if a.trace.endswith(".db"):  # rocprofv3 >= 7 default output (rocpd SQLite)
@@ -26,9 +30,16 @@ def main():
     rows.sort()
     t_end = max(e for _, e, _ in rows)
     if a.last:
-        hits = [r for r in rows if a.last[0] in r[2]][-int(a.last[1]):]
+        hits = [r for r in rows if a.last[0] in r[2]]
+        if a.skip_last:
+            hits = hits[:-a.skip_last]
+        hits = hits[-int(a.last[1]):]
         lo, t_end = hits[0][0], hits[-1][1]
         rows = [r for r in rows if lo <= r[0] and r[1] <= t_end]
+        if a.durations:
+            d = [e - s for s, e, _ in hits]
+            print(f"{a.last[0]}: {len(d)} launches, average duration {sum(d) / len(d) / 1e6:.4f} ms, "
+                  f"min {min(d) / 1e6:.4f} ms, max {max(d) / 1e6:.4f} ms")
     elif a.window > 0:
         rows = [r for r in rows if r[0] >= t_end - a.window * 1e9]
     t0 = min(s for s, _, _ in rows)
