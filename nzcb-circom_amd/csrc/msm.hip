@@ -224,10 +224,10 @@ msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t strid
 // Entries (one per scalar and window) are grouped by bucket in two counting passes, over
 // the key's high byte and then its low byte, reduce-then-scan, with every counter in LDS
 // or fully written (no look-back spinning, no fills):
-//   1. msm_bin_hist_kernel    per tile of 1024 scalars: the digits, and the histogram of
+//   1. msm_bin_hist_kernel    per tile of 512 scalars: the digits, and the histogram of
 //                             the keys' high byte -> counts[hi][tile]
-//   2. msm_bin_rowscan/starts per high byte: exclusive scan over the tiles and the row
-//                             total, then the regions' starts (scan of the 256 totals)
+//   2. msm_bin_rowscan_kernel per high byte: exclusive scan over the tiles and the row
+//                             total (consumers scan the 256 totals for the region starts)
 //   3. msm_bin_scatter_kernel per tile: the digits again (32 B read per scalar instead of
 //                             the 15 entries), ranked in LDS by high byte, then written
 //                             out run by run (coalesced) into the high-byte regions: the
@@ -236,9 +236,13 @@ msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t strid
 //                             region, local scan -> the 256 bucket offsets, scatter
 // Order inside a bucket is whatever the LDS atomics give: the accumulation adds the
 // bucket's points in any order and the sum is the same point.
-static constexpr int kBinThreads = 1024;
-static constexpr uint32_t kTileScalars = kBinThreads;   // one scalar per thread and tile
-static constexpr int kLoThreads = 1024;
+// 256- and 512-thread workgroups with modest LDS: under 5 proof lanes these kernels share
+// the CUs with the accumulation's waves, and a 1024-thread or 95 KB-LDS workgroup waits
+// for a whole CU to drain (measured: 5.3 ms average scatter launch in the pipeline)
+static constexpr int kBinThreads = 256;
+static constexpr int kBinPer = 2;                                  // scalars per thread and tile
+static constexpr uint32_t kTileScalars = kBinThreads * kBinPer;    // 512
+static constexpr int kLoThreads = 512;
 
 // the (key, value) of every window of scalar i: zero digits -> key 0 and the table's
 // infinity entry, which the accumulation skips
@@ -264,17 +268,20 @@ msm_bin_hist_kernel(const Fr* __restrict__ scalars, size_t n, int mont, uint32_t
                     uint32_t ntiles) {
   constexpr int NW = (255 + C - 1) / C;
   __shared__ uint32_t h[256];
-  if (threadIdx.x < 256) h[threadIdx.x] = 0;
+  h[threadIdx.x] = 0;
   __syncthreads();
-  const size_t i = (size_t)blockIdx.x * kTileScalars + threadIdx.x;
-  if (i < n) {
-    uint32_t kk[NW], vv[NW];
-    bin_entries<C, NW>(scalars, i, mont, 0, 0, kk, vv);
 #pragma unroll
-    for (int w = 0; w < NW; w++) atomicAdd(&h[kk[w] >> 8], 1u);
+  for (int j = 0; j < kBinPer; j++) {
+    const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)j * kBinThreads + threadIdx.x;
+    if (i < n) {
+      uint32_t kk[NW], vv[NW];
+      bin_entries<C, NW>(scalars, i, mont, 0, 0, kk, vv);
+#pragma unroll
+      for (int w = 0; w < NW; w++) atomicAdd(&h[kk[w] >> 8], 1u);
+    }
   }
   __syncthreads();
-  if (threadIdx.x < 256) counts[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+  counts[(size_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
 // wave64 inclusive scan
@@ -288,49 +295,36 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-// one workgroup per high byte hb: exclusive scan of counts[hb][0..ntiles) in place
-// (coalesced 1024-wide chunks with a running carry), row total -> tail[hb]
-__global__ void __launch_bounds__(1024)
-msm_bin_rowscan_kernel(uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* __restrict__ tail) {
-  __shared__ uint32_t wsum[16];
-  uint32_t* row = counts + (size_t)blockIdx.x * ntiles;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t carry = 0;
-  for (uint32_t c0 = 0; c0 < ntiles; c0 += 1024) {
-    const uint32_t t = c0 + threadIdx.x;
-    const uint32_t v = t < ntiles ? row[t] : 0u;
-    const uint32_t inc = wave_incl_scan(v);
-    if (lane == 63) wsum[wave] = inc;
-    __syncthreads();
-    if (wave == 0) {
-      const uint32_t w = lane < 16 ? wsum[lane] : 0u;
-      const uint32_t wi = wave_incl_scan(w);
-      if (lane < 16) wsum[lane] = wi - w;  // exclusive wave offsets
-    }
-    __syncthreads();
-    const uint32_t ex = carry + wsum[wave] + inc - v;
-    if (t < ntiles) row[t] = ex;
-    const uint32_t chunk_total = __shfl(inc, 63, 64) + wsum[wave];  // valid in the last wave
-    __syncthreads();
-    if (threadIdx.x == 1023) wsum[0] = chunk_total;
-    __syncthreads();
-    carry += wsum[0];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) tail[blockIdx.x] = carry;
-}
-
-// tail[256 + hb] = sum of the row totals tail[0..hb): the start of high byte hb's region
-__global__ void __launch_bounds__(256) msm_bin_starts_kernel(uint32_t* __restrict__ tail) {
-  __shared__ uint32_t wsum[4];
-  const uint32_t v = tail[threadIdx.x];
-  const uint32_t inc = wave_incl_scan(v);
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 63) wsum[wave] = inc;
+// exclusive scan of v over the first 256 threads of the workgroup (blockDim >= 256; every
+// thread calls it): returns the thread's exclusive prefix (threads >= 256: 0) and the
+// total of the 256 values
+__device__ __forceinline__ uint32_t scan256_excl(uint32_t v, uint32_t* wsum4, uint32_t& total) {
+  const uint32_t inc = wave_incl_scan(threadIdx.x < 256 ? v : 0u);
+  if (threadIdx.x < 256 && (threadIdx.x & 63) == 63) wsum4[threadIdx.x >> 6] = inc;
   __syncthreads();
   uint32_t off = 0;
-  for (int w = 0; w < wave; w++) off += wsum[w];
-  tail[256 + threadIdx.x] = off + inc - v;
+  for (int w = 0; w < (int)(threadIdx.x >> 6) && w < 4; w++) off += wsum4[w];
+  total = wsum4[0] + wsum4[1] + wsum4[2] + wsum4[3];
+  __syncthreads();
+  return threadIdx.x < 256 ? off + inc - v : 0u;
+}
+
+// one workgroup (256 threads) per high byte hb: exclusive scan of counts[hb][0..ntiles) in
+// place (coalesced 256-wide chunks with a running carry), row total -> tail[hb]
+__global__ void __launch_bounds__(256)
+msm_bin_rowscan_kernel(uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* __restrict__ tail) {
+  __shared__ uint32_t wsum[4];
+  uint32_t* row = counts + (size_t)blockIdx.x * ntiles;
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < ntiles; c0 += 256) {
+    const uint32_t t = c0 + threadIdx.x;
+    const uint32_t v = t < ntiles ? row[t] : 0u;
+    uint32_t tot;
+    const uint32_t ex = scan256_excl(v, wsum, tot);
+    if (t < ntiles) row[t] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) tail[blockIdx.x] = carry;
 }
 
 template <int C>
@@ -344,45 +338,45 @@ msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_
   __shared__ uint32_t lval[TE];
   __shared__ uint16_t lkey[TE];
   __shared__ uint32_t wsum[4];
-  if (threadIdx.x < 256) {
+  const uint32_t* tail = counts + (size_t)256 * ntiles;  // row totals
+  {
+    uint32_t tot;
+    const uint32_t st = scan256_excl(tail[threadIdx.x], wsum, tot);  // start of region threadIdx.x
+    gbase[threadIdx.x] = st + counts[(size_t)threadIdx.x * ntiles + blockIdx.x];
     lcount[threadIdx.x] = 0;
-    const uint32_t* starts = counts + (size_t)256 * ntiles + 256;
-    gbase[threadIdx.x] = starts[threadIdx.x] + counts[(size_t)threadIdx.x * ntiles + blockIdx.x];
   }
   __syncthreads();
-  const size_t i = (size_t)blockIdx.x * kTileScalars + threadIdx.x;
-  uint32_t kk[NW], vv[NW], rk[NW];
-  const bool live = i < n;
-  if (live) {
-    bin_entries<C, NW>(scalars, i, mont, stride, skip_val, kk, vv);
+  uint32_t kk[kBinPer][NW], vv[kBinPer][NW], rk[kBinPer][NW];
 #pragma unroll
-    for (int w = 0; w < NW; w++) rk[w] = atomicAdd(&lcount[kk[w] >> 8], 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x < 256) {  // exclusive scan of the tile's 256 high-byte counts
-    const uint32_t v = lcount[threadIdx.x];
-    const uint32_t inc = wave_incl_scan(v);
-    if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
-    lstart[threadIdx.x] = inc - v;
-  }
-  __syncthreads();
-  if (threadIdx.x < 256) {
-    uint32_t off = 0;
-    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) off += wsum[w];
-    lstart[threadIdx.x] += off;
-  }
-  __syncthreads();
-  if (live) {
+  for (int j = 0; j < kBinPer; j++) {
+    const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)j * kBinThreads + threadIdx.x;
+    if (i < n) {
+      bin_entries<C, NW>(scalars, i, mont, stride, skip_val, kk[j], vv[j]);
 #pragma unroll
-    for (int w = 0; w < NW; w++) {
-      const uint32_t q = lstart[kk[w] >> 8] + rk[w];
-      lkey[q] = (uint16_t)kk[w];
-      lval[q] = vv[w];
+      for (int w = 0; w < NW; w++) rk[j][w] = atomicAdd(&lcount[kk[j][w] >> 8], 1u);
     }
   }
   __syncthreads();
-  const uint32_t total = n - (size_t)blockIdx.x * kTileScalars < kTileScalars
-                             ? (uint32_t)(n - (size_t)blockIdx.x * kTileScalars) * NW : (uint32_t)TE;
+  {  // exclusive scan of the tile's 256 high-byte counts
+    uint32_t tot;
+    lstart[threadIdx.x] = scan256_excl(lcount[threadIdx.x], wsum, tot);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kBinPer; j++) {
+    const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)j * kBinThreads + threadIdx.x;
+    if (i < n) {
+#pragma unroll
+      for (int w = 0; w < NW; w++) {
+        const uint32_t q = lstart[kk[j][w] >> 8] + rk[j][w];
+        lkey[q] = (uint16_t)kk[j][w];
+        lval[q] = vv[j][w];
+      }
+    }
+  }
+  __syncthreads();
+  const size_t left = n - (size_t)blockIdx.x * kTileScalars;
+  const uint32_t total = left < kTileScalars ? (uint32_t)left * NW : (uint32_t)TE;
   for (uint32_t q = threadIdx.x; q < total; q += kBinThreads) {  // runs of one high byte: coalesced
     const uint32_t key = lkey[q], hb = key >> 8;
     const uint32_t pos = gbase[hb] + (q - lstart[hb]);
@@ -396,15 +390,21 @@ msm_bucket_lo_kernel(const uint8_t* __restrict__ lo2, const uint32_t* __restrict
                      const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t m, uint32_t nkeys,
                      uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted, uint32_t* __restrict__ large) {
   constexpr uint32_t U = 8;
-  __shared__ uint32_t h[256], lcnt[256], lst[256];
+  __shared__ uint32_t h[256], lcnt[256], lst[256];  // lst[0] first holds the region start
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t lv[U * kLoThreads];
   __shared__ uint8_t lk[U * kLoThreads];
   const uint32_t hb = blockIdx.x;
-  const uint32_t* tail = counts + (size_t)256 * ntiles;  // row totals, then region starts
-  const uint32_t s = tail[256 + hb];
+  const uint32_t* tail = counts + (size_t)256 * ntiles;  // row totals
+  {
+    uint32_t tot;
+    const uint32_t st = scan256_excl(threadIdx.x < 256 ? tail[threadIdx.x] : 0u, wsum, tot);
+    if (threadIdx.x == hb) lst[0] = st;  // this region's start
+    if (threadIdx.x < 256) h[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const uint32_t s = lst[0];
   const uint32_t e = s + tail[hb];
-  if (threadIdx.x < 256) h[threadIdx.x] = 0;
   __syncthreads();
   // 8 independent loads in flight per thread before their atomics (the loop is
   // latency-bound otherwise: one workgroup per CU walks ~n*15/256 entries)
@@ -437,7 +437,7 @@ msm_bucket_lo_kernel(const uint8_t* __restrict__ lo2, const uint32_t* __restrict
     large[0] = 0;  // the finalize's count of long bucket runs (no fill kernel)
   }
   __syncthreads();
-  // scatter in chunks of U * 1024 entries, each ranked by low byte in LDS first and
+  // scatter in chunks of U * kLoThreads entries, each ranked by low byte in LDS first and
   // written out run by run (coalesced)
   for (uint32_t p0 = s; p0 < e; p0 += U * kLoThreads) {
     uint32_t k8[U], v8[U], r8[U];
@@ -1135,7 +1135,7 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
     buckets29.alloc(max_keys);
     carry_own29.alloc(nthreads);
     carry_cont29.alloc(nthreads);
-    bin_counts.alloc((size_t)256 * ((maxp + kTileScalars - 1) / kTileScalars) + 512);  // + totals, starts
+    bin_counts.alloc((size_t)256 * ((maxp + kTileScalars - 1) / kTileScalars) + 256);  // + row totals
     vals_mid.alloc(max_entries);
   }
   carry_cont.alloc(nthreads);
@@ -1232,8 +1232,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                          sc.bin_counts.p, ntiles);
     NZ_HIP(hipGetLastError());
     mark(1);
-    hipLaunchKernelGGL(msm_bin_rowscan_kernel, dim3(256), dim3(1024), 0, st, sc.bin_counts.p, ntiles, tail);
-    hipLaunchKernelGGL(msm_bin_starts_kernel, dim3(1), dim3(256), 0, st, tail);
+    hipLaunchKernelGGL(msm_bin_rowscan_kernel, dim3(256), dim3(256), 0, st, sc.bin_counts.p, ntiles, tail);
     if (p.c == 17)
       hipLaunchKernelGGL(msm_bin_scatter_kernel<17>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
                          table->stride, inf_idx, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
