@@ -590,9 +590,17 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
   uint32_t kstart = offsets[k], kend = offsets[k + 1];
   Xyzz29 acc;
   bool inf = true;
+  // software pipeline: the next entry's table point is loaded before this entry's
+  // addition, so the gather's latency hides behind ~8k cycles of arithmetic
+  uint32_t ent = kDirect ? 0u : sorted[s];
+  G1Affine P = bases[kDirect ? s : ent & 0x7fffffffu];
   for (uint32_t pos = s; pos < e;) {
-    const uint32_t ent = kDirect ? 0u : sorted[pos];
-    const G1Affine P = bases[kDirect ? pos : ent & 0x7fffffffu];
+    uint32_t ent_n = 0;
+    G1Affine Pn;
+    if (pos + 1 < e) {
+      ent_n = kDirect ? 0u : sorted[pos + 1];
+      Pn = bases[kDirect ? pos + 1 : ent_n & 0x7fffffffu];
+    }
     if (!P.is_inf()) {
       const F29 x = split29(P.x);
       F29 y = split29(P.y);
@@ -638,12 +646,16 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
       else if (!starts) carry_cont[t] = out;
       else carry_own[t] = out;
       inf = true;
-      if (pos < e) {
-        k = find_key(offsets, nkeys, pos);
-        kstart = offsets[k];
+      // next non-empty bucket: a linear walk (one load per bucket; runs average
+      // entries / nkeys ~ 480 at 2^21, so a chunk crosses at most a few boundaries)
+      while (pos < e && kend <= pos) {
+        k++;
+        kstart = kend;
         kend = offsets[k + 1];
       }
     }
+    ent = ent_n;
+    P = Pn;
   }
 }
 
