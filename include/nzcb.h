@@ -180,6 +180,13 @@ int nzcb_verify(const uint8_t* vk, const uint8_t* proof, const uint8_t* pub, int
 /* snarkjs `zkey export soliditycalldata` for PLONK (/root/reference/Makefile:57,62 verifier):
  * "0x<proof hex>,[\"0x<pub>\",...]"; returns 0, or the needed size if cap is short. */
 int nzcb_proof_to_calldata(const uint8_t* proof, const uint8_t* pub, int n_public, char* out, size_t cap);
+/* snarkjs `zkey export solidityverifier` (/root/reference/Makefile:57,62; the contract
+ * /root/reference/deploy-script.js:4-7 deploys): a Solidity PLONK verifier for this key,
+ * verifyProof(bytes proof, uint256[] pubSignals) taking the soliditycalldata arguments
+ * above. contract_name: NULL = "PlonkVerifier" (snarkjs's name; the reference's deploy
+ * script asks for "Verifier"). transcript_public as nzcb_verify. Returns 0, the needed
+ * size if cap is short, or -1 for a bad key or name. Parity unpinned (csrc/solidity.cpp). */
+int nzcb_vk_to_solidity(const uint8_t* vk, const char* contract_name, int transcript_public, char* out, size_t cap);
 
 /* ---- nzcp witness -----------------------------------
  * The semantic signals and public outputs of NZCPPubIdentity

@@ -436,6 +436,34 @@ napi_value Calldata(napi_env env, napi_callback_info info) {
   return json_string(env, s);
 }
 
+// vkToSolidity(vk: Buffer, name: string, transcriptPublic: bool) -> string
+// (snarkjs `zkey export solidityverifier`)
+napi_value VkToSolidity(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  const uint8_t* vk;
+  size_t vl;
+  char name[80] = {0};
+  size_t nl = 0;
+  bool tp = true;
+  if (argc < 3 || !buf_arg(env, argv[0], &vk, &vl) || vl != NZCB_VK_BYTES ||
+      napi_get_value_string_utf8(env, argv[1], name, sizeof(name), &nl) != napi_ok ||
+      napi_get_value_bool(env, argv[2], &tp) != napi_ok) {
+    napi_throw_type_error(env, nullptr, "vkToSolidity(vk: Buffer, name: string, transcriptPublic: boolean)");
+    return nullptr;
+  }
+  const int need = nzcb_vk_to_solidity(vk, name, tp ? 1 : 0, nullptr, 0);
+  if (need < 0) {
+    napi_throw_error(env, nullptr, "solidity verifier: bad verification key or contract name");
+    return nullptr;
+  }
+  std::string s((size_t)need, '\0');
+  nzcb_vk_to_solidity(vk, name, tp ? 1 : 0, &s[0], s.size());
+  s.resize(std::strlen(s.c_str()));
+  return json_string(env, s);
+}
+
 // nzcpWitness(inputs: Buffer, count: number, params: [isLive, maxTbsBytes, maxArrayLenVC,
 // maxMapLenVC], device: number) -> Buffer of count nzcb_nzcp_record (include/nzcb.h).
 // Synchronous: one launch of the nzcp witness kernel, well under a millisecond.
@@ -513,6 +541,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"vkToJson", nullptr, VkToJson, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"verify", nullptr, Verify, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"calldata", nullptr, Calldata, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"vkToSolidity", nullptr, VkToSolidity, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"nzcpWitness", nullptr, NzcpWitness, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"plonkSetup", nullptr, PlonkSetup, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"createContextFile", nullptr, CreateContextFile, nullptr, nullptr, nullptr, napi_default, nullptr},

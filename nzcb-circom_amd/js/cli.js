@@ -4,6 +4,10 @@
 //   node cli.js plonk setup     <circuit.r1cs> <pot.ptau> <circuit.zkey>
 //   node cli.js plonk prove     <circuit.zkey> <witness.wtns> <proof.json> <public.json>
 //   node cli.js plonk fullprove <input.json> <circuit.wasm> <circuit.zkey> <proof.json> <public.json>
+// and `snarkjs zkey export verificationkey|solidityverifier|soliditycalldata` (Makefile:56-62):
+//   node cli.js zkey export verificationkey <circuit.zkey> <verification_key.json>
+//   node cli.js zkey export solidityverifier <circuit.zkey> <Verifier.sol> [contract name]
+//   node cli.js zkey export soliditycalldata <public.json> <proof.json>
 // Output JSON is written like snarkjs's CLI (stringifyBigInts, 1-space indent).
 const fs = require('fs');
 const nz = require('./index.js');
@@ -11,11 +15,32 @@ const nz = require('./index.js');
 function usage() {
   console.error('usage: cli.js plonk setup <r1cs> <ptau> <zkey>\n' +
                 '       cli.js plonk prove <zkey> <wtns> <proof.json> <public.json>\n' +
-                '       cli.js plonk fullprove <input.json> <wasm> <zkey> <proof.json> <public.json>');
+                '       cli.js plonk fullprove <input.json> <wasm> <zkey> <proof.json> <public.json>\n' +
+                '       cli.js zkey export verificationkey <zkey> <verification_key.json>\n' +
+                '       cli.js zkey export solidityverifier <zkey> <verifier.sol> [contract name]\n' +
+                '       cli.js zkey export soliditycalldata <public.json> <proof.json>');
   process.exit(1);
 }
 
+async function zkeyExport(argv) {
+  if (argv[1] !== 'export') usage();
+  if (argv[2] === 'verificationkey' && argv.length === 5) {
+    const vk = await nz.zKey.exportVerificationKey(argv[3]);
+    fs.writeFileSync(argv[4], JSON.stringify(vk, null, 1), 'utf-8');
+  } else if (argv[2] === 'solidityverifier' && (argv.length === 5 || argv.length === 6)) {
+    const src = await nz.zKey.exportSolidityVerifier(argv[3], null, null, { name: argv[5] });
+    fs.writeFileSync(argv[4], src, 'utf-8');
+  } else if (argv[2] === 'soliditycalldata' && argv.length === 5) {
+    const pub = JSON.parse(fs.readFileSync(argv[3], 'utf8'));
+    const proof = JSON.parse(fs.readFileSync(argv[4], 'utf8'));
+    console.log(await nz.plonk.exportSolidityCallData(proof, pub));
+  } else {
+    usage();
+  }
+}
+
 async function main(argv) {
+  if (argv[0] === 'zkey') return zkeyExport(argv);
   if (argv[0] !== 'plonk') usage();
   const logger = process.env.NZCB_VERBOSE ? { debug: (m) => console.error(m) } : null;
   let res, out;

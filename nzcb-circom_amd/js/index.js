@@ -307,6 +307,19 @@ async function exportVerificationKey(zkeyFileName) {
   return JSON.parse(addon.vkToJson(addon.vkFromZkey(readBin(zkeyFileName))));
 }
 
+// snarkjs zKey.exportSolidityVerifier(zkeyName, templates, logger) (`zkey export
+// solidityverifier`, /root/reference/Makefile:57,62): the verifier contract's source.
+// The snarkjs templates argument is not used (the contract is rendered by the library);
+// options.name sets the contract name (the reference's deploy-script.js asks for "Verifier").
+async function exportSolidityVerifier(zkeyFileName, templates, logger, options) {
+  options = options || {};
+  const tp = options.transcriptPublic === undefined ? true : !!options.transcriptPublic;
+  const src = addon.vkToSolidity(addon.vkFromZkey(readBin(zkeyFileName)), options.name || 'PlonkVerifier', tp);
+  const log = loggerFn(logger);
+  if (log) log(`Solidity verifier: ${src.length} bytes`);
+  return src;
+}
+
 async function verify(vkVerifier, publicSignals, proof, logger, options) {
   options = options || {};
   const tp = options.transcriptPublic === undefined ? true : !!options.transcriptPublic;
@@ -373,7 +386,7 @@ function nzcpWitness(inputs, options) {
 
 module.exports = {
   plonk: { setup, prove, fullProve, verify, exportSolidityCallData },
-  zKey: { exportVerificationKey },
+  zKey: { exportVerificationKey, exportSolidityVerifier },
   nzcp: Object.assign({}, require('./nzcp.js'), { witness: nzcpWitness }),
   wtns: { calculate: wtnsCalculate },
   version: addon.version,

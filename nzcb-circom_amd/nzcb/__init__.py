@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_engine_time_ntt", "nzcb_engine_fr_mul", "nzcb_engine_random_fr", "nzcb_engine_fixed_base",
     "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_to_json", "nzcb_verify",
-    "nzcb_proof_to_calldata", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
+    "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d", "nzcb_msm_set_pair_rounds",
     "nzcb_plonk_setup", "nzcb_prove_batch_status",
 ]
@@ -114,6 +114,7 @@ def load(path: str | None = None):
         "nzcb_vk_to_json": (c_int, [u8p, ctypes.c_char_p, c_size_t]),
         "nzcb_verify": (c_int, [u8p, u8p, u8p, c_int, c_int, POINTER(c_int), POINTER(_Err)]),
         "nzcb_proof_to_calldata": (c_int, [u8p, u8p, c_int, ctypes.c_char_p, c_size_t]),
+        "nzcb_vk_to_solidity": (c_int, [u8p, ctypes.c_char_p, c_int, ctypes.c_char_p, c_size_t]),
         "nzcb_ctx_lanes": (c_int, [c_void_p]),
         "nzcb_prove_batch": (c_int, [c_void_p, POINTER(c_void_p), c_size_t, c_int, c_int, u8p, u8p, u8p, c_size_t,
                                      POINTER(_Err)]),
@@ -834,6 +835,20 @@ def verify(vk: bytes, proof: bytes, public: bytes, transcript_public: bool = Tru
 def proof_to_calldata(proof: bytes, public: bytes) -> str:
     """snarkjs `zkey export soliditycalldata` text for a PLONK proof."""
     return _json_text(load().nzcb_proof_to_calldata, _buf(proof), _buf(public), len(public) // 32)
+
+
+def vk_to_solidity(vk: bytes, contract_name: str = "PlonkVerifier", transcript_public: bool = True) -> str:
+    """snarkjs `zkey export solidityverifier`: the Solidity PLONK verifier of a binary
+    verification key (include/nzcb.h nzcb_vk_to_solidity)."""
+    fn = load().nzcb_vk_to_solidity
+    name = contract_name.encode()
+    need = fn(_buf(vk), name, int(transcript_public), None, 0)
+    if need < 0:
+        raise NzcbError(1, f"solidity verifier: bad verification key or contract name {contract_name!r}")
+    out = ctypes.create_string_buffer(need)
+    if fn(_buf(vk), name, int(transcript_public), out, need) != 0:
+        raise NzcbError(11, "solidity verifier: rendering failed")
+    return out.value.decode()
 
 
 class plonk:
