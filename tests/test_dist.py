@@ -48,6 +48,44 @@ def test_batch_shard_and_max_over_ranks_gloo(count):
         assert max(len(p) for p in gathered) - min(len(p) for p in gathered) <= 1
 
 
+def _prove_worker(rank, world, port, count, out):
+    """Each rank proves its shard of a batch (bench.shard) with the C port, as bench.py's
+    ranks do on their GPUs; rank 0 gathers the proofs (in production they stay per rank)."""
+    import json
+    import torch.distributed as dist
+    from oracle import cbind
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    gold = os.path.join(ROOT, "tests", "golden")
+    meta = json.load(open(os.path.join(gold, "p5.json")))
+    zkey = open(os.path.join(gold, "p5.zkey"), "rb").read()
+    wtns = open(os.path.join(gold, "p5.wtns"), "rb").read()
+    bl = bytes.fromhex(meta["proofs"]["fixed"]["blinding"])
+    mine = {i: cbind.prove(zkey, wtns, bl, threads=1)[0].hex() for i in bench.shard(count, rank, world)}
+    gathered = [None] * world
+    dist.all_gather_object(gathered, mine)
+    out[rank] = gathered
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_batch_shards_prove_gloo():
+    """World size 2: every proof index is proved by exactly one rank, and every proof equals
+    the golden one (same witness and blinding)."""
+    import json
+    count, world = 5, 2
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_prove_worker, args=(world, _free_port(), count, out), nprocs=world, join=True)
+        res = dict(out)
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "p5.json")))["proofs"]["fixed"]["proof_bin"]
+    merged = {}
+    for part in res[0]:
+        assert not set(part) & set(merged)
+        merged.update(part)
+    assert sorted(merged) == list(range(count))
+    assert all(v == want for v in merged.values())
+
+
 def test_shard_edge_cases():
     assert [list(bench.shard(3, r, 8)) for r in range(8)] == [[0], [1], [2], [], [], [], [], []]
     assert list(bench.shard(0, 0, 1)) == []
