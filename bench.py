@@ -294,8 +294,13 @@ def main():
         # roofline's launch time (profiles/: the last 10 accumulation launches of the trace)
         iso_ms = probe["accumulate"] if probe else None
         launch_ms = iso_ms or shared_ms
-        mads_t = MADS_PER_ENTRY * ent_per_launch / (launch_ms / 1e3) / 1e12 if launch_ms else 0.0
-        hbm_gbs = MSM_BYTES_PER_POINT * pts_per_launch / (launch_ms / 1e3) / 1e9 if launch_ms else 0.0
+        # the probe's launch: its own entries (random scalars: ~15 per point); the timed
+        # region's average also holds the A, B, C MSMs of small witness values
+        probe_entries = probe.get("entries") if probe else None
+        launch_entries = probe_entries or ent_per_launch
+        launch_points = (n + 6) if probe else pts_per_launch
+        mads_t = MADS_PER_ENTRY * launch_entries / (launch_ms / 1e3) / 1e12 if launch_ms else 0.0
+        hbm_gbs = MSM_BYTES_PER_POINT * launch_points / (launch_ms / 1e3) / 1e9 if launch_ms else 0.0
         traffic = None
         tf = os.environ.get("NZCB_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "accumulate_traffic.json"))
         if tf and os.path.exists(tf):
@@ -354,13 +359,14 @@ def main():
                 "timed_region_avg_launch_ms": round(shared_ms, 4),
                 "single_proof_avg_launch_ms": round(lat_kms / max(lat_klaunch, 1), 4),
                 "launches_timed": int(klaunch),
-                "points_per_launch": int(pts_per_launch),
-                "bucket_entries_per_launch": int(ent_per_launch),
+                "points_per_launch": int(launch_points),
+                "bucket_entries_per_launch": int(launch_entries),
+                "timed_region_avg_entries_per_launch": int(ent_per_launch),
                 "mads_per_entry": MADS_PER_ENTRY,
-                "hbm": {"algorithmic_bytes_per_launch": int(MSM_BYTES_PER_POINT * pts_per_launch),
+                "hbm": {"algorithmic_bytes_per_launch": int(MSM_BYTES_PER_POINT * launch_points),
                         "bytes_per_point": MSM_BYTES_PER_POINT, "achieved_GBs": round(hbm_gbs, 2),
                         "peak_GBs": HBM_PEAK_GBS, "frac": round(hbm_gbs / HBM_PEAK_GBS, 5)},
-                "probe_phase_ms": {k: round(v, 4) for k, v in probe.items()} if probe else None,
+                "probe_phase_ms": {k: round(v, 4) for k, v in probe.items() if k != "entries"} if probe else None,
             },
             "proof_roofline": {
                 "algorithmic_bytes": PROOF_BYTES_PER_N * n,

@@ -327,6 +327,11 @@ int nzcb_engine_time_ntt(nzcb_engine* e, const void* in, void* out, int log_n, i
  * from `seed`, and [s_i]G1 bases (LEM affine) from Montgomery scalars. Device pointers. */
 int nzcb_engine_random_fr(nzcb_engine* e, void* dev_out, size_t n, uint64_t seed, nzcb_err* err);
 int nzcb_engine_fixed_base(nzcb_engine* e, const void* dev_scalars_mont, size_t n, void* dev_out, nzcb_err* err);
+/* Lagrange-basis SRS (csrc/lagrange.hip): dev_out[k] = [L_k(tau)] for k < 2^log_n, then
+ * [tau^n] - [1] and [tau^(n+1)] - [tau], from ptau_n >= 2^log_n + 2 PTau points (LEM affine,
+ * device pointers). The prover commits A, B, C from their evaluations with it. */
+int nzcb_engine_lagrange_basis(nzcb_engine* e, const void* dev_ptau, size_t ptau_n, int log_n, void* dev_out,
+                               nzcb_err* err);
 /* Average wall ms per MSM over `reps` (host-synchronised) and the average bucket-
  * accumulation kernel ms (HIP events). */
 int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont, int reps,
@@ -353,7 +358,7 @@ int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table,
 int nzcb_msm_set_pair_rounds(int rounds);
 /* Per-phase MSM timing (HIP events, average over reps after one warm-up):
  * out[0] wall ms, out[1..7] keys, sort, offsets, accumulate, finalize, reduce, sums,
- * out[8] table build ms (fixed_base only). */
+ * out[8] table build ms (fixed_base only), out[9] bucket entries per MSM (nonzero digits). */
 int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
                           int fixed_base, int reps, double* out, nzcb_err* err);
 /* Field self-test helpers: out[i] = a[i] * b[i] (Montgomery, device), n elements. */

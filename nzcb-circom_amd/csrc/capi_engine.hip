@@ -6,6 +6,7 @@
 
 #include "../../include/nzcb.h"
 #include "engine.h"
+#include "lagrange.h"
 
 namespace nzcb {
 
@@ -222,6 +223,16 @@ int nzcb_engine_fixed_base(nzcb_engine* e, const void* dev_scalars_mont, size_t 
   NZ_GUARD_END(err)
 }
 
+int nzcb_engine_lagrange_basis(nzcb_engine* e, const void* dev_ptau, size_t ptau_n, int log_n, void* dev_out,
+                               nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  lagrange_basis((const G1Affine*)dev_ptau, ptau_n, log_n, (G1Affine*)dev_out, g.stream);
+  return 0;
+  NZ_GUARD_END(err)
+}
+
 int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont, int reps,
                          double* ms, double* acc_ms, nzcb_err* err) {
   NZ_GUARD_BEGIN
@@ -285,6 +296,7 @@ int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars
   sc->prof_phases = true;
   sc->prof_ms = 0;
   sc->prof_launches = 0;
+  sc->prof_entries = 0;
   for (double& x : sc->phase_ms) x = 0;
   auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < reps; i++)
@@ -293,6 +305,7 @@ int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars
   out[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / r;
   for (int i = 0; i < 7; i++) out[1 + i] = sc->phase_ms[i] / r;
   out[8] = table_ms;
+  out[9] = (double)sc->prof_entries / r;
   sc->prof = sc->prof_phases = false;
   return 0;
   NZ_GUARD_END(err)

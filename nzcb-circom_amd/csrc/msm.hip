@@ -244,22 +244,26 @@ static constexpr int kBinPer = 2;                                  // scalars pe
 static constexpr uint32_t kTileScalars = kBinThreads * kBinPer;    // 512
 static constexpr int kLoThreads = 512;
 
-// the (key, value) of every window of scalar i: zero digits -> key 0 and the table's
-// infinity entry, which the accumulation skips
+// the (key, value) of every window of scalar i; bit w of the result is set for the
+// windows with a nonzero digit (zero digits make no entry: a scalar of b bits costs about
+// b / C entries, which the Lagrange-basis commitments of small witness values rely on)
 template <int C, int NW>
-__device__ __forceinline__ void bin_entries(const Fr* __restrict__ scalars, size_t i, int mont, size_t stride,
-                                            uint32_t skip_val, uint32_t (&kk)[NW], uint32_t (&vv)[NW]) {
+__device__ __forceinline__ uint32_t bin_entries(const Fr* __restrict__ scalars, size_t i, int mont, size_t stride,
+                                                uint32_t (&kk)[NW], uint32_t (&vv)[NW]) {
   Fr s = scalars[i];
   if (mont) s = from_mont_fr29(s);
+  uint32_t live = 0;
 #pragma unroll
   for (int w = 0; w < NW; w++) {
     kk[w] = 0;
-    vv[w] = skip_val;
+    vv[w] = 0;
   }
   for_each_digit<C>(s, [&](int w, uint32_t b, uint32_t sign) {
     kk[w] = b;
     vv[w] = (uint32_t)((size_t)w * stride + i) | (sign << 31);
+    live |= 1u << w;
   });
+  return live;
 }
 
 template <int C>
@@ -275,9 +279,10 @@ msm_bin_hist_kernel(const Fr* __restrict__ scalars, size_t n, int mont, uint32_t
     const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)j * kBinThreads + threadIdx.x;
     if (i < n) {
       uint32_t kk[NW], vv[NW];
-      bin_entries<C, NW>(scalars, i, mont, 0, 0, kk, vv);
+      const uint32_t live = bin_entries<C, NW>(scalars, i, mont, 0, kk, vv);
 #pragma unroll
-      for (int w = 0; w < NW; w++) atomicAdd(&h[kk[w] >> 8], 1u);
+      for (int w = 0; w < NW; w++)
+        if ((live >> w) & 1u) atomicAdd(&h[kk[w] >> 8], 1u);
     }
   }
   __syncthreads();
@@ -329,11 +334,11 @@ msm_bin_rowscan_kernel(uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t*
 
 template <int C>
 __global__ void __launch_bounds__(kBinThreads)
-msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t stride, uint32_t skip_val,
+msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t stride,
                        const uint32_t* __restrict__ counts, uint32_t ntiles, uint8_t* __restrict__ lo2,
                        uint32_t* __restrict__ vals2) {
   constexpr int NW = (255 + C - 1) / C;
-  constexpr int TE = kTileScalars * NW;  // entries per tile
+  constexpr int TE = kTileScalars * NW;  // entries per tile, at most
   __shared__ uint32_t lcount[256], lstart[256], gbase[256];
   __shared__ uint32_t lval[TE];
   __shared__ uint16_t lkey[TE];
@@ -346,28 +351,29 @@ msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_
     lcount[threadIdx.x] = 0;
   }
   __syncthreads();
-  uint32_t kk[kBinPer][NW], vv[kBinPer][NW], rk[kBinPer][NW];
+  uint32_t kk[kBinPer][NW], vv[kBinPer][NW], rk[kBinPer][NW], live[kBinPer];
 #pragma unroll
   for (int j = 0; j < kBinPer; j++) {
     const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)j * kBinThreads + threadIdx.x;
+    live[j] = 0;
     if (i < n) {
-      bin_entries<C, NW>(scalars, i, mont, stride, skip_val, kk[j], vv[j]);
+      live[j] = bin_entries<C, NW>(scalars, i, mont, stride, kk[j], vv[j]);
 #pragma unroll
-      for (int w = 0; w < NW; w++) rk[j][w] = atomicAdd(&lcount[kk[j][w] >> 8], 1u);
+      for (int w = 0; w < NW; w++)
+        if ((live[j] >> w) & 1u) rk[j][w] = atomicAdd(&lcount[kk[j][w] >> 8], 1u);
     }
   }
   __syncthreads();
-  {  // exclusive scan of the tile's 256 high-byte counts
-    uint32_t tot;
-    lstart[threadIdx.x] = scan256_excl(lcount[threadIdx.x], wsum, tot);
+  uint32_t total;
+  {  // exclusive scan of the tile's 256 high-byte counts; total = the tile's entries
+    lstart[threadIdx.x] = scan256_excl(lcount[threadIdx.x], wsum, total);
   }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kBinPer; j++) {
-    const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)j * kBinThreads + threadIdx.x;
-    if (i < n) {
 #pragma unroll
-      for (int w = 0; w < NW; w++) {
+    for (int w = 0; w < NW; w++) {
+      if ((live[j] >> w) & 1u) {
         const uint32_t q = lstart[kk[j][w] >> 8] + rk[j][w];
         lkey[q] = (uint16_t)kk[j][w];
         lval[q] = vv[j][w];
@@ -375,8 +381,6 @@ msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_
     }
   }
   __syncthreads();
-  const size_t left = n - (size_t)blockIdx.x * kTileScalars;
-  const uint32_t total = left < kTileScalars ? (uint32_t)left * NW : (uint32_t)TE;
   for (uint32_t q = threadIdx.x; q < total; q += kBinThreads) {  // runs of one high byte: coalesced
     const uint32_t key = lkey[q], hb = key >> 8;
     const uint32_t pos = gbase[hb] + (q - lstart[hb]);
@@ -387,7 +391,7 @@ msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_
 
 __global__ void __launch_bounds__(kLoThreads)
 msm_bucket_lo_kernel(const uint8_t* __restrict__ lo2, const uint32_t* __restrict__ vals2,
-                     const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t m, uint32_t nkeys,
+                     const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t nkeys,
                      uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted, uint32_t* __restrict__ large) {
   constexpr uint32_t U = 8;
   __shared__ uint32_t h[256], lcnt[256], lst[256];  // lst[0] first holds the region start
@@ -432,10 +436,8 @@ msm_bucket_lo_kernel(const uint8_t* __restrict__ lo2, const uint32_t* __restrict
     const uint32_t key = (hb << 8) | threadIdx.x;
     if (key < nkeys) offsets[key] = off + inc - v;
   }
-  if (hb == 0 && threadIdx.x == 0) {
-    offsets[nkeys] = m;
-    large[0] = 0;  // the finalize's count of long bucket runs (no fill kernel)
-  }
+  if (hb == 255 && threadIdx.x == 0) offsets[nkeys] = e;  // entries in all: the last region's end
+  if (hb == 0 && threadIdx.x == 0) large[0] = 0;          // the finalize's count of long bucket runs
   __syncthreads();
   // scatter in chunks of U * kLoThreads entries, each ranked by low byte in LDS first and
   // written out run by run (coalesced)
@@ -1232,7 +1234,6 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   const bool bins = table && (p.c == 16 || p.c == 17) && !use_library_sort() && sc.bin_counts.p;
   if (bins) {  // hand-written bucketing (see msm_bin_hist_kernel)
     const uint32_t ntiles = (uint32_t)((n + kTileScalars - 1) / kTileScalars);
-    const uint32_t inf_idx = (uint32_t)((size_t)table->nw * table->stride);
     uint8_t* lo2 = (uint8_t*)sc.keys_out.p;
     uint32_t* tail = sc.bin_counts.p + (size_t)256 * ntiles;
     const int m = mont ? 1 : 0;
@@ -1247,15 +1248,14 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     hipLaunchKernelGGL(msm_bin_rowscan_kernel, dim3(256), dim3(256), 0, st, sc.bin_counts.p, ntiles, tail);
     if (p.c == 17)
       hipLaunchKernelGGL(msm_bin_scatter_kernel<17>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
-                         table->stride, inf_idx, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
+                         table->stride, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
     else
       hipLaunchKernelGGL(msm_bin_scatter_kernel<16>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
-                         table->stride, inf_idx, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
+                         table->stride, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
     NZ_HIP(hipGetLastError());
     mark(2);
     hipLaunchKernelGGL(msm_bucket_lo_kernel, dim3(256), dim3(kLoThreads), 0, st, lo2, sc.vals_mid.p,
-                       sc.bin_counts.p, ntiles, (uint32_t)p.entries, p.nkeys, sc.offsets.p, sc.sorted.p,
-                       sc.large.p);
+                       sc.bin_counts.p, ntiles, p.nkeys, sc.offsets.p, sc.sorted.p, sc.large.p);
     NZ_HIP(hipGetLastError());
   } else {
     keys_dispatch(p.c, scalars, n, mont ? 1 : 0, table, sc, st);

@@ -50,6 +50,12 @@ struct Prover {
   // resident zkey data (LEM, as in the file)
   DevBuf<G1Affine> ptau;
   MsmBaseTable ptab;  // shifted PTau bases for the fixed-base MSM schedule
+  // Lagrange-basis SRS (csrc/lagrange.hip): [L_k(tau)] (k < n), [tau^n] - [1],
+  // [tau^(n+1)] - [tau], and its shifted-base table: A, B, C are committed from their
+  // evaluations (mostly small scalars) instead of their coefficients
+  DevBuf<G1Affine> ltau;
+  MsmBaseTable ltab;
+  bool lcommit = false;
   DevBuf<Fr> qm, ql, qr, qo, qc;  // [n coefs | 4n evals]
   DevBuf<Fr> sigma;               // 3 x [n | 4n]
   DevBuf<Fr> lagrange;            // nLagrange x [n | 4n]
@@ -64,7 +70,7 @@ struct Prover {
   // per-proof working set
   DevBuf<Fr> wit;                 // nVars (witness + internal), Montgomery
   DevBuf<Fr> wtns_in;             // raw witness upload (normal form)
-  DevBuf<Fr> A, B, C, Z;          // n
+  DevBuf<Fr> A, B, C, Z;          // n (A, B, C: n + 2, the blinding scalars b_lo, b_hi at n, n + 1)
   DevBuf<Fr> pol_a, pol_b, pol_c, pol_z;  // n+2 / n+3
   DevBuf<Fr> A4, B4, C4, Z4, T, Tz, t;  // 4n (A4..Z4: coset evaluations)
   DevBuf<Fr> pol_r, pol_wxi, pol_wxiw;    // n+3, n+6, n+3
@@ -104,7 +110,8 @@ struct Prover {
   void init_slots();
   void alloc_workspace();
   void to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb);
-  void commit_start(int slot, const Fr* coefs, size_t len);
+  void commit_start(int slot, const Fr* scalars, size_t len, const MsmBaseTable* tab = nullptr,
+                    const G1Affine* bases = nullptr);
   G1Affine commit_finish(int slot);
   Fr eval_poly(const Fr* p, size_t len, const Fr& x);
   void prefix_product(Fr* x, size_t m, Fr* level_tmp);

@@ -15,6 +15,7 @@
 //   * divPol1          -> suffix linear-recurrence scan y_i = x_i + d*y_{i+1}
 //   * evalPol (Horner) -> chunked Horner * x^(chunk start) + tree sum
 #include <rocprofiler-sdk-roctx/roctx.h>
+#include "lagrange.h"
 #include "prover.h"
 #include "transcript.h"
 
@@ -78,6 +79,27 @@ __global__ void k_blind(Fr* pol, size_t n, const Fr* __restrict__ bl, BlindIdx b
     pol[n + k] = b;
     pol[k] = pol[k] - b;
   }
+}
+
+// A, B, C committed in the Lagrange basis (Prover::ltau): their blinding scalars follow
+// the n evaluations, matching ltau[n] = [tau^n] - [1] and ltau[n+1] = [tau^(n+1)] - [tau]
+// (k_blind's b_lo + b_hi X times X^n - 1)
+__global__ void k_abc_tail(Fr* A, Fr* B, Fr* C, size_t n, const Fr* __restrict__ bl) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  A[n] = bl[2];
+  A[n + 1] = bl[1];
+  B[n] = bl[4];
+  B[n + 1] = bl[3];
+  C[n] = bl[6];
+  C[n + 1] = bl[5];
+}
+
+static bool lagrange_commit_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("NZCB_LAGRANGE_COMMIT");
+    return !e || std::atoi(e) != 0;
+  }();
+  return v;
 }
 
 // w4^i from two small tables (4n-th roots of unity)
@@ -543,6 +565,12 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   };
   up(ptau, z.ptau);
   ptab.build(ptau.p, ptau.n, fixed_base_window(), s);
+  lcommit = lagrange_commit_enabled() && ptau.n >= (size_t)n + 2;
+  if (lcommit) {  // one elliptic-curve iNTT per context (csrc/lagrange.hip)
+    ltau.alloc((size_t)n + 2);
+    lagrange_basis(ptau.p, ptau.n, power, ltau.p, s);
+    ltab.build(ltau.p, ltau.n, fixed_base_window(), s);
+  }
   up(qm, z.qm);
   up(ql, z.ql);
   up(qr, z.qr);
@@ -675,7 +703,7 @@ void Prover::init_slots() {
 void Prover::alloc_workspace() {
   wit.alloc(nVars ? nVars : 1);
   wtns_in.alloc(nWit ? nWit : 1);
-  A.alloc(n); B.alloc(n); C.alloc(n); Z.alloc(n);
+  A.alloc(n + 2); B.alloc(n + 2); C.alloc(n + 2); Z.alloc(n);
   pol_a.alloc(n + 2); pol_b.alloc(n + 2); pol_c.alloc(n + 2); pol_z.alloc(n + 3);
   A4.alloc(n4); B4.alloc(n4); C4.alloc(n4); Z4.alloc(n4);
   T.alloc(n4); Tz.alloc(n4); t.alloc(n4);
@@ -708,6 +736,10 @@ Prover::Prover(const Prover& pk, int) {
   ptau.alias(pk.ptau);
   ptab.q.alias(pk.ptab.q);
   ptab.n = pk.ptab.n; ptab.stride = pk.ptab.stride; ptab.c = pk.ptab.c; ptab.nw = pk.ptab.nw;
+  lcommit = pk.lcommit;
+  ltau.alias(pk.ltau);
+  ltab.q.alias(pk.ltab.q);
+  ltab.n = pk.ltab.n; ltab.stride = pk.ltab.stride; ltab.c = pk.ltab.c; ltab.nw = pk.ltab.nw;
   qm.alias(pk.qm); ql.alias(pk.ql); qr.alias(pk.qr); qo.alias(pk.qo); qc.alias(pk.qc);
   sigma.alias(pk.sigma); lagrange.alias(pk.lagrange);
   amap.alias(pk.amap); bmap.alias(pk.bmap); cmap.alias(pk.cmap); adds.alias(pk.adds);
@@ -741,7 +773,7 @@ void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int n
 // Commitments run on their own streams: the MSM of one polynomial overlaps the NTTs
 // of the next and the other MSMs of the same round (their sort / reduction kernels are
 // latency-bound and fill the gaps of the compute-bound bucket accumulation).
-void Prover::commit_start(int slot, const Fr* coefs, size_t len) {
+void Prover::commit_start(int slot, const Fr* coefs, size_t len, const MsmBaseTable* tab, const G1Affine* bases) {
   NZ_HIP(hipEventRecord(ready[slot], st()));
   NZ_HIP(hipStreamWaitEvent(aux[slot], ready[slot], 0));
   if (!shards.empty()) {
@@ -764,7 +796,7 @@ void Prover::commit_start(int slot, const Fr* coefs, size_t len) {
       throw Error(NZCB_ERR_INTERNAL, "msm split: sending the scalars to the other ranks failed");
     len = std::min(len, split_own);
   }
-  msm_enqueue(*msc[slot], ptau.p, coefs, len, true, aux[slot], &ptab);
+  msm_enqueue(*msc[slot], bases ? bases : ptau.p, coefs, len, true, aux[slot], tab ? tab : &ptab);
   static const bool serial = std::getenv("NZCB_SERIAL") != nullptr;  // profiling: one kernel at a time
   if (serial) NZ_HIP(hipStreamSynchronize(aux[slot]));
 }
@@ -980,15 +1012,31 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   G1Affine pA, pB, pC, pZ, pT1, pT2, pT3, pWxi, pWxiw;
   {
     const int ba[2] = {2, 1}, bb[2] = {4, 3}, bc[2] = {6, 5};
-    to4t(A.p, pol_a.p, A4.p, ba, 2);
-    lg("multiexp A");
-    commit_start(0, pol_a.p, n + 2);
-    to4t(B.p, pol_b.p, B4.p, bb, 2);
-    lg("multiexp B");
-    commit_start(1, pol_b.p, n + 2);
-    to4t(C.p, pol_c.p, C4.p, bc, 2);
-    lg("multiexp C");
-    commit_start(2, pol_c.p, n + 2);
+    if (lcommit && shards.empty() && !split_send) {
+      // evaluations + blinding scalars against the Lagrange basis: the same points, and the
+      // MSMs start before the interpolations (they run on the commitment streams)
+      hipLaunchKernelGGL(k_abc_tail, dim3(1), dim3(64), 0, s, A.p, B.p, C.p, (size_t)n, blind.p);
+      NZ_HIP(hipGetLastError());
+      lg("multiexp A");
+      commit_start(0, A.p, n + 2, &ltab, ltau.p);
+      lg("multiexp B");
+      commit_start(1, B.p, n + 2, &ltab, ltau.p);
+      lg("multiexp C");
+      commit_start(2, C.p, n + 2, &ltab, ltau.p);
+      to4t(A.p, pol_a.p, A4.p, ba, 2);
+      to4t(B.p, pol_b.p, B4.p, bb, 2);
+      to4t(C.p, pol_c.p, C4.p, bc, 2);
+    } else {
+      to4t(A.p, pol_a.p, A4.p, ba, 2);
+      lg("multiexp A");
+      commit_start(0, pol_a.p, n + 2);
+      to4t(B.p, pol_b.p, B4.p, bb, 2);
+      lg("multiexp B");
+      commit_start(1, pol_b.p, n + 2);
+      to4t(C.p, pol_c.p, C4.p, bc, 2);
+      lg("multiexp C");
+      commit_start(2, pol_c.p, n + 2);
+    }
     pA = commit_finish(0);
     pB = commit_finish(1);
     pC = commit_finish(2);

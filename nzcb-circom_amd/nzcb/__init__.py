@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_engine_time_ntt", "nzcb_engine_fr_mul", "nzcb_engine_random_fr", "nzcb_engine_fixed_base",
     "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_to_json", "nzcb_verify",
-    "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
+    "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_engine_lagrange_basis", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d", "nzcb_msm_set_pair_rounds",
     "nzcb_plonk_setup", "nzcb_prove_batch_status",
 ]
@@ -115,6 +115,7 @@ def load(path: str | None = None):
         "nzcb_verify": (c_int, [u8p, u8p, u8p, c_int, c_int, POINTER(c_int), POINTER(_Err)]),
         "nzcb_proof_to_calldata": (c_int, [u8p, u8p, c_int, ctypes.c_char_p, c_size_t]),
         "nzcb_vk_to_solidity": (c_int, [u8p, ctypes.c_char_p, c_int, ctypes.c_char_p, c_size_t]),
+        "nzcb_engine_lagrange_basis": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p, POINTER(_Err)]),
         "nzcb_ctx_lanes": (c_int, [c_void_p]),
         "nzcb_prove_batch": (c_int, [c_void_p, POINTER(c_void_p), c_size_t, c_int, c_int, u8p, u8p, u8p, c_size_t,
                                      POINTER(_Err)]),
@@ -310,6 +311,11 @@ class Engine:
         err = _Err()
         _check(self.lib.nzcb_engine_fixed_base(self.h, dev_scalars, n, dev_out, ctypes.byref(err)), err)
 
+    def lagrange_basis(self, dev_ptau: int, ptau_n: int, log_n: int, dev_out: int):
+        """dev_out[k] = [L_k(tau)] (k < 2^log_n), then [tau^n] - [1], [tau^(n+1)] - [tau]."""
+        err = _Err()
+        _check(self.lib.nzcb_engine_lagrange_basis(self.h, dev_ptau, ptau_n, log_n, dev_out, ctypes.byref(err)), err)
+
     def time_msm(self, dev_bases: int, dev_scalars: int, n: int, scalars_mont: bool, reps: int):
         ms = c_double()
         acc = c_double()
@@ -323,11 +329,11 @@ class Engine:
     def time_msm_phases(self, dev_bases: int, dev_scalars: int, n: int, scalars_mont: bool, fixed_base: bool,
                         reps: int) -> dict:
         """Wall ms per MSM and HIP-event ms per phase (generic or fixed-base schedule)."""
-        out = (c_double * 9)()
+        out = (c_double * 10)()
         err = _Err()
         _check(self.lib.nzcb_engine_time_msm2(self.h, dev_bases, dev_scalars, n, int(scalars_mont), int(fixed_base),
                                               reps, out, ctypes.byref(err)), err)
-        d = {"wall": out[0], "table_build": out[8]}
+        d = {"wall": out[0], "table_build": out[8], "entries": out[9]}
         d.update({k: out[1 + i] for i, k in enumerate(self.MSM_PHASES)})
         return d
 

@@ -40,7 +40,7 @@ def main():
             ms = ph["wall"]
             gbs = 96 * n / (ms / 1e3) / 1e9
             print(json.dumps({"kernel": "msm_fixed_base" if fixed else "msm", "log_n": lg, "ms": round(ms, 4),
-                              "phases_ms": {k: round(v, 4) for k, v in ph.items() if k != "wall"},
+                              "phases_ms": {k: round(v, 4) for k, v in ph.items() if k not in ("wall", "entries")}, "entries": int(ph.get("entries", 0)),
                               "points_per_s": round(n / (ms / 1e3), 1), "GBs": round(gbs, 1),
                               "frac": round(gbs / PEAK, 5)}), flush=True)
     for p in (sc, out, bases):

@@ -145,7 +145,8 @@ def _msm_fixed(engine, pts, sc, n_table=None, mont=False):
 
 
 @pytest.mark.parametrize("n,kind", [(1, "rand"), (100, "rand"), (2000, "rand"), (300, "zeros"), (300, "ones"),
-                                    (300, "equal"), (300, "rminus1"), (300, "mixed"), (300, "top")])
+                                    (300, "equal"), (300, "rminus1"), (300, "mixed"), (300, "top"),
+                                    (3000, "witness")])
 def test_msm_fixed_base(engine, n, kind):
     rng = random.Random(1000 + n + len(kind))
     pts = _bases(n + 5, n + 1)
@@ -159,6 +160,10 @@ def test_msm_fixed_base(engine, n, kind):
         sc = [rng.randrange(R_MOD)] * n
     elif kind == "rminus1":
         sc = [R_MOD - 1] * n
+    elif kind == "witness":  # gate values as the Lagrange-basis commitments see them: mostly zero
+        # digits (0, 1, -1, bytes, 17/34-bit sums), a few full-size inverses
+        sc = [rng.choice([0, 0, 1, 1, R_MOD - 1, rng.randrange(256), rng.randrange(1 << 17),
+                          rng.randrange(1 << 34), rng.randrange(R_MOD)]) for _ in range(n)]
     elif kind == "top":  # digits at the top window edge: 2^240.., 2^253, half-window carries
         sc = [rng.choice([1 << 253, (1 << 240) - 1, (1 << 239) * 3, (1 << 19) * 5, R_MOD - (1 << 19)])
               for _ in range(n)]
@@ -263,3 +268,36 @@ def test_msm_large_chunks_schedules_agree_and_split_linearly():
         eng.close()
     assert generic is not None and generic == fixed
     assert bn.g1_add(lo, hi) == fixed
+
+
+@pytest.mark.parametrize("log_n", [1, 3, 6, 9])
+def test_lagrange_basis_vs_oracle(engine, log_n):
+    """csrc/lagrange.hip (an elliptic-curve iNTT of PTau): [L_k(tau)] for every k, then
+    [tau^n] - [1] and [tau^(n+1)] - [tau], against the oracle's scalars times G1 with the
+    trapdoor tau known."""
+    import nzcb
+    n = 1 << log_n
+    tau = 0x6E7A6362746175 + log_n
+    pts = [bn.g1_mul(bn.G1_GEN, pow(tau, i, R_MOD)) for i in range(n + 6)]
+    w = bn.FR_W[log_n]
+    tn = pow(tau, n, R_MOD)
+    inv_n = pow(n, R_MOD - 2, R_MOD)
+    want = []
+    for k in range(n):
+        wk = pow(w, k, R_MOD)
+        # L_k(tau) = w^k (tau^n - 1) / (n (tau - w^k))
+        lk = wk * (tn - 1) * inv_n * pow((tau - wk) % R_MOD, R_MOD - 2, R_MOD) % R_MOD
+        want.append(bn.g1_mul(bn.G1_GEN, lk))
+    want.append(bn.g1_add(pts[n], bn.g1_neg(pts[0])))
+    want.append(bn.g1_add(pts[n + 1], bn.g1_neg(pts[1])))
+    dp, do = nzcb.dev_alloc(64 * (n + 6)), nzcb.dev_alloc(64 * (n + 2))
+    try:
+        nzcb.h2d(dp, b"".join(bn.g1_to_lem(p) for p in pts))
+        engine.lagrange_basis(dp, n + 6, log_n, do)
+        out = nzcb.d2h(do, 64 * (n + 2))
+    finally:
+        nzcb.dev_free(dp)
+        nzcb.dev_free(do)
+    got = [bn.g1_from_lem(out[64 * k:64 * k + 64]) for k in range(n + 2)]
+    assert got == want
+
