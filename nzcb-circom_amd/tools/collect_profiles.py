@@ -23,9 +23,12 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 KERNEL = "msm_accumulate29"
 
 
-def pmc_avg(path, counter):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+def pmc_avg(path, counter, last=10):
+    """Average of the kernel's last `last` dispatches: bench.py's isolated probe, the same
+    launch shape as roofline.avg_launch_ms (the timed region's A, B, C MSMs are smaller)."""
+    rows = [(int(r["Dispatch_Id"]), float(r["Counter_Value"])) for r in csv.DictReader(open(path))
             if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    vals = [v for _, v in sorted(rows)][-last:]
     return len(vals), (sum(vals) / len(vals) if vals else None)
 
 
@@ -44,12 +47,12 @@ def main():
     with open(os.path.join(out, f"{a.prefix}_bench_line.txt"), "w") as f:
         f.write("# rocprofv3 --kernel-trace --stats -- python3 bench.py   (defaults)\n" + line)
     launches = bench["roofline"]["launches_timed"]
-    probe = 10   # bench.py accumulate_probe: 1 warm + 10 timed launches, the last of the run
+    probe = 10   # bench.py accumulate_probe: 2 + 1 warm-up and 10 timed launches, the last of the run
     ts = os.path.join(HERE, "trace_summary.py")
     trace = os.path.join(prof, "run_kernel_trace.csv")
     psumm = subprocess.run([sys.executable, ts, trace, "--last", KERNEL, str(probe), "--durations", "--top", "12"],
                            check=True, capture_output=True, text=True).stdout
-    summ = subprocess.run([sys.executable, ts, trace, "--last", KERNEL, str(launches), "--skip-last", str(probe + 1),
+    summ = subprocess.run([sys.executable, ts, trace, "--last", KERNEL, str(launches), "--skip-last", str(probe + 3),
                            "--durations", "--top", "30"], check=True, capture_output=True, text=True).stdout
     with open(os.path.join(out, f"{a.prefix}_bench_trace_summary.txt"), "w") as f:
         f.write(f"# isolated probe: the last {probe} {KERNEL} launches of the profiled bench.py run "
@@ -60,7 +63,8 @@ def main():
     nw, write_kb = pmc_avg(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     fetch_raw = fetch_kb * 1024
     traffic = {
-        "kernel": "msm_accumulate29_kernel<4> (fixed-base bucket accumulation, 2^21-point MSM, c=17)",
+        "kernel": "msm_accumulate29_kernel<4> (fixed-base bucket accumulation, 2^21+6-point MSM of random scalars, "
+                  "c=17: bench.py's probe, the last 10 launches of each pass)",
         "command": "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate passes) -- python3 bench.py "
                    "--no-cpu-baseline --steps 8",
         "counters_kb_per_launch": {"FETCH_SIZE": {"launches": nf, "avg_kb_per_launch": round(fetch_kb, 1)},
