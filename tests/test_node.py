@@ -256,3 +256,46 @@ const fs = require('fs');
     d = json.loads(run_node(script, timeout=600))
     assert d["pub"] == [str(v) for v in want]
     assert d["ok"] is True
+
+
+@needs_node
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_node_full_prove_nzcp_example_moh_pass(tmp_path):
+    """configs[0]: plonk.fullProve of nzcp_example (NZCPPubIdentity(0,314,0,4,2,4),
+    /root/reference/circuits/nzcp_example.circom) on the Ministry of Health example pass
+    (test/nzcp.js:71), input built as test/nzcp.js:33-42 does, from Node. publicSignals are
+    SURVEY.md §8c's three values (pinned by the reference's decode at test/nzcp.js:44-68);
+    the proof verifies."""
+    import ctypes
+    import nzcb
+    from nzcb import nzcp, nzcpgen, nzcplive
+    r1cs, prog, _ = nzcplive.build(nzcpgen.EXAMPLE)
+    zp, zl = nzcplive.setup_raw(r1cs)
+    try:
+        with open(tmp_path / "example.zkey", "wb") as f:
+            f.write((ctypes.c_uint8 * zl).from_address(zp))
+        vk = nzcb.vk_to_json(nzcb.vk_from_zkey((zp, zl)))
+    finally:
+        nzcb.free_ptr(zp)
+    (tmp_path / "example.wprog").write_bytes(prog)
+    (tmp_path / "vk.json").write_text(json.dumps(vk))
+    tbs = nzcp.to_be_signed(nzcp.EXAMPLE_PASS_URI)
+    inp = nzcp.circuit_input(tbs, bytes(range(1, 21)), nzcp.EXAMPLE_TOBESIGNED_MAX)
+    (tmp_path / "input.json").write_text(json.dumps(inp))
+    script = f"""
+const m = require('./');
+const fs = require('fs');
+(async () => {{
+  const input = JSON.parse(fs.readFileSync('{tmp_path}/input.json'));
+  const r = await m.plonk.fullProve(input, '{tmp_path}/example.wprog', '{tmp_path}/example.zkey');
+  const vk = JSON.parse(fs.readFileSync('{tmp_path}/vk.json'));
+  const ok = await m.plonk.verify(vk, r.publicSignals, r.proof);
+  console.log(JSON.stringify({{pub: r.publicSignals, ok}}));
+}})().catch((e) => {{ console.error(e); process.exit(1); }});
+"""
+    d = json.loads(run_node(script, timeout=600))
+    assert d["pub"] == ["8464235439336389695359576364537904521787463454426143836621154307990710930",
+                        "334204042160295982690797293769892102755483197293558786265320143920457223185",
+                        "430989588176824417852954207888075491695208395262355815151652761069951123456"]
+    assert d["ok"] is True
