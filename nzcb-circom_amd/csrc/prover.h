@@ -46,6 +46,7 @@ struct Prover {
   std::unique_ptr<MsmScratch> msc[kSlots];
   hipStream_t aux[kSlots] = {nullptr, nullptr, nullptr};
   hipEvent_t ready[kSlots] = {nullptr, nullptr, nullptr};
+  bool slot_local[kSlots] = {false, false, false};  // slot's MSM stays on this device (Lagrange basis)
   ~Prover();
   // resident zkey data (LEM, as in the file)
   DevBuf<G1Affine> ptau;

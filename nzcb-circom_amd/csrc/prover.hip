@@ -776,7 +776,11 @@ void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int n
 void Prover::commit_start(int slot, const Fr* coefs, size_t len, const MsmBaseTable* tab, const G1Affine* bases) {
   NZ_HIP(hipEventRecord(ready[slot], st()));
   NZ_HIP(hipStreamWaitEvent(aux[slot], ready[slot], 0));
-  if (!shards.empty()) {
+  // the Lagrange-basis commitments (A, B, C: mostly small scalars) are not split: the
+  // devices and ranks of a split hold PTau ranges
+  const bool local = tab != nullptr && tab != &ptab;
+  slot_local[slot] = local;
+  if (!local && !shards.empty()) {
     for (auto& sh : shards) {
       const size_t cnt = len > sh->lo ? std::min(len, sh->hi) - sh->lo : 0;
       NZ_HIP(hipSetDevice(sh->device));
@@ -790,7 +794,7 @@ void Prover::commit_start(int slot, const Fr* coefs, size_t len, const MsmBaseTa
     NZ_HIP(hipSetDevice(eng->device));
     len = std::min(len, own_hi);
   }
-  if (split_send) {  // other ranks take [split_own, len): hand them the scalars once ready
+  if (!local && split_send) {  // other ranks take [split_own, len): hand them the scalars once ready
     NZ_HIP(hipEventSynchronize(ready[slot]));
     if (split_send(split_user, slot, coefs, len) != 0)
       throw Error(NZCB_ERR_INTERNAL, "msm split: sending the scalars to the other ranks failed");
@@ -826,12 +830,14 @@ G1xyzz xyzz_from_le(const uint8_t* in) {
 G1Affine Prover::commit_finish(int slot) {
   auto t0 = std::chrono::steady_clock::now();
   G1xyzz r = msm_finish(*msc[slot], aux[slot]);
+  const bool local = slot_local[slot];
   for (auto& sh : shards) {  // partial sums of the other devices' point ranges
+    if (local) break;
     NZ_HIP(hipSetDevice(sh->device));
     r = xyzz_add(r, msm_finish(*sh->sc[slot], sh->st[slot]));
   }
   if (!shards.empty()) NZ_HIP(hipSetDevice(eng->device));
-  if (split_gather) {  // every rank's partial (ours included), added in rank order
+  if (!local && split_gather) {  // every rank's partial (ours included), added in rank order
     const G1Affine own = xyzz_to_affine(r);
     uint8_t own_le[64];
     affine_to_le(own, own_le);
@@ -1012,7 +1018,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   G1Affine pA, pB, pC, pZ, pT1, pT2, pT3, pWxi, pWxiw;
   {
     const int ba[2] = {2, 1}, bb[2] = {4, 3}, bc[2] = {6, 5};
-    if (lcommit && shards.empty() && !split_send) {
+    if (lcommit) {
       // evaluations + blinding scalars against the Lagrange basis: the same points, and the
       // MSMs start before the interpolations (they run on the commitment streams)
       hipLaunchKernelGGL(k_abc_tail, dim3(1), dim3(64), 0, s, A.p, B.p, C.p, (size_t)n, blind.p);
