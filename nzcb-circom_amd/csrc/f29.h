@@ -249,6 +249,53 @@ NZ_HD F29 add2x29(const F29& a, const F29& b) {  // a + 2b
   return r;
 }
 
+// Unnormalized forms for operands whose next use tolerates wider limbs. mul29 and
+// mul2sum29 accept one factor of each product with limbs < 2^31 when the other factor is
+// normalized: a column then stays below 9 (2^60.5 + 2^58) + 2^35 < 2^64 (mul29) and
+// 9 (2^59.6 + 2^59 + 2^58) + 2^35 < 2^64 (mul2sum29 with b < 2^30.6, c < 2^30). Saves the
+// 24-instruction carry normalisation where the value feeds a product next. Every limb,
+// the top one included, must stay non-negative: K's top limb must exceed b's.
+// a + K - b with K borrowed (limbs >= 2^29 - 1), a, b normalized: limbs < 2^29 + K_i
+NZ_HD F29 sub29_nn(const F29& a, const F29& b, const uint32_t (&K)[9]) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = a.v[i] + K[i] - b.v[i];
+  return r;
+}
+// 4p - y for a normalized y < 2p (a product output): limbs < 2^30
+NZ_HD F29 neg4p29_nn(const F29& y) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = Fq29::K4[i] - y.v[i];
+  return r;
+}
+// 2p - y for a normalized y <= p: limbs < 2^30. (p - y would leave the top limb at -1
+// when y's top limb equals p's: the borrowed form needs the next multiple.)
+NZ_HD F29 neg29_nn(const F29& y) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = Fq29::K2[i] - y.v[i];
+  return r;
+}
+// a + 6p - b - 2c for normalized a, b, c with b, c < 2p, normalized: 6p in a wide borrowed
+// form (limbs 0..7 in [2^31 - 4, 2^31 + 2^29), so a limb never goes negative and never
+// passes 2^32; the top limb may wrap, the normalised value a + 6p - b - 2c >= 0 is exact)
+struct Fq29W {
+  // 10p borrowed (limbs 0..7 in [2^29 - 1, 2^30)): Q - X3 + 10p for X3 < 8p keeps every
+  // limb, the top one included, non-negative (8p's top limb would not)
+  static constexpr uint32_t K10[9] = {0x34e1e4c6u, 0x2a2bc722u, 0x3c7a6115u, 0x3c535c27u, 0x373a7eafu,
+                                      0x3c908785u, 0x2684cc89u, 0x2f997e07u, 0x01e3eb0fu};
+  static constexpr uint32_t K6W[9] = {0x92edefaau, 0x861a4444u, 0x8aafd3d6u, 0x90fed0e1u, 0x812318ccu,
+                                      0x91238480u, 0x83e94782u, 0x9628e534u, 0x012259d2u};
+};
+NZ_HD F29 sub2x29(const F29& a, const F29& b, const F29& c) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.v[i] = a.v[i] + Fq29W::K6W[i] - b.v[i] - (c.v[i] << 1);
+  norm29(r);
+  return r;
+}
+
 // 4p - y for y < 4p (K4 borrowed form), normalized
 NZ_HD F29 neg4p29(const F29& y) {
   F29 r;
@@ -278,6 +325,13 @@ NZ_HD bool is0p29(const F29& x) {
     op |= x.v[i] ^ Fq29::P[i];
   }
   return o0 == 0 || op == 0;
+}
+
+// is0p29 for a product output, with a one-limb early exit (a nonzero product almost
+// never has a low limb of 0 or p's; the full test runs only then)
+NZ_HD bool is0p29_fast(const F29& x) {
+  if (x.v[0] != 0u && x.v[0] != Fq29::P[0]) return false;
+  return is0p29(x);
 }
 
 // radix change of the same integer (< 2^256, no Montgomery change)

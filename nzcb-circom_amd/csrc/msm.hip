@@ -606,8 +606,9 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
     if (!P.is_inf()) {
       const F29 x = split29(P.x);
       F29 y = split29(P.y);
-      if (ent >> 31) y = neg29(y);
+      if (ent >> 31) y = neg29_nn(y);  // 2p - y, limbs < 2^30: only S2's product reads it
       if (inf) {
+        norm29(y);
         acc.X = x;
         acc.Y = y;
         acc.ZZ = f29_const(Fq29::ONE);
@@ -620,17 +621,22 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
         const F29 Pd = sub29(U2, acc.X, Fq29::K8);   // < 10p
         const F29 R = sub29(S2, acc.Y, Fq29::K4);    // < 6p
         const F29 PP = sqr29(Pd);
-        if (is0p29(PP)) {  // same abscissa: doubling (equal points) or infinity (opposite)
-          if (is0p29(sqr29(R))) mdbl29_rare(x, y, &acc);
-          else inf = true;
+        if (is0p29_fast(PP)) {  // same abscissa: doubling (equal points) or infinity (opposite)
+          if (is0p29(sqr29(R))) {
+            norm29(y);
+            mdbl29_rare(x, y, &acc);
+          } else {
+            inf = true;
+          }
         } else {  // x, y are dead from here on (lower register pressure in the common path)
           const F29 PPP = mul29(Pd, PP);
           const F29 Q = mul29(acc.X, PP);
           const F29 RR = sqr29(R);
-          const F29 X3 = sub29(RR, add2x29(PPP, Q), Fq29::K6);  // < 8p
+          const F29 X3 = sub2x29(RR, PPP, Q);  // RR + 6p - PPP - 2Q < 8p
           acc.ZZ = mul29(acc.ZZ, PP);
-          // Y3 = R (Q - X3) + (4p - Y1) PPP, one reduction: (6p 10p + 4p 2p) / 2^261 + p < 2p
-          acc.Y = mul2sum29(R, sub29(Q, X3, Fq29::K8), neg4p29(acc.Y), PPP);
+          // Y3 = R (Q - X3) + (4p - Y1) PPP, one reduction: (6p 12p + 4p 2p) / 2^261 + p < 2p;
+          // Q - X3 + 10p (limbs < 2^30.6) and 4p - Y1 (limbs < 2^30) stay unnormalized
+          acc.Y = mul2sum29(R, sub29_nn(Q, X3, Fq29W::K10), neg4p29_nn(acc.Y), PPP);
           acc.ZZZ = mul29(acc.ZZZ, PPP);
           acc.X = X3;
         }
