@@ -24,8 +24,8 @@
 //  2. sort:       rocPRIM onesweep radix sort of (key, base index|sign), 2 passes of
 //                 <= 10 key bits (16-bit keys for the fixed-base c <= 17)
 //  3. offsets:    bucket start positions by binary search in the sorted keys
-//  4. accumulate: thread per fixed 32-entry chunk of the sorted stream (doubled past
-//                 2^25 entries, chunk_for; load balance
+//  4. accumulate: thread per fixed 48-entry chunk of the sorted stream (doubled past
+//                 2^26 entries, chunk_for; load balance
 //                 independent of the digit distribution): XYZZ mixed adds of the
 //                 gathered affine bases; bucket runs inside one chunk are written
 //                 directly, runs crossing a chunk edge go to per-chunk carries
@@ -88,13 +88,23 @@ static void radix_sort(void* tmp, size_t& tmp_bytes, const K* kin, K* kout, cons
       NZ_HIP(rocprim::radix_sort_pairs<SortConfig<10>>(tmp, tmp_bytes, kin, kout, vin, vout, m, 0, end_bit, st));
   }
 }
-static constexpr uint32_t kChunk = 32;  // entries per accumulation thread, up to 2^25 entries
+// entries per accumulation thread, up to 2^26 entries: 48 cuts the carries the finalize
+// adds by a third against 32 (same box: bench 32.5 -> 32.9 proofs/s; isolated
+// accumulate + finalize 2.8 ms for 32, 40 and 48, 2.9 ms for 64, whose 1.9 rounds of
+// waves leave a tail)
+static constexpr uint32_t kChunk = 48;
+static constexpr uint32_t kMinChunk = 32;  // NZCB_ACC_CHUNK lower bound (carry buffers are sized by it)
 
-// Entries per accumulation thread: kChunk up to 2^25 entries, then doubled so the grid
-// stays ~2^20 threads and a bucket spans ~15 chunks at every size (at 2^24 points a
-// 32-entry chunk left ~120 carries per bucket and the finalize took 360 ms).
+// Entries per accumulation thread: kChunk up to 2^26 entries, then doubled so the grid
+// stays ~2^19-2^20 threads and a bucket spans ~10 chunks at every size (at 2^24 points a
+// fixed 32-entry chunk left ~120 carries per bucket and the finalize took 360 ms).
 static uint32_t chunk_for(size_t entries) {
-  uint32_t c = kChunk;
+  static const uint32_t base = [] {  // NZCB_ACC_CHUNK: A/B measurements of the chunk size
+    const char* e = std::getenv("NZCB_ACC_CHUNK");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= (int)kMinChunk && v <= 256 ? (uint32_t)v : kChunk;
+  }();
+  uint32_t c = base;
   while (entries / c > (size_t(1) << 20)) c *= 2;
   return c;
 }
@@ -1139,7 +1149,7 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
   sort_tmp_bytes = std::max(sort_tmp_bytes, tmp16);
   sort_tmp.alloc(sort_tmp_bytes + 16);
   buckets.alloc(max_keys);
-  size_t nthreads = (max_entries + kChunk - 1) / kChunk + 1;
+  size_t nthreads = (max_entries + kMinChunk - 1) / kMinChunk + 1;  // the smallest chunk chunk_for allows
   carry_own.alloc(nthreads);
   large.alloc(max_keys + 1);
   if (fixed_base) {
