@@ -115,6 +115,12 @@ def test_nzcp_live_full_prove_real_circuit():
         assert _ints(pub) == exp
         assert nzcb.verify(ctx.vk, proof, pub)
     assert res[0][0] != res[1][0]
+    # the generated Solidity verifier (zkey export solidityverifier) accepts the real
+    # statement's proof, executed by tests/yul.py on the calldata's proof bytes
+    from tests import yul
+    sol = nzcb.vk_to_solidity(ctx.vk, "Verifier")
+    words = bytes.fromhex(nzcb.proof_to_calldata(res[0][0], b"").split(",")[0][2:])
+    assert yul.run_verify_proof(sol, words, _ints(res[0][1]))[0]
     ctx.close()
     try:
         ref_proof, ref_pub, _ = cbind.prove(zkey, nzcplive.wtns_file(wit0), bl, npub=3)
