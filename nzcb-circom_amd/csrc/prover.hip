@@ -110,6 +110,7 @@ __device__ __forceinline__ Fr root4(const Fr* __restrict__ lo, const Fr* __restr
 struct PermArgs {
   Fr beta, gamma, k1, k2;
   F29 beta29, k1beta29, k2beta29;  // beta, k1 beta, k2 beta as mul_fr29 operands
+  int k23;                         // k1 = 2, k2 = 3 (snarkjs getK1K2 for BN254): k beta w by additions
 };
 
 // c * 2^5 split into the 9x29 radix: the Montgomery-261 operand of mul_fr29 for a
@@ -135,8 +136,11 @@ k_perm_ratio(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __res
   for (size_t i = s; i < e; i++) {
     Fr w = root4(rlo, rhi, 4 * i);
     Fr a = A[i], b = B[i], c = C[i];
-    Fr num = (a + mul_fr29(w, pa.beta29) + pa.gamma) * (b + mul_fr29(w, pa.k1beta29) + pa.gamma);
-    num = num * (c + mul_fr29(w, pa.k2beta29) + pa.gamma);
+    const Fr bw = mul_fr29(w, pa.beta29);
+    const Fr k1bw = pa.k23 ? bw + bw : mul_fr29(w, pa.k1beta29);
+    const Fr k2bw = pa.k23 ? k1bw + bw : mul_fr29(w, pa.k2beta29);
+    Fr num = (a + bw + pa.gamma) * (b + k1bw + pa.gamma);
+    num = num * (c + k2bw + pa.gamma);
     Fr den = (a + mul_fr29(s1[4 * i], pa.beta29) + pa.gamma) * (b + mul_fr29(s2[4 * i], pa.beta29) + pa.gamma);
     den = den * (c + mul_fr29(s3[4 * i], pa.beta29) + pa.gamma);
     ratio[i] = num;
@@ -285,6 +289,7 @@ constexpr uint32_t kQ29MaxPub = 8;
 struct QArgs29 {
   F29 beta, bk1, bk2, alpha2, zhinv[4];  // exponent 261
   F29 gamma, negone;                     // exponent 256 (negone = r - 1)
+  int k23;                               // k1 = 2, k2 = 3: k beta x as 2 beta x, 3 beta x
   F29 alpha;                             // exponent 276 (multiplies the exponent-241 permutation term)
 };
 
@@ -330,9 +335,12 @@ k_quotient_coset29(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr*
   if (npub > 4) gate = add29(gate, q29_pi(cl, Apub, 4, npub - 4, n4, i));  // < 7r
   // permutation: (a + b x + g)(b + b k1 x + g)(c + b k2 x + g) z - (a + b s1 + g)(..)(..) z(w x)
   const F29 x = mul29<Fr29>(split29(xlo[i & 4095]), split29(xhi[i >> 12]));
-  const F29 f1 = add29(add29(a, mul29<Fr29>(q.beta, x)), q.gamma);  // < 4r
-  const F29 f2 = add29(add29(b, mul29<Fr29>(q.bk1, x)), q.gamma);
-  const F29 f3 = add29(add29(c, mul29<Fr29>(q.bk2, x)), q.gamma);
+  const F29 bx = mul29<Fr29>(q.beta, x);                   // < 2r
+  const F29 bx2 = q.k23 ? add29(bx, bx) : mul29<Fr29>(q.bk1, x);  // < 4r
+  const F29 bx3 = q.k23 ? add29(bx2, bx) : mul29<Fr29>(q.bk2, x);  // < 6r
+  const F29 f1 = add29(add29(a, bx), q.gamma);   // < 4r
+  const F29 f2 = add29(add29(b, bx2), q.gamma);  // < 6r
+  const F29 f3 = add29(add29(c, bx3), q.gamma);  // < 8r < 2^257 (mul29's input limit)
   const F29 num = mul29<Fr29>(mul29<Fr29>(mul29<Fr29>(f1, f2), f3), z);  // exponent 241
   const F29 g1 = add29(add29(a, mul29<Fr29>(q.beta, split29(cs[i]))), q.gamma);
   const F29 g2 = add29(add29(b, mul29<Fr29>(q.beta, split29(cs[n4 + i]))), q.gamma);
@@ -1080,7 +1088,8 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     lg("gamma: " + fr_dec(gamma));
   }
   {
-    PermArgs pa{beta, gamma, k1, k2, fr29_operand(beta), fr29_operand(k1 * beta), fr29_operand(k2 * beta)};
+    PermArgs pa{beta, gamma, k1, k2, fr29_operand(beta), fr29_operand(k1 * beta), fr29_operand(k2 * beta),
+                k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0};
     size_t nchunks = (n + kScanChunk - 1) / kScanChunk;
     hipLaunchKernelGGL(k_perm_ratio, dim3(grid_for(nchunks, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, sigma.p,
                        (size_t)n, root_lo.p, root_hi.p, pa, Z.p, T.p, Tz.p);
@@ -1124,6 +1133,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     if (nPublic <= kQ29MaxPub) {
       QArgs29 q29;
       q29.beta = f29_exp(beta, 5);
+      q29.k23 = k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0;
       q29.bk1 = f29_exp(q.bk1, 5);
       q29.bk2 = f29_exp(q.bk2, 5);
       q29.alpha2 = f29_exp(q.alpha2, 5);
