@@ -32,6 +32,59 @@ def pmc_avg(path, counter, last=10):
     return len(vals), (sum(vals) / len(vals) if vals else None)
 
 
+def valu_by_kernel(path):
+    """SQ_INSTS_VALU per kernel per proof, dispatches from the first proof on (context
+    setup excluded): rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES -- bench.py --lanes 1 ..."""
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == "SQ_INSTS_VALU"]
+    first = min(int(r["Dispatch_Id"]) for r in rows if "k_wit_to_mont" in r["Kernel_Name"])
+    nproofs = sum(1 for r in rows if "k_wit_to_mont" in r["Kernel_Name"])
+    agg = {}
+    for r in rows:
+        if int(r["Dispatch_Id"]) < first:
+            continue
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")[:60]
+        c, v = agg.get(k, (0, 0.0))
+        agg[k] = (c + 1, v + float(r["Counter_Value"]))
+    tot = sum(v for _, v in agg.values())
+    lines = ["# rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES -- python3 bench.py --lanes 1 --steps 4 --warmup 1 "
+             "--no-cpu-baseline --no-probe",
+             f"# dispatches from the first proof on (context setup excluded): {nproofs} proofs (latency/PCIe runs, "
+             f"warm-up, timed)",
+             f"# {tot / 1e9:.2f} G wave-level VALU instructions, {tot / nproofs / 1e9:.2f} G per proof"]
+    for k, (c, v) in sorted(agg.items(), key=lambda x: -x[1][1])[:30]:
+        lines.append(f"{k:62s} {c:5d} launches {v / nproofs / 1e9:8.3f} G/proof {100 * v / tot:5.1f}%")
+    return "\n".join(lines) + "\n"
+
+
+def acc_pmc(src):
+    """SQ / GRBM counters of the isolated accumulation (tools/acc_probe.py, two passes)."""
+    vals, lines = {}, ["# rocprofv3 --pmc (two passes) -- python3 nzcb-circom_amd/tools/acc_probe.py",
+                       "# fixed-base MSM alone, 2^21 + 6 points of random scalars, c = 17; "
+                       "msm_accumulate29_kernel<4, false>, averages over each pass's launches"]
+    for d in ("pmcA", "pmcB"):
+        agg = {}
+        for f in glob.glob(os.path.join(src, d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if KERNEL in r["Kernel_Name"]:
+                    agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        lines.append(f"pass {d[-1]}:")
+        for k, v in sorted(agg.items()):
+            vals[k] = sum(v) / len(v)
+            lines.append(f"  {k:24s} launches {len(v)}  avg {vals[k]:.6g}")
+    ent = 31457085  # nonzero digits of the probe's 2^21 + 6 random scalars (15 per scalar)
+    wc = vals["SQ_WAVE_CYCLES"]
+    quad = 1024 * vals["GRBM_GUI_ACTIVE"] / 8 / 4
+    lines += ["derived (SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles, MI355X_MICROARCH.md):",
+              f"  VALU instructions per bucket entry (lane level) = SQ_INSTS_VALU x 64 / {ent} = "
+              f"{vals['SQ_INSTS_VALU'] * 64 / ent:.0f}",
+              f"  wave time: issuing {100 * vals['SQ_ACTIVE_INST_ANY'] / wc:.1f} %, issue-stalled (SQ_WAIT_INST_ANY) "
+              f"{100 * vals['SQ_WAIT_INST_ANY'] / wc:.1f} %, parked (SQ_WAIT_ANY) {100 * vals['SQ_WAIT_ANY'] / wc:.1f} %",
+              f"  GRBM_GUI_ACTIVE / 8 XCDs = {vals['GRBM_GUI_ACTIVE'] / 8 / 1e6:.2f} M cycles per launch",
+              f"  {100 * vals['SQ_INSTS_VALU'] / quad:.1f} % of the 1024 SIMDs' quad-cycles issue a VALU instruction "
+              f"(v_mad_u64_u32 measures ~5 cycles, profiles/r1_isa_bench.txt: the VALU is saturated)"]
+    return "\n".join(lines) + "\n"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--prefix", default="r1")
@@ -79,6 +132,13 @@ def main():
     with open(os.path.join(out, "accumulate_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
         f.write("\n")
+    pv = os.path.join(src, "pmcv", "run_counter_collection.csv")
+    if os.path.exists(pv):
+        with open(os.path.join(out, f"{a.prefix}_valu_by_kernel.txt"), "w") as f:
+            f.write(valu_by_kernel(pv))
+    if os.path.isdir(os.path.join(src, "pmcA")) and os.path.isdir(os.path.join(src, "pmcB")):
+        with open(os.path.join(out, f"{a.prefix}_acc_pmc.txt"), "w") as f:
+            f.write(acc_pmc(src))
     mb = os.path.join(src, "microbench.log")
     if os.path.exists(mb):
         shutil.copy(mb, os.path.join(out, f"{a.prefix}_microbench.txt"))
