@@ -103,3 +103,41 @@ def test_msm_2p24_schedules_agree_and_split_linearly():
         eng.close()
     assert generic is not None and generic == fixed
     assert bn.g1_add(lo, hi) == fixed
+
+
+@pytest.mark.timeout(600)
+def test_msm_2p21_witness_scalars_schedules_agree():
+    """The Lagrange-basis commitments' regime at full size: 2^21 + 2 scalars shaped like
+    nzcp_live gate values (mostly 0, 1, -1, bytes and short sums, ~5 % full-size), so most
+    digits are zero and the bucketing drops them, and bucket 0 (|digit| = 1) holds ~40 %
+    of the entries (long carry runs through the finalize's workgroup path). The fixed-base
+    schedule equals the generic one, which keeps every digit, and splits linearly."""
+    import random
+    import numpy as np
+    import nzcb
+    from oracle import bn254 as bn
+    n, h = (1 << 21) + 2, (1 << 20) + 777
+    rng = random.Random(0x6E7A)
+    r = bn.R_MOD
+    kinds = rng.choices(range(7), weights=[35, 30, 10, 10, 8, 2, 5], k=n)
+    vals = [0 if k == 0 else 1 if k == 1 else r - 1 if k == 2 else rng.randrange(256) if k == 3 else
+            rng.randrange(1 << 17) if k == 4 else rng.randrange(1 << 40) if k == 5 else rng.randrange(r)
+            for k in kinds]
+    raw = b"".join(v.to_bytes(32, "little") for v in vals)
+    assert np.frombuffer(raw, dtype=np.uint8).size == 32 * n
+    eng = nzcb.Engine(0, max_log_ntt=-1, max_msm_points=n + 8)
+    sc, bases = nzcb.dev_alloc(n * 32), nzcb.dev_alloc(n * 64)
+    try:
+        eng.random_fr(sc, n, 0x1A6A)
+        eng.fixed_base(sc, n, bases)
+        nzcb.h2d(sc, raw)                       # normal-form scalars
+        generic = _affine(eng.msm_dev(bases, sc, n, False))
+        fixed = _affine(eng.msm_fixed_dev(bases, n, sc, n, False))
+        lo = _affine(eng.msm_fixed_dev(bases, h, sc, h, False))
+        hi = _affine(eng.msm_fixed_dev(bases + h * 64, n - h, sc + h * 32, n - h, False))
+    finally:
+        nzcb.dev_free(sc)
+        nzcb.dev_free(bases)
+        eng.close()
+    assert generic is not None and generic == fixed
+    assert bn.g1_add(lo, hi) == fixed
