@@ -25,6 +25,8 @@
 //          of the block (all in {0, 1, -1}) written by the workgroup
 // A failing BITS/CHECK does an atomicMin of (creation order << 8 | err) on the pass's
 // status word, so the host sees the first failure in template order, as circom throws.
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -33,24 +35,38 @@
 namespace nzcb {
 namespace wvm {
 
-constexpr int kThreads = 256;
 constexpr uint32_t kInvTable = 4096;
 constexpr uint32_t kNoWire = 0xFFFFFFFFu;
+constexpr uint32_t kWaveTerms = 16;
+// NZCB_WVM_LEVEL_CLOCK record per level: [0] after the barrier, [1 + w] wave w done with the
+// thread segment, [17 + w] done with the wave segment (pass 0; development aid)
+constexpr int kClockSlots = 33;
 enum { OP_LIN = 0, OP_MUL, OP_INV, OP_BITS, OP_CHECK, OP_QUIN, OP_SHA256, OP_SHA512 };
 
 struct Op {
   uint32_t code, dst, a_off, a_n, b_off, b_n, c_off, c_n;
 };
-struct Term {
+struct Term {  // program file
   uint32_t wire, ci;
+};
+struct DTerm {  // device: sc = the coefficient as a small signed integer, or kBigCoef
+  uint32_t wire, ci;
+  int32_t sc;
+  uint32_t pad;
+};
+constexpr int32_t kBigCoef = INT32_MIN;
+
+// a level's ops, reordered by the loader: [s, w) one per thread, [w, m) one per wave
+// (QUIN and scalar ops with more than kWaveTerms terms), [m, e) one per workgroup (SHA)
+struct Level {
+  uint32_t s, w, m, e;
 };
 
 struct Prog {
   const Fr* consts;   // coefficient * R^2 mod r
-  const Term* terms;
+  const DTerm* terms;
   const Op* ops;
-  const uint32_t* starts;
-  const uint32_t* mstarts;
+  const Level* levels;
   const Fr* inv_small;  // 1/i (normal form), i < kInvTable
   uint32_t n_levels, n_wires, n_inputs, in_base;
 };
@@ -332,13 +348,144 @@ __device__ void sha_block(Fr* W, const Op& op, ShaShared& sh) {
   __syncthreads();
 }
 
-__device__ __forceinline__ Fr lc_mont(const Prog& P, const Fr* W, uint32_t off, uint32_t n) {
-  Fr acc = Fr::zero();
-  for (uint32_t i = 0; i < n; i++) {
-    const Term t = P.terms[off + i];
-    acc = acc + W[t.wire] * P.consts[t.ci];
+// A linear combination is summed in two parts: terms whose coefficient is a small signed
+// integer (|c| < 2^31, DTerm.sc) and whose wire value is below 2^32 go into an exact
+// 128-bit integer; any other term is a Montgomery product w (c R^2) = w c R into a field
+// accumulator. In nzcp_live 99% of the terms are of the first kind (bits, bytes and
+// positions with coefficients +-1, +-2^k), so an op rarely multiplies in the field at all:
+// a level's latency is then its loads, not a chain of 8 x 32-bit Montgomery products.
+struct LcAcc {
+  __int128 i;
+  Fr m;
+  bool slow;
+};
+
+__device__ __forceinline__ LcAcc lc_zero() {
+  LcAcc a;
+  a.i = 0;
+  a.m = Fr::zero();
+  a.slow = false;
+  return a;
+}
+
+__device__ __forceinline__ bool below_2p32(const Fr& w) {
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 1; k < 8; k++) hi |= w.v[k];
+  return hi == 0;
+}
+
+// x mod r for |x| < 2^127
+__device__ __forceinline__ Fr i128_to_fr(__int128 x) {
+  const bool ng = x < 0;
+  const unsigned __int128 m = ng ? (unsigned __int128)(-x) : (unsigned __int128)x;
+  Fr f = Fr::zero();
+  f.v[0] = (uint32_t)m;
+  f.v[1] = (uint32_t)(m >> 32);
+  f.v[2] = (uint32_t)(m >> 64);
+  f.v[3] = (uint32_t)(m >> 96);
+  return ng ? neg(f) : f;
+}
+
+__device__ __forceinline__ Fr lc_value(const LcAcc& a) {
+  Fr r = i128_to_fr(a.i);
+  if (a.slow) r = r + from_mont(a.m);
+  return r;
+}
+
+// the combination as an int64 when it is one (no field part, in range)
+__device__ __forceinline__ bool lc_int64(const LcAcc& a, int64_t& v) {
+  if (a.slow || a.i < (__int128)INT64_MIN || a.i > (__int128)INT64_MAX) return false;
+  v = (int64_t)a.i;
+  return true;
+}
+
+__device__ __forceinline__ bool lc_is_zero(const LcAcc& a) {
+  return a.slow ? lc_value(a).is_zero() : a.i == 0;
+}
+
+// Term lists a | b | c (counts na, nb, nc) of an op, loading four terms, then their wires,
+// at a time: a level's latency is its longest chain of dependent loads.
+__device__ __forceinline__ void lcs_gather(const Prog& P, const Fr* W, const Op& op, uint32_t na, uint32_t nb,
+                                           uint32_t nc, LcAcc& a, LcAcc& b, LcAcc& c) {
+  a = lc_zero();
+  b = lc_zero();
+  c = lc_zero();
+  const uint32_t nab = na + nb, tot = nab + nc;
+  for (uint32_t j0 = 0; j0 < tot; j0 += 4) {
+    DTerm t[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t j = j0 + q;
+      if (j < tot) t[q] = P.terms[j < na ? op.a_off + j : (j < nab ? op.b_off + (j - na) : op.c_off + (j - nab))];
+    }
+    Fr w[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (j0 + q < tot) w[q] = W[t[q].wire];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t j = j0 + q;
+      if (j < tot) {
+        int64_t p = 0;
+        Fr x = Fr::zero();
+        const bool fast = t[q].sc != kBigCoef && below_2p32(w[q]);
+        if (fast)
+          p = (int64_t)t[q].sc * (int64_t)w[q].v[0];
+        else
+          x = w[q] * P.consts[t[q].ci];
+        const int seg = j < na ? 0 : (j < nab ? 1 : 2);  // selects, not a reference (scratch)
+        a.i += seg == 0 ? p : 0;
+        b.i += seg == 1 ? p : 0;
+        c.i += seg == 2 ? p : 0;
+        if (!fast) {
+          if (seg == 0) {
+            a.m = a.m + x;
+            a.slow = true;
+          } else if (seg == 1) {
+            b.m = b.m + x;
+            b.slow = true;
+          } else {
+            c.m = c.m + x;
+            c.slow = true;
+          }
+        }
+      }
+    }
   }
-  return acc;
+}
+
+// one linear combination over a whole wave: lane i sums terms i, i + 64, ..., then a
+// butterfly of shuffles leaves the total (a sum mod r, so order-free) in every lane
+__device__ __forceinline__ Fr lc_wave(const Prog& P, const Fr* W, uint32_t off, uint32_t n, int lane) {
+  LcAcc acc = lc_zero();
+  for (uint32_t i = lane; i < n; i += 64) {
+    const DTerm t = P.terms[off + i];
+    const Fr w = W[t.wire];
+    if (t.sc != kBigCoef && below_2p32(w)) {
+      acc.i += (int64_t)t.sc * (int64_t)w.v[0];
+    } else {
+      acc.m = acc.m + w * P.consts[t.ci];
+      acc.slow = true;
+    }
+  }
+  Fr v = lc_value(acc);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    Fr o;
+#pragma unroll
+    for (int k = 0; k < 8; k++) o.v[k] = (uint32_t)__shfl_xor((int)v.v[k], d, 64);
+    v = v + o;
+  }
+  return v;
+}
+
+// limb k of x without indexing a register array by a variable (that would go to scratch)
+__device__ __forceinline__ uint32_t limb(const Fr& x, uint32_t k) {
+  uint32_t r = x.v[0];
+#pragma unroll
+  for (int q = 1; q < 8; q++) r = k == (uint32_t)q ? x.v[q] : r;
+  return r;
 }
 
 // normal-form x as a small signed integer: 1 = non-negative (val), -1 = negative (r - val), 0 = large
@@ -376,69 +523,106 @@ __device__ __forceinline__ void fail(uint32_t* status, uint32_t order, uint32_t 
   atomicMin(status, (order << 8) | err);
 }
 
-__device__ void scalar_op(const Prog& P, Fr* W, const Op& op, uint32_t* status) {
+// term lists a scalar op evaluates: LIN/INV/BITS a; CHECK a, b; MUL a, b, c
+__device__ __host__ __forceinline__ void op_counts(const Op& op, uint32_t& na, uint32_t& nb, uint32_t& nc) {
+  const uint32_t typ = op.code & 0xFF;
+  na = op.a_n;
+  nb = (typ == OP_MUL || typ == OP_CHECK) ? op.b_n : 0;
+  nc = typ == OP_MUL ? op.c_n : 0;
+}
+
+// a scalar op from its linear combinations; lane / stride split the stores (1 thread:
+// 0 / 1; a wave: every lane holds the same values, lane 0 stores, BITS spread over lanes)
+template <class V>
+__device__ void finish_op(const Prog& P, Fr* W, const Op& op, V va, V vb, V vc, uint32_t* status, uint32_t lane,
+                          uint32_t stride) {
   const uint32_t typ = op.code & 0xFF, err = (op.code >> 8) & 0xFF, n = op.code >> 16;
   switch (typ) {
-    case OP_LIN:
-      W[op.dst] = from_mont(lc_mont(P, W, op.a_off, op.a_n));
-      break;
-    case OP_MUL: {
-      const Fr a = lc_mont(P, W, op.a_off, op.a_n);
-      const Fr b = lc_mont(P, W, op.b_off, op.b_n);
-      const Fr c = lc_mont(P, W, op.c_off, op.c_n);
-      W[op.dst] = from_mont(a * b + c);
+    case OP_LIN: {
+      const Fr r = va();
+      if (lane == 0) W[op.dst] = r;
       break;
     }
-    case OP_INV:
-      W[op.dst] = inv_normal(P, from_mont(lc_mont(P, W, op.a_off, op.a_n)));
+    case OP_MUL: {
+      const Fr r = va.mul_add(vb, vc);
+      if (lane == 0) W[op.dst] = r;
       break;
+    }
+    case OP_INV: {
+      const Fr r = inv_normal(P, va());
+      if (lane == 0) W[op.dst] = r;
+      break;
+    }
     case OP_BITS: {
-      const Fr x = from_mont(lc_mont(P, W, op.a_off, op.a_n));
-      for (uint32_t i = 0; i < n; i++) {
-        Fr b = Fr::zero();
-        b.v[0] = (x.v[i >> 5] >> (i & 31)) & 1u;
-        W[op.dst + i] = b;
+      const Fr x = va();
+      for (uint32_t i = lane; i < n; i += stride) {
+        Fr bit = Fr::zero();
+        bit.v[0] = (limb(x, i >> 5) >> (i & 31)) & 1u;
+        W[op.dst + i] = bit;
       }
-      bool big = false;
-      for (uint32_t i = n; i < 256; i++) big |= ((x.v[i >> 5] >> (i & 31)) & 1u) != 0;
-      if (big) fail(status, op.c_off, err);
+      uint32_t big = 0;  // any bit >= n set
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        const uint32_t lo = 32 * k;
+        const uint32_t keep = n <= lo ? ~0u : (n >= lo + 32 ? 0u : ~0u << (n - lo));
+        big |= x.v[k] & keep;
+      }
+      if (big && lane == 0) fail(status, op.c_off, err);
       break;
     }
     case OP_CHECK: {
-      Fr x = lc_mont(P, W, op.a_off, op.a_n);
-      if (op.b_n) x = x * lc_mont(P, W, op.b_off, op.b_n);
-      if (!x.is_zero()) fail(status, op.c_off, err);
+      // a (x b when b is present) == 0; a field has no zero divisors
+      const bool zero = va.is_zero() || (op.b_n && vb.is_zero());
+      if (!zero && lane == 0) fail(status, op.c_off, err);
       break;
     }
     default:
-      fail(status, 0xFFFFFFu, 0xFE);
+      if (lane == 0) fail(status, 0xFFFFFFu, 0xFE);
   }
 }
 
-struct QuinShared {
-  int sign;
-  uint32_t mag;
-  Fr idx;
-  Fr sel;
+// an op's combination as summed by one thread (exact integer + field part)
+struct LcVal {
+  const LcAcc& a;
+  __device__ Fr operator()() const { return lc_value(a); }
+  __device__ bool is_zero() const { return lc_is_zero(a); }
+  __device__ Fr mul_add(const LcVal& b, const LcVal& c) const {
+    int64_t x, y, z;
+    if (lc_int64(a, x) && lc_int64(b.a, y) && lc_int64(c.a, z)) return i128_to_fr((__int128)x * y + z);
+    return to_mont(lc_value(a)) * lc_value(b.a) + lc_value(c.a);  // (a R) b / R = a b
+  }
 };
 
-__device__ void quin(const Prog& P, Fr* W, const Op& op, QuinShared& qs) {
+// an op's combination as a field element (wave reductions)
+struct FrVal {
+  Fr x;
+  __device__ Fr operator()() const { return x; }
+  __device__ bool is_zero() const { return x.is_zero(); }
+  __device__ Fr mul_add(const FrVal& b, const FrVal& c) const { return to_mont(x) * b.x + c.x; }
+};
+
+__device__ __forceinline__ void scalar_op(const Prog& P, Fr* W, const Op& op, uint32_t* status) {
+  uint32_t na, nb, nc;
+  op_counts(op, na, nb, nc);
+  LcAcc a, b, c;
+  lcs_gather(P, W, op, na, nb, nc, a, b, c);
+  finish_op(P, W, op, LcVal{a}, LcVal{b}, LcVal{c}, status, 0, 1);
+}
+
+// QuinSelector on one wave: every lane evaluates the index (same loads, so no exchange),
+// then the lanes write the 2n + m signals
+__device__ void quin_wave(const Prog& P, Fr* W, const Op& op, int lane) {
   const uint32_t n = op.code >> 16, m = op.b_n;
-  if (threadIdx.x == 0) {
-    const Fr idx = from_mont(lc_mont(P, W, op.a_off, op.a_n));
-    uint32_t mag = 0;
-    qs.sign = small_int(idx, mag);
-    qs.mag = mag;
-    qs.idx = idx;
-    const bool hit = qs.sign > 0 && mag < m;
-    qs.sel = hit ? W[op.b_off + mag] : Fr::zero();
-  }
-  __syncthreads();
-  const int sign = qs.sign;
-  const uint32_t mag = qs.mag;
+  LcAcc a, b, c;
+  lcs_gather(P, W, op, op.a_n, 0, 0, a, b, c);
+  const Fr fidx = lc_value(a);
+  uint32_t mag = 0;
+  const int sign = small_int(fidx, mag);
+  const bool hit = sign > 0 && mag < m;
+  const Fr sel = hit ? W[op.b_off + mag] : Fr::zero();
   const int64_t idx = sign > 0 ? (int64_t)mag : -(int64_t)mag;
   const Fr one = fr_small(1);
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+  for (uint32_t i = lane; i < n; i += 64) {
     Fr eq = Fr::zero(), inv;
     if (sign != 0) {
       const int64_t d = (int64_t)i - idx;
@@ -460,22 +644,39 @@ __device__ void quin(const Prog& P, Fr* W, const Op& op, QuinShared& qs) {
     } else {
       Fr fi = Fr::zero();
       fi.v[0] = i;
-      inv = from_mont(inverse(to_mont(fi - qs.idx)));
+      inv = from_mont(inverse(to_mont(fi - fidx)));
     }
     W[op.dst + i] = eq;
     W[op.dst + n + i] = inv;
   }
-  const bool hit = sign > 0 && mag < m;
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
-    W[op.dst + 2 * n + i] = (hit && i >= mag) ? qs.sel : Fr::zero();
-  __syncthreads();
+  for (uint32_t i = lane; i < m; i += 64) W[op.dst + 2 * n + i] = (hit && i >= mag) ? sel : Fr::zero();
 }
 
-__global__ void __launch_bounds__(kThreads) wvm_kernel(Prog P, const Fr* __restrict__ inputs, Fr* witness,
-                                                        size_t stride_elems, uint32_t* status) {
+// an op of a level's wave segment: a QuinSelector or a scalar op with a long linear combination
+__device__ __forceinline__ void wave_op(const Prog& P, Fr* W, const Op& op, uint32_t* status, int lane) {
+  if ((op.code & 0xFF) == OP_QUIN) {
+    quin_wave(P, W, op, lane);
+    return;
+  }
+  uint32_t na, nb, nc;
+  op_counts(op, na, nb, nc);
+  const Fr a = lc_wave(P, W, op.a_off, na, lane);
+  const Fr b = nb ? lc_wave(P, W, op.b_off, nb, lane) : Fr::zero();
+  const Fr c = nc ? lc_wave(P, W, op.c_off, nc, lane) : Fr::zero();
+  finish_op(P, W, op, FrVal{a}, FrVal{b}, FrVal{c}, status, lane, 64);
+}
+
+// One workgroup per pass; per level: the thread segment spread over threads, the wave
+// segment over waves, the workgroup segment (SHA blocks) one op at a time, one barrier.
+// Ops of one level are independent, so the three segments need no barrier between them.
+template <int NT>
+__global__ void __launch_bounds__(NT) wvm_kernel(Prog P, const Fr* __restrict__ inputs, Fr* witness,
+                                                 size_t stride_elems, uint32_t* status,
+                                                 uint64_t* __restrict__ level_clock) {
   __shared__ ShaShared sh;
-  __shared__ QuinShared qs;
+  constexpr int NW = NT / 64;
   const uint32_t pass = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   Fr* W = witness + (size_t)pass * stride_elems;
   const Fr* in = inputs + (size_t)pass * P.n_inputs;
   uint32_t* st = status + pass;
@@ -491,21 +692,26 @@ __global__ void __launch_bounds__(kThreads) wvm_kernel(Prog P, const Fr* __restr
     for (int k = 0; k < 6; k++) x = reduce_once(x);
     W[P.in_base + i] = x;
   }
+  Level nxt = P.n_levels ? P.levels[0] : Level{0, 0, 0, 0};
   __syncthreads();
+  if (level_clock && pass == 0 && threadIdx.x == 0) level_clock[0] = wall_clock64();
   for (uint32_t lv = 0; lv < P.n_levels; lv++) {
-    const uint32_t s0 = P.starts[lv], m0 = P.mstarts[lv], e0 = P.starts[lv + 1];
-    for (uint32_t k = s0 + threadIdx.x; k < m0; k += blockDim.x) scalar_op(P, W, P.ops[k], st);
-    for (uint32_t k = m0; k < e0; k++) {
+    const Level L = nxt;
+    if (lv + 1 < P.n_levels) nxt = P.levels[lv + 1];  // static table: fetched a level ahead
+    const bool clk = level_clock && pass == 0 && lane == 0;
+    for (uint32_t k = L.s + threadIdx.x; k < L.w; k += NT) scalar_op(P, W, P.ops[k], st);
+    if (clk) level_clock[(size_t)(lv + 1) * kClockSlots + 1 + wave] = wall_clock64();
+    for (uint32_t k = L.w + wave; k < L.m; k += NW) wave_op(P, W, P.ops[k], st, lane);
+    if (clk) level_clock[(size_t)(lv + 1) * kClockSlots + 17 + wave] = wall_clock64();
+    for (uint32_t k = L.m; k < L.e; k++) {
       const Op op = P.ops[k];
-      const uint32_t typ = op.code & 0xFF;
-      if (typ == OP_QUIN)
-        quin(P, W, op, qs);
-      else if (typ == OP_SHA256)
+      if ((op.code & 0xFF) == OP_SHA256)
         sha_block<32>(W, op, sh);
       else
         sha_block<64>(W, op, sh);
     }
     __syncthreads();
+    if (level_clock && pass == 0 && threadIdx.x == 0) level_clock[(size_t)(lv + 1) * kClockSlots] = wall_clock64();
   }
 }
 
@@ -513,9 +719,9 @@ struct Program {
   int device = 0;
   uint32_t n_wires = 0, n_out = 0, n_pub = 0, n_prv = 0, n_levels = 0;
   DevBuf<Fr> consts, inv_small;
-  DevBuf<Term> terms;
+  DevBuf<DTerm> terms;
   DevBuf<Op> ops;
-  DevBuf<uint32_t> starts, mstarts;
+  DevBuf<Level> levels;
   DevBuf<uint32_t> status;
   size_t status_cap = 0;
 };
@@ -567,11 +773,24 @@ Program* load(const uint8_t* data, size_t len, int device) {
     const uint8_t* p = data + 40;
     // coefficients c -> c R^2 (Montgomery of Montgomery), checked < r
     std::vector<Fr> cs(nc);
+    std::vector<int32_t> sc(nc);
     for (uint32_t i = 0; i < nc; i++) {
       Fr c;
       std::memcpy(c.v, p + 32 * (size_t)i, 32);
       if (reduce_once(c) != c) throw Error(NZCB_ERR_FORMAT, "witness program: coefficient >= r");
       cs[i] = to_mont(to_mont(c));
+      const Fr nc_ = neg(c);
+      bool lo = true, nlo = true;
+      for (int k = 1; k < 8; k++) {
+        lo = lo && c.v[k] == 0;
+        nlo = nlo && nc_.v[k] == 0;
+      }
+      if (lo && c.v[0] < 0x80000000u)
+        sc[i] = (int32_t)c.v[0];
+      else if (nlo && nc_.v[0] < 0x80000000u)
+        sc[i] = -(int32_t)nc_.v[0];
+      else
+        sc[i] = kBigCoef;
     }
     p += (size_t)nc * 32;
     const Term* tm = (const Term*)p;
@@ -627,12 +846,38 @@ Program* load(const uint8_t* data, size_t len, int device) {
       inv[i] = from_mont(ia * pre[i]);
       ia = ia * to_mont(fi);
     }
+    // each level's ops regrouped into its thread, wave and workgroup segments
+    std::vector<Op> ro;
+    ro.reserve(no);
+    std::vector<Level> lt(P->n_levels);
+    for (uint32_t i = 0; i < P->n_levels; i++) {
+      const uint32_t s = lv[i], e = lv[i + 1];
+      auto cls = [&](const Op& o) {  // 0 thread, 1 wave, 2 workgroup
+        const uint32_t typ = o.code & 0xFF;
+        if (typ == OP_SHA256 || typ == OP_SHA512) return 2;
+        if (typ == OP_QUIN) return 1;
+        uint32_t na, nb, nc;
+        op_counts(o, na, nb, nc);
+        return (uint64_t)na + nb + nc > kWaveTerms ? 1 : 0;
+      };
+      Level L;
+      L.s = (uint32_t)ro.size();
+      for (int c = 0; c < 3; c++) {
+        if (c == 1) L.w = (uint32_t)ro.size();
+        if (c == 2) L.m = (uint32_t)ro.size();
+        for (uint32_t k = s; k < e; k++)
+          if (cls(op[k]) == c) ro.push_back(op[k]);
+      }
+      L.e = (uint32_t)ro.size();
+      lt[i] = L;
+    }
     NZ_HIP(hipSetDevice(device));
     upload(P->consts, cs.data(), nc);
-    upload(P->terms, tm, nt);
-    upload(P->ops, op, no);
-    upload(P->starts, lv, P->n_levels + 1);
-    upload(P->mstarts, lv + P->n_levels + 1, P->n_levels);
+    std::vector<DTerm> dt(nt);
+    for (uint32_t i = 0; i < nt; i++) dt[i] = DTerm{tm[i].wire, tm[i].ci, sc[tm[i].ci], 0};
+    upload(P->terms, dt.data(), nt);
+    upload(P->ops, ro.data(), no);
+    upload(P->levels, lt.data(), P->n_levels);
     upload(P->inv_small, inv.data(), kInvTable);
   } catch (...) {
     delete P;
@@ -656,19 +901,41 @@ void run(Program* P, const void* dev_inputs, int count, void* dev_witness, size_
   g.consts = P->consts.p;
   g.terms = P->terms.p;
   g.ops = P->ops.p;
-  g.starts = P->starts.p;
-  g.mstarts = P->mstarts.p;
+  g.levels = P->levels.p;
   g.inv_small = P->inv_small.p;
   g.n_levels = P->n_levels;
   g.n_wires = P->n_wires;
   g.n_inputs = P->n_pub + P->n_prv;
   g.in_base = 1 + P->n_out;
-  hipLaunchKernelGGL(wvm_kernel, dim3((unsigned)count), dim3(kThreads), 0, s, g, (const Fr*)dev_inputs,
-                     (Fr*)dev_witness, stride_bytes / 32, P->status.p);
+  // NZCB_WVM_LEVEL_CLOCK=<file>: pass 0's wall clocks per level (kClockSlots u64 ticks
+  // each, level 0 = kernel start), appended to <file> (tools/wvm_bench.py; off by default)
+  const char* clock_path = std::getenv("NZCB_WVM_LEVEL_CLOCK");
+  DevBuf<uint64_t> lclk;
+  if (clock_path && *clock_path) {
+    lclk.alloc(((size_t)P->n_levels + 1) * kClockSlots);
+    NZ_HIP(hipMemsetAsync(lclk.p, 0, ((size_t)P->n_levels + 1) * kClockSlots * 8, s));
+  }
+  // NZCB_WVM_THREADS = 256 | 512 | 1024 workgroup size (A/B runs; default 512)
+  static const int nt = [] {
+    const char* v = std::getenv("NZCB_WVM_THREADS");
+    const int t = v ? std::atoi(v) : 512;
+    return t == 256 || t == 1024 ? t : 512;
+  }();
+  auto kern = nt == 256 ? wvm_kernel<256> : (nt == 1024 ? wvm_kernel<1024> : wvm_kernel<512>);
+  hipLaunchKernelGGL(kern, dim3((unsigned)count), dim3(nt), 0, s, g, (const Fr*)dev_inputs, (Fr*)dev_witness,
+                     stride_bytes / 32, P->status.p, lclk.p);
   NZ_HIP(hipGetLastError());
   std::vector<uint32_t> st((size_t)count);
   NZ_HIP(hipMemcpyAsync(st.data(), P->status.p, (size_t)count * 4, hipMemcpyDeviceToHost, s));
   NZ_HIP(hipStreamSynchronize(s));
+  if (lclk.p) {
+    std::vector<uint64_t> h(((size_t)P->n_levels + 1) * kClockSlots, 0);
+    NZ_HIP(hipMemcpy(h.data(), lclk.p, h.size() * 8, hipMemcpyDeviceToHost));
+    if (FILE* f = std::fopen(clock_path, "ab")) {
+      std::fwrite(h.data(), 8, h.size(), f);
+      std::fclose(f);
+    }
+  }
   for (int i = 0; i < count; i++) status_out[i] = st[i] == 0xFFFFFFFFu ? 0 : (int32_t)(st[i] & 0xFF);
 }
 
