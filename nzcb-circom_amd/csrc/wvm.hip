@@ -40,7 +40,7 @@ constexpr uint32_t kNoWire = 0xFFFFFFFFu;
 constexpr uint32_t kWaveTerms = 16;
 // NZCB_WVM_LEVEL_CLOCK record per level: [0] after the barrier, [1 + w] wave w done with the
 // thread segment, [17 + w] done with the wave segment (pass 0; development aid)
-constexpr int kClockSlots = 33;
+constexpr int kClockSlots = 37;  // + [33..36] SHA phases (message/state read, words, compression, signals)
 enum { OP_LIN = 0, OP_MUL, OP_INV, OP_BITS, OP_CHECK, OP_QUIN, OP_SHA256, OP_SHA512 };
 
 struct Op {
@@ -157,33 +157,34 @@ __device__ __forceinline__ Fr fr_small(int v) {  // v in {0, 1, -1}
 
 __device__ __forceinline__ int bit_of(uint64_t x, int i) { return (int)((x >> i) & 1u); }
 
-// value of XOR-signal o of ROTR r1 ^ ROTR r2 ^ (SHR|ROTR) r3 of word x
+__device__ __forceinline__ void put(Fr* p, int v) {  // v in {0, 1, -1}
+  *p = fr_small(v);
+}
+
+// The signals of bit i of ROTR r1 ^ ROTR r2 ^ (SHR|ROTR) r3 of word x, from o = 0 of its
+// block: a XOR3 bit (i + r3 inside the word) is the pair (b & c, a ? (b == c ? 1 : -1) : 0)
+// at 2i, 2i + 1; past the shift (SHR, i >= B - r3) a XOR2 bit is the single a & b at
+// 2 (B - r3) + (i - (B - r3)).
 template <int B>
-__device__ int xor_value(uint64_t x, int r1, int r2, int r3, bool shr, int o) {
+__device__ __forceinline__ void put_xor(Fr* row, uint64_t x, int r1, int r2, int r3, bool shr, int i) {
   const int n3 = shr ? B - r3 : B;
-  int i, which;
-  bool x3;
-  if (o < 2 * n3) {
-    i = o >> 1;
-    which = o & 1;
-    x3 = true;
-  } else {
-    i = n3 + (o - 2 * n3);
-    which = 0;
-    x3 = false;
-  }
   const int a = bit_of(x, (i + r1) % B), b = bit_of(x, (i + r2) % B);
-  if (!x3) return a & b;
-  const int c = shr ? bit_of(x, i + r3) : bit_of(x, (i + r3) % B);
-  const int mid = b & c;
-  if (which == 0) return mid;
-  return a ? (b == c ? 1 : -1) : 0;
+  if (i < n3) {
+    const int c = bit_of(x, shr ? i + r3 : (i + r3) % B);
+    put(row + 2 * i, b & c);
+    put(row + 2 * i + 1, a ? (b == c ? 1 : -1) : 0);
+  } else {
+    put(row + 2 * n3 + (i - n3), a & b);
+  }
 }
 
 template <int B>
 __device__ __forceinline__ uint64_t rotr(uint64_t x, int n) {
-  const uint64_t m = B == 64 ? ~0ull : 0xffffffffull;
-  return ((x >> n) | (x << (B - n))) & m;
+  if (B == 32) {
+    const uint32_t y = (uint32_t)x;
+    return (uint32_t)((y >> n) | (y << (32 - n)));
+  }
+  return (x >> n) | (x << (64 - n));
 }
 
 template <int B>
@@ -204,70 +205,80 @@ __device__ __forceinline__ uint64_t addw(uint64_t acc, uint64_t x, uint32_t& car
   return s;
 }
 
+// One SHA-2 block gadget: the workgroup reads the message bits and the input state, lane 0
+// runs the compression with the working variables in registers (writing each round's words
+// and carries to LDS, never reading them back), then every signal of the block is written
+// bit-sliced: one work item per (row, bit) writes all of that bit's signals, so no item
+// branches on its position inside a row.
 template <int B>
-__device__ void sha_block(Fr* W, const Op& op, ShaShared& sh) {
+__device__ void sha_block(Fr* W, const Op& op, ShaShared& sh, uint64_t* clk) {
   using L = ShaLayout<B>;
   using S = Sha<B>;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, nt = blockDim.x;
   const uint64_t mask = B == 64 ? ~0ull : 0xffffffffull;
   // message bytes from the byte-wise bit wires (LSB first); a wire that is not a bit
   // (only in a witness that already failed a check) contributes its lowest bit
-  for (int k = tid; k < 64; k += blockDim.x) {
+  for (int k = tid; k < 64; k += nt) {
     uint32_t byte = 0;
+#pragma unroll
     for (int j = 0; j < 8; j++) byte |= (W[op.b_off + 8 * k + j].v[0] & 1u) << j;
     sh.msg[k] = (uint8_t)byte;
   }
   // input state: the previous block's final sums (bits LSB first + 1 carry per word)
   if (op.a_off != kNoWire) {
-    for (int k = tid; k < 8 * B; k += blockDim.x) {
+    for (int k = tid; k < 8 * B; k += nt) {
       const int j = k / B, i = k % B;
       const uint32_t bit = W[op.a_off + L::final_base + j * (B + 1) + i].v[0] & 1u;
       if (bit) atomicOr(&sh.state_bits[k >> 5], 1u << (k & 31));
     }
   }
   __syncthreads();
-  if (tid == 0) {
+  if (clk && tid == 0) clk[33] = wall_clock64();
+  if (tid < 16) {  // message words (big endian)
     const int nbw = B / 8;
-    const int nw = B == 32 ? 16 : 8;
-    for (int t = 0; t < nw; t++) {
-      uint64_t x = 0;
-      for (int q = 0; q < nbw; q++) x = (x << 8) | sh.msg[nbw * t + q];
-      sh.W[t] = x;
+    uint64_t x = 0;
+    if (B == 32 || tid < 8) {
+      for (int q = 0; q < nbw; q++) x = (x << 8) | sh.msg[nbw * tid + q];
+    } else {  // SHA-512 of a 64-byte message: 0x80, zeros, 128-bit length 512
+      x = tid == 8 ? 1ull << 63 : (tid == 15 ? 512 : 0);
     }
-    if (B == 64) {  // SHA-512 of a 64-byte message: 0x80, zeros, 128-bit length 512
-      sh.W[8] = 1ull << 63;
-      for (int t = 9; t < 15; t++) sh.W[t] = 0;
-      sh.W[15] = 512;
-    }
-    uint64_t H[8];
-    for (int j = 0; j < 8; j++) {
-      if (op.a_off == kNoWire) {
-        H[j] = B == 32 ? (uint64_t)kSha256IV[j] : kSha512IV[j];
-      } else {
-        uint64_t x = 0;
-        for (int i = 0; i < B; i++) {
-          const int k = j * B + i;
-          x |= (uint64_t)((sh.state_bits[k >> 5] >> (k & 31)) & 1u) << i;
-        }
-        H[j] = x;
+    sh.W[tid] = x;
+  } else if (tid >= 64 && tid < 72) {  // input state words
+    const int j = tid - 64;
+    uint64_t x = 0;
+    if (op.a_off == kNoWire) {
+      x = B == 32 ? (uint64_t)kSha256IV[j] : kSha512IV[j];
+    } else {
+      for (int i = 0; i < B; i++) {
+        const int k = j * B + i;
+        x |= (uint64_t)((sh.state_bits[k >> 5] >> (k & 31)) & 1u) << i;
       }
-      sh.H[j] = H[j];
     }
-    for (int t = 16; t < S::R; t++) {
-      uint32_t c = 0;
-      uint64_t s = sig<B>(sh.W[t - 2], S::s1a, S::s1b, S::s1c, true);
-      s = addw<B>(s, sh.W[t - 7], c);
-      s = addw<B>(s, sig<B>(sh.W[t - 15], S::s0a, S::s0b, S::s0c, true), c);
-      s = addw<B>(s, sh.W[t - 16], c);
-      sh.W[t] = s;
-      sh.wc[t] = (uint8_t)c;
-    }
+    sh.H[j] = x;
+  }
+  __syncthreads();
+  if (clk && tid == 0) clk[34] = wall_clock64();
+  if (tid == 0) {
+    uint64_t H[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) H[j] = sh.H[j];
     // A[0..3] = d, c, b, a; E[0..3] = h, g, f, e
     sh.A[3] = H[0]; sh.A[2] = H[1]; sh.A[1] = H[2]; sh.A[0] = H[3];
     sh.E[3] = H[4]; sh.E[2] = H[5]; sh.E[1] = H[6]; sh.E[0] = H[7];
+    uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
     for (int t = 0; t < S::R; t++) {
-      const uint64_t a = sh.A[t + 3], b = sh.A[t + 2], c = sh.A[t + 1], d = sh.A[t];
-      const uint64_t e = sh.E[t + 3], f = sh.E[t + 2], g = sh.E[t + 1], h = sh.E[t];
+      uint64_t wt;
+      if (t < 16) {
+        wt = sh.W[t];
+      } else {
+        uint32_t cw = 0;
+        wt = sig<B>(sh.W[t - 2], S::s1a, S::s1b, S::s1c, true);
+        wt = addw<B>(wt, sh.W[t - 7], cw);
+        wt = addw<B>(wt, sig<B>(sh.W[t - 15], S::s0a, S::s0b, S::s0c, true), cw);
+        wt = addw<B>(wt, sh.W[t - 16], cw);
+        sh.W[t] = wt;
+        sh.wc[t] = (uint8_t)cw;
+      }
       const uint64_t S1 = sig<B>(e, S::S1a, S::S1b, S::S1c, false);
       const uint64_t ch = (e & f) ^ (~e & g & mask);
       const uint64_t S0 = sig<B>(a, S::S0a, S::S0b, S::S0c, false);
@@ -277,7 +288,7 @@ __device__ void sha_block(Fr* W, const Op& op, ShaShared& sh) {
       uint64_t t1 = addw<B>(h, S1, c1);
       t1 = addw<B>(t1, ch, c1);
       t1 = addw<B>(t1, k, c1);
-      t1 = addw<B>(t1, sh.W[t], c1);
+      t1 = addw<B>(t1, wt, c1);
       uint32_t ca = c1;
       uint64_t na = addw<B>(t1, S0, ca);
       na = addw<B>(na, mj, ca);
@@ -287,64 +298,56 @@ __device__ void sha_block(Fr* W, const Op& op, ShaShared& sh) {
       sh.E[t + 4] = ne;
       sh.ac[t] = (uint8_t)ca;
       sh.ec[t] = (uint8_t)ce;
+      h = g; g = f; f = e; e = ne;
+      d = c; c = b; b = a; a = na;
     }
-    const int R = S::R;
-    const uint64_t V[8] = {sh.A[R + 3], sh.A[R + 2], sh.A[R + 1], sh.A[R], sh.E[R + 3], sh.E[R + 2], sh.E[R + 1],
-                           sh.E[R]};
+    const uint64_t V[8] = {a, b, c, d, e, f, g, h};
+#pragma unroll
     for (int j = 0; j < 8; j++) {
-      uint32_t c = 0;
-      const uint64_t s = addw<B>(H[j], V[j], c);
-      sh.hc[j] = (uint8_t)c;
-      sh.H[j] = s;  // final sums (H_in no longer needed)
+      uint32_t cf = 0;
+      sh.H[j] = addw<B>(H[j], V[j], cf);  // final sums (the input state is no longer needed)
+      sh.hc[j] = (uint8_t)cf;
     }
   }
   __syncthreads();
-  // every signal of the block
-  const Fr one = fr_small(1), zero = Fr::zero(), mone = fr_small(-1);
+  if (clk && tid == 0) clk[35] = wall_clock64();
   Fr* out = W + op.dst;
-  for (int s = tid; s < L::size; s += blockDim.x) {
-    int v;
-    if (s < L::round_base) {
-      const int t = 16 + s / L::sched;
-      int o = s % L::sched;
-      if (o < L::nx0) {
-        v = xor_value<B>(sh.W[t - 15], S::s0a, S::s0b, S::s0c, true, o);
-      } else if ((o -= L::nx0) < L::nx1) {
-        v = xor_value<B>(sh.W[t - 2], S::s1a, S::s1b, S::s1c, true, o);
-      } else {
-        o -= L::nx1;
-        v = o < B ? bit_of(sh.W[t], o) : (int)((sh.wc[t] >> (o - B)) & 1u);
-      }
-    } else if (s < L::final_base) {
-      const int q = s - L::round_base;
-      const int t = q / L::round;
-      int o = q % L::round;
-      const uint64_t a = sh.A[t + 3], b = sh.A[t + 2], c = sh.A[t + 1];
-      const uint64_t e = sh.E[t + 3], f = sh.E[t + 2], g = sh.E[t + 1];
-      if (o < 2 * B) {
-        v = xor_value<B>(e, S::S1a, S::S1b, S::S1c, false, o);
-      } else if ((o -= 2 * B) < B) {
-        v = bit_of(e, o) ? bit_of(f, o) - bit_of(g, o) : 0;
-      } else if ((o -= B) < 2 * B) {
-        v = xor_value<B>(a, S::S0a, S::S0b, S::S0c, false, o);
-      } else if ((o -= 2 * B) < 2 * B) {
-        const int i = o >> 1;
-        v = (o & 1) ? (bit_of(a, i) & (bit_of(b, i) ^ bit_of(c, i))) : (bit_of(b, i) & bit_of(c, i));
-      } else if ((o -= 2 * B) < B + 3) {
-        v = o < B ? bit_of(sh.A[t + 4], o) : (int)((sh.ac[t] >> (o - B)) & 1u);
-      } else {
-        o -= B + 3;
-        v = o < B ? bit_of(sh.E[t + 4], o) : (int)((sh.ec[t] >> (o - B)) & 1u);
-      }
-    } else {
-      const int q = s - L::final_base;
-      const int j = q / (B + 1), i = q % (B + 1);
-      v = i < B ? bit_of(sh.H[j], i) : (int)(sh.hc[j] & 1u);
+  // message schedule rows t = 16 .. R-1: sigma0(W[t-15]) signals, sigma1(W[t-2]), W[t] bits + 2 carries
+  for (int it = tid; it < L::n_sched * B; it += nt) {
+    const int t = 16 + it / B, i = it % B;
+    Fr* row = out + (t - 16) * L::sched;
+    put_xor<B>(row, sh.W[t - 15], S::s0a, S::s0b, S::s0c, true, i);
+    put_xor<B>(row + L::nx0, sh.W[t - 2], S::s1a, S::s1b, S::s1c, true, i);
+    Fr* wb = row + L::nx0 + L::nx1;
+    put(wb + i, bit_of(sh.W[t], i));
+    if (i < 2) put(wb + B + i, (sh.wc[t] >> i) & 1);
+  }
+  // rounds: Sigma1(e) pairs, Ch, Sigma0(a) pairs, Maj pairs, new a bits + 3 carries, new e bits + 3 carries
+  for (int it = tid; it < S::R * B; it += nt) {
+    const int t = it / B, i = it % B;
+    Fr* row = out + L::round_base + t * L::round;
+    const uint64_t a = sh.A[t + 3], b = sh.A[t + 2], c = sh.A[t + 1];
+    const uint64_t e = sh.E[t + 3], f = sh.E[t + 2], g = sh.E[t + 1];
+    put_xor<B>(row, e, S::S1a, S::S1b, S::S1c, false, i);
+    put(row + 2 * B + i, bit_of(e, i) ? bit_of(f, i) - bit_of(g, i) : 0);
+    put_xor<B>(row + 3 * B, a, S::S0a, S::S0b, S::S0c, false, i);
+    put(row + 5 * B + 2 * i, bit_of(b, i) & bit_of(c, i));
+    put(row + 5 * B + 2 * i + 1, bit_of(a, i) & (bit_of(b, i) ^ bit_of(c, i)));
+    put(row + 7 * B + i, bit_of(sh.A[t + 4], i));
+    put(row + 8 * B + 3 + i, bit_of(sh.E[t + 4], i));
+    if (i < 3) {
+      put(row + 8 * B + i, (sh.ac[t] >> i) & 1);
+      put(row + 9 * B + 3 + i, (sh.ec[t] >> i) & 1);
     }
-    out[s] = v == 0 ? zero : (v > 0 ? one : mone);
+  }
+  // final sums: 8 words of B bits + 1 carry
+  for (int it = tid; it < 8 * (B + 1); it += nt) {
+    const int j = it / (B + 1), i = it % (B + 1);
+    put(out + L::final_base + it, i < B ? bit_of(sh.H[j], i) : (int)(sh.hc[j] & 1u));
   }
   __syncthreads();
-  for (int k = tid; k < 8 * 64 / 32; k += blockDim.x) sh.state_bits[k] = 0;
+  if (clk && tid == 0) clk[36] = wall_clock64();
+  for (int k = tid; k < 8 * 64 / 32; k += nt) sh.state_bits[k] = 0;
   __syncthreads();
 }
 
@@ -706,9 +709,9 @@ __global__ void __launch_bounds__(NT) wvm_kernel(Prog P, const Fr* __restrict__ 
     for (uint32_t k = L.m; k < L.e; k++) {
       const Op op = P.ops[k];
       if ((op.code & 0xFF) == OP_SHA256)
-        sha_block<32>(W, op, sh);
+        sha_block<32>(W, op, sh, level_clock && pass == 0 ? level_clock + (size_t)(lv + 1) * kClockSlots : nullptr);
       else
-        sha_block<64>(W, op, sh);
+        sha_block<64>(W, op, sh, level_clock && pass == 0 ? level_clock + (size_t)(lv + 1) * kClockSlots : nullptr);
     }
     __syncthreads();
     if (level_clock && pass == 0 && threadIdx.x == 0) level_clock[(size_t)(lv + 1) * kClockSlots] = wall_clock64();

@@ -16,7 +16,7 @@ import bench  # noqa: E402
 import nzcb  # noqa: E402
 from nzcb import nzcplive  # noqa: E402
 
-SLOTS = 33  # wvm.hip kClockSlots
+SLOTS = 37  # wvm.hip kClockSlots
 OPS = ["LIN", "MUL", "INV", "BITS", "CHECK", "QUIN", "SHA256", "SHA512"]
 
 
@@ -76,6 +76,12 @@ def main():
             for key, (n, t, a, b) in sorted(by.items(), key=lambda kv: -kv[1][1]):
                 print(f"  {key:28s} {n:4d} levels {t / 1e3:7.3f} ms  {t / n:7.2f} us/level "
                       f"(threads {a / n:6.2f}, waves {b / n:6.2f})")
+            for i in range(len(rec) - 1):
+                r = rec[i + 1]
+                if r[33]:
+                    ph = [(r[k + 1] - r[k]) / 100.0 for k in range(33, 36)]
+                    print(f"  level {i:4d} SHA phases: words {(r[34] - r[33]) / 100.0:6.2f} us, compression "
+                          f"{ph[1]:6.2f} us, signals {ph[2]:6.2f} us (from the block start {(r[36] - r[33]) / 100.0:6.2f})")
             top = sorted(range(len(us)), key=lambda i: -us[i])[:12]
             for i in top:
                 print(f"  level {i:4d}: {us[i]:8.2f} us (threads {seg_t[i]:7.2f}, waves {seg_w[i]:7.2f})  {dict(mix[i])}")
