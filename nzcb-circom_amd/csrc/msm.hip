@@ -603,16 +603,17 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
   Xyzz29 acc;
   bool inf = true;
   // software pipeline: the next entry's table point is loaded before this entry's
-  // addition, so the gather's latency hides behind ~8k cycles of arithmetic
+  // addition, so the gather's latency hides behind ~8k cycles of arithmetic, and the
+  // entry after it is read one step earlier still, so that gather's address is in a
+  // register when it is issued (no wait on the index load inside an iteration)
   uint32_t ent = kDirect ? 0u : sorted[s];
   G1Affine P = bases[kDirect ? s : ent & 0x7fffffffu];
+  uint32_t ent_n = (!kDirect && s + 1 < e) ? sorted[s + 1] : 0u;
   for (uint32_t pos = s; pos < e;) {
-    uint32_t ent_n = 0;
     G1Affine Pn;
-    if (pos + 1 < e) {
-      ent_n = kDirect ? 0u : sorted[pos + 1];
-      Pn = bases[kDirect ? pos + 1 : ent_n & 0x7fffffffu];
-    }
+    uint32_t ent_nn = 0;
+    if (pos + 1 < e) Pn = bases[kDirect ? pos + 1 : ent_n & 0x7fffffffu];
+    if (!kDirect && pos + 2 < e) ent_nn = sorted[pos + 2];
     if (!P.is_inf()) {
       const F29 x = split29(P.x);
       F29 y = split29(P.y);
@@ -673,6 +674,7 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
       }
     }
     ent = ent_n;
+    ent_n = ent_nn;
     P = Pn;
   }
 }

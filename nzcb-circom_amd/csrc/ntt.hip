@@ -193,14 +193,24 @@ ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s,
       const int i0 = (j << logC) + c, i1 = ((j + h) << logC) + c, i2 = ((j + 2 * h) << logC) + c,
                 i3 = ((j + 3 * h) << logC) + c;
       const Fr x0 = tile[i0], x1 = tile[i1], x2 = tile[i2], x3 = tile[i3];
-      Fr t1 = x1, t3 = x3;
+      // x2 +- w x3 only feed the products by wb, wc: they stay in radix 2^29, unreduced
+      // (w x3 < r + 2^249 with limbs < 2^29; x2 + 2r - w x3 < 3r with limbs < 2^30.6,
+      // which mul29 accepts against a canonical twiddle, f29.h), saving a join, two
+      // 8 x 32 modular add/subs and two splits per group
+      Fr t1 = x1;
+      F29 t3 = split29(x3);
       if (g) {
         const F29 wa = twa[ka];
         t1 = mul_fr29(x1, wa);
-        t3 = mul_fr29(x3, wa);
+        t3 = mul29<Fr29>(t3, wa);
       }
-      const Fr y0 = x0 + t1, y1 = x0 - t1, y2 = x2 + t3, y3 = x2 - t3;
-      const Fr u2 = mul_fr29(y2, wb), u3 = mul_fr29(y3, wc);
+      const Fr y0 = x0 + t1, y1 = x0 - t1;
+      const F29 x2s = split29(x2);
+      F29 y2;
+#pragma unroll
+      for (int l = 0; l < 9; l++) y2.v[l] = x2s.v[l] + t3.v[l];
+      const F29 y3 = sub29_nn(x2s, t3, Fr29::K2);
+      const Fr u2 = join_fr29(mul29<Fr29>(y2, wb)), u3 = join_fr29(mul29<Fr29>(y3, wc));
       tile[i0] = y0 + u2;
       tile[i2] = y0 - u2;
       tile[i1] = y1 + u3;
