@@ -1329,19 +1329,25 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   }
   const uint32_t chunk = chunk_for(acc_entries);
   const size_t nthreads = (acc_entries + chunk - 1) / chunk;
+  // waves per SIMD the accumulation is compiled for (NZCB_ACC29_WAVES = 2..4 for A/B
+  // runs). 3 (<= 168 VGPRs): at 4 (<= 128) the prefetched next point spilled to scratch,
+  // 80 B stored and reloaded per entry (WRITE_SIZE 2.5 GB per launch); 2.55 -> 2.29 ms
   static const int acc_waves = [] {
     const char* e = std::getenv("NZCB_ACC29_WAVES");
-    return e ? std::atoi(e) : 4;
+    const int w = e ? std::atoi(e) : 3;
+    return w >= 2 && w <= 4 ? w : 3;
   }();
   const dim3 agrid(grid_for(nthreads, kMsmThreads, 1u << 30));
   if (table) {
     if (!sc.buckets29.p) throw Error(NZCB_ERR_ARG, "msm scratch was not sized for the fixed-base schedule");
     if (rounds)
-      hipLaunchKernelGGL((msm_accumulate29_kernel<4, true>), agrid, dim3(kMsmThreads), 0, st, chunk, acc_src,
+      hipLaunchKernelGGL((msm_accumulate29_kernel<3, true>), agrid, dim3(kMsmThreads), 0, st, chunk, acc_src,
                          sc.sorted.p, acc_off, p.nkeys, nthreads, sc.buckets29.p, sc.carry_own29.p,
                          sc.carry_cont29.p);
     else
-      hipLaunchKernelGGL(acc_waves >= 4 ? msm_accumulate29_kernel<4> : msm_accumulate29_kernel<3>, agrid,
+      hipLaunchKernelGGL(acc_waves == 4 ? msm_accumulate29_kernel<4>
+                                        : (acc_waves == 2 ? msm_accumulate29_kernel<2> : msm_accumulate29_kernel<3>),
+                         agrid,
                          dim3(kMsmThreads), 0, st, chunk, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads,
                          sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
   } else {
