@@ -936,19 +936,10 @@ msm_bucket_reduce_kernel(const G1xyzz* __restrict__ buckets, const uint32_t* __r
   const int g = (int)(t % nseg);
   const size_t base = (size_t)w * nb + (size_t)g * seglen;
   G1xyzz run = G1xyzz::inf(), tot = G1xyzz::inf();
-  for (int st = 0; st < 2 * seglen; st++) {
-    const bool is_run = !(st & 1);
-    G1xyzz rhs;
-    if (is_run) {
-      const uint32_t k = (uint32_t)(base + seglen - 1 - (st >> 1));
-      if (offsets[k + 1] == offsets[k]) continue;
-      rhs = buckets[k];
-    } else {
-      if (run.is_inf()) continue;
-      rhs = run;
-    }
-    const G1xyzz r = xyzz_add(is_run ? run : tot, rhs);
-    if (is_run) run = r; else tot = r;
+  for (int j = seglen - 1; j >= 0; j--) {  // two addition sites, no selected operand (scratch)
+    const uint32_t k = (uint32_t)(base + j);
+    if (offsets[k + 1] != offsets[k]) run = xyzz_add(run, buckets[k]);
+    if (!run.is_inf()) tot = xyzz_add(tot, run);
   }
   seg_tot[t] = tot;  // sum_j (j+1) * bucket_{g*L+j}
   seg_run[t] = run;  // sum_j bucket_{g*L+j}
