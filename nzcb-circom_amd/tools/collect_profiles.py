@@ -60,7 +60,7 @@ def acc_pmc(src):
     """SQ / GRBM counters of the isolated accumulation (tools/acc_probe.py, two passes)."""
     vals, lines = {}, ["# rocprofv3 --pmc (two passes) -- python3 nzcb-circom_amd/tools/acc_probe.py",
                        "# fixed-base MSM alone, 2^21 + 6 points of random scalars, c = 17; "
-                       "msm_accumulate29_kernel<4, false>, averages over each pass's launches"]
+                       "msm_accumulate29_kernel<3, false>, averages over each pass's launches"]
     for d in ("pmcA", "pmcB"):
         agg = {}
         for f in glob.glob(os.path.join(src, d, "**", "*counter_collection.csv"), recursive=True):
@@ -116,7 +116,7 @@ def main():
     nw, write_kb = pmc_avg(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     fetch_raw = fetch_kb * 1024
     traffic = {
-        "kernel": "msm_accumulate29_kernel<4> (fixed-base bucket accumulation, 2^21+6-point MSM of random scalars, "
+        "kernel": "msm_accumulate29_kernel<3> (fixed-base bucket accumulation, 2^21+6-point MSM of random scalars, "
                   "c=17: bench.py's probe, the last 10 launches of each pass)",
         "command": "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate passes) -- python3 bench.py "
                    "--no-cpu-baseline --steps 8",
