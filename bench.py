@@ -211,7 +211,8 @@ def main():
     root = backend_range = comm = None
     if split:
         # configs[4]: rank 0 proves one proof at a time, every commitment MSM split by PTau
-        # range over all ranks (scalars by broadcast, partials by all-gather; nzcb/msmsplit.py)
+        # range over all ranks (each rank's slice of the scalars by scatter, partials gathered to
+        # rank 0; nzcb/msmsplit.py)
         from nzcb import msmsplit
         comm = msmsplit.Comm(dist, f"cuda:{device}" if backend == "nccl" else "cpu")
         args.lanes = 1
@@ -235,7 +236,7 @@ def main():
         """The step loop of this rank: proofs (and, in split mode, the STOP that ends the
         servers' loop), or serving rank 0's commitments."""
         if split and rank != 0:
-            msmsplit.serve(comm, backend_range[0])
+            msmsplit.serve(comm, backend_range[0], n + 6)
             return []
         res = prover.full_prove_staged(count_or_none, blindings) if count_or_none else []
         if root is not None:

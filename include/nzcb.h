@@ -21,6 +21,11 @@
  *                 OS CSPRNG per proof, as snarkjs's Fr.random() (zero-knowledge).
  *                 Fixed bytes (352 zero bytes included) give reproducible,
  *                 bit-exact proofs for tests; zero blinding is NOT zero-knowledge.
+ *
+ * This header is the product ABI. Kernel-level entry points for tests,
+ * microbenchmarks and tuning (nzcb_engine_*, the synthetic-circuit setup, kernel timing,
+ * the pairing-round knob) are in nzcb_internal.h: they are exported by the same library but
+ * are not part of the drop-in boundary and may change between releases.
  */
 #ifndef NZCB_H
 #define NZCB_H
@@ -155,11 +160,6 @@ int nzcb_prove_batch_status(nzcb_ctx* ctx, const void* const* witnesses, size_t 
  * [7] all MSMs [8] all NTTs. Returns the number of values written. */
 int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap);
 
-/* HIP-event timing of the MSM bucket-accumulation kernel (the dominant kernel):
- * out = {total ms, launches, MSM points, bucket entries} accumulated since the last
- * reset; enable = 1 / 0 turns timing on / off and resets, -1 only reads. */
-int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]);
-
 /* snarkjs-format JSON ({proof}, [publicSignals]) from the binary outputs. */
 int nzcb_proof_to_json(const uint8_t* proof, char* out, size_t cap);
 int nzcb_public_to_json(const uint8_t* pub, int n_public, char* out, size_t cap);
@@ -171,6 +171,10 @@ int nzcb_public_to_json(const uint8_t* pub, int n_public, char* out, size_t cap)
  * Replaces snarkjs `zkey export verificationkey` (/root/reference/Makefile:56,61). */
 #define NZCB_VK_BYTES (8 + 2 * 32 + 8 * 64 + 4 * 32 + 32)
 int nzcb_vk_from_zkey(const uint8_t* zkey, size_t zkey_len, uint8_t* vk_out, nzcb_err* err);
+/* The same from a zkey file, memory-mapped (zkeys past 2 GiB, e.g. nzcp_live's ~3.9 GB, which
+ * `snarkjs zkey export verificationkey|solidityverifier nzcp_live_final.zkey` reads,
+ * /root/reference/Makefile:61-62). */
+int nzcb_vk_from_zkey_file(const char* zkey_path, uint8_t* vk_out, nzcb_err* err);
 /* verification_key.json text (snarkjs layout); returns 0, or the needed size if cap is short. */
 int nzcb_vk_to_json(const uint8_t* vk, char* out, size_t cap);
 /* snarkjs plonk.verify: *valid = 1 if the proof (NZCB_PROOF_BYTES) is valid for the public
@@ -248,13 +252,6 @@ int nzcb_nzcp_witness_dev(int device, const nzcb_nzcp_params* prm, const void* d
                           void* dev_records, void* dev_witness, size_t witness_stride, void* stream,
                           nzcb_err* err);
 
-/* ---- Synthetic circuit + setup ------- */
-/* Builds the seeded synthetic circuit of oracle/synth.py and its snarkjs-0.4
- * PLONK zkey with trapdoor tau (32-byte LE normal) on `device`. Buffers are
- * malloc'ed by the library; free them with nzcb_free. */
-int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints,
-                     const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len, uint8_t** wtns_out,
-                     size_t* wtns_len, nzcb_err* err);
 /* ---- Witness programs: the circom witness calculator on the GPU ------------------
  * Replaces circom_runtime's calculateWitness / snarkjs wtns_calculate (circom_runtime
  * 0.1.17, /root/reference/yarn.lock:2496) for circuits
@@ -280,13 +277,7 @@ int nzcb_wprog_run_dev(nzcb_wprog* prog, const void* dev_inputs, int count, void
 int nzcb_wprog_run(nzcb_wprog* prog, const uint8_t* inputs, int count, uint8_t* witness_out,
                    int32_t* status_out, nzcb_err* err);
 
-/* Same with flags: NZCB_SYNTH_FREE_PUBLIC keeps the public signals off every gate but
- * their public-input gate, so any public values satisfy the circuit. The bench's
- * fullProve pipeline writes the nzcp outputs of each pass there (nzcb_nzcp_witness_dev). */
-#define NZCB_SYNTH_FREE_PUBLIC 1u
-int nzcb_synth_setup_ex(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints, uint32_t flags,
-                        const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len, uint8_t** wtns_out,
-                        size_t* wtns_len, nzcb_err* err);
+/* ---- Setup ------------------------------------------ */
 /* snarkjs `plonk setup <r1cs> <ptau> <zkey>` (snarkjs 0.4.12 plonk_setup.js, run at
  * /root/reference/Makefile:55,60): iden3 r1cs + powers-of-tau file -> snarkjs-0.4 PLONK
  * zkey (malloc'ed, release with nzcb_free). Uses the ptau's tauG1 (section 2) and
@@ -300,45 +291,14 @@ int nzcb_plonk_setup(const uint8_t* r1cs, size_t r1cs_len, const uint8_t* ptau, 
 int nzcb_ptau_synth(int power, const uint8_t* tau, int device, uint8_t** ptau_out, size_t* ptau_len, nzcb_err* err);
 void nzcb_free(void* p);
 
-/* ---- Kernel-level entry points (tests / microbench) */
-typedef struct nzcb_engine nzcb_engine;
-nzcb_engine* nzcb_engine_create(int device, int max_log_ntt, size_t max_msm_points, nzcb_err* err);
-void nzcb_engine_destroy(nzcb_engine* e);
-/* Host-buffer variants. Field elements are 32-byte LE Montgomery ("LEM", zkey layout). */
-int nzcb_engine_ntt(nzcb_engine* e, const uint8_t* in_lem, uint8_t* out_lem, int log_n, int inverse, nzcb_err* err);
-/* bases: n x 64-byte LEM affine; scalars: n x 32 B LE (Montgomery if scalars_mont);
- * out: 64-byte affine x||y LE normal (infinity = zeros). */
-int nzcb_engine_msm(nzcb_engine* e, const uint8_t* bases_lem, const uint8_t* scalars, size_t n, int scalars_mont,
-                    uint8_t* out_affine, nzcb_err* err);
-/* Device-resident variants for benchmarks (pointers from nzcb_dev_alloc). */
+/* ---- HBM buffers (witnesses for nzcb_prove_device / nzcb_prove_batch on device) ---- */
 void* nzcb_dev_alloc(size_t bytes);
 void nzcb_dev_free(void* p);
 int nzcb_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int nzcb_memcpy_d2h(void* dst, const void* src, size_t bytes);
 int nzcb_memcpy_d2d(void* dst, const void* src, size_t bytes);
-int nzcb_engine_ntt_dev(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, nzcb_err* err);
-int nzcb_engine_msm_dev(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
-                        uint8_t* out_affine, nzcb_err* err);
-/* Average milliseconds per call of `reps` back-to-back device NTTs, timed with HIP
- * events on the engine's stream. */
-int nzcb_engine_time_ntt(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, int reps, double* ms,
-                         nzcb_err* err);
-/* Microbench inputs: n pseudo-random Fr (Montgomery, < 2^253)
- * from `seed`, and [s_i]G1 bases (LEM affine) from Montgomery scalars. Device pointers. */
-int nzcb_engine_random_fr(nzcb_engine* e, void* dev_out, size_t n, uint64_t seed, nzcb_err* err);
-int nzcb_engine_fixed_base(nzcb_engine* e, const void* dev_scalars_mont, size_t n, void* dev_out, nzcb_err* err);
-/* Lagrange-basis SRS (csrc/lagrange.hip): dev_out[k] = [L_k(tau)] for k < 2^log_n, then
- * [tau^n] - [1] and [tau^(n+1)] - [tau], from ptau_n >= 2^log_n + 2 PTau points (LEM affine,
- * device pointers). The prover commits A, B, C from their evaluations with it. */
-int nzcb_engine_lagrange_basis(nzcb_engine* e, const void* dev_ptau, size_t ptau_n, int log_n, void* dev_out,
-                               nzcb_err* err);
-/* Average wall ms per MSM over `reps` (host-synchronised) and the average bucket-
- * accumulation kernel ms (HIP events). */
-int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont, int reps,
-                         double* ms, double* acc_ms, nzcb_err* err);
-/* Fixed-base schedule (the prover's): builds the shifted-base table of the first
- * n_table bases (2^(20w) multiples, 13 rows), then runs the MSM of the first n.
- * One-shot (table and scratch freed on return); for parity tests. */
+
+/* ---- Serving side of nzcb_ctx_set_msm_split (one per serving rank) ---------------- */
 /* A resident fixed-base MSM table over n device bases (affine LEM, e.g. a PTau range),
  * the prover's c = 17 shifted-base schedule: the serving ranks of nzcb_ctx_set_msm_split
  * keep one and answer every commitment with one run. out_affine: 64 bytes, x || y normal
@@ -349,21 +309,6 @@ nzcb_msm_table* nzcb_msm_table_create(int device, const void* dev_bases, size_t 
 int nzcb_msm_table_run(nzcb_msm_table* t, const void* dev_scalars, size_t count, int scalars_mont,
                        uint8_t* out_affine, nzcb_err* err);
 void nzcb_msm_table_destroy(nzcb_msm_table* t);
-int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
-                              int scalars_mont, uint8_t* out_affine, nzcb_err* err);
-/* Batch-affine pairing rounds ahead of the fixed-base bucket accumulation (each halves
- * every bucket's run): rounds >= 0 forces that many (at most 6; 0 = XYZZ accumulation
- * only), rounds < 0 restores the automatic choice (NZCB_PAIR_ROUNDS, default 0, while
- * the average run is >= 8 entries). Process-wide; for tests and tuning. */
-int nzcb_msm_set_pair_rounds(int rounds);
-/* Per-phase MSM timing (HIP events, average over reps after one warm-up):
- * out[0] wall ms, out[1..7] keys, sort, offsets, accumulate, finalize, reduce, sums,
- * out[8] table build ms (fixed_base only), out[9] bucket entries per MSM (nonzero digits). */
-int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
-                          int fixed_base, int reps, double* out, nzcb_err* err);
-/* Field self-test helpers: out[i] = a[i] * b[i] (Montgomery, device), n elements. */
-int nzcb_engine_fr_mul(nzcb_engine* e, const uint8_t* a_lem, const uint8_t* b_lem, uint8_t* out_lem, size_t n,
-                       int field_q, nzcb_err* err);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,87 @@
+/*
+ * nzcb internal ABI: kernel-level entry points for tests, microbenchmarks and tuning
+ * (SURVEY.md §8d config 2). Exported by libnzcb.so next to the product ABI of nzcb.h, but
+ * not part of the drop-in boundary and not stable.
+ */
+#ifndef NZCB_INTERNAL_H
+#define NZCB_INTERNAL_H
+
+#include "nzcb.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* HIP-event timing of the MSM bucket-accumulation kernel (the dominant kernel):
+ * out = {total ms, launches, MSM points, bucket entries} accumulated since the last
+ * reset; enable = 1 / 0 turns timing on / off and resets, -1 only reads. */
+int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]);
+
+/* ---- Synthetic circuit + setup ------- */
+/* Builds the seeded synthetic circuit of oracle/synth.py and its snarkjs-0.4
+ * PLONK zkey with trapdoor tau (32-byte LE normal) on `device`. Buffers are
+ * malloc'ed by the library; free them with nzcb_free. */
+int nzcb_synth_setup(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints,
+                     const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len, uint8_t** wtns_out,
+                     size_t* wtns_len, nzcb_err* err);
+/* Same with flags: NZCB_SYNTH_FREE_PUBLIC keeps the public signals off every gate but
+ * their public-input gate, so any public values satisfy the circuit. The bench's
+ * fullProve pipeline writes the nzcp outputs of each pass there (nzcb_nzcp_witness_dev). */
+#define NZCB_SYNTH_FREE_PUBLIC 1u
+int nzcb_synth_setup_ex(int power, int n_public, int n_inputs, uint64_t seed, uint32_t n_constraints, uint32_t flags,
+                        const uint8_t* tau, int device, uint8_t** zkey_out, size_t* zkey_len, uint8_t** wtns_out,
+                        size_t* wtns_len, nzcb_err* err);
+/* ---- Kernel-level entry points ------------------------------------------------ */
+typedef struct nzcb_engine nzcb_engine;
+nzcb_engine* nzcb_engine_create(int device, int max_log_ntt, size_t max_msm_points, nzcb_err* err);
+void nzcb_engine_destroy(nzcb_engine* e);
+/* Host-buffer variants. Field elements are 32-byte LE Montgomery ("LEM", zkey layout). */
+int nzcb_engine_ntt(nzcb_engine* e, const uint8_t* in_lem, uint8_t* out_lem, int log_n, int inverse, nzcb_err* err);
+/* bases: n x 64-byte LEM affine; scalars: n x 32 B LE (Montgomery if scalars_mont);
+ * out: 64-byte affine x||y LE normal (infinity = zeros). */
+int nzcb_engine_msm(nzcb_engine* e, const uint8_t* bases_lem, const uint8_t* scalars, size_t n, int scalars_mont,
+                    uint8_t* out_affine, nzcb_err* err);
+/* Device-resident variants for benchmarks (pointers from nzcb_dev_alloc, nzcb.h). */
+int nzcb_engine_ntt_dev(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, nzcb_err* err);
+int nzcb_engine_msm_dev(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
+                        uint8_t* out_affine, nzcb_err* err);
+/* Average milliseconds per call of `reps` back-to-back device NTTs, timed with HIP
+ * events on the engine's stream. */
+int nzcb_engine_time_ntt(nzcb_engine* e, const void* in, void* out, int log_n, int inverse, int reps, double* ms,
+                         nzcb_err* err);
+/* Microbench inputs: n pseudo-random Fr (Montgomery, < 2^253)
+ * from `seed`, and [s_i]G1 bases (LEM affine) from Montgomery scalars. Device pointers. */
+int nzcb_engine_random_fr(nzcb_engine* e, void* dev_out, size_t n, uint64_t seed, nzcb_err* err);
+int nzcb_engine_fixed_base(nzcb_engine* e, const void* dev_scalars_mont, size_t n, void* dev_out, nzcb_err* err);
+/* Lagrange-basis SRS (csrc/lagrange.hip): dev_out[k] = [L_k(tau)] for k < 2^log_n, then
+ * [tau^n] - [1] and [tau^(n+1)] - [tau], from ptau_n >= 2^log_n + 2 PTau points (LEM affine,
+ * device pointers). The prover commits A, B, C from their evaluations with it. */
+int nzcb_engine_lagrange_basis(nzcb_engine* e, const void* dev_ptau, size_t ptau_n, int log_n, void* dev_out,
+                               nzcb_err* err);
+/* Average wall ms per MSM over `reps` (host-synchronised) and the average bucket-
+ * accumulation kernel ms (HIP events). */
+int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont, int reps,
+                         double* ms, double* acc_ms, nzcb_err* err);
+/* Fixed-base schedule (the prover's): builds the shifted-base table of the first
+ * n_table bases (c = 17: 2^(17w) multiples, 15 rows), then runs the MSM of the first n.
+ * One-shot (table and scratch freed on return); for parity tests. */
+int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
+                              int scalars_mont, uint8_t* out_affine, nzcb_err* err);
+/* Batch-affine pairing rounds ahead of the fixed-base bucket accumulation (each halves
+ * every bucket's run): rounds >= 0 forces that many (at most 6; 0 = XYZZ accumulation
+ * only), rounds < 0 restores the automatic choice (NZCB_PAIR_ROUNDS, default 0, while
+ * the average run is >= 8 entries). Process-wide; for tests and tuning. */
+int nzcb_msm_set_pair_rounds(int rounds);
+/* Per-phase MSM timing (HIP events, average over reps after one warm-up):
+ * out[0] wall ms, out[1..7] keys, sort, offsets, accumulate, finalize, reduce, sums,
+ * out[8] table build ms (fixed_base only), out[9] bucket entries per MSM (nonzero digits). */
+int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
+                          int fixed_base, int reps, double* out, nzcb_err* err);
+/* Field self-test helpers: out[i] = a[i] * b[i] (Montgomery, device), n elements. */
+int nzcb_engine_fr_mul(nzcb_engine* e, const uint8_t* a_lem, const uint8_t* b_lem, uint8_t* out_lem, size_t n,
+                       int field_q, nzcb_err* err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -4,7 +4,7 @@
 #include <memory>
 #include <vector>
 
-#include "../../include/nzcb.h"
+#include "../../include/nzcb_internal.h"
 #include "engine.h"
 #include "lagrange.h"
 

@@ -11,7 +11,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/nzcb.h"
+#include "../../include/nzcb_internal.h"
 #include "prover.h"
 
 namespace nzcb {

@@ -7,7 +7,7 @@
 #include <stdexcept>
 #include <string>
 
-#include "../../include/nzcb.h"
+#include "../../include/nzcb_internal.h"
 #include "field.h"
 
 namespace nzcb {

@@ -20,6 +20,8 @@
 #include "transcript.h"
 
 #include <cstring>
+#include <cerrno>
+#include <string>
 #include <sys/random.h>
 
 #include "keccak.h"
@@ -957,7 +959,11 @@ Fr random_fr() {
     size_t got = 0;
     while (got < sizeof(b)) {
       ssize_t k = getrandom(b + got, sizeof(b) - got, 0);
-      if (k < 0) throw Error(NZCB_ERR_ARG, "getrandom failed: no entropy for the blinding scalars");
+      if (k < 0) {
+        if (errno == EINTR || errno == EAGAIN) continue;  // a signal during the read: draw again
+        throw Error(NZCB_ERR_INTERNAL, std::string("getrandom failed: ") + std::strerror(errno) +
+                                           " (no entropy for the blinding scalars)");
+      }
       got += (size_t)k;
     }
     b[31] &= 0x3f;

@@ -16,7 +16,7 @@
 #include <functional>
 #include <vector>
 
-#include "../../include/nzcb.h"
+#include "../../include/nzcb_internal.h"
 #include "engine.h"
 
 namespace nzcb {

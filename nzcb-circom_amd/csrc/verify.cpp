@@ -14,6 +14,11 @@
 // D-type twist (x, y) -> (x w^2, y w^3), Miller loop over 6x + 2 with affine Fq2 steps
 // and sparse lines, Frobenius corrections, and the exponent (p^12 - 1)/r. The CPU
 // oracle oracle/pairing.py states the same algorithm; tests/test_verify.py pins both.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <cstring>
 #include <string>
 #include <vector>
@@ -454,6 +459,35 @@ int nzcb_vk_from_zkey(const uint8_t* zkey, size_t zkey_len, uint8_t* vk_out, nzc
     set_err(err, NZCB_ERR_INTERNAL, e.what());
     return NZCB_ERR_INTERNAL;
   }
+}
+
+// the same from a zkey file, memory-mapped (a nzcp_live zkey is ~3.9 GB: larger than a
+// Node Buffer, so `zkey export verificationkey|solidityverifier` read it through here)
+int nzcb_vk_from_zkey_file(const char* zkey_path, uint8_t* vk_out, nzcb_err* err) {
+  if (!zkey_path || !vk_out) {
+    set_err(err, NZCB_ERR_ARG, "null argument");
+    return NZCB_ERR_ARG;
+  }
+  const int fd = open(zkey_path, O_RDONLY);
+  if (fd < 0) {
+    set_err(err, NZCB_ERR_ARG, (std::string("cannot open ") + zkey_path).c_str());
+    return NZCB_ERR_ARG;
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0 || st.st_size <= 0) {
+    close(fd);
+    set_err(err, NZCB_ERR_FORMAT, "zkey file is empty");
+    return NZCB_ERR_FORMAT;
+  }
+  void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) {
+    set_err(err, NZCB_ERR_INTERNAL, "mmap of the zkey failed");
+    return NZCB_ERR_INTERNAL;
+  }
+  const int rc = nzcb_vk_from_zkey(static_cast<const uint8_t*>(m), (size_t)st.st_size, vk_out, err);
+  munmap(m, (size_t)st.st_size);
+  return rc;
 }
 
 int nzcb_vk_to_json(const uint8_t* vk, char* out, size_t cap) {

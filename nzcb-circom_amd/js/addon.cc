@@ -72,16 +72,28 @@ napi_value CreateContext(napi_env env, napi_callback_info info) {
   return ext;
 }
 
+// a JS string argument as UTF-8 (false if it is not a string)
+bool str_arg(napi_env env, napi_value v, std::string* out) {
+  napi_valuetype t;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_string) return false;
+  size_t plen = 0;
+  if (napi_get_value_string_utf8(env, v, nullptr, 0, &plen) != napi_ok) return false;
+  out->assign(plen + 1, '\0');
+  if (napi_get_value_string_utf8(env, v, &(*out)[0], out->size(), &plen) != napi_ok) return false;
+  out->resize(plen);
+  return true;
+}
+
 // createContextFile(path: string, device: number) -> external (zkeys larger than a Buffer)
 napi_value CreateContextFile(napi_env env, napi_callback_info info) {
   size_t argc = 2;
   napi_value argv[2];
   CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
-  size_t plen = 0;
-  CHECK(napi_get_value_string_utf8(env, argv[0], nullptr, 0, &plen));
-  std::string path(plen + 1, '\0');
-  CHECK(napi_get_value_string_utf8(env, argv[0], &path[0], path.size(), &plen));
-  path.resize(plen);
+  std::string path;
+  if (argc < 1 || !str_arg(env, argv[0], &path)) {
+    napi_throw_type_error(env, nullptr, "createContextFile(path: string, device?: number)");
+    return nullptr;
+  }
   int32_t device = 0;
   if (argc > 1) napi_get_value_int32(env, argv[1], &device);
   nzcb_err err{};
@@ -376,6 +388,28 @@ napi_value VkFromZkey(napi_env env, napi_callback_info info) {
   return res;
 }
 
+// vkFromZkeyFile(path: string) -> Buffer (NZCB_VK_BYTES): the zkey is memory-mapped by the
+// library, so files past a Buffer's 2 GiB limit (nzcp_live_final.zkey) work
+napi_value VkFromZkeyFile(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  std::string path;
+  if (argc < 1 || !str_arg(env, argv[0], &path)) {
+    napi_throw_type_error(env, nullptr, "vkFromZkeyFile(path: string)");
+    return nullptr;
+  }
+  void* out = nullptr;
+  napi_value res;
+  CHECK(napi_create_buffer(env, NZCB_VK_BYTES, &out, &res));
+  nzcb_err err{};
+  if (nzcb_vk_from_zkey_file(path.c_str(), static_cast<uint8_t*>(out), &err) != 0) {
+    napi_throw(env, make_error(env, err.code, err.msg));
+    return nullptr;
+  }
+  return res;
+}
+
 // vkToJson(vk: Buffer) -> string (verification_key.json)
 napi_value VkToJson(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -538,6 +572,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"vkFromZkey", nullptr, VkFromZkey, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"vkFromZkeyFile", nullptr, VkFromZkeyFile, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"vkToJson", nullptr, VkToJson, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"verify", nullptr, Verify, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"calldata", nullptr, Calldata, nullptr, nullptr, nullptr, napi_default, nullptr},

@@ -303,8 +303,15 @@ async function setup(r1csName, ptauName, zkeyName, logger, options) {
   return 0;
 }
 
+// binary verification key of a zkey: a file name is memory-mapped by the library
+// (nzcb_vk_from_zkey_file), so nzcp_live's ~3.9 GB zkey is never read into a Buffer
+// (fs.readFileSync refuses files past 2 GiB)
+function vkOf(zkey) {
+  return typeof zkey === 'string' ? addon.vkFromZkeyFile(zkey) : addon.vkFromZkey(readBin(zkey));
+}
+
 async function exportVerificationKey(zkeyFileName) {
-  return JSON.parse(addon.vkToJson(addon.vkFromZkey(readBin(zkeyFileName))));
+  return JSON.parse(addon.vkToJson(vkOf(zkeyFileName)));
 }
 
 // snarkjs zKey.exportSolidityVerifier(zkeyName, templates, logger) (`zkey export
@@ -314,7 +321,7 @@ async function exportVerificationKey(zkeyFileName) {
 async function exportSolidityVerifier(zkeyFileName, templates, logger, options) {
   options = options || {};
   const tp = options.transcriptPublic === undefined ? true : !!options.transcriptPublic;
-  const src = addon.vkToSolidity(addon.vkFromZkey(readBin(zkeyFileName)), options.name || 'PlonkVerifier', tp);
+  const src = addon.vkToSolidity(vkOf(zkeyFileName), options.name || 'PlonkVerifier', tp);
   const log = loggerFn(logger);
   if (log) log(`Solidity verifier: ${src.length} bytes`);
   return src;

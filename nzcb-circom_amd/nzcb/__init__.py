@@ -40,7 +40,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_dev_free", "nzcb_memcpy_h2d", "nzcb_memcpy_d2h", "nzcb_engine_ntt_dev", "nzcb_engine_msm_dev",
     "nzcb_engine_time_ntt", "nzcb_engine_fr_mul", "nzcb_engine_random_fr", "nzcb_engine_fixed_base",
     "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
-    "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_to_json", "nzcb_verify",
+    "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_from_zkey_file", "nzcb_vk_to_json", "nzcb_verify",
     "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_engine_lagrange_basis", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d", "nzcb_msm_set_pair_rounds",
     "nzcb_plonk_setup", "nzcb_prove_batch_status",
@@ -111,6 +111,7 @@ def load(path: str | None = None):
         "nzcb_ctx_set_lanes": (c_int, [c_void_p, c_int, POINTER(_Err)]),
         "nzcb_ctx_set_msm_devices": (c_int, [c_void_p, POINTER(c_int), c_int, POINTER(_Err)]),
         "nzcb_vk_from_zkey": (c_int, [u8p, c_size_t, u8p, POINTER(_Err)]),
+        "nzcb_vk_from_zkey_file": (c_int, [ctypes.c_char_p, u8p, POINTER(_Err)]),
         "nzcb_vk_to_json": (c_int, [u8p, ctypes.c_char_p, c_size_t]),
         "nzcb_verify": (c_int, [u8p, u8p, u8p, c_int, c_int, POINTER(c_int), POINTER(_Err)]),
         "nzcb_proof_to_calldata": (c_int, [u8p, u8p, c_int, ctypes.c_char_p, c_size_t]),
@@ -789,11 +790,13 @@ def vk_from_zkey(zkey) -> bytes:
     a (pointer, length) library buffer (nzcb.plonk_setup_raw)."""
     out = _out(VK_BYTES)
     err = _Err()
+    if isinstance(zkey, str):   # memory-mapped by the library (zkeys past 2 GiB)
+        _check(load().nzcb_vk_from_zkey_file(zkey.encode(), out, ctypes.byref(err)), err)
+        return bytes(out)
     if isinstance(zkey, tuple):
         ptr, size = ctypes.cast(zkey[0], POINTER(c_uint8)), zkey[1]
     else:
-        data = open(zkey, "rb").read() if isinstance(zkey, str) else zkey
-        ptr, size = _buf(data), len(data)
+        ptr, size = _buf(zkey), len(zkey)
     _check(load().nzcb_vk_from_zkey(ptr, size, out, ctypes.byref(err)), err)
     return bytes(out)
 

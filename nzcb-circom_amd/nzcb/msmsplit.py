@@ -5,21 +5,33 @@ Rank 0 proves. Every commitment MSM sum_i s_i [tau^i]G1 is split by PTau point r
 rank r taking [r N / W, (r+1) N / W) of N = n + 6 points; each rank holds the
 shifted-base table of its range resident in HBM (nzcb_msm_table). Per commitment:
 
-  rank 0: header (SCALARS, slot, count), then the `count` scalars      -- broadcast
-  rank r: partial over its range of those scalars (GPU)
-  rank 0: header (GATHER, slot), then one 64-byte affine partial per rank -- all-gather
+  rank 0: its scalars cut into W slices (one device copy into the send rows)
+  rank 0: header (SCALARS, slot, count)                                  -- broadcast, 24 B
+  rank r: receives ONLY its slice [lo_r, hi_r) of the scalars            -- scatter
+  rank r: partial over its range (GPU)
+  rank 0: header (GATHER, slot)                                          -- broadcast, 24 B
+  rank 0: one 64-byte affine partial from every rank                     -- gather to rank 0
   rank 0: adds the partials in rank order (csrc/prover.hip commit_finish)
 
-RCCL has no elliptic-curve reduction, so the "one reduce over xGMI" of the north star is
-the all-gather of W x 64 bytes plus W - 1 point additions on rank 0. The header
-broadcast keeps every rank's collective sequence identical while up to three
-commitments are in flight. Rounds 2-5 (Fiat-Shamir) stay on rank 0, so the split only
-shortens the MSM share of a proof (Amdahl).
+Bytes on the wire per commitment: 32 (N - N/W) of scalars plus 64 (W - 1) of partials and
+two 24-byte headers, instead of the W - 1 full copies of the scalars a broadcast moves (at
+n = 2^21 and W = 8: 59 MB instead of 470 MB per commitment). Slices are
+padded to the longest range so every rank's scatter buffer has one size.
 
-``SplitRoot`` installs the callbacks on rank 0's ProverContext; ``serve`` is the loop of
-the other ranks. Both take a ``Comm`` (torch.distributed + the tensor device) and the
-serving side a ``partial(slot, scalars, count) -> 64 bytes`` backend: ``GpuRange`` in
-production, anything with the same signature in tests (the CPU port over gloo).
+RCCL has no elliptic-curve reduction, so the "one reduce over xGMI" of the north star is
+the gather of W x 64 bytes plus W - 1 point additions on rank 0. The header broadcast
+keeps every rank's collective sequence identical while up to three commitments are in
+flight. A header is only sent once its payload is ready, so a failing scalar source
+leaves the serving ranks waiting for the next header, in step with rank 0. Rounds 2-5
+(Fiat-Shamir) stay on rank 0, so the split only shortens the MSM share of a proof (Amdahl).
+
+``SplitRoot`` installs the callbacks on rank 0's ProverContext (use it as a context
+manager, or call ``stop``, so the serving ranks leave their loop); ``serve`` is the loop
+of the other ranks. Both take a ``Comm`` (torch.distributed + the tensor device) and the
+serving side a ``partial(slot, slice_tensor, count) -> 64 bytes`` backend, where the
+tensor holds this rank's ``count`` scalars starting at its range's first point:
+``GpuRange`` in production, anything with the same signature in tests (the CPU port
+over gloo).
 """
 from __future__ import annotations
 
@@ -33,6 +45,19 @@ def point_ranges(n_points: int, world: int) -> list:
     return [(r * n_points // world, (r + 1) * n_points // world) for r in range(world)]
 
 
+def slice_counts(count: int, ranges: list) -> list:
+    """Scalars of an MSM of length `count` that fall into each rank's point range."""
+    return [max(0, min(count, hi) - lo) for lo, hi in ranges]
+
+
+def wire_bytes(count: int, world: int, n_points: int) -> int:
+    """Bytes one split commitment moves between ranks (scatter rows to ranks 1.., partials
+    to rank 0, two headers to ranks 1..), for DESIGN.md §6."""
+    ranges = point_ranges(n_points, world)
+    row = 32 * max(hi - lo for lo, hi in ranges)
+    return (world - 1) * (row + 64 + 2 * 24) if count else (world - 1) * (64 + 2 * 24)
+
+
 class Comm:
     """torch.distributed collectives on byte tensors (cuda tensors for nccl, cpu for gloo)."""
 
@@ -41,27 +66,36 @@ class Comm:
         self.torch, self.dist, self.device = torch, dist, device
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
 
-    def _sync(self):
+    def sync(self):
+        """Host wait for torch's stream (before another stream or the host reads a result)."""
         if self.device.startswith("cuda"):
             self.torch.cuda.current_stream().synchronize()
 
-    def header(self, kind: int = 0, slot: int = 0, count: int = 0) -> tuple:
+    def send_header(self, kind: int, slot: int = 0, count: int = 0):
+        """Rank 0: no read-back, no host wait (the tensor is ordered on torch's stream)."""
         t = self.torch.tensor([kind, slot, count], dtype=self.torch.int64, device=self.device)
         self.dist.broadcast(t, 0)
-        self._sync()
-        return tuple(int(x) for x in t.cpu().tolist())
 
-    def bcast(self, t):
+    def recv_header(self) -> tuple:
+        t = self.torch.empty(3, dtype=self.torch.int64, device=self.device)
         self.dist.broadcast(t, 0)
-        self._sync()
-        return t
+        return tuple(int(x) for x in t.cpu().tolist())   # .cpu() waits for the broadcast
 
-    def allgather64(self, own: bytes) -> bytes:
+    def scatter_rows(self, rows, out):
+        """rows: rank 0's [world, row_bytes] tensor (None elsewhere); out: this rank's row.
+        Returns the collective's work handle (wait on it before rows are rewritten)."""
+        return self.dist.scatter(out, list(rows.unbind(0)) if rows is not None else None, src=0,
+                                 async_op=True)
+
+    def gather64(self, own: bytes) -> bytes | None:
+        """Every rank's 64-byte partial to rank 0 (None on the other ranks)."""
         src = self.torch.tensor(list(own), dtype=self.torch.uint8, device=self.device)
-        out = [self.torch.empty(64, dtype=self.torch.uint8, device=self.device) for _ in range(self.world)]
-        self.dist.all_gather(out, src)
-        self._sync()
-        return b"".join(bytes(o.cpu().tolist()) for o in out)
+        if self.rank == 0:
+            out = [self.torch.empty(64, dtype=self.torch.uint8, device=self.device) for _ in range(self.world)]
+            self.dist.gather(src, out, dst=0)
+            return bytes(self.torch.cat(out).cpu().tolist())
+        self.dist.gather(src, None, dst=0)
+        return None
 
     def empty(self, nbytes: int):
         return self.torch.empty(max(nbytes, 1), dtype=self.torch.uint8, device=self.device)
@@ -70,56 +104,85 @@ class Comm:
 class SplitRoot:
     """Rank 0: the send/gather callbacks of nzcb_ctx_set_msm_split over `comm`."""
 
+    SLOTS = 3   # commitments in flight (csrc/prover.hip)
+
     def __init__(self, comm: Comm, n_points: int, scalar_source=None):
         self.comm = comm
         self.ranges = point_ranges(n_points, comm.world)
         self.own_points = self.ranges[0][1]
-        # scalar_source(dev_ptr, count, tensor): fills the broadcast tensor (device copy by
-        # default; tests pass host bytes instead)
+        self.row = 32 * max(hi - lo for lo, hi in self.ranges)
+        # scalar_source(src, lo, cnt, row_tensor): copies scalars [lo, lo + cnt) of the
+        # commitment into a send row (device copy by default; tests pass host bytes)
         self.scalar_source = scalar_source or self._device_copy
+        self._rows = {}     # slot -> [world, row] send rows (kept until the next use of the slot)
         self.sent = 0
+        self.stopped = False
 
-    def _device_copy(self, src, count: int, t):
+    def _device_copy(self, src, lo: int, cnt: int, row):
         import nzcb
         if self.comm.device.startswith("cuda"):
-            nzcb.d2d(t.data_ptr(), src, 32 * count)
+            nzcb.d2d(row.data_ptr(), src + 32 * lo, 32 * cnt)
         else:
-            t.copy_(self.comm.torch.frombuffer(bytearray(nzcb.d2h(src, 32 * count)), dtype=self.comm.torch.uint8))
+            row[:32 * cnt].copy_(self.comm.torch.frombuffer(bytearray(nzcb.d2h(src + 32 * lo, 32 * cnt)),
+                                                            dtype=self.comm.torch.uint8))
 
     def send(self, slot: int, src, count: int):
-        self.comm.header(HDR_SCALARS, slot, count)
-        t = self.comm.empty(32 * count)
-        if count:
-            self.scalar_source(src, count, t)
-        self.comm.bcast(t)
+        rows, work = self._rows.get(slot, (None, None))
+        if rows is None:
+            rows = self.comm.torch.empty((self.comm.world, max(self.row, 1)), dtype=self.comm.torch.uint8,
+                                         device=self.comm.device)
+        elif work is not None:   # the slot's previous scatter must have read its rows
+            work.wait()
+            self.comm.sync()
+        # fill first: if the source fails, no header is out and the servers stay in step
+        for r, ((lo, _), cnt) in enumerate(zip(self.ranges, slice_counts(count, self.ranges))):
+            if r and cnt:
+                self.scalar_source(src, lo, cnt, rows[r])
+        self.comm.send_header(HDR_SCALARS, slot, count)
+        out = self.comm.empty(self.row)
+        self._rows[slot] = (rows, self.comm.scatter_rows(rows, out))
         self.sent += 1
 
     def gather(self, slot: int, own: bytes) -> bytes:
-        self.comm.header(HDR_GATHER, slot, 0)
-        return self.comm.allgather64(own)
+        self.comm.send_header(HDR_GATHER, slot, 0)
+        return self.comm.gather64(own)
 
     def install(self, ctx):
         ctx.set_msm_split(self.comm.world, self.own_points, self.send, self.gather)
 
     def stop(self):
-        self.comm.header(HDR_STOP, 0, 0)
+        if not self.stopped:
+            self.stopped = True
+            self.comm.send_header(HDR_STOP)
+            self.comm.sync()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.stop()
+        return False
 
 
-def serve(comm: Comm, partial) -> int:
-    """Ranks 1..: answer rank 0's commitments until STOP. partial(slot, scalars_tensor,
-    count) -> 64 bytes over this rank's point range. Returns the commitments served."""
+def serve(comm: Comm, partial, n_points: int) -> int:
+    """Ranks 1..: answer rank 0's commitments until STOP. partial(slot, slice_tensor, count)
+    -> 64 bytes over this rank's point range. Returns the commitments served."""
+    ranges = point_ranges(n_points, comm.world)
+    row = 32 * max(hi - lo for lo, hi in ranges)
     parts = {}
     served = 0
     while True:
-        kind, slot, count = comm.header()
+        kind, slot, count = comm.recv_header()
         if kind == HDR_STOP:
             return served
         if kind == HDR_SCALARS:
-            t = comm.bcast(comm.empty(32 * count))
-            parts[slot] = partial(slot, t, count)
+            t = comm.empty(row)
+            comm.scatter_rows(None, t).wait()
+            comm.sync()   # the backend reads the slice on its own stream
+            parts[slot] = partial(slot, t, slice_counts(count, ranges)[comm.rank])
             served += 1
         elif kind == HDR_GATHER:
-            comm.allgather64(parts.pop(slot))
+            comm.gather64(parts.pop(slot))
         else:
             raise RuntimeError(f"msm split: unknown header {kind}")
 
@@ -134,11 +197,10 @@ class GpuRange:
         self.table = nzcb.MsmTable(dev_ptau + 64 * lo, hi - lo, device)
         self.staging = None   # HBM copy of this range's scalars when they arrive in host tensors (gloo)
 
-    def __call__(self, slot: int, t, count: int) -> bytes:
-        cnt = max(0, min(count, self.hi) - self.lo)
+    def __call__(self, slot: int, t, cnt: int) -> bytes:
         if not cnt:
             return bytes(64)
-        src = t.data_ptr() + 32 * self.lo
+        src = t.data_ptr()
         if not getattr(t, "is_cuda", True):
             if self.staging is None:
                 self.staging = self.nzcb.dev_alloc(32 * (self.hi - self.lo))

@@ -13,16 +13,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
 
 
-def _declared():
-    with open(os.path.join(ROOT, "include", "nzcb.h")) as f:
+def _declared(header="nzcb.h"):
+    with open(os.path.join(ROOT, "include", header)) as f:
         src = f.read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(nzcb_[a-z0-9_]+)\s*\(", src)))
 
 
+def test_product_header_excludes_internal_entry_points():
+    """include/nzcb.h is the §8b product ABI; engine, synthetic setup, kernel
+    timing and tuning knobs live in include/nzcb_internal.h (same library)."""
+    product, internal = set(_declared()), set(_declared("nzcb_internal.h"))
+    assert not product & internal
+    assert not [s for s in product if s.startswith(("nzcb_engine_", "nzcb_synth_"))]
+    assert {"nzcb_msm_set_pair_rounds", "nzcb_ctx_kernel_stats", "nzcb_engine_msm_dev"} <= internal
+    assert {"nzcb_ctx_create_devices", "nzcb_prove_batch", "nzcb_msm_table_run", "nzcb_dev_alloc"} <= product
+
+
 def test_library_exports_header():
     lib = nzcb.load()
-    declared = _declared()
+    declared = sorted(set(_declared()) | set(_declared("nzcb_internal.h")))
     assert len(declared) >= 25
     missing = [s for s in declared if not hasattr(lib, s)]
     assert missing == []

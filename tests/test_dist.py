@@ -103,7 +103,7 @@ def _split_points(n):
     return pts
 
 
-def _split_worker(rank, world, port, n, jobs, out):
+def _split_worker(rank, world, port, n, jobs, fail, out):
     """Rank 0 drives the protocol as the prover does (sends of up to three commitments in
     flight, then gathers); ranks 1.. serve with the CPU port's MSM over their range."""
     import torch.distributed as dist
@@ -115,40 +115,52 @@ def _split_worker(rank, world, port, n, jobs, out):
     ranges = msmsplit.point_ranges(n, world)
     lo, hi = ranges[rank]
 
-    def cpu_partial(scalars: bytes, count):
-        cnt = max(0, min(count, hi) - lo)
+    def cpu_partial(own_slice: bytes, cnt):
+        """This rank's range partial from ITS slice of the scalars (what the scatter sends)."""
         if cnt == 0:
             return bytes(64)
-        return cbind.msm(b"".join(pts[lo:lo + cnt]), scalars[32 * lo:32 * (lo + cnt)], threads=1)
+        return cbind.msm(b"".join(pts[lo:lo + cnt]), own_slice[:32 * cnt], threads=1)
 
     if rank == 0:
-        def source(src, count, t):
+        def source(src, first, cnt, row):
             import torch
-            t.copy_(torch.frombuffer(bytearray(src), dtype=torch.uint8))
+            row[:32 * cnt].copy_(torch.frombuffer(bytearray(src[32 * first:32 * (first + cnt)]), dtype=torch.uint8))
 
-        root = msmsplit.SplitRoot(comm, n, scalar_source=source)
-        assert root.own_points == hi
-        folded = []
-        for batch in jobs:                    # up to 3 commitments in flight, as the prover
-            owns = {}
-            for slot, sc in enumerate(batch):
-                count = len(sc) // 32
-                root.send(slot, sc, count)
-                owns[slot] = cpu_partial(sc, count)
-            for slot in range(len(batch)):
-                folded.append(root.gather(slot, owns[slot]))
-        root.stop()
+        with msmsplit.SplitRoot(comm, n, scalar_source=source) as root:
+            assert root.own_points == hi
+            folded = []
+            for batch in jobs:                    # up to 3 commitments in flight, as the prover
+                owns = {}
+                for slot, sc in enumerate(batch):
+                    count = len(sc) // 32
+                    root.send(slot, sc, count)
+                    owns[slot] = cpu_partial(sc, msmsplit.slice_counts(count, ranges)[0])
+                for slot in range(len(batch)):
+                    folded.append(root.gather(slot, owns[slot]))
+            if fail:
+                # a scalar source that raises sends nothing: the servers stay in step
+                def bad(*_):
+                    raise RuntimeError("scalar source failed")
+                root.scalar_source = bad
+                with pytest.raises(RuntimeError):
+                    root.send(0, jobs[0][0], len(jobs[0][0]) // 32)
+                root.scalar_source = source
+                sc = jobs[0][0]
+                root.send(0, sc, len(sc) // 32)
+                folded.append(root.gather(0, cpu_partial(sc, msmsplit.slice_counts(len(sc) // 32, ranges)[0])))
         out[0] = folded
     else:
-        out[rank] = msmsplit.serve(comm, lambda slot, t, count: cpu_partial(bytes(t.tolist()), count))
+        out[rank] = msmsplit.serve(comm, lambda slot, t, cnt: cpu_partial(bytes(t.tolist()), cnt), n)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_msm_split_across_ranks_gloo(world):
+@pytest.mark.parametrize("world,fail", [(2, False), (3, False), (2, True)])
+def test_msm_split_across_ranks_gloo(world, fail):
     """Every commitment's folded partials equal the unsplit MSM (C port), for MSM lengths
-    shorter than, equal to and crossing the rank boundaries (the prover's n+2 .. n+6)."""
+    shorter than, equal to and crossing the rank boundaries (the prover's n+2 .. n+6). Each
+    serving rank receives only its slice of the scalars. With `fail`, a send whose scalar
+    source raises leaves the protocol in step: the next commitment still folds."""
     import random
     from oracle import bn254 as bn
     from oracle import cbind
@@ -161,11 +173,12 @@ def test_msm_split_across_ranks_gloo(world):
     jobs = [[scal(66), scal(66), scal(66)], [scal(67)], [scal(64), scal(64), scal(70)], [scal(1), scal(0)]]
     with mp.Manager() as m:
         out = m.dict()
-        mp.spawn(_split_worker, args=(world, _free_port(), n, jobs, out), nprocs=world, join=True)
+        mp.spawn(_split_worker, args=(world, _free_port(), n, jobs, fail, out), nprocs=world, join=True)
         res = dict(out)
     pts = _split_points(n)
-    flat = [sc for batch in jobs for sc in batch]
+    flat = [sc for batch in jobs for sc in batch] + ([jobs[0][0]] if fail else [])
     assert [res[r] for r in range(1, world)] == [len(flat)] * (world - 1)
+    assert len(res[0]) == len(flat)
     for sc, parts in zip(flat, res[0]):
         count = len(sc) // 32
         acc = None

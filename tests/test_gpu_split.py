@@ -39,6 +39,11 @@ class _Ptr:
         return self.p
 
 
+def msmsplit_counts(count, ranges):
+    from nzcb import msmsplit
+    return msmsplit.slice_counts(count, ranges)
+
+
 class _LocalRanks:
     """The serving ranks of msmsplit, in-process: each range's partial is computed from a
     private copy of the scalars as soon as they are sent (as serve() does on its GPU)."""
@@ -57,7 +62,9 @@ class _LocalRanks:
 
     def send(self, slot, ptr, count):
         self.nzcb.d2d(self.scal, ptr, 32 * count)
-        self.pending[slot] = b"".join(b(slot, _Ptr(self.scal), count) for b in self.backends)
+        cnts = msmsplit_counts(count, self.ranges)
+        self.pending[slot] = b"".join(b(slot, _Ptr(self.scal + 32 * lo), c)
+                                      for b, (lo, _), c in zip(self.backends, self.ranges[1:], cnts[1:]))
         self.calls += 1
 
     def gather(self, slot, own):

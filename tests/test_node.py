@@ -31,6 +31,30 @@ def test_addon_exports():
 
 
 @needs_node
+def test_node_zkey_export_past_2gib(tmp_path):
+    """zKey.exportVerificationKey / exportSolidityVerifier on a zkey file past
+    Node's 2 GiB readFileSync limit (nzcp_live_final.zkey is ~3.9 GB): a golden zkey grown to
+    3 GiB by a sparse tail exports the same key and contract as the library's."""
+    import nzcb
+    big = tmp_path / "big.zkey"
+    big.write_bytes(open(os.path.join(GOLD, "p8.zkey"), "rb").read())
+    with open(big, "r+b") as f:
+        f.truncate(3 << 30)
+    script = f"""
+const m = require('./');
+(async () => {{
+  const vk = await m.zKey.exportVerificationKey('{big}');
+  const sol = await m.zKey.exportSolidityVerifier('{big}', null, null, {{name: 'Verifier'}});
+  console.log(JSON.stringify({{vk, sol}}));
+}})().catch((e) => {{ console.error(e); process.exit(1); }});
+"""
+    d = json.loads(run_node(script))
+    vk = nzcb.vk_from_zkey(os.path.join(GOLD, "p8.zkey"))
+    assert d["vk"] == nzcb.vk_to_json(vk)
+    assert d["sol"] == nzcb.vk_to_solidity(vk, "Verifier")
+
+
+@needs_node
 @pytest.mark.gpu
 def test_node_plonk_prove_golden():
     meta = json.load(open(os.path.join(GOLD, "p8.json")))

@@ -50,6 +50,21 @@ def test_vk_json_matches_oracle(name):
     assert nzcb.vk_from_json(got) == vk
 
 
+def test_vk_from_zkey_file_past_2gib(tmp_path):
+    """`zkey export` on nzcp_live's ~3.9 GB zkey. The path entry
+    (nzcb_vk_from_zkey_file) maps the file: a golden zkey grown to 3 GiB by a sparse tail
+    (the reader ignores bytes past the sections) gives the same key; a missing file fails."""
+    meta, zkey = _gold("p8")
+    big = tmp_path / "big.zkey"
+    big.write_bytes(zkey)
+    with open(big, "r+b") as f:
+        f.truncate(3 << 30)
+    assert os.path.getsize(big) > (2 << 30)
+    assert nzcb.vk_from_zkey(str(big)) == nzcb.vk_from_zkey(zkey)
+    with pytest.raises(nzcb.NzcbError, match="cannot open"):
+        nzcb.vk_from_zkey(str(tmp_path / "missing.zkey"))
+
+
 @pytest.mark.parametrize("name", ["p5", "p8"])
 @pytest.mark.parametrize("bl", ["zero", "fixed"])
 def test_verify_golden_and_tampered(name, bl):
