@@ -124,12 +124,27 @@ def accumulate_probe(n_points: int, device: int, reps: int = 10) -> dict:
     return ph
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (BASELINE.md asks for it next to the core count)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline_sample(zkey_raw, wtns: bytes, n: int):
     """Time the CPU port (oracle) proving one proof of the same zkey and witness; rank 0,
     N=1 only."""
     from oracle import cbind
-    return cbind.timed_prove(zkey_raw, wtns, f"1 full proof of nzcp_live (n=2^{n.bit_length() - 1}, same zkey "
-                                             f"and GPU-computed witness)")
+    out = cbind.timed_prove(zkey_raw, wtns, f"1 full proof of nzcp_live (n=2^{n.bit_length() - 1}, same zkey "
+                                            f"and GPU-computed witness)")
+    out["cpu_model"] = cpu_model()
+    return out
 
 
 def main():
@@ -145,7 +160,7 @@ def main():
                          "(one process; lanes forced to 1)")
     ap.add_argument("--msm-split", action="store_true",
                     help="configs[4] across ranks: rank 0 proves --steps proofs one at a time, every commitment "
-                         "MSM split by point range over all ranks (RCCL broadcast + all-gather)")
+                         "MSM split by point range over all ranks (scatter of scalar slices + gather of partials)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the isolated accumulation-kernel probe")
     args = ap.parse_args()
@@ -339,8 +354,9 @@ def main():
                 "n_additions": ctx.n_additions,
                 "proofs_per_gpu": steps,
                 "total_proofs": total_proofs,
-                "parallelism": (f"single-proof MSM split x{world} (RCCL broadcast of scalars + all-gather of "
-                                f"64-byte partials)" if split else f"batch-shard x{world} (no collective)"),
+                "parallelism": (f"single-proof MSM split x{world} ({backend}: each rank's scalar slice by "
+                                f"scatter, 64-byte partials gathered to rank 0)" if split
+                                else f"batch-shard x{world} (no collective)"),
                 "proofs_in_flight_per_gpu": args.lanes,
                 "msm_devices": msm_devices or None,
             },

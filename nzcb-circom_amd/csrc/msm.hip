@@ -118,6 +118,16 @@ static constexpr int kPartThreads = 64;  // level-2 sums: block size
 static constexpr uint32_t kSeqSpan = 64;  // finalize: longest carry run summed by one thread
 static constexpr int kLargeBlocks = 32;  // finalize: workgroups for the longer runs
 
+// LDS-staged bucket indices in the accumulation (msm_accumulate29_kernel kLdsIdx);
+// NZCB_ACC_LDS=0 reads them from HBM as before (A/B runs)
+static bool lds_indices() {
+  static const bool on = [] {
+    const char* e = std::getenv("NZCB_ACC_LDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int fixed_base_window() {
   static const int c = [] {
     const char* e = std::getenv("NZCB_FB_WINDOW");
@@ -586,18 +596,40 @@ __device__ __forceinline__ G1xyzz load_point(const Xyzz29& a) {
 
 // kDirect: entries are the pairing rounds' affine sums (msm_pair29_kernel), read in
 // place (position = entry), instead of signed table indices in `sorted`.
-template <int WAVES, bool kDirect = false>
+// kLdsIdx (chunk == kChunk): the workgroup's kMsmThreads x kChunk slice of `sorted` is
+// staged into LDS by coalesced loads before the additions. Read from HBM one index per
+// addition, each lane's chunk 192 B from its neighbour's, the index lines were evicted
+// between uses by the table gathers and fetched again (~1 GB of the 3.3 GB a launch
+// moved, profiles/r2_fetch_calibration.txt); a gather-only probe over the same stream
+// ran 1.08 ms with HBM indices and 0.65 ms with LDS ones (tools/table_probe.hip).
+// 49 KB per workgroup: three workgroups (12 waves, the 3 waves per SIMD the kernel is
+// compiled for) fit the CU's 160 KB.
+static constexpr uint32_t kLdsStride = kMsmThreads + 1;  // slot-major rows, +1: conflict-free fill
+template <int WAVES, bool kDirect = false, bool kLdsIdx = false>
 __global__ void __launch_bounds__(kMsmThreads) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
                         const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
                         Xyzz29* __restrict__ buckets, Xyzz29* __restrict__ carry_own,
                         Xyzz29* __restrict__ carry_cont) {
+  __shared__ uint32_t sidx[kLdsIdx ? kChunk * kLdsStride : 1];
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nthreads) return;
   const uint32_t M = offsets[nkeys];
+  if (kLdsIdx) {  // every thread of the workgroup takes part before any exits
+    const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * kChunk;
+    for (uint32_t j = threadIdx.x; j < kMsmThreads * kChunk; j += kMsmThreads) {
+      const uint32_t thr = j / kChunk, slot = j - thr * kChunk;
+      sidx[slot * kLdsStride + thr] = wg0 + j < M ? sorted[wg0 + j] : 0u;
+    }
+    __syncthreads();
+  }
+  if (t >= nthreads) return;
   const uint32_t s = (uint32_t)t * chunk;
   if (s >= M) return;
   const uint32_t e = (s + chunk < M) ? s + chunk : M;
+  // index of stream position q (kLdsIdx: q - s is this thread's slot)
+  auto index_at = [&](uint32_t q) -> uint32_t {
+    return kLdsIdx ? sidx[(q - s) * kLdsStride + threadIdx.x] : sorted[q];
+  };
   uint32_t k = find_key(offsets, nkeys, s);
   uint32_t kstart = offsets[k], kend = offsets[k + 1];
   Xyzz29 acc;
@@ -606,14 +638,14 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
   // addition, so the gather's latency hides behind ~8k cycles of arithmetic, and the
   // entry after it is read one step earlier still, so that gather's address is in a
   // register when it is issued (no wait on the index load inside an iteration)
-  uint32_t ent = kDirect ? 0u : sorted[s];
+  uint32_t ent = kDirect ? 0u : index_at(s);
   G1Affine P = bases[kDirect ? s : ent & 0x7fffffffu];
-  uint32_t ent_n = (!kDirect && s + 1 < e) ? sorted[s + 1] : 0u;
+  uint32_t ent_n = (!kDirect && s + 1 < e) ? index_at(s + 1) : 0u;
   for (uint32_t pos = s; pos < e;) {
     G1Affine Pn;
     uint32_t ent_nn = 0;
     if (pos + 1 < e) Pn = bases[kDirect ? pos + 1 : ent_n & 0x7fffffffu];
-    if (!kDirect && pos + 2 < e) ent_nn = sorted[pos + 2];
+    if (!kDirect && pos + 2 < e) ent_nn = index_at(pos + 2);
     if (!P.is_inf()) {
       const F29 x = split29(P.x);
       F29 y = split29(P.y);
@@ -1334,6 +1366,10 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     if (rounds)
       hipLaunchKernelGGL((msm_accumulate29_kernel<3, true>), agrid, dim3(kMsmThreads), 0, st, chunk, acc_src,
                          sc.sorted.p, acc_off, p.nkeys, nthreads, sc.buckets29.p, sc.carry_own29.p,
+                         sc.carry_cont29.p);
+    else if (chunk == kChunk && acc_waves == 3 && lds_indices())
+      hipLaunchKernelGGL((msm_accumulate29_kernel<3, false, true>), agrid, dim3(kMsmThreads), 0, st, chunk, gather,
+                         sc.sorted.p, sc.offsets.p, p.nkeys, nthreads, sc.buckets29.p, sc.carry_own29.p,
                          sc.carry_cont29.p);
     else
       hipLaunchKernelGGL(acc_waves == 4 ? msm_accumulate29_kernel<4>

@@ -84,8 +84,11 @@ class Comm:
     def scatter_rows(self, rows, out):
         """rows: rank 0's [world, row_bytes] tensor (None elsewhere); out: this rank's row.
         Returns the collective's work handle (wait on it before rows are rewritten)."""
-        return self.dist.scatter(out, list(rows.unbind(0)) if rows is not None else None, src=0,
+        work = self.dist.scatter(out, list(rows.unbind(0)) if rows is not None else None, src=0,
                                  async_op=True)
+        if not self.device.startswith("cuda"):   # gloo: complete in submission order
+            work.wait()
+        return work
 
     def gather64(self, own: bytes) -> bytes | None:
         """Every rank's 64-byte partial to rank 0 (None on the other ranks)."""
@@ -139,6 +142,7 @@ class SplitRoot:
             if r and cnt:
                 self.scalar_source(src, lo, cnt, rows[r])
         self.comm.send_header(HDR_SCALARS, slot, count)
+        self.stopped = False        # a new serving session (serve() runs until the next STOP)
         out = self.comm.empty(self.row)
         self._rows[slot] = (rows, self.comm.scatter_rows(rows, out))
         self.sent += 1
@@ -151,16 +155,17 @@ class SplitRoot:
         ctx.set_msm_split(self.comm.world, self.own_points, self.send, self.gather)
 
     def stop(self):
-        if not self.stopped:
-            self.stopped = True
-            self.comm.send_header(HDR_STOP)
-            self.comm.sync()
+        """Ends the serving ranks' serve() loop (one STOP per serve() call they make)."""
+        self.stopped = True
+        self.comm.send_header(HDR_STOP)
+        self.comm.sync()
 
     def __enter__(self):
         return self
 
     def __exit__(self, *exc):
-        self.stop()
+        if not self.stopped:     # the servers are still in serve(): release them
+            self.stop()
         return False
 
 

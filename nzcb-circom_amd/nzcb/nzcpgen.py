@@ -105,18 +105,41 @@ def read_type(c: Circuit, b: Bytes, pos):
     return add(pos, 1), typ, v
 
 
+def skip_value_scalar(c: Circuit, b: Bytes, pos):
+    """SkipValueScalar (cbortpl.circom:266-297): ints and strings."""
+    nxt, typ, v = read_type(c, b, pos)
+    value, dnext = decode_uint(c, v, b, nxt)
+    is_int = c.is_equal(typ, MAJOR_INT)
+    is_string = c.is_equal(typ, MAJOR_STRING)
+    return c.lin(add(c.mul(is_int, dnext), c.mul(is_string, add(dnext, value))))
+
+
 def skip_value(c: Circuit, b: Bytes, pos, max_array_len: int):
-    """SkipValue (cbortpl.circom:301-366); MaxArrayLen = 0 for nzcp_live (no array loop,
-    QuinSelector(0) outputs 0)."""
-    if max_array_len:
-        raise NotImplementedError("SkipValue with arrays is not used by NZCPPubIdentity(1, 351, 0, 4, 2, 4)")
+    """SkipValue (cbortpl.circom:306-366): SkipValueScalar's ints and strings plus arrays of
+    up to MaxArrayLen scalars. Every element slot i runs a SkipValueScalar from the previous
+    slot's end, gated by shouldConsider[i] = isArray * (i < isArray * len); a
+    QuinSelector(MaxArrayLen) picks the end of element len - 1. nzcp_live has
+    MaxArrayLen = 0: no loop, and QuinSelector(0) outputs 0 (quinSelector.circom:19-41)."""
     nxt, typ, v = read_type(c, b, pos)
     value, dnext = decode_uint(c, v, b, nxt)
     is_int = c.is_equal(typ, MAJOR_INT)
     is_string = c.is_equal(typ, MAJOR_STRING)
     is_array = c.is_equal(typ, MAJOR_ARRAY)
-    c.mul(is_array, sub(value, 1))        # qs.index <== isArray.out * (decodeUint.value - 1)
-    return c.lin(add(c.mul(is_int, dnext), c.mul(is_string, add(dnext, value))))
+    arr_len = c.mul(is_array, value) if max_array_len else None     # lt[i].in[1] <== isArray.out * value
+    ends = c.alloc(max_array_len)                                   # nextPosArray[i] = qs.in[i]
+    prev = dnext
+    bits = log2(max_array_len) + 1
+    for i in range(max_array_len):
+        lt = c.less_than(i, arr_len, bits, ERR_RANGE)
+        consider = c.mul(is_array, lt)                              # shouldConsider[i]
+        end = skip_value_scalar(c, b, c.mul(prev, consider))
+        c.lin(end, dst=ends + i)
+        prev = w(ends + i)
+    index = c.mul(is_array, sub(value, 1))     # qs.index <== isArray.out * (decodeUint.value - 1)
+    terms = [c.mul(is_int, dnext), c.mul(is_string, add(dnext, value))]
+    if max_array_len:
+        terms.append(c.mul(is_array, get_v(c, Bytes(ends, max_array_len), index)))
+    return c.lin(add(*terms))
 
 
 def string_equals(c: Circuit, b: Bytes, const: list, pos, length):
@@ -184,10 +207,34 @@ def find_cwt_claims(c: Circuit, b: Bytes, map_len, pos, max_array_len: int, max_
     return vc_pos, exp
 
 
-def read_cred_subj(c: Circuit, b: Bytes, pos, max_buffer_len: int):
+def find_cred_subj(c: Circuit, b: Bytes, map_len, pos, max_array_len: int, max_map_len: int):
+    """FindCredSubj (nzcptpl.circom:152-226; not used by NZCPPubIdentity, tested by the
+    reference at test/nzcp.js:144-215). Returns needlePos, the position of the
+    "credentialSubject" key's value."""
+    needle_str = [99, 114, 101, 100, 101, 110, 116, 105, 97, 108, 83, 117, 98, 106, 101, 99, 116]
+    found = []
+    for k in range(max_map_len):
+        nxt, typ, v = read_type(c, b, pos)
+        value, dnext = decode_uint(c, v, b, nxt)
+        is_string = c.is_equal(typ, MAJOR_STRING)
+        next_pos = skip_value(c, b, c.mul(value, is_string, dnext), max_array_len)
+        needle = string_equals(c, b, needle_str, dnext, value)
+        within = c.less_than(k, map_len, 8, ERR_RANGE)
+        is_needle = c.mul(is_string, needle)
+        accepted = c.mul(is_needle, within)
+        found.append(c.mul(accepted, add(dnext, value)))
+        pos = next_pos
+    return c.lin(add(*found))
+
+
+def read_cred_subj(c: Circuit, b: Bytes, pos, max_buffer_len: int, map_len=None):
     """ReadCredSubj (nzcptpl.circom:232-360). Returns ((givenName base, len), (familyName ...),
-    (dob ...)); each name is max_buffer_len / 3 contiguous signals (zeros past them)."""
+    (dob ...)); each name is max_buffer_len / 3 contiguous signals (zeros past them).
+    map_len: the mapLen input, checked against 3 (``hardcore_assert``, :261); NZCPPubIdentity
+    passes the constant 3 (:552), which leaves no constraint."""
     n_map = 3
+    if map_len is not None:
+        c.check_zero(sub(map_len, n_map), ERR_RANGE)
     max_str = max_buffer_len // n_map
     given = [103, 105, 118, 101, 110, 78, 97, 109, 101]
     family = [102, 97, 109, 105, 108, 121, 78, 97, 109, 101]
@@ -389,3 +436,138 @@ def nzcp_pub_identity(is_live: int, max_tbs_bytes: int, max_array_len_vc: int, m
         c.lin(add(*[scale(x, 1 << i) if isinstance(x, dict) else 0 for i, x in enumerate(ins[j])]),
               dst=c.out_wires[j])
     return c
+
+
+# ------------------------------------------------------------ the reference's test mains
+# The wrapper circuits the reference's tests compile (/root/reference/circuits/*_test.circom,
+# *Test.circom), built from the same gadgets as NZCPPubIdentity: main's outputs first, then
+# its inputs in declaration order (circom's wire order), so witness[1..] is what the
+# reference's tests read (test/cbor.js, test/quinSelector.js, test/nzcp.js).
+WRAPPERS = {
+    "getType_test": ("GetType", ()),
+    "getX_test": ("GetX", ()),
+    "getV3_test": ("GetV", (3,)),
+    "getV4_test": ("GetV", (4,)),
+    "getV5_test": ("GetV", (5,)),
+    "decodeUint32_test": ("DecodeUint23", ()),
+    "decodeUint_test": ("DecodeUint", (4,)),
+    "readType_test": ("ReadType", (3,)),
+    "skipValueScalar_test": ("SkipValueScalar", (5,)),
+    "skipValue5_test": ("SkipValue", (5, 4)),
+    "skipValue6_test": ("SkipValue", (6, 4)),
+    "stringEquals_test": ("StringEquals", (5, (97, 98, 99, 100, 101), 5)),
+    "readStringLength_test": ("ReadStringLength", (5,)),
+    "readMapLength_test": ("ReadMapLength", (7,)),
+    "copyString_test": ("CopyString", (5, 4)),
+    "quinSelector0_test": ("QuinSelector", (0,)),
+    "quinSelector1_test": ("QuinSelector", (1,)),
+    "quinSelector2_test": ("QuinSelector", (2,)),
+    "quinSelector3_test": ("QuinSelector", (3,)),
+    "quinSelector4_test": ("QuinSelector", (4,)),
+    "quinSelector5_test": ("QuinSelector", (5,)),
+    "findCWTClaims_exampleTest": ("FindCWTClaims", (314, 0, 4)),
+    "findCWTClaims_liveTest": ("FindCWTClaims", (351, 0, 4)),
+    "findCredSubj_exampleTest": ("FindCredSubj", (314, 2, 4)),
+    "findCredSubj_liveTest": ("FindCredSubj", (351, 2, 4)),
+    "readCredSubj_exampleTest": ("ReadCredSubj", (314, 32)),
+    "readCredSubj_liveTest": ("ReadCredSubj", (351, 64)),
+    "constructNullifier_test": ("ConstructNullifier", (64,)),
+}
+
+
+def template_circuit(template: str, *params) -> Circuit:
+    """``component main = <template>(<params>)`` as an r1cs + witness program. Inputs are
+    private (circom's default for main), named as the template declares them."""
+    def io(outs, ins):
+        n_out = sum(k for _, k in outs)
+        c = Circuit(n_out, 0, sum(k for _, k in ins), input_names=list(ins))
+        wires, o = {}, c.in_base
+        for name, k in ins:
+            wires[name] = o
+            o += k
+        return c, wires
+
+    def put(c, values):
+        """main's outputs (LCs or ints), in declaration order"""
+        for i, x in enumerate(values):
+            c.lin(lc(x), dst=c.out_wires[i])
+
+    if template in ("GetType", "GetX", "DecodeUint23"):
+        c, wi = io([("out", 1)], [("v", 1)])
+        fn = {"GetType": get_type, "GetX": get_x, "DecodeUint23": decode_uint23}[template]
+        put(c, [fn(c, w(wi["v"]))])
+    elif template == "GetV":
+        (n,) = params
+        c, wi = io([("v", 1)], [("bytes", n), ("pos", 1)])
+        put(c, [get_v(c, Bytes(wi["bytes"], n), w(wi["pos"]))])
+    elif template == "DecodeUint":
+        (n,) = params
+        c, wi = io([("value", 1), ("nextPos", 1)], [("v", 1), ("bytes", n), ("pos", 1)])
+        put(c, list(decode_uint(c, w(wi["v"]), Bytes(wi["bytes"], n), w(wi["pos"]))))
+    elif template == "ReadType":
+        (n,) = params
+        c, wi = io([("nextPos", 1), ("type", 1), ("v", 1)], [("bytes", n), ("pos", 1)])
+        put(c, list(read_type(c, Bytes(wi["bytes"], n), w(wi["pos"]))))
+    elif template in ("SkipValueScalar", "SkipValue"):
+        n = params[0]
+        c, wi = io([("nextPos", 1)], [("bytes", n), ("pos", 1)])
+        b, pos = Bytes(wi["bytes"], n), w(wi["pos"])
+        put(c, [skip_value_scalar(c, b, pos) if template == "SkipValueScalar" else skip_value(c, b, pos, params[1])])
+    elif template == "StringEquals":
+        n, const, clen = params
+        c, wi = io([("out", 1)], [("bytes", n), ("pos", 1), ("len", 1)])
+        put(c, [string_equals(c, Bytes(wi["bytes"], n), list(const[:clen]), w(wi["pos"]), w(wi["len"]))])
+    elif template == "ReadStringLength":
+        (n,) = params
+        c, wi = io([("len", 1), ("nextPos", 1)], [("bytes", n), ("pos", 1)])
+        put(c, list(read_string_length(c, Bytes(wi["bytes"], n), w(wi["pos"]))))
+    elif template == "ReadMapLength":
+        (n,) = params
+        c, wi = io([("len", 1), ("nextPos", 1)], [("pos", 1), ("bytes", n)])
+        put(c, list(read_map_length(c, Bytes(wi["bytes"], n), w(wi["pos"]))))
+    elif template == "CopyString":
+        n, max_len = params
+        c, wi = io([("outbytes", max_len), ("nextPos", 1), ("len", 1)], [("bytes", n), ("pos", 1)])
+        out, nxt, ln = copy_string(c, Bytes(wi["bytes"], n), w(wi["pos"]), max_len)
+        put(c, out + [nxt, ln])
+    elif template == "QuinSelector":
+        (n,) = params
+        c, wi = io([("out", 1)], [("in", n), ("index", 1)])
+        if n:
+            put(c, [c.quin(n, wi["in"], n, w(wi["index"]), ERR_SELECT, ERR_SELECT)])
+        else:   # QuinSelector(0): no range check, out <== 0 (quinSelector.circom:21, 41)
+            put(c, [0])
+    elif template in ("FindCWTClaims", "FindCredSubj"):
+        n, max_arr, max_map = params
+        outs = [("vcPos", 1), ("exp", 1)] if template == "FindCWTClaims" else [("needlePos", 1)]
+        c, wi = io(outs, [("mapLen", 1), ("bytes", n), ("pos", 1)])
+        args = (c, Bytes(wi["bytes"], n), w(wi["mapLen"]), w(wi["pos"]), max_arr, max_map)
+        put(c, list(find_cwt_claims(*args)) if template == "FindCWTClaims" else [find_cred_subj(*args)])
+    elif template == "ReadCredSubj":
+        n, max_buf = params
+        outs = [("givenName", max_buf), ("givenNameLen", 1), ("familyName", max_buf), ("familyNameLen", 1),
+                ("dob", max_buf), ("dobLen", 1)]
+        c, wi = io(outs, [("mapLen", 1), ("bytes", n), ("pos", 1)])
+        names, max_str = read_cred_subj(c, Bytes(wi["bytes"], n), w(wi["pos"]), max_buf, map_len=w(wi["mapLen"]))
+        vals = []
+        for base, ln in names:
+            vals += [w(base + h) for h in range(max_str)] + [0] * (max_buf - max_str) + [ln]
+        put(c, vals)
+    elif template == "ConstructNullifier":
+        (max_buf,) = params
+        ins = [("givenName", max_buf), ("givenNameLen", 1), ("familyName", max_buf), ("familyNameLen", 1),
+               ("dob", max_buf), ("dobLen", 1)]
+        c, wi = io([("result", max_buf), ("resultLen", 1)], ins)
+        names = [(wi[k], w(wi[k + "Len"])) for k in ("givenName", "familyName", "dob")]
+        result = construct_nullifier(c, names, max_buf, max_buf)
+        total = add(*[ln for _, ln in names], 2)       # resultLen (nzcptpl.circom:432)
+        put(c, result + [total])
+    else:
+        raise ValueError(f"unknown template {template}")
+    return c
+
+
+def wrapper_circuit(name: str) -> Circuit:
+    """One of the reference's test mains by file stem (WRAPPERS), e.g. "skipValue5_test"."""
+    template, params = WRAPPERS[name]
+    return template_circuit(template, *params)

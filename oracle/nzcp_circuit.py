@@ -260,6 +260,25 @@ def find_cwt_claims(bs, pos: int, map_len: int, max_array_len: int, max_map_len:
     return vc_pos, exp
 
 
+CREDENTIAL_SUBJECT = b"credentialSubject"   # nzcptpl.circom:154-155
+
+
+def find_cred_subj(bs, pos: int, map_len: int, max_array_len: int, max_map_len: int) -> int:
+    """FindCredSubj (nzcptpl.circom:152-226) -> needlePos (not used by NZCPPubIdentity)."""
+    found = 0
+    p = pos
+    for k in range(max_map_len):
+        nt, t, v = read_type(bs, p)
+        value, np_ = decode_uint(bs, nt, v)
+        is_str = int(t == MAJOR_STRING)
+        p_next = skip_value(bs, np_ + value * is_str, max_array_len)
+        needle = string_equals(bs, np_, value, CREDENTIAL_SUBJECT)
+        within = less_than(8, k, map_len)
+        found += is_str * needle * within * (np_ + value)
+        p = p_next
+    return found
+
+
 def read_cred_subj(bs, pos: int, map_len: int = CREDENTIAL_SUBJECT_MAP_LEN, max_buffer_len: int = NULLIFIER_BYTES):
     """ReadCredSubj (nzcptpl.circom:232-380) -> (given, givenLen, family, familyLen, dob, dobLen)."""
     if map_len != CREDENTIAL_SUBJECT_MAP_LEN:

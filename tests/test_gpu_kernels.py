@@ -41,13 +41,13 @@ def test_ntt(engine, log_n, inverse):
     assert got == want
 
 
-@pytest.mark.parametrize("log_n", [21, 23])
+@pytest.mark.parametrize("log_n", [21, 23, 24])
 def test_ntt_full_size_properties(log_n):
-    """The prover's NTT sizes (n = 2^21, 4n = 2^23), size-independent properties on
-    pseudo-random Montgomery inputs: iNTT(NTT(x)) = x bit-exactly; NTT(x)[0] = sum x;
-    NTT(x)[n/2] = alternating sum; at 2^21 also NTT(x)[1] and NTT(x)[n-1] against Horner
-    at w and w^-1 (every twiddle contributes). All linear, so the checks run on the raw
-    Montgomery values."""
+    """The prover's NTT sizes (n = 2^21, 4n = 2^23) and the top of BASELINE configs[1]
+    (2^24), size-independent properties on pseudo-random Montgomery inputs:
+    iNTT(NTT(x)) = x bit-exactly; NTT(x)[0] = sum x; NTT(x)[n/2] = alternating sum;
+    NTT(x)[1] and NTT(x)[n-1] against Horner at w and w^-1 (every twiddle contributes;
+    at 2^21 and 2^24). All linear, so the checks run on the raw Montgomery values."""
     import nzcb
     n = 1 << log_n
     eng = nzcb.Engine(0, max_log_ntt=log_n, max_msm_points=0)
@@ -64,7 +64,7 @@ def test_ntt_full_size_properties(log_n):
     y = [int.from_bytes(fwd[i:i + 32], "little") for i in (0, 32, 32 * (n // 2), 32 * (n - 1))]
     assert y[0] == sum(x) % R_MOD
     assert y[2] == (sum(x[0::2]) - sum(x[1::2])) % R_MOD
-    if log_n <= 21:
+    if log_n != 23:
         w = bn.FR_W[log_n]
         assert y[1] == bn.eval_pol(x, w)
         assert y[3] == bn.eval_pol(x, bn.fr_inv(w))

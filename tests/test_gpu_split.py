@@ -48,12 +48,18 @@ class _LocalRanks:
     """The serving ranks of msmsplit, in-process: each range's partial is computed from a
     private copy of the scalars as soon as they are sent (as serve() does on its GPU)."""
 
-    def __init__(self, nzcb, msmsplit, zkey: bytes, n_points: int, world: int):
-        _, sec = binfmt.read_binfile(zkey, b"zkey")
-        (o, ln), = sec[14]
+    def __init__(self, nzcb, msmsplit, zkey, n_points: int, world: int):
+        """zkey: bytes, or a (pointer, length) library buffer (nzcb.plonk_setup_raw)."""
         self.nzcb = nzcb
-        self.ptau = nzcb.dev_alloc(ln)
-        nzcb.h2d(self.ptau, zkey[o:o + ln])
+        if isinstance(zkey, tuple):
+            addr, ln = msmsplit.zkey_section(zkey[0], zkey[1], 14)   # PTau [tau^i]G1
+            self.ptau = nzcb.dev_alloc(ln)
+            nzcb.memcpy_h2d_ptr(self.ptau, addr, ln)
+        else:
+            _, sec = binfmt.read_binfile(zkey, b"zkey")
+            (o, ln), = sec[14]
+            self.ptau = nzcb.dev_alloc(ln)
+            nzcb.h2d(self.ptau, zkey[o:o + ln])
         self.ranges = msmsplit.point_ranges(n_points, world)
         self.backends = [msmsplit.GpuRange(self.ptau, lo, hi, 0) for lo, hi in self.ranges[1:]]
         self.scal = nzcb.dev_alloc(32 * n_points)

@@ -121,9 +121,24 @@ def test_nzcp_live_full_prove_real_circuit():
     sol = nzcb.vk_to_solidity(ctx.vk, "Verifier")
     words = bytes.fromhex(nzcb.proof_to_calldata(res[0][0], b"").split(",")[0][2:])
     assert yul.run_verify_proof(sol, words, _ints(res[0][1]))[0]
+    # configs[4] on one GPU: every split commitment divided into 8 PTau ranges, ranks 1..7
+    # served in-process from resident range tables (what msmsplit.serve does per GPU), the
+    # partials folded in rank order; the proof must not change by a bit
+    from nzcb import msmsplit
+    from tests.test_gpu_split import _LocalRanks
+    ranks = _LocalRanks(nzcb, msmsplit, zkey, ctx.domain_size + 6, 8)
+    try:
+        ctx.set_lanes(1)
+        ctx.set_msm_split(8, ranks.ranges[0][1], ranks.send, ranks.gather)
+        split_proof, split_pub = ctx.prove_witness_raw(wit0, bl)
+        ctx.set_msm_split(1, 0, None, None)
+        assert ranks.calls == 6 and not ranks.pending     # Z, T1..T3, Wxi, Wxiw split; A, B, C local
+    finally:
+        ranks.close()
     ctx.close()
     try:
         ref_proof, ref_pub, _ = cbind.prove(zkey, nzcplive.wtns_file(wit0), bl, npub=3)
     finally:
         nzcb.free_ptr(zkey[0])
     assert res[0][0] == ref_proof and res[0][1] == ref_pub[:96]
+    assert split_proof == ref_proof and split_pub == res[0][1]

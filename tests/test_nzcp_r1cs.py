@@ -162,6 +162,53 @@ def test_live_failing_passes(live, kind):
         tbs[30] = 0x61          # claims at byte 30 are not a map
         case = C.case("map", nz.LIVE_PARAMS, bytes(tbs))
     exp = C.oracle_record(case)
-    _, fail = wvm.evaluate(prog, _case_inputs(case))
+    wit, fail = wvm.evaluate(prog, _case_inputs(case))
     assert exp["status"] != 0 and fail is not None
     assert fail[1] == exp["status"]
+    # soundness: the witness carried past the failure is not a satisfying
+    # assignment; the rejection is a constraint of the r1cs, not only a calculator check
+    assert _unsat(c, wit) != []
+
+
+def test_live_every_sampled_signal_is_constrained(live):
+    """Soundness probe on NZCPPubIdentity(1, 351, 0, 4, 2, 4): for a seeded sample of 4000
+    computed signals of a valid pass's witness (SHA-256/512 rounds, CBOR parsing,
+    QuinSelectors, nullifier bytes alike), +1 on the signal breaks a constraint that
+    mentions it. IsZero / QuinSelector inverses of zero inputs are circomlib's free
+    signals and are skipped."""
+    c, prog = live
+    case = C.case("live", nz.LIVE_PARAMS, C.live_tbs(), data=bytes(range(1, 21)))
+    wit, fail = wvm.evaluate(prog, _case_inputs(case))
+    assert fail is None
+    free = set()
+    for typ, err, n, dst, a, b, cc, extra in c.ops:
+        if typ == circuit.OP_INV and wit[dst] == 0:
+            free.add(dst)
+        elif typ == circuit.OP_QUIN:
+            free.update(i for i in range(dst + n, dst + 2 * n) if wit[i] == 0)
+    first = c.in_base + c.n_pub_in + c.n_prv_in
+    cand = [k for k in list(range(1, c.in_base)) + list(range(first, c.n_wires)) if k not in free]
+    sample = set(random.Random(0x50554E44).sample(cand, 4000))
+    touching = {}
+    for k, cons in enumerate(c.constraints):
+        for part in cons:
+            for wire in part:
+                if wire in sample:
+                    touching.setdefault(wire, []).append(k)
+    loose = []
+    for k in sorted(sample):
+        old = wit[k]
+        wit[k] = (old + 1) % R
+        ok = False
+        for j in touching.get(k, ()):
+            A, B, Cc = c.constraints[j]
+            a = sum(v * wit[i] for i, v in A.items()) % R
+            b = sum(v * wit[i] for i, v in B.items()) % R
+            cv = sum(v * wit[i] for i, v in Cc.items()) % R
+            if (a * b - cv) % R:
+                ok = True
+                break
+        wit[k] = old
+        if not ok:
+            loose.append(k)
+    assert loose == []
