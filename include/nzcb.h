@@ -276,6 +276,18 @@ int nzcb_wprog_run_dev(nzcb_wprog* prog, const void* dev_inputs, int count, void
 /* Host buffers: witness_out receives count x n_wires x 32 bytes. */
 int nzcb_wprog_run(nzcb_wprog* prog, const uint8_t* inputs, int count, uint8_t* witness_out,
                    int32_t* status_out, nzcb_err* err);
+/* Re-index a witness program to another wire order by signal name (a zkey
+ * built from circom's own r1cs, /root/reference/Makefile:12-15,59-62, expects circom's
+ * wire order). own_sym: the program's .sym text (nzcb/circuit.py Circuit.write_sym);
+ * target_sym: the .sym of the target order (e.g. circom's nzcp_live.sym; lines
+ * "label,wire,component,name", wire -1 = optimized out). Target wire t gets the program
+ * signal of the same name; wire 0 stays the constant 1. The result (malloc'ed, release
+ * with nzcb_free) runs like any program and writes witnesses of the target's wire count.
+ * Fails with NZCB_ERR_FORMAT, *unmatched = the count, when a target signal has no
+ * counterpart. Parity of the names with circom's own .sym is unpinned (nzcb/nzcpgen.py). */
+int nzcb_wprog_remap(const uint8_t* prog, size_t prog_len, const char* own_sym, size_t own_len,
+                     const char* target_sym, size_t target_len, uint8_t** prog_out, size_t* prog_out_len,
+                     uint32_t* unmatched, nzcb_err* err);
 
 /* ---- Setup ------------------------------------------ */
 /* snarkjs `plonk setup <r1cs> <ptau> <zkey>` (snarkjs 0.4.12 plonk_setup.js, run at

@@ -17,6 +17,10 @@ struct NttTables {
   // The same twiddles as split29 of their Montgomery-261 form (w * 2^261 mod r), the
   // operand of mul_fr29 (f29.h) in the butterflies
   DevBuf<F29> fwd29, inv29;
+  // Inter-pass scratch of the 9x29 pipeline (ntt29_pass_kernel): limb-major [9][2^max_log]
+  // u32, the transform's values between its HBM passes (one transform at a time: every
+  // caller runs its NTTs on one stream)
+  DevBuf<uint32_t> scratch29;
   void init(int max_log, hipStream_t st);
 };
 

@@ -73,6 +73,7 @@ __global__ void __launch_bounds__(256) ntt_tw29_kernel(F29* __restrict__ out, co
 
 void NttTables::init(int L, hipStream_t st) {
   max_log = L;
+  if (L > 8) scratch29.alloc((size_t)9 << L);  // the 9x29 pipeline's inter-pass values
   const size_t half = L >= 1 ? (size_t(1) << (L - 1)) : 1;
   const size_t total = (size_t(1) << L) - 1;
   fwd.alloc(total ? total : 1);
@@ -240,6 +241,210 @@ ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s,
   }
 }
 
+// ---- 9x29-bit pipeline (default) ----------------------------------------------------
+// The transform's values stay in the redundant radix 2^29 of f29.h from the first pass's
+// load to the last pass's store: LDS tiles, registers and the inter-pass HBM scratch hold
+// 9 x 29-bit limbs, so a butterfly is one mul29 plus limb adds, with none of the 8x32
+// split / join / modular add-sub chains of ntt_pass_kernel.
+// Bounds (r = the BN254 scalar modulus):
+//  * every twiddle product is mul29<Fr29>(x, w) with w < r canonical: for x < 2^261 the
+//    result is < x r / 2^261 + r < 1.4 r, limbs normalized; x may have limbs < 2^31.6
+//    (column sum 9 (2^60.6 + 2^58) + 2^35 < 2^64, f29.h);
+//  * a butterfly y0 = x0 + t, y1 = x0 + 2r - t (Fr29::K2 borrowed: every limb >= t's) adds
+//    at most 2r to the value bound of its inputs, so after the L <= 24 stages of a
+//    transform from inputs < 1.4 r the values are < 50 r < 2^260 (every product input
+//    < 2^261 holds throughout, no value reduction is ever needed);
+//  * limbs: a radix-4 group's outputs are < 2^31.4 before normalisation; they are
+//    normalized (norm29) once per group (and after the odd radix-2 stage), so every
+//    group starts from limbs < 2^29;
+//  * the last pass maps v < 50 r to canonical Fr: q = floor(v_8 / (r_8 + 1)) <= v / r
+//    (v_8 = the top limb, bits 232..), v - q r < r + (q + 1) 2^232 < 2r, then one
+//    conditional subtraction (join_fr29); with an output factor the product < 1.4 r is
+//    joined directly.
+static constexpr int kTile29 = 2048;   // elements per tile: 9 x 8 KiB of limbs = 72 KiB LDS
+
+__device__ __forceinline__ F29 tile_ld(const uint32_t* sl, int e) {
+  F29 x;
+#pragma unroll
+  for (int l = 0; l < 9; l++) x.v[l] = sl[l * kTile29 + e];
+  return x;
+}
+__device__ __forceinline__ void tile_st(uint32_t* sl, int e, const F29& x) {
+#pragma unroll
+  for (int l = 0; l < 9; l++) sl[l * kTile29 + e] = x.v[l];
+}
+__device__ __forceinline__ F29 add_nn29(const F29& a, const F29& b) {
+  F29 r;
+#pragma unroll
+  for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + b.v[l];
+  return r;
+}
+__device__ __forceinline__ F29 sub2r_nn29(const F29& a, const F29& b) {  // a + 2r - b, b < 2r normalized
+  F29 r;
+#pragma unroll
+  for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + Fr29::K2[l] - b.v[l];
+  return r;
+}
+__device__ __forceinline__ Fr canon_fr29(const F29& x) {  // normalized x < 64 r -> canonical Fr
+  const uint32_t q = x.v[8] / (Fr29::P[8] + 1u);
+  F29 y;
+  int64_t carry = 0;
+#pragma unroll
+  for (int l = 0; l < 9; l++) {
+    const int64_t t = (int64_t)x.v[l] + carry - (int64_t)((uint64_t)q * Fr29::P[l]);
+    y.v[l] = l < 8 ? ((uint32_t)t & Fr29::MASK) : (uint32_t)t;
+    carry = t >> 29;
+  }
+  return join_fr29(y);
+}
+
+// One pass of stages [s, s+q) on tiles of (2^q rows) x (2^logC columns). IN29: values from
+// the F29 scratch (else the Fr input, first pass only); OUT29: values to the F29 scratch
+// (else canonical Fr to `out`, last pass only).
+template <bool IN29, bool OUT29>
+__global__ void __launch_bounds__(kNttThreads)
+ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29* __restrict__ tw, int L, int s,
+                  int q, int logC, F29 scale29, int do_scale, NttIo io, int sparse4) {
+  __shared__ uint32_t sl[9 * kTile29];
+  const int C = 1 << logC;
+  const int rows = 1 << q;
+  const int n_el = rows << logC;
+  const int tid = threadIdx.x;
+  const size_t t = blockIdx.x;
+  size_t base = 0, c0 = 0, lo0 = 0;
+  if (!IN29) {  // first pass: bit-reversed gather of the Fr input, prologue factors
+    c0 = t << logC;
+    for (int e = tid; e < n_el; e += kNttThreads) {
+      const int j = e >> logC, c = e & (C - 1);
+      const size_t src = ((size_t)bit_rev((uint32_t)j, q) << (L - q)) + c0 + c;
+      F29 x;
+#pragma unroll
+      for (int l = 0; l < 9; l++) x.v[l] = 0;
+      if (src < io.in_len) {
+        x = split29(in[src]);
+        if (io.in_f) x = mul29<Fr29>(x, io.in_f[src]);
+        if (do_scale) x = mul29<Fr29>(x, scale29);
+      }
+      tile_st(sl, e, x);
+    }
+  } else {
+    const size_t groups_lo = ((size_t)1 << s) >> logC;
+    const size_t hi = t / groups_lo;
+    lo0 = (t % groups_lo) << logC;
+    base = (hi << (s + q)) + lo0;
+    for (int e = tid; e < n_el; e += kNttThreads) {
+      const int j = e >> logC, c = e & (C - 1);
+      tile_st(sl, e, in29[base + ((size_t)j << s) + c]);
+    }
+  }
+  __syncthreads();
+  const int nbf = n_el >> 1;
+  const bool first = !IN29;
+  int st = 0;
+  if (sparse4 && blockIdx.x != 0) {
+    // zero-padded input past tile 0: of every four bit-reversed rows 4m..4m+3 only row 4m
+    // is nonzero, and stages 0-1 map (x, 0, 0, 0) to (x, x, x, x): the first radix-4 step
+    // is a copy
+    for (int e = tid; e < n_el; e += kNttThreads) {
+      const int j = e >> logC;
+      if (j & 3) tile_st(sl, e, tile_ld(sl, ((j & ~3) << logC) + (e & (C - 1))));
+    }
+    __syncthreads();
+    st = 2;
+  } else if (q & 1) {  // odd stage count: one radix-2 stage first
+    const int g = s;
+    const F29* __restrict__ twg = tw + (((size_t)1 << g) - 1);
+#pragma unroll
+    for (int u = 0; u < kBfPerThread; u++) {
+      const int b = tid + u * kNttThreads;
+      if (b >= nbf) continue;
+      const int c = b & (C - 1);
+      const int j0 = b >> logC;
+      const int i0 = ((2 * j0) << logC) + c, i1 = ((2 * j0 + 1) << logC) + c;
+      const size_t k = first ? 0 : (lo0 + c);
+      const F29 x0 = tile_ld(sl, i0);
+      const F29 x1 = tile_ld(sl, i1);
+      const F29 tt = g ? mul29<Fr29>(x1, twg[k]) : x1;
+      F29 y0 = add_nn29(x0, tt), y1 = sub2r_nn29(x0, tt);
+      norm29(y0);
+      norm29(y1);
+      tile_st(sl, i0, y0);
+      tile_st(sl, i1, y1);
+    }
+    __syncthreads();
+    st = 1;
+  }
+  const int ngroups = n_el >> 2;
+#pragma unroll 1
+  for (; st < q; st += 2) {
+    const int h = 1 << st;
+    const int g = s + st;
+    const F29* __restrict__ twa = tw + (((size_t)1 << g) - 1);
+    const F29* __restrict__ twb = tw + (((size_t)1 << (g + 1)) - 1);
+    const int b = tid;
+    if (b < ngroups) {
+      const int c = b & (C - 1);
+      const int pr = b >> logC;
+      const int low = pr & (h - 1);
+      const int j = ((pr >> st) << (st + 2)) | low;
+      const size_t ka = first ? (size_t)low : (((size_t)low << s) + lo0 + c);
+      const size_t kc = first ? (size_t)(low + h) : (((size_t)(low + h) << s) + lo0 + c);
+      const int i0 = (j << logC) + c, i1 = ((j + h) << logC) + c, i2 = ((j + 2 * h) << logC) + c,
+                i3 = ((j + 3 * h) << logC) + c;
+      F29 t1 = tile_ld(sl, i1), t3 = tile_ld(sl, i3);
+      if (g) {
+        const F29 wa = twa[ka];
+        t1 = mul29<Fr29>(t1, wa);
+        t3 = mul29<Fr29>(t3, wa);
+      }
+      const F29 x0 = tile_ld(sl, i0), x2 = tile_ld(sl, i2);
+      const F29 y0 = add_nn29(x0, t1), y1 = sub2r_nn29(x0, t1);
+      const F29 y2 = add_nn29(x2, t3), y3 = sub2r_nn29(x2, t3);
+      const F29 u2 = mul29<Fr29>(y2, twb[ka]);
+      const F29 u3 = mul29<Fr29>(y3, twb[kc]);
+      F29 z0 = add_nn29(y0, u2), z2 = sub2r_nn29(y0, u2), z1 = add_nn29(y1, u3), z3 = sub2r_nn29(y1, u3);
+      norm29(z0);
+      norm29(z1);
+      norm29(z2);
+      norm29(z3);
+      tile_st(sl, i0, z0);
+      tile_st(sl, i1, z1);
+      tile_st(sl, i2, z2);
+      tile_st(sl, i3, z3);
+    }
+    __syncthreads();
+  }
+  auto store = [&](size_t dst, const F29& x) {
+    if (OUT29) {
+      out29[dst] = x;
+    } else {
+      const Fr v = io.out_f ? join_fr29(mul29<Fr29>(x, io.out_f[dst])) : canon_fr29(x);
+      if (io.out_flags && dst >= io.out_limit && !v.is_zero()) atomicOr(io.out_flags, 1u);
+      out[dst] = v;
+    }
+  };
+  if (first) {
+    for (int e = tid; e < n_el; e += kNttThreads) {
+      const int j = e & (rows - 1), c = e >> q;
+      const size_t dst = ((size_t)bit_rev((uint32_t)(c0 + c), L - q) << q) + j;
+      store(dst, tile_ld(sl, (j << logC) + c));
+    }
+  } else {
+    for (int e = tid; e < n_el; e += kNttThreads) {
+      const int j = e >> logC, c = e & (C - 1);
+      store(base + ((size_t)j << s) + c, tile_ld(sl, e));
+    }
+  }
+}
+
+static bool ntt29_enabled() {  // NZCB_NTT29=0: the 8x32 pipeline (ntt_pass_kernel) for A/B runs
+  static const bool on = [] {
+    const char* e = std::getenv("NZCB_NTT29");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hipStream_t st, const Fr* scale,
          const NttIo* iop) {
   const NttIo io = iop ? *iop : NttIo();
@@ -279,6 +484,34 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   }();
   const int sparse4 = sparse_ok && L >= 2 && q1 >= 2 && !(q1 & 1) &&
                       io.in_len <= ((size_t)1 << (L - 2)) + ((size_t)1 << logC1);
+  if (ntt29_enabled() && (q1 == L || t.scratch29.n >= ((size_t)9 << L))) {
+    F29* scr = (F29*)t.scratch29.p;
+    if (q1 == L) {
+      hipLaunchKernelGGL((ntt29_pass_kernel<false, false>), dim3((unsigned)tiles), dim3(kNttThreads), 0, st, in,
+                         (const F29*)nullptr, out, (F29*)nullptr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4);
+      NZ_HIP(hipGetLastError());
+      return;
+    }
+    hipLaunchKernelGGL((ntt29_pass_kernel<false, true>), dim3((unsigned)tiles), dim3(kNttThreads), 0, st, in,
+                       (const F29*)nullptr, (Fr*)nullptr, scr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4);
+    NZ_HIP(hipGetLastError());
+    int s = q1;
+    while (s < L) {
+      const int q = (L - s) < 8 ? (L - s) : 8;
+      int logC = 0;
+      while (logC + 1 <= s && (1 << (q + logC + 1)) <= kTile29) logC++;
+      const size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
+      if (s + q == L)
+        hipLaunchKernelGGL((ntt29_pass_kernel<true, false>), dim3((unsigned)ntiles), dim3(kNttThreads), 0, st,
+                           (const Fr*)nullptr, (const F29*)scr, out, (F29*)nullptr, tw, L, s, q, logC, sc29, 0, io, 0);
+      else
+        hipLaunchKernelGGL((ntt29_pass_kernel<true, true>), dim3((unsigned)ntiles), dim3(kNttThreads), 0, st,
+                           (const Fr*)nullptr, (const F29*)scr, (Fr*)nullptr, scr, tw, L, s, q, logC, sc29, 0, io, 0);
+      NZ_HIP(hipGetLastError());
+      s += q;
+    }
+    return;
+  }
   hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)tiles), dim3(kNttThreads), lds, st, in, out, tw, L, 0, q1, logC1,
                      1, sc29, do_scale, q1 == L ? 1 : 0, io, sparse4);
   NZ_HIP(hipGetLastError());

@@ -10,6 +10,9 @@
 //   ops[n_ops] 8 x u32 {type | err << 8 | n << 16, dst, a_off, a_n, b_off, b_n, c_off, c_n}
 //   level_start[n_levels + 1] u32 | level_macro_start[n_levels] u32 |
 //   u32 n_names, then per main input: u32 len, name bytes, u32 size (declaration order)
+//   [optional, nzcb_wprog_remap] "wmap" u32 T, T x u32: output wire t = program wire
+//   map[t], so the witness comes out in another wire order (e.g. circom's, by signal
+//   name from two .sym files); the program runs into scratch and a gather reorders
 // Ops are sorted by dependency level; inside a level the scalar ops (LIN MUL INV BITS
 // CHECK) come first and are spread over the workgroup's threads, the macro ops (QUIN,
 // SHA256, SHA512) follow and each runs on the whole workgroup. One barrier per level.
@@ -28,6 +31,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -727,7 +733,26 @@ struct Program {
   DevBuf<Level> levels;
   DevBuf<uint32_t> status;
   size_t status_cap = 0;
+  // wire map of a remapped program (nzcb_wprog_remap): output wire t = program wire
+  // wmap[t]; the program runs into `scratch` and a gather writes the target order
+  uint32_t n_target = 0;
+  DevBuf<uint32_t> wmap;
+  DevBuf<Fr> scratch;
+  size_t scratch_cap = 0;
+  uint32_t out_wires() const { return n_target ? n_target : n_wires; }
 };
+
+// witness i, target wire t = scratch witness i, program wire map[t]
+__global__ void __launch_bounds__(256)
+wvm_gather_kernel(const Fr* __restrict__ src, size_t src_stride, const uint32_t* __restrict__ map, uint32_t T,
+                  Fr* __restrict__ dst, size_t dst_stride) {
+  const size_t i = blockIdx.y;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < T; t += (size_t)gridDim.x * blockDim.x)
+    dst[i * dst_stride + t] = src[i * src_stride + map[t]];
+}
+
+// End offset of the input-names section (the program proper); throws on a malformed one
+static size_t names_end(const uint8_t* data, size_t len, size_t need);
 
 static uint32_t rd32(const uint8_t* p) {
   uint32_t x;
@@ -757,21 +782,21 @@ Program* load(const uint8_t* data, size_t len, int device) {
     const size_t need = 40 + (size_t)nc * 32 + (size_t)nt * 8 + (size_t)no * 32 + ((size_t)P->n_levels * 2 + 1) * 4;
     if (len < need + 4) throw Error(NZCB_ERR_FORMAT, "witness program: truncated");
     {  // input names (host-side mapping of input objects; checked here, not used on the GPU)
-      size_t o = need;
-      const uint32_t nn = rd32(data + o);
-      o += 4;
-      uint64_t total = 0;
-      for (uint32_t i = 0; i < nn; i++) {
-        if (o + 4 > len) throw Error(NZCB_ERR_FORMAT, "witness program: truncated input names");
-        const uint32_t ln = rd32(data + o);
-        o += 4 + (size_t)ln;
-        if (o + 4 > len) throw Error(NZCB_ERR_FORMAT, "witness program: truncated input names");
-        total += rd32(data + o);
-        o += 4;
+      size_t o = names_end(data, len, need);
+      if (o != len) {  // optional wire map (nzcb_wprog_remap): "wmap" u32 T, T x u32
+        if (o + 8 > len || std::memcmp(data + o, "wmap", 4) != 0)
+          throw Error(NZCB_ERR_FORMAT, "witness program: oversized");
+        const uint32_t T = rd32(data + o + 4);
+        if (T == 0 || o + 8 + (size_t)T * 4 != len) throw Error(NZCB_ERR_FORMAT, "witness program: bad wire map");
+        std::vector<uint32_t> m(T);
+        std::memcpy(m.data(), data + o + 8, (size_t)T * 4);
+        if (m[0] != 0) throw Error(NZCB_ERR_FORMAT, "witness program: wire map must keep wire 0");
+        for (uint32_t t = 0; t < T; t++)
+          if (m[t] >= P->n_wires) throw Error(NZCB_ERR_FORMAT, "witness program: wire map out of range");
+        NZ_HIP(hipSetDevice(device));
+        upload(P->wmap, m.data(), T);
+        P->n_target = T;
       }
-      if (o != len) throw Error(NZCB_ERR_FORMAT, "witness program: oversized");
-      if (nn && total != (uint64_t)rd32(data + 16) + rd32(data + 20))
-        throw Error(NZCB_ERR_FORMAT, "witness program: input names do not cover the inputs");
     }
     const uint8_t* p = data + 40;
     // coefficients c -> c R^2 (Montgomery of Montgomery), checked < r
@@ -889,13 +914,42 @@ Program* load(const uint8_t* data, size_t len, int device) {
   return P;
 }
 
+static size_t names_end(const uint8_t* data, size_t len, size_t need) {
+  size_t o = need;
+  const uint32_t nn = rd32(data + o);
+  o += 4;
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < nn; i++) {
+    if (o + 4 > len) throw Error(NZCB_ERR_FORMAT, "witness program: truncated input names");
+    const uint32_t ln = rd32(data + o);
+    o += 4 + (size_t)ln;
+    if (o + 4 > len) throw Error(NZCB_ERR_FORMAT, "witness program: truncated input names");
+    total += rd32(data + o);
+    o += 4;
+  }
+  if (o > len) throw Error(NZCB_ERR_FORMAT, "witness program: truncated input names");
+  if (nn && total != (uint64_t)rd32(data + 16) + rd32(data + 20))
+    throw Error(NZCB_ERR_FORMAT, "witness program: input names do not cover the inputs");
+  return o;
+}
+
 void run(Program* P, const void* dev_inputs, int count, void* dev_witness, size_t stride_bytes, int32_t* status_out,
          hipStream_t s) {
   if (count <= 0) return;
   if (!dev_inputs || !dev_witness || !status_out) throw Error(NZCB_ERR_ARG, "witness program: null buffer");
-  if (stride_bytes % 32 || stride_bytes < (size_t)P->n_wires * 32)
+  if (stride_bytes % 32 || stride_bytes < (size_t)P->out_wires() * 32)
     throw Error(NZCB_ERR_ARG, "witness program: witness stride below n_wires x 32 B");
   NZ_HIP(hipSetDevice(P->device));
+  Fr* run_dst = (Fr*)dev_witness;
+  size_t run_stride = stride_bytes / 32;
+  if (P->n_target) {  // remapped: the program's own wire order into scratch, then the gather
+    if ((size_t)count > P->scratch_cap) {
+      P->scratch.alloc((size_t)count * P->n_wires);
+      P->scratch_cap = (size_t)count;
+    }
+    run_dst = P->scratch.p;
+    run_stride = P->n_wires;
+  }
   if ((size_t)count > P->status_cap) {
     P->status.alloc((size_t)count);
     P->status_cap = (size_t)count;
@@ -925,9 +979,15 @@ void run(Program* P, const void* dev_inputs, int count, void* dev_witness, size_
     return t == 256 || t == 1024 ? t : 512;
   }();
   auto kern = nt == 256 ? wvm_kernel<256> : (nt == 1024 ? wvm_kernel<1024> : wvm_kernel<512>);
-  hipLaunchKernelGGL(kern, dim3((unsigned)count), dim3(nt), 0, s, g, (const Fr*)dev_inputs, (Fr*)dev_witness,
-                     stride_bytes / 32, P->status.p, lclk.p);
+  hipLaunchKernelGGL(kern, dim3((unsigned)count), dim3(nt), 0, s, g, (const Fr*)dev_inputs, run_dst, run_stride,
+                     P->status.p, lclk.p);
   NZ_HIP(hipGetLastError());
+  if (P->n_target) {
+    const unsigned gx = (unsigned)std::min<size_t>(((size_t)P->n_target + 255) / 256, 1024);
+    hipLaunchKernelGGL(wvm_gather_kernel, dim3(gx, (unsigned)count), dim3(256), 0, s, (const Fr*)run_dst,
+                       run_stride, P->wmap.p, P->n_target, (Fr*)dev_witness, stride_bytes / 32);
+    NZ_HIP(hipGetLastError());
+  }
   std::vector<uint32_t> st((size_t)count);
   NZ_HIP(hipMemcpyAsync(st.data(), P->status.p, (size_t)count * 4, hipMemcpyDeviceToHost, s));
   NZ_HIP(hipStreamSynchronize(s));
@@ -982,7 +1042,7 @@ void nzcb_wprog_destroy(nzcb_wprog* h) {
 
 int nzcb_wprog_info(const nzcb_wprog* h, uint32_t info[5]) {
   if (!h || !info) return NZCB_ERR_ARG;
-  info[0] = h->p->n_wires;
+  info[0] = h->p->out_wires();
   info[1] = h->p->n_out;
   info[2] = h->p->n_pub;
   info[3] = h->p->n_prv;
@@ -1013,11 +1073,102 @@ int nzcb_wprog_run(nzcb_wprog* h, const uint8_t* inputs, int count, uint8_t* wit
     if (!inputs || !witness_out || !status_out) throw Error(NZCB_ERR_ARG, "witness program: null buffer");
     NZ_HIP(hipSetDevice(h->p->device));
     const size_t nin = (size_t)(h->p->n_pub + h->p->n_prv) * 32 * count;
-    const size_t nw = (size_t)h->p->n_wires * 32;
+    const size_t nw = (size_t)h->p->out_wires() * 32;
     DevBuf<uint8_t> din(nin ? nin : 1), dw(nw * count);
     if (nin) NZ_HIP(hipMemcpy(din.p, inputs, nin, hipMemcpyHostToDevice));
     wvm::run(h->p, din.p, count, dw.p, nw, status_out, nullptr);
     NZ_HIP(hipMemcpy(witness_out, dw.p, nw * count, hipMemcpyDeviceToHost));
+    return NZCB_OK;
+  } catch (const Error& e) {
+    set_err(err, e.code, e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+    return NZCB_ERR_INTERNAL;
+  }
+}
+
+// circom .sym text: "label,wire,component,name" per line; wire < 0 = optimized out
+static void parse_sym(const char* text, size_t len,
+                      const std::function<void(int64_t wire, const std::string& name)>& f) {
+  size_t o = 0;
+  while (o < len) {
+    size_t e = o;
+    while (e < len && text[e] != '\n') e++;
+    std::string line(text + o, e - o);
+    o = e + 1;
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    if (line.empty()) continue;
+    const size_t c1 = line.find(','), c2 = c1 == std::string::npos ? c1 : line.find(',', c1 + 1),
+                 c3 = c2 == std::string::npos ? c2 : line.find(',', c2 + 1);
+    if (c3 == std::string::npos) throw Error(NZCB_ERR_FORMAT, "sym: malformed line: " + line.substr(0, 80));
+    char* end = nullptr;
+    const std::string ws = line.substr(c1 + 1, c2 - c1 - 1);
+    const long long wire = std::strtoll(ws.c_str(), &end, 10);
+    if (!end || *end) throw Error(NZCB_ERR_FORMAT, "sym: bad wire index: " + line.substr(0, 80));
+    f(wire, line.substr(c3 + 1));
+  }
+}
+
+int nzcb_wprog_remap(const uint8_t* prog, size_t len, const char* own_sym, size_t own_len, const char* target_sym,
+                     size_t target_len, uint8_t** out, size_t* out_len, uint32_t* unmatched, nzcb_err* err) {
+  try {
+    if (!prog || !own_sym || !target_sym || !out || !out_len) throw Error(NZCB_ERR_ARG, "null argument");
+    if (unmatched) *unmatched = 0;
+    if (len < 40 || std::memcmp(prog, "nzwp", 4) != 0) throw Error(NZCB_ERR_FORMAT, "witness program: bad magic");
+    const uint32_t n_wires = wvm::rd32(prog + 8), nc = wvm::rd32(prog + 24), nt = wvm::rd32(prog + 28),
+                   no = wvm::rd32(prog + 32), nl = wvm::rd32(prog + 36);
+    const size_t need = 40 + (size_t)nc * 32 + (size_t)nt * 8 + (size_t)no * 32 + ((size_t)nl * 2 + 1) * 4;
+    if (len < need + 4) throw Error(NZCB_ERR_FORMAT, "witness program: truncated");
+    if (wvm::names_end(prog, len, need) != len)
+      throw Error(NZCB_ERR_FORMAT, "witness program: already remapped (or oversized)");
+    std::unordered_map<std::string, uint32_t> own;
+    own.reserve(n_wires);
+    parse_sym(own_sym, own_len, [&](int64_t wire, const std::string& name) {
+      if (wire >= 0) {
+        if (wire >= n_wires) throw Error(NZCB_ERR_FORMAT, "sym: wire beyond the program's: " + name);
+        own.emplace(name, (uint32_t)wire);
+      }
+    });
+    std::vector<std::vector<std::string>> names;  // target wire -> its names
+    parse_sym(target_sym, target_len, [&](int64_t wire, const std::string& name) {
+      if (wire < 0) return;
+      if (wire >= (1ll << 31)) throw Error(NZCB_ERR_FORMAT, "sym: wire index too large");
+      if ((size_t)wire >= names.size()) names.resize((size_t)wire + 1);
+      names[(size_t)wire].push_back(name);
+    });
+    const uint32_t T = names.size() ? (uint32_t)names.size() : 1;
+    std::vector<uint32_t> map(T, 0);
+    uint32_t miss = 0;
+    std::string first;
+    for (uint32_t t = 1; t < T; t++) {
+      bool ok = false;
+      for (const auto& nm : names[t]) {
+        auto it = own.find(nm);
+        if (it != own.end()) {
+          map[t] = it->second;
+          ok = true;
+          break;
+        }
+      }
+      if (!ok) {
+        if (!miss) first = names[t].empty() ? "(wire " + std::to_string(t) + " has no name)" : names[t][0];
+        miss++;
+      }
+    }
+    if (unmatched) *unmatched = miss;
+    if (miss)
+      throw Error(NZCB_ERR_FORMAT, std::to_string(miss) + " of " + std::to_string(T - 1) +
+                                       " target signals have no counterpart in the program, e.g. " + first);
+    const size_t total = len + 8 + (size_t)T * 4;
+    uint8_t* buf = (uint8_t*)std::malloc(total);
+    if (!buf) throw Error(NZCB_ERR_INTERNAL, "out of host memory");
+    std::memcpy(buf, prog, len);
+    std::memcpy(buf + len, "wmap", 4);
+    std::memcpy(buf + len + 4, &T, 4);
+    std::memcpy(buf + len + 8, map.data(), (size_t)T * 4);
+    *out = buf;
+    *out_len = total;
     return NZCB_OK;
   } catch (const Error& e) {
     set_err(err, e.code, e.what());

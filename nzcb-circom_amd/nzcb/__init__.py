@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_from_zkey_file", "nzcb_vk_to_json", "nzcb_verify",
     "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_engine_lagrange_basis", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d", "nzcb_msm_set_pair_rounds",
-    "nzcb_plonk_setup", "nzcb_prove_batch_status",
+    "nzcb_plonk_setup", "nzcb_prove_batch_status", "nzcb_wprog_remap",
 ]
 
 
@@ -175,6 +175,8 @@ def load(path: str | None = None):
         "nzcb_wprog_run_dev": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_size_t, POINTER(ctypes.c_int32),
                                        c_void_p, POINTER(_Err)]),
         "nzcb_wprog_run": (c_int, [c_void_p, ctypes.c_char_p, c_int, u8p, POINTER(ctypes.c_int32), POINTER(_Err)]),
+        "nzcb_wprog_remap": (c_int, [ctypes.c_char_p, c_size_t, ctypes.c_char_p, c_size_t, ctypes.c_char_p, c_size_t,
+                                     POINTER(POINTER(c_uint8)), POINTER(c_size_t), POINTER(c_uint32), POINTER(_Err)]),
     }
     lib.missing_symbols = []
     for name, (res, args) in sigs.items():
@@ -664,6 +666,28 @@ class WitnessProgram:
         _check(self.lib.nzcb_wprog_run_dev(self.h, dev_inputs, count, dev_witness, stride, st, None,
                                            ctypes.byref(err)), err)
         return [st[i] for i in range(count)]
+
+
+def wprog_remap(program: bytes, own_sym: bytes, target_sym: bytes) -> bytes:
+    """nzcb_wprog_remap: the witness program re-indexed to the wire order of target_sym
+    (a circom .sym), matching signals by name against the program's own .sym
+    (Circuit.write_sym). Raises NzcbError (unmatched count in .unmatched) when a target
+    signal has no counterpart."""
+    lib = load()
+    out = POINTER(c_uint8)()
+    n = c_size_t(0)
+    miss = c_uint32(0)
+    err = _Err()
+    rc = lib.nzcb_wprog_remap(program, len(program), own_sym, len(own_sym), target_sym, len(target_sym),
+                              ctypes.byref(out), ctypes.byref(n), ctypes.byref(miss), ctypes.byref(err))
+    if rc:
+        e = NzcbError(err.code, err.msg.decode(errors="replace"))
+        e.unmatched = miss.value
+        raise e
+    try:
+        return ctypes.string_at(out, n.value)
+    finally:
+        lib.nzcb_free(out)
 
 
 class NzcpProver:

@@ -37,6 +37,7 @@ throws at the first failed check.
 """
 from __future__ import annotations
 
+import contextlib
 import struct
 
 R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
@@ -164,10 +165,11 @@ SHA512_IV = [0x6a09e667f3bcc908, 0xbb67ae8584caa73b, 0x3c6ef372fe94f82b, 0xa54ff
 class Circuit:
     """Signals, constraints and witness operations of one circuit (see module docstring)."""
 
-    def __init__(self, n_out: int, n_pub_in: int, n_prv_in: int, input_names=None):
+    def __init__(self, n_out: int, n_pub_in: int, n_prv_in: int, input_names=None, output_names=None):
         """input_names: [(name, size)] of the main's inputs in declaration order (sizes add
         up to n_pub_in + n_prv_in); written into the program so a caller can map an input
-        object ({name: value | array}) onto the input signals, as circom's calculator does."""
+        object ({name: value | array}) onto the input signals, as circom's calculator does.
+        output_names: [(name, size)] of the main's outputs (default: out[n_out])."""
         self.n_out, self.n_pub_in, self.n_prv_in = n_out, n_pub_in, n_prv_in
         self.input_names = list(input_names or [])
         if self.input_names and sum(k for _, k in self.input_names) != n_pub_in + n_prv_in:
@@ -177,12 +179,63 @@ class Circuit:
         self.ops = []                  # (type, err, n, dst, A, B, C, extra) in creation order
         self.out_wires = list(range(1, 1 + n_out))
         self.in_base = 1 + n_out
+        # signal names, circom's hierarchical "main.<component>.<signal>[i]" (write_sym)
+        self.names = {}
+        self._path = ["main"]
+        self._seq = {}
+        o = 1
+        for name, k in list(output_names or [("out", n_out)]) + self.input_names:
+            self._name(o, k, name)
+            o += k
 
     # ---- allocation --------------------------------------------------------------
-    def alloc(self, n: int) -> int:
+    def _name(self, base: int, n: int, sig: str, scalar: bool | None = None):
+        prefix = ".".join(self._path)
+        one = n == 1 if scalar is None else scalar
+        for i in range(n):
+            self.names[base + i] = f"{prefix}.{sig}" if one else f"{prefix}.{sig}[{i}]"
+
+    def _next(self, kind: str) -> int:
+        key = (len(self._path), ".".join(self._path), kind)
+        k = self._seq.get(key, 0)
+        self._seq[key] = k + 1
+        return k
+
+    @contextlib.contextmanager
+    def component(self, kind: str, name: str | None = None):
+        """Signals allocated inside are named <path>.<name>.<signal>. name: the component's
+        name in its parent template (circom source); default <kind>[k], numbered per parent."""
+        if name == "":          # the template's body inlined at the current level (a main)
+            yield
+            return
+        if name is None:
+            name = f"{kind}[{self._next(kind)}]"
+        self._path.append(name)
+        try:
+            yield
+        finally:
+            self._path.pop()
+
+    def alloc(self, n: int, name: str | None = None) -> int:
         base = self.n_wires
         self.n_wires += n
+        if name is None:
+            name = f"_s{self._next('_s')}"
+            self._name(base, n, name, scalar=n == 1)
+        else:
+            self._name(base, n, name)
         return base
+
+    def write_sym(self) -> bytes:
+        """circom's .sym text: one line per named signal, "label,wire,component,name", in
+        wire order (every allocated wire has a name; wire 0 = the constant one has none,
+        as in circom)."""
+        comps, lines = {}, []
+        for label, wire in enumerate(sorted(self.names), 1):
+            name = self.names[wire]
+            comp = comps.setdefault(name.rsplit(".", 1)[0], len(comps))
+            lines.append(f"{label},{wire},{comp},{name}\n")
+        return "".join(lines).encode()
 
     def constrain(self, a, b, c):
         """A * B = C (A and B empty for a linear constraint)."""
@@ -192,23 +245,24 @@ class Circuit:
         self.ops.append((typ, err, n, dst, a, b, c, extra))
 
     # ---- signals -----------------------------------------------------------------
-    def lin(self, x, dst: int | None = None, force: bool = False):
+    def lin(self, x, dst: int | None = None, force: bool = False, name: str | None = None):
         """``s <== x`` for linear x: short combinations stay aliases (circom --O2
         substitutes them), longer ones become a signal with one linear constraint."""
         x = lc(x)
         if dst is None and not force and len(x) <= 2:
             return x
-        s = self.alloc(1) if dst is None else dst
+        s = self.alloc(1, name) if dst is None else dst
         self.constrain(None, None, sub(x, w(s)))
         self._op(OP_LIN, s, x)
         return w(s)
 
-    def mul(self, a, b, c=0, dst: int | None = None):
+    def mul(self, a, b, c=0, dst: int | None = None, name: str | None = None):
         """``s <== a * b + c``."""
         a, b, c = lc(a), lc(b), lc(c)
         if is_const(a) or is_const(b):
-            return self.lin(add(scale(b, const_value(a)) if is_const(a) else scale(a, const_value(b)), c), dst)
-        s = self.alloc(1) if dst is None else dst
+            return self.lin(add(scale(b, const_value(a)) if is_const(a) else scale(a, const_value(b)), c), dst,
+                            name=name)
+        s = self.alloc(1, name) if dst is None else dst
         self.constrain(a, b, sub(w(s), c))
         self._op(OP_MUL, s, a, b, c)
         return w(s)
@@ -229,9 +283,10 @@ class Circuit:
         self.constrain(a, b, 0)
         self._op(OP_CHECK, 0, a, b, err=err)
 
-    def num2bits(self, x, n: int, err: int) -> list:
+    def num2bits(self, x, n: int, err: int, name: str | None = None) -> list:
         """circomlib Num2Bits(n): n bit signals, LSB first."""
-        base = self.alloc(n)
+        with self.component("Num2Bits", name):
+            base = self.alloc(n, "out")
         bits = [w(base + i) for i in range(n)]
         for b in bits:
             self.constrain(b, sub(b, 1), 0)
@@ -239,31 +294,45 @@ class Circuit:
         self._op(OP_BITS, base, lc(x), n=n, err=err)
         return bits
 
-    def is_zero(self, x) -> dict:
+    def is_zero(self, x, name: str | None = None) -> dict:
         """circomlib IsZero: inv <-- x != 0 ? 1/x : 0; out <== -x inv + 1; x out === 0."""
         x = lc(x)
-        inv = self.alloc(1)
-        self._op(OP_INV, inv, x)
-        out = self.mul(scale(x, -1), w(inv), 1)
+        with self.component("IsZero", name):
+            inv = self.alloc(1, "inv")
+            self._op(OP_INV, inv, x)
+            out = self.mul(scale(x, -1), w(inv), 1, name="out")
         self.constrain(x, out, 0)
         return out
 
-    def is_equal(self, a, b) -> dict:
-        return self.is_zero(sub(b, a))
+    def is_equal(self, a, b, name: str | None = None) -> dict:
+        with self.component("IsEqual", name):
+            return self.is_zero(sub(b, a), name="isz")
 
-    def less_than(self, a, b, n: int, err: int) -> dict:
+    def less_than(self, a, b, n: int, err: int, name: str | None = None) -> dict:
         """circomlib LessThan(n): Num2Bits(n+1) of a + 2^n - b, out = 1 - bit n."""
-        bits = self.num2bits(add(a, 1 << n, scale(b, -1)), n + 1, err)
+        with self.component("LessThan", name):
+            bits = self.num2bits(add(a, 1 << n, scale(b, -1)), n + 1, err, name="n2b")
         return sub(1, bits[n])
 
-    def quin(self, n: int, in_base: int, m: int, index, err_range: int, err_select: int) -> dict:
+    def quin(self, n: int, in_base: int, m: int, index, err_range: int, err_select: int,
+             name: str | None = None) -> dict:
         """QuinSelector(n) (quinSelector.circom:11-42) over in[k] = wire in_base + k for
         k < m and 0 beyond: LessThan range check, then the IsZero/sum core as one op."""
+        with self.component("QuinSelector", name):
+            return self._quin(n, in_base, m, index, err_range, err_select)
+
+    def _quin(self, n, in_base, m, index, err_range, err_select):
         bits = n.bit_length()          # log2(choices) + 1
-        lt = self.less_than(index, n, bits, err_range)
+        lt = self.less_than(index, n, bits, err_range, name="lessThan")
         self.check_zero(sub(lt, 1), err_select)
         index = lc(index)
-        base = self.alloc(2 * n + m)
+        base = self.alloc(2 * n + m, "_block")
+        prefix = ".".join(self._path)
+        for i in range(n):
+            self.names[base + i] = f"{prefix}.eqs[{i}].out"
+            self.names[base + n + i] = f"{prefix}.eqs[{i}].inv"
+        for i in range(m):
+            self.names[base + 2 * n + i] = f"{prefix}.sums[{i}]"
         eq = lambda i: w(base + i)            # noqa: E731
         inv = lambda i: w(base + n + i)       # noqa: E731
         sums = lambda i: w(base + 2 * n + i)  # noqa: E731
@@ -284,7 +353,8 @@ class Circuit:
         L = sha_block_layout(spec)
         B = L["bits"]
         mask = (1 << B) - 1
-        base = self.alloc(L["size"])
+        with self.component("Sha256compression" if B == 32 else "Sha512compression"):
+            base = self.alloc(L["size"], "w")
         cur = [base]
 
         def take(k=1):

@@ -21,6 +21,8 @@ reference's own test vectors pin (test/nzcp.js, test/cbor.js, test/utils.js).
 """
 from __future__ import annotations
 
+import functools
+
 from .circuit import (OP_SHA256, OP_SHA512, SHA256_IV, SHA256_SPEC, SHA512_IV, SHA512_SPEC, Circuit, add, lc,
                       scale, sub, w)
 
@@ -38,6 +40,19 @@ def log2(x: int) -> int:
     return x.bit_length() - 1
 
 
+def _template(kind: str):
+    """A gadget as a circom component: its signals are named <parent>.<cname>.<signal>
+    (cname: the component's name in the caller's template; default <kind>[k]; "" = the
+    template is the main itself)."""
+    def deco(f):
+        @functools.wraps(f)
+        def g(c, *args, cname=None, **kw):
+            with c.component(kind, cname):
+                return f(c, *args, **kw)
+        return g
+    return deco
+
+
 class Bytes:
     """A byte array as contiguous wires (``bytes[BytesLen]`` of the cbor templates)."""
 
@@ -46,18 +61,21 @@ class Bytes:
 
 
 # ---------------------------------------------------------------------------- cbortpl
+@_template("GetType")
 def get_type(c: Circuit, v):
     """GetType (cbortpl.circom:26-52): Num2Bits(8), ShR(8, 5), Bits2Num(3)."""
     bits = c.num2bits(v, 8, ERR_RANGE)
     return c.lin(add(*[scale(bits[5 + i], 1 << i) for i in range(3)]))
 
 
+@_template("GetX")
 def get_x(c: Circuit, v):
     """GetX (cbortpl.circom:57-72): the 5 low bits of v."""
     bits = c.num2bits(v, 8, ERR_RANGE)
     return c.lin(add(*[scale(bits[i], 1 << i) for i in range(5)]))
 
 
+@_template("GetV")
 def get_v(c: Circuit, b: Bytes, pos):
     """GetV (cbortpl.circom:78-90): QuinSelector(BytesLen). Both of QuinSelector's checks
     (the LessThan's Num2Bits and ``lessThan.out === 1``) report ERR_SELECT, as the
@@ -65,6 +83,7 @@ def get_v(c: Circuit, b: Bytes, pos):
     return c.quin(b.n, b.base, b.n, pos, ERR_SELECT, ERR_SELECT)
 
 
+@_template("DecodeUint23")
 def decode_uint23(c: Circuit, v):
     """DecodeUint23 (cbortpl.circom:95-114)."""
     x = get_x(c, v)
@@ -73,6 +92,7 @@ def decode_uint23(c: Circuit, v):
     return x
 
 
+@_template("DecodeUint")
 def decode_uint(c: Circuit, v, b: Bytes, pos):
     """DecodeUint (cbortpl.circom:120-241): every branch is evaluated. Returns (value, nextPos)."""
     x = get_x(c, v)
@@ -98,6 +118,7 @@ def decode_uint(c: Circuit, v, b: Bytes, pos):
     return value, next_pos
 
 
+@_template("ReadType")
 def read_type(c: Circuit, b: Bytes, pos):
     """ReadType (cbortpl.circom:246-261). Returns (nextPos, type, v)."""
     v = get_v(c, b, pos)
@@ -105,6 +126,7 @@ def read_type(c: Circuit, b: Bytes, pos):
     return add(pos, 1), typ, v
 
 
+@_template("SkipValueScalar")
 def skip_value_scalar(c: Circuit, b: Bytes, pos):
     """SkipValueScalar (cbortpl.circom:266-297): ints and strings."""
     nxt, typ, v = read_type(c, b, pos)
@@ -114,6 +136,7 @@ def skip_value_scalar(c: Circuit, b: Bytes, pos):
     return c.lin(add(c.mul(is_int, dnext), c.mul(is_string, add(dnext, value))))
 
 
+@_template("SkipValue")
 def skip_value(c: Circuit, b: Bytes, pos, max_array_len: int):
     """SkipValue (cbortpl.circom:306-366): SkipValueScalar's ints and strings plus arrays of
     up to MaxArrayLen scalars. Every element slot i runs a SkipValueScalar from the previous
@@ -142,6 +165,7 @@ def skip_value(c: Circuit, b: Bytes, pos, max_array_len: int):
     return c.lin(add(*terms))
 
 
+@_template("StringEquals")
 def string_equals(c: Circuit, b: Bytes, const: list, pos, length):
     """StringEquals (cbortpl.circom:373-404)."""
     is_same_len = c.is_equal(length, len(const))
@@ -151,6 +175,7 @@ def string_equals(c: Circuit, b: Bytes, const: list, pos, length):
     return c.is_zero(sub(len(const) + 1, add(*cond)))
 
 
+@_template("ReadStringLength")
 def read_string_length(c: Circuit, b: Bytes, pos):
     """ReadStringLength (cbortpl.circom:410-428). Returns (len, nextPos = pos + 1)."""
     nxt, typ, v = read_type(c, b, pos)
@@ -159,6 +184,7 @@ def read_string_length(c: Circuit, b: Bytes, pos):
     return value, nxt
 
 
+@_template("ReadMapLength")
 def read_map_length(c: Circuit, b: Bytes, pos):
     """ReadMapLength (cbortpl.circom:434-453). Returns (len, nextPos)."""
     nxt, typ, v = read_type(c, b, pos)
@@ -166,6 +192,7 @@ def read_map_length(c: Circuit, b: Bytes, pos):
     return decode_uint23(c, v), nxt
 
 
+@_template("CopyString")
 def copy_string(c: Circuit, b: Bytes, pos, max_len: int, out_base: int | None = None):
     """CopyString (cbortpl.circom:460-503). Returns (outbytes, nextPos, len)."""
     length, nxt = read_string_length(c, b, pos)
@@ -179,6 +206,7 @@ def copy_string(c: Circuit, b: Bytes, pos, max_len: int, out_base: int | None = 
 
 
 # --------------------------------------------------------------------------- nzcptpl
+@_template("FindCWTClaims")
 def find_cwt_claims(c: Circuit, b: Bytes, map_len, pos, max_array_len: int, max_map_len: int):
     """FindCWTClaims (nzcptpl.circom:33-145). Returns (vcPos, exp)."""
     vc = [118, 99]
@@ -207,6 +235,7 @@ def find_cwt_claims(c: Circuit, b: Bytes, map_len, pos, max_array_len: int, max_
     return vc_pos, exp
 
 
+@_template("FindCredSubj")
 def find_cred_subj(c: Circuit, b: Bytes, map_len, pos, max_array_len: int, max_map_len: int):
     """FindCredSubj (nzcptpl.circom:152-226; not used by NZCPPubIdentity, tested by the
     reference at test/nzcp.js:144-215). Returns needlePos, the position of the
@@ -227,6 +256,7 @@ def find_cred_subj(c: Circuit, b: Bytes, map_len, pos, max_array_len: int, max_m
     return c.lin(add(*found))
 
 
+@_template("ReadCredSubj")
 def read_cred_subj(c: Circuit, b: Bytes, pos, max_buffer_len: int, map_len=None):
     """ReadCredSubj (nzcptpl.circom:232-360). Returns ((givenName base, len), (familyName ...),
     (dob ...)); each name is max_buffer_len / 3 contiguous signals (zeros past them).
@@ -258,6 +288,7 @@ def read_cred_subj(c: Circuit, b: Bytes, pos, max_buffer_len: int, map_len=None)
     return res, max_str
 
 
+@_template("ConstructNullifier")
 def construct_nullifier(c: Circuit, names, max_str: int, max_buffer_len: int):
     """ConstructNullifier (nzcptpl.circom:364-440). Returns the result[] LCs."""
     comma = 44
@@ -297,6 +328,7 @@ def msg_word_bits(base: int, t: int, bits: int) -> list:
     return out
 
 
+@_template("Sha256Var")
 def sha256_var(c: Circuit, msg_bits_msb: list, len_bytes, block_space: int):
     """Sha256Var(BlockSpace) (noway/sha256-var-circom, not on disk; used at
     nzcptpl.circom:509-517): SHA-256 of the first ``len_bytes`` bytes of the input bits,
@@ -356,6 +388,7 @@ def sha256_var(c: Circuit, msg_bits_msb: list, len_bytes, block_space: int):
     return out
 
 
+@_template("Sha512")
 def sha512_64(c: Circuit, byte_base: int):
     """Sha512(512) (Electron-Labs/sha512, not on disk; used at nzcptpl.circom:577-580) for
     a 64-byte message over byte wires with LSB-first bits: one block, constant padding
@@ -384,26 +417,27 @@ def nzcp_pub_identity(is_live: int, max_tbs_bytes: int, max_array_len_vc: int, m
     for i in range(max_bits):
         c.check_quad(tbs[i], sub(tbs[i], 1), ERR_BIT)
     # toBeSignedLen < Max + 1 (:500-505)
-    lt_max = c.less_than(tbs_len, max_tbs_bytes + 1, log2(max_tbs_bytes + 1) + 1, ERR_RANGE)
+    lt_max = c.less_than(tbs_len, max_tbs_bytes + 1, log2(max_tbs_bytes + 1) + 1, ERR_RANGE,
+                         name="lteMaxToBeSignedBytes")
     c.check_zero(sub(lt_max, 1), ERR_LEN)
     # SHA-256 of ToBeSigned (:509-517)
-    sha256 = sha256_var(c, tbs, tbs_len, 3)
+    sha256 = sha256_var(c, tbs, tbs_len, 3, cname="tbsSha256")
     # bits -> bytes, zero past the length (:521-533)
-    tb = c.alloc(max_tbs_bytes)
+    tb = c.alloc(max_tbs_bytes, "ToBeSigned")
     bits = log2(max_tbs_bytes) + 1
     for k in range(max_tbs_bytes):
         b2n = add(*[scale(tbs[8 * k + 7 - i], 1 << i) for i in range(8)])
-        lt = c.less_than(k, tbs_len, bits, ERR_RANGE)
+        lt = c.less_than(k, tbs_len, bits, ERR_RANGE, name=f"ltLen[{k}]")
         c.mul(b2n, lt, dst=tb + k)
     tbytes = Bytes(tb, max_tbs_bytes)
-    map_len, nxt = read_map_length(c, tbytes, claims_skip)
-    vc_pos, exp = find_cwt_claims(c, tbytes, map_len, nxt, max_array_len_vc, max_map_len_vc)
-    names, max_str = read_cred_subj(c, tbytes, add(vc_pos, cred_subj_offset), null_bytes)
-    result = construct_nullifier(c, names, max_str, null_bytes)
-    nb = [c.num2bits(result[k], 8, ERR_RANGE) for k in range(null_bytes)]
+    map_len, nxt = read_map_length(c, tbytes, claims_skip, cname="readMapLengthClaims")
+    vc_pos, exp = find_cwt_claims(c, tbytes, map_len, nxt, max_array_len_vc, max_map_len_vc, cname="findVC")
+    names, max_str = read_cred_subj(c, tbytes, add(vc_pos, cred_subj_offset), null_bytes, cname="readCredSubj")
+    result = construct_nullifier(c, names, max_str, null_bytes, cname="nullifier")
+    nb = [c.num2bits(result[k], 8, ERR_RANGE, name=f"n2bNullifier[{k}]") for k in range(null_bytes)]
     nbase = next(iter(nb[0][0]))            # byte wires: nbase + 8k + j (LSB-first bits)
-    sha512 = sha512_64(c, nbase)
-    exp_bits = c.num2bits(exp, 32, ERR_RANGE)
+    sha512 = sha512_64(c, nbase, cname="nullifierSha512")
+    exp_bits = c.num2bits(exp, 32, ERR_RANGE, name="n2bExp")
     ins = [[0] * chunk_bits for _ in range(3)]
     for k in range(chunk_bytes):                                   # nullifier hash part (:596-601)
         b = chunk_bytes - 1 - k
@@ -480,7 +514,7 @@ def template_circuit(template: str, *params) -> Circuit:
     private (circom's default for main), named as the template declares them."""
     def io(outs, ins):
         n_out = sum(k for _, k in outs)
-        c = Circuit(n_out, 0, sum(k for _, k in ins), input_names=list(ins))
+        c = Circuit(n_out, 0, sum(k for _, k in ins), input_names=list(ins), output_names=list(outs))
         wires, o = {}, c.in_base
         for name, k in ins:
             wires[name] = o
@@ -493,48 +527,49 @@ def template_circuit(template: str, *params) -> Circuit:
             c.lin(lc(x), dst=c.out_wires[i])
 
     if template in ("GetType", "GetX", "DecodeUint23"):
-        c, wi = io([("out", 1)], [("v", 1)])
+        c, wi = io([({"GetType": "type", "GetX": "x"}.get(template, "value"), 1)], [("v", 1)])
         fn = {"GetType": get_type, "GetX": get_x, "DecodeUint23": decode_uint23}[template]
-        put(c, [fn(c, w(wi["v"]))])
+        put(c, [fn(c, w(wi["v"]), cname="")])
     elif template == "GetV":
         (n,) = params
         c, wi = io([("v", 1)], [("bytes", n), ("pos", 1)])
-        put(c, [get_v(c, Bytes(wi["bytes"], n), w(wi["pos"]))])
+        put(c, [get_v(c, Bytes(wi["bytes"], n), w(wi["pos"]), cname="")])
     elif template == "DecodeUint":
         (n,) = params
         c, wi = io([("value", 1), ("nextPos", 1)], [("v", 1), ("bytes", n), ("pos", 1)])
-        put(c, list(decode_uint(c, w(wi["v"]), Bytes(wi["bytes"], n), w(wi["pos"]))))
+        put(c, list(decode_uint(c, w(wi["v"]), Bytes(wi["bytes"], n), w(wi["pos"]), cname="")))
     elif template == "ReadType":
         (n,) = params
         c, wi = io([("nextPos", 1), ("type", 1), ("v", 1)], [("bytes", n), ("pos", 1)])
-        put(c, list(read_type(c, Bytes(wi["bytes"], n), w(wi["pos"]))))
+        put(c, list(read_type(c, Bytes(wi["bytes"], n), w(wi["pos"]), cname="")))
     elif template in ("SkipValueScalar", "SkipValue"):
         n = params[0]
         c, wi = io([("nextPos", 1)], [("bytes", n), ("pos", 1)])
         b, pos = Bytes(wi["bytes"], n), w(wi["pos"])
-        put(c, [skip_value_scalar(c, b, pos) if template == "SkipValueScalar" else skip_value(c, b, pos, params[1])])
+        put(c, [skip_value_scalar(c, b, pos, cname="") if template == "SkipValueScalar"
+                else skip_value(c, b, pos, params[1], cname="")])
     elif template == "StringEquals":
         n, const, clen = params
         c, wi = io([("out", 1)], [("bytes", n), ("pos", 1), ("len", 1)])
-        put(c, [string_equals(c, Bytes(wi["bytes"], n), list(const[:clen]), w(wi["pos"]), w(wi["len"]))])
+        put(c, [string_equals(c, Bytes(wi["bytes"], n), list(const[:clen]), w(wi["pos"]), w(wi["len"]), cname="")])
     elif template == "ReadStringLength":
         (n,) = params
         c, wi = io([("len", 1), ("nextPos", 1)], [("bytes", n), ("pos", 1)])
-        put(c, list(read_string_length(c, Bytes(wi["bytes"], n), w(wi["pos"]))))
+        put(c, list(read_string_length(c, Bytes(wi["bytes"], n), w(wi["pos"]), cname="")))
     elif template == "ReadMapLength":
         (n,) = params
         c, wi = io([("len", 1), ("nextPos", 1)], [("pos", 1), ("bytes", n)])
-        put(c, list(read_map_length(c, Bytes(wi["bytes"], n), w(wi["pos"]))))
+        put(c, list(read_map_length(c, Bytes(wi["bytes"], n), w(wi["pos"]), cname="")))
     elif template == "CopyString":
         n, max_len = params
         c, wi = io([("outbytes", max_len), ("nextPos", 1), ("len", 1)], [("bytes", n), ("pos", 1)])
-        out, nxt, ln = copy_string(c, Bytes(wi["bytes"], n), w(wi["pos"]), max_len)
+        out, nxt, ln = copy_string(c, Bytes(wi["bytes"], n), w(wi["pos"]), max_len, cname="")
         put(c, out + [nxt, ln])
     elif template == "QuinSelector":
         (n,) = params
         c, wi = io([("out", 1)], [("in", n), ("index", 1)])
         if n:
-            put(c, [c.quin(n, wi["in"], n, w(wi["index"]), ERR_SELECT, ERR_SELECT)])
+            put(c, [c._quin(n, wi["in"], n, w(wi["index"]), ERR_SELECT, ERR_SELECT)])
         else:   # QuinSelector(0): no range check, out <== 0 (quinSelector.circom:21, 41)
             put(c, [0])
     elif template in ("FindCWTClaims", "FindCredSubj"):
@@ -542,13 +577,15 @@ def template_circuit(template: str, *params) -> Circuit:
         outs = [("vcPos", 1), ("exp", 1)] if template == "FindCWTClaims" else [("needlePos", 1)]
         c, wi = io(outs, [("mapLen", 1), ("bytes", n), ("pos", 1)])
         args = (c, Bytes(wi["bytes"], n), w(wi["mapLen"]), w(wi["pos"]), max_arr, max_map)
-        put(c, list(find_cwt_claims(*args)) if template == "FindCWTClaims" else [find_cred_subj(*args)])
+        put(c, list(find_cwt_claims(*args, cname="")) if template == "FindCWTClaims"
+            else [find_cred_subj(*args, cname="")])
     elif template == "ReadCredSubj":
         n, max_buf = params
         outs = [("givenName", max_buf), ("givenNameLen", 1), ("familyName", max_buf), ("familyNameLen", 1),
                 ("dob", max_buf), ("dobLen", 1)]
         c, wi = io(outs, [("mapLen", 1), ("bytes", n), ("pos", 1)])
-        names, max_str = read_cred_subj(c, Bytes(wi["bytes"], n), w(wi["pos"]), max_buf, map_len=w(wi["mapLen"]))
+        names, max_str = read_cred_subj(c, Bytes(wi["bytes"], n), w(wi["pos"]), max_buf, map_len=w(wi["mapLen"]),
+                                        cname="")
         vals = []
         for base, ln in names:
             vals += [w(base + h) for h in range(max_str)] + [0] * (max_buf - max_str) + [ln]
@@ -559,7 +596,7 @@ def template_circuit(template: str, *params) -> Circuit:
                ("dob", max_buf), ("dobLen", 1)]
         c, wi = io([("result", max_buf), ("resultLen", 1)], ins)
         names = [(wi[k], w(wi[k + "Len"])) for k in ("givenName", "familyName", "dob")]
-        result = construct_nullifier(c, names, max_buf, max_buf)
+        result = construct_nullifier(c, names, max_buf, max_buf, cname="")
         total = add(*[ln for _, ln in names], 2)       # resultLen (nzcptpl.circom:432)
         put(c, result + [total])
     else:

@@ -39,8 +39,20 @@ def parse(prog: bytes) -> dict:
     starts = struct.unpack_from(f"<{n_lev + 1}I", prog, o)
     if ver != 2:
         raise ValueError("unsupported witness program version")
+    o += 4 * (n_lev + 1) + 4 * n_lev
+    (n_names,) = struct.unpack_from("<I", prog, o)
+    o += 4
+    for _ in range(n_names):
+        (ln,) = struct.unpack_from("<I", prog, o)
+        o += 8 + ln
+    wmap = None
+    if o != len(prog):     # nzcb_wprog_remap's wire map: output wire t = program wire map[t]
+        if prog[o:o + 4] != b"wmap":
+            raise ValueError("witness program: trailing bytes")
+        (T,) = struct.unpack_from("<I", prog, o + 4)
+        wmap = list(struct.unpack_from(f"<{T}I", prog, o + 8))
     return dict(n_wires=n_wires, n_out=n_out, n_pub=n_pub, n_prv=n_prv, consts=consts, terms=terms, ops=ops,
-                levels=starts)
+                levels=starts, wmap=wmap)
 
 
 def _lc(p, wit, off, n):
@@ -215,6 +227,8 @@ def evaluate(prog: bytes, inputs: list) -> tuple:
             wit[dst:dst + len(vals)] = vals
         else:
             raise ValueError(f"unknown op {typ}")
+    if p["wmap"] is not None:
+        wit = [wit[k] for k in p["wmap"]]
     return wit, fail
 
 
