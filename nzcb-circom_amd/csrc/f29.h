@@ -66,9 +66,28 @@ __device__ __forceinline__ void mad29(uint64_t& acc, uint32_t x, uint32_t y) {
 __device__ __forceinline__ void mad29c(uint64_t& acc, uint32_t x, uint32_t y) {
   asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(x), "s"(y) : "vcc");
 }
+// two independent mads in one asm statement (mul29x2): the compiler's s_nop between
+// inline-asm statements is paid once per pair
+__device__ __forceinline__ void mad29x2(uint64_t& acc, uint32_t x, uint32_t y, uint64_t& bcc, uint32_t u,
+                                        uint32_t v) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_mad_u64_u32 %1, vcc, %4, %5, %1"
+      : "+v"(acc), "+v"(bcc) : "v"(x), "v"(y), "v"(u), "v"(v) : "vcc");
+}
+__device__ __forceinline__ void mad29cx2(uint64_t& acc, uint32_t x, uint64_t& bcc, uint32_t u, uint32_t y) {
+  asm("v_mad_u64_u32 %0, vcc, %2, %4, %0\n\tv_mad_u64_u32 %1, vcc, %3, %4, %1"
+      : "+v"(acc), "+v"(bcc) : "v"(x), "v"(u), "s"(y) : "vcc");
+}
 #else
 NZ_HD void mad29(uint64_t& acc, uint32_t x, uint32_t y) { acc += (uint64_t)x * y; }
 NZ_HD void mad29c(uint64_t& acc, uint32_t x, uint32_t y) { acc += (uint64_t)x * y; }
+NZ_HD void mad29x2(uint64_t& acc, uint32_t x, uint32_t y, uint64_t& bcc, uint32_t u, uint32_t v) {
+  acc += (uint64_t)x * y;
+  bcc += (uint64_t)u * v;
+}
+NZ_HD void mad29cx2(uint64_t& acc, uint32_t x, uint64_t& bcc, uint32_t u, uint32_t y) {
+  acc += (uint64_t)x * y;
+  bcc += (uint64_t)u * y;
+}
 #endif
 
 NZ_HD F29 f29_const(const uint32_t (&c)[9]) {
@@ -110,6 +129,44 @@ NZ_HD F29 mul29(const F29& a, const F29& b) {
   return r;
 }
 
+// mul29 of two independent products with their instructions interleaved: two dependent
+// v_mad_u64_u32 chains side by side, so a wave with few co-resident waves (the NTT's
+// 72 KiB-LDS tiles leave 2 per SIMD while the other workgroup loads) keeps issuing
+// while one chain waits on its previous mad
+template <class Q = Fr29>
+NZ_HD void mul29x2(const F29& a, const F29& b, const F29& c, const F29& d, F29& r1, F29& r2) {
+  uint32_t m[9], n[9];
+  uint64_t acc = 0, bcc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+#pragma unroll
+    for (int j = 0; j < i; j++) {
+      mad29x2(acc, a.v[j], b.v[i - j], bcc, c.v[j], d.v[i - j]);
+      mad29cx2(acc, m[j], bcc, n[j], Q::P[i - j]);
+    }
+    mad29x2(acc, a.v[i], b.v[0], bcc, c.v[i], d.v[0]);
+    m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
+    n[i] = ((uint32_t)bcc * Q::INV) & Q::MASK;
+    mad29cx2(acc, m[i], bcc, n[i], Q::P[0]);
+    acc >>= 29;
+    bcc >>= 29;
+  }
+#pragma unroll
+  for (int i = 9; i < 17; i++) {
+#pragma unroll
+    for (int j = i - 8; j < 9; j++) {
+      mad29x2(acc, a.v[j], b.v[i - j], bcc, c.v[j], d.v[i - j]);
+      mad29cx2(acc, m[j], bcc, n[j], Q::P[i - j]);
+    }
+    r1.v[i - 9] = (uint32_t)acc & Q::MASK;
+    r2.v[i - 9] = (uint32_t)bcc & Q::MASK;
+    acc >>= 29;
+    bcc >>= 29;
+  }
+  r1.v[8] = (uint32_t)acc;
+  r2.v[8] = (uint32_t)bcc;
+}
+
 // a^2 * 2^-261 mod p: the cross products a_j a_k (j < k) once, against 2 a_k
 // (45 instead of 81 product terms; same bounds as mul29, products < 2^59 for
 // normalized limbs, so a column stays < 2^64)
@@ -143,6 +200,45 @@ NZ_HD F29 sqr29(const F29& a) {
   }
   r.v[8] = (uint32_t)acc;
   return r;
+}
+
+// sqr29 of two independent values, interleaved as mul29x2
+NZ_HD void sqr29x2(const F29& a, const F29& c, F29& r1, F29& r2) {
+  using Q = Fq29;
+  uint32_t a2[9], c2[9], m[9], n[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    a2[i] = a.v[i] << 1;
+    c2[i] = c.v[i] << 1;
+  }
+  uint64_t acc = 0, bcc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+#pragma unroll
+    for (int j = 0; 2 * j < i; j++) mad29x2(acc, a.v[j], a2[i - j], bcc, c.v[j], c2[i - j]);
+    if (!(i & 1)) mad29x2(acc, a.v[i >> 1], a.v[i >> 1], bcc, c.v[i >> 1], c.v[i >> 1]);
+#pragma unroll
+    for (int j = 0; j < i; j++) mad29cx2(acc, m[j], bcc, n[j], Q::P[i - j]);
+    m[i] = ((uint32_t)acc * Q::INV) & Q::MASK;
+    n[i] = ((uint32_t)bcc * Q::INV) & Q::MASK;
+    mad29cx2(acc, m[i], bcc, n[i], Q::P[0]);
+    acc >>= 29;
+    bcc >>= 29;
+  }
+#pragma unroll
+  for (int i = 9; i < 17; i++) {
+#pragma unroll
+    for (int j = i - 8; 2 * j < i; j++) mad29x2(acc, a.v[j], a2[i - j], bcc, c.v[j], c2[i - j]);
+    if (!(i & 1)) mad29x2(acc, a.v[i >> 1], a.v[i >> 1], bcc, c.v[i >> 1], c.v[i >> 1]);
+#pragma unroll
+    for (int j = i - 8; j < 9; j++) mad29cx2(acc, m[j], bcc, n[j], Q::P[i - j]);
+    r1.v[i - 9] = (uint32_t)acc & Q::MASK;
+    r2.v[i - 9] = (uint32_t)bcc & Q::MASK;
+    acc >>= 29;
+    bcc >>= 29;
+  }
+  r1.v[8] = (uint32_t)acc;
+  r2.v[8] = (uint32_t)bcc;
 }
 
 // (a b + c d) * 2^-261 mod p with one Montgomery reduction. Needs every limb < 2^29

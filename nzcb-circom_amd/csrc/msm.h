@@ -44,6 +44,8 @@ struct MsmScratch {
   DevBuf<uint32_t> pair_off[2];
   DevBuf<uint32_t> pair_pre;
   DevBuf<uint32_t> large;     // [count, bucket ids...] of buckets with long carry runs
+  DevBuf<uint32_t> large_off;  // fixed base: piece offsets of the listed buckets (msm_large_scan_kernel)
+  DevBuf<Xyzz29> large_part;   // fixed base: one partial sum per piece
   DevBuf<G1xyzz> seg_tot;     // per (bucket set, segment): sum_j (j+1) * bucket_j
   DevBuf<G1xyzz> seg_run;     // per (bucket set, segment): sum_j bucket_j
   DevBuf<G1xyzz> parts;       // per (set, sum slot, part): partial plain sums

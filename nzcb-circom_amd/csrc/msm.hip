@@ -117,12 +117,31 @@ static constexpr int kSumPer = 4;        // level-1 sums: sequential adds per th
 static constexpr int kPartThreads = 64;  // level-2 sums: block size
 static constexpr uint32_t kSeqSpan = 64;  // finalize: longest carry run summed by one thread
 static constexpr int kLargeBlocks = 32;  // finalize: workgroups for the longer runs
+static constexpr int kLargePieceBlocks = 512;  // fixed base: workgroups over the pieces of the longer runs
 
 // LDS-staged bucket indices in the accumulation (msm_accumulate29_kernel kLdsIdx);
 // NZCB_ACC_LDS=0 reads them from HBM as before (A/B runs)
 static bool lds_indices() {
   static const bool on = [] {
     const char* e = std::getenv("NZCB_ACC_LDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// interleaved product pairs in the accumulation (kPair); NZCB_ACC_PAIR=0 for A/B runs
+// (same box: isolated accumulation 2.295 -> 2.254 ms, bench +1.3 %)
+static bool paired_products() {
+  static const bool on = [] {
+    const char* e = std::getenv("NZCB_ACC_PAIR");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// long carry runs summed in pieces (msm_large_piece29_kernel); NZCB_LARGE_PIECES=0 for A/B
+static bool large_pieces() {
+  static const bool on = [] {
+    const char* e = std::getenv("NZCB_LARGE_PIECES");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -605,7 +624,9 @@ __device__ __forceinline__ G1xyzz load_point(const Xyzz29& a) {
 // 49 KB per workgroup: three workgroups (12 waves, the 3 waves per SIMD the kernel is
 // compiled for) fit the CU's 160 KB.
 static constexpr uint32_t kLdsStride = kMsmThreads + 1;  // slot-major rows, +1: conflict-free fill
-template <int WAVES, bool kDirect = false, bool kLdsIdx = false>
+// kPair: the addition's independent products in interleaved pairs (mul29x2 / sqr29x2:
+// U2 | S2, PP | RR, PPP | Q, ZZ3 | ZZZ3), two v_mad_u64_u32 chains per asm statement
+template <int WAVES, bool kDirect = false, bool kLdsIdx = false, bool kPair = false>
 __global__ void __launch_bounds__(kMsmThreads) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
                         const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
@@ -657,6 +678,30 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
         acc.ZZ = f29_const(Fq29::ONE);
         acc.ZZZ = f29_const(Fq29::ONE);
         inf = false;
+      } else if (kPair) {
+        // madd-2008-s as above, products paired
+        F29 U2, S2, PP, RR;
+        mul29x2<Fq29>(x, acc.ZZ, y, acc.ZZZ, U2, S2);
+        const F29 Pd = sub29(U2, acc.X, Fq29::K8);   // < 10p
+        const F29 R = sub29(S2, acc.Y, Fq29::K4);    // < 6p
+        sqr29x2(Pd, R, PP, RR);
+        if (is0p29_fast(PP)) {  // same abscissa: doubling (equal points) or infinity (opposite)
+          if (is0p29(RR)) {
+            norm29(y);
+            mdbl29_rare(x, y, &acc);
+          } else {
+            inf = true;
+          }
+        } else {
+          F29 PPP, Q, ZZ3, ZZZ3;
+          mul29x2<Fq29>(Pd, PP, acc.X, PP, PPP, Q);
+          const F29 X3 = sub2x29(RR, PPP, Q);  // RR + 6p - PPP - 2Q < 8p
+          mul29x2<Fq29>(acc.ZZ, PP, acc.ZZZ, PPP, ZZ3, ZZZ3);
+          acc.Y = mul2sum29(R, sub29_nn(Q, X3, Fq29W::K10), neg4p29_nn(acc.Y), PPP);
+          acc.ZZ = ZZ3;
+          acc.ZZZ = ZZZ3;
+          acc.X = X3;
+        }
       } else {
         // madd-2008-s (XYZZ + affine): 8 products + 2 squares
         const F29 U2 = mul29(x, acc.ZZ);
@@ -977,20 +1022,32 @@ msm_bucket_reduce_kernel(const G1xyzz* __restrict__ buckets, const uint32_t* __r
   seg_run[t] = run;  // sum_j bucket_{g*L+j}
 }
 
+// point addition / infinity for the block sums: 8x32 XYZZ (G1xyzz) or radix-2^29 (Xyzz29)
+__device__ __forceinline__ G1xyzz padd(const G1xyzz& a, const G1xyzz& b) { return xyzz_add(a, b); }
+__device__ __forceinline__ Xyzz29 padd(const Xyzz29& a, const Xyzz29& b) { return add29(a, b); }
+template <class P> __device__ __forceinline__ P pinf();
+template <> __device__ __forceinline__ G1xyzz pinf<G1xyzz>() { return G1xyzz::inf(); }
+template <> __device__ __forceinline__ Xyzz29 pinf<Xyzz29>() {
+  Xyzz29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.X.v[i] = r.Y.v[i] = r.ZZ.v[i] = r.ZZZ.v[i] = 0;
+  return r;
+}
+
 // Block tree sum with a single EC-addition site: `per` sequential steps in which
 // load(step, rhs) supplies the thread's next term, then log2(T) LDS tree levels.
-template <int T, class Load>
-__device__ __forceinline__ G1xyzz block_sum(int per, G1xyzz* sh, Load&& load) {
+template <int T, class Load, class Pt = G1xyzz>
+__device__ __forceinline__ Pt block_sum(int per, Pt* sh, Load&& load) {
   constexpr int LG = T == 256 ? 8 : T == 128 ? 7 : T == 64 ? 6 : 5;
   const int tid = threadIdx.x;
-  G1xyzz acc = G1xyzz::inf();
+  Pt acc = pinf<Pt>();
   for (int step = 0; step < per + LG; step++) {
     if (step == per) {
       sh[tid] = acc;
       __syncthreads();
     }
     bool doit;
-    G1xyzz lhs, rhs;
+    Pt lhs, rhs;
     if (step < per) {
       doit = load(step, rhs);
       lhs = acc;
@@ -1002,8 +1059,8 @@ __device__ __forceinline__ G1xyzz block_sum(int per, G1xyzz* sh, Load&& load) {
         rhs = sh[tid + stride];
       }
     }
-    G1xyzz r;
-    if (doit) r = xyzz_add(lhs, rhs);
+    Pt r;
+    if (doit) r = padd(lhs, rhs);
     if (step < per) {
       if (doit) acc = r;
     } else {
@@ -1037,6 +1094,88 @@ msm_bucket_large_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, co
     if (threadIdx.x == 0) buckets[k] = r;
     __syncthreads();
   }
+}
+
+// Fixed-base schedule, long carry runs (e.g. the Lagrange-basis commitments, whose small
+// witness values put ~40 % of the entries in bucket 0: ~12 k carries): the runs are cut
+// into pieces of kPieceCarries, each summed by one workgroup in radix 2^29 (kSumPer-deep
+// sequential adds + LDS tree), then one thread per bucket adds its pieces. One workgroup
+// per bucket (msm_bucket_large_kernel) took ~40 dependent additions plus conversions.
+static constexpr uint32_t kPieceCarries = (uint32_t)kSumThreads * kSumPer;
+
+__device__ __forceinline__ uint32_t carry_span(uint32_t chunk, const uint32_t* offsets, uint32_t k, uint32_t* c0) {
+  *c0 = offsets[k] / chunk;
+  return (offsets[k + 1] - 1) / chunk - *c0 + 1;
+}
+
+// off[i] = pieces of the listed buckets before i, off[count] = all (one workgroup)
+__global__ void __launch_bounds__(1024)
+msm_large_scan_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
+                      uint32_t* __restrict__ off) {
+  __shared__ uint32_t sh[1024];
+  const uint32_t count = large[0];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (count + 1023u) / 1024u;
+  const uint32_t i0 = tid * per < count ? tid * per : count;
+  const uint32_t i1 = i0 + per < count ? i0 + per : count;
+  auto pieces = [&](uint32_t i) {
+    uint32_t c0;
+    return (carry_span(chunk, offsets, large[1 + i], &c0) + kPieceCarries - 1) / kPieceCarries;
+  };
+  uint32_t sum = 0;
+  for (uint32_t i = i0; i < i1; i++) sum += pieces(i);
+  sh[tid] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint32_t v = tid >= d ? sh[tid - d] : 0u;
+    __syncthreads();
+    sh[tid] += v;
+    __syncthreads();
+  }
+  uint32_t base = sh[tid] - sum;
+  for (uint32_t i = i0; i < i1; i++) {
+    off[i] = base;
+    base += pieces(i);
+  }
+  if (tid == 1023) off[count] = sh[1023];
+}
+
+__global__ void __launch_bounds__(kSumThreads)
+msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
+                         const uint32_t* __restrict__ off, const Xyzz29* __restrict__ carry_own,
+                         const Xyzz29* __restrict__ carry_cont, Xyzz29* __restrict__ part) {
+  __shared__ Xyzz29 sh[kSumThreads];
+  const uint32_t count = large[0];
+  const uint32_t total = off[count];
+  for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
+    uint32_t lo = 0, hi = count;  // largest i with off[i] <= item
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (off[mid] <= item) lo = mid; else hi = mid;
+    }
+    uint32_t c0;
+    const uint32_t span = carry_span(chunk, offsets, large[1 + lo], &c0);
+    const uint32_t first = (item - off[lo]) * kPieceCarries;
+    const uint32_t n = span - first < kPieceCarries ? span - first : kPieceCarries;
+    const Xyzz29 r = block_sum<kSumThreads>(kSumPer, sh, [&](int step, Xyzz29& rhs) {
+      const uint32_t u = (uint32_t)step * kSumThreads + threadIdx.x;
+      if (u >= n) return false;
+      rhs = first + u ? carry_cont[c0 + first + u] : carry_own[c0];
+      return true;
+    });
+    if (threadIdx.x == 0) part[item] = r;
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(kMsmThreads)
+msm_large_final29_kernel(const uint32_t* __restrict__ large, const uint32_t* __restrict__ off,
+                         const Xyzz29* __restrict__ part, G1xyzz* __restrict__ buckets) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= large[0]) return;
+  Xyzz29 v = part[off[i]];
+  for (uint32_t j = off[i] + 1; j < off[i + 1]; j++) v = add29(v, part[j]);
+  buckets[large[1 + i]] = load_point(v);
 }
 
 // level 1: block (set w, slot j, part p). Slot 0 sums seg_tot[w][g] over all g; slot b+1
@@ -1188,6 +1327,9 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
     pair_off[1].alloc((size_t)fp.nkeys + 1);
     pair_pre.alloc(pair_grid(b1) * kPairThreads * kPairPer * 9);
     buckets29.alloc(max_keys);
+    large_off.alloc(max_keys + 2);
+    // pieces: sum over listed buckets of ceil(span / kPieceCarries) <= chunks / kPieceCarries + buckets
+    large_part.alloc(nthreads / kPieceCarries + max_keys + 1);
     carry_own29.alloc(nthreads);
     carry_cont29.alloc(nthreads);
     bin_counts.alloc((size_t)256 * ((maxp + kTileScalars - 1) / kTileScalars) + 256);  // + row totals
@@ -1368,9 +1510,10 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                          sc.sorted.p, acc_off, p.nkeys, nthreads, sc.buckets29.p, sc.carry_own29.p,
                          sc.carry_cont29.p);
     else if (chunk == kChunk && acc_waves == 3 && lds_indices())
-      hipLaunchKernelGGL((msm_accumulate29_kernel<3, false, true>), agrid, dim3(kMsmThreads), 0, st, chunk, gather,
-                         sc.sorted.p, sc.offsets.p, p.nkeys, nthreads, sc.buckets29.p, sc.carry_own29.p,
-                         sc.carry_cont29.p);
+      hipLaunchKernelGGL((paired_products() ? msm_accumulate29_kernel<3, false, true, true>
+                                            : msm_accumulate29_kernel<3, false, true, false>),
+                         agrid, dim3(kMsmThreads), 0, st, chunk, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads,
+                         sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
     else
       hipLaunchKernelGGL(acc_waves == 4 ? msm_accumulate29_kernel<4>
                                         : (acc_waves == 2 ? msm_accumulate29_kernel<2> : msm_accumulate29_kernel<3>),
@@ -1390,9 +1533,21 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                        (const Xyzz29*)sc.buckets29.p, (const Xyzz29*)sc.carry_own29.p,
                        (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p, sc.large.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_bucket_large_kernel<Xyzz29>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, chunk,
-                       acc_off,
-                       sc.large.p, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p);
+    if (!large_pieces()) {  // NZCB_LARGE_PIECES=0: one workgroup per long run (A/B runs)
+      hipLaunchKernelGGL(msm_bucket_large_kernel<Xyzz29>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, chunk,
+                         acc_off, sc.large.p, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p,
+                         sc.buckets.p);
+    } else {
+    hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, acc_off, sc.large.p,
+                       sc.large_off.p);
+    NZ_HIP(hipGetLastError());
+    hipLaunchKernelGGL(msm_large_piece29_kernel, dim3(kLargePieceBlocks), dim3(kSumThreads), 0, st, chunk, acc_off,
+                       sc.large.p, sc.large_off.p, (const Xyzz29*)sc.carry_own29.p,
+                       (const Xyzz29*)sc.carry_cont29.p, sc.large_part.p);
+    NZ_HIP(hipGetLastError());
+    hipLaunchKernelGGL(msm_large_final29_kernel, dim3(grid_for(p.nkeys, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0,
+                       st, sc.large.p, sc.large_off.p, sc.large_part.p, sc.buckets.p);
+    }
   } else {
     hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
                        (const G1xyzz*)nullptr, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p,

@@ -394,14 +394,16 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       F29 t1 = tile_ld(sl, i1), t3 = tile_ld(sl, i3);
       if (g) {
         const F29 wa = twa[ka];
-        t1 = mul29<Fr29>(t1, wa);
-        t3 = mul29<Fr29>(t3, wa);
+        F29 p1, p3;
+        mul29x2<Fr29>(t1, wa, t3, wa, p1, p3);
+        t1 = p1;
+        t3 = p3;
       }
       const F29 x0 = tile_ld(sl, i0), x2 = tile_ld(sl, i2);
       const F29 y0 = add_nn29(x0, t1), y1 = sub2r_nn29(x0, t1);
       const F29 y2 = add_nn29(x2, t3), y3 = sub2r_nn29(x2, t3);
-      const F29 u2 = mul29<Fr29>(y2, twb[ka]);
-      const F29 u3 = mul29<Fr29>(y3, twb[kc]);
+      F29 u2, u3;
+      mul29x2<Fr29>(y2, twb[ka], y3, twb[kc], u2, u3);
       F29 z0 = add_nn29(y0, u2), z2 = sub2r_nn29(y0, u2), z1 = add_nn29(y1, u3), z3 = sub2r_nn29(y1, u3);
       norm29(z0);
       norm29(z1);

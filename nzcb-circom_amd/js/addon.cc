@@ -410,6 +410,40 @@ napi_value VkFromZkeyFile(napi_env env, napi_callback_info info) {
   return res;
 }
 
+// remapWitnessProgram(program: Buffer, ownSym: Buffer, targetSym: Buffer) -> Buffer
+// (nzcb_wprog_remap); throws with .unmatched when target signals have no counterpart
+napi_value RemapWitnessProgram(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  const uint8_t *prog, *own, *tgt;
+  size_t pl, ol, tl;
+  if (argc < 3 || !buf_arg(env, argv[0], &prog, &pl) || !buf_arg(env, argv[1], &own, &ol) ||
+      !buf_arg(env, argv[2], &tgt, &tl)) {
+    napi_throw_type_error(env, nullptr, "remapWitnessProgram(program: Buffer, ownSym: Buffer, targetSym: Buffer)");
+    return nullptr;
+  }
+  uint8_t* out = nullptr;
+  size_t out_len = 0;
+  uint32_t miss = 0;
+  nzcb_err err{};
+  if (nzcb_wprog_remap(prog, pl, reinterpret_cast<const char*>(own), ol, reinterpret_cast<const char*>(tgt), tl, &out,
+                       &out_len, &miss, &err) != 0) {
+    napi_value e = make_error(env, err.code, err.msg);
+    napi_value m;
+    napi_create_uint32(env, miss, &m);
+    napi_set_named_property(env, e, "unmatched", m);
+    napi_throw(env, e);
+    return nullptr;
+  }
+  void* dst = nullptr;
+  napi_value res;
+  const napi_status stc = napi_create_buffer_copy(env, out_len, out, &dst, &res);
+  nzcb_free(out);
+  CHECK(stc);
+  return res;
+}
+
 // vkToJson(vk: Buffer) -> string (verification_key.json)
 napi_value VkToJson(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -573,6 +607,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"deviceCount", nullptr, DeviceCount, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"vkFromZkey", nullptr, VkFromZkey, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"vkFromZkeyFile", nullptr, VkFromZkeyFile, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"remapWitnessProgram", nullptr, RemapWitnessProgram, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"vkToJson", nullptr, VkToJson, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"verify", nullptr, Verify, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"calldata", nullptr, Calldata, nullptr, nullptr, nullptr, napi_default, nullptr},

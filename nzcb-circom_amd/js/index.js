@@ -199,7 +199,16 @@ function programInputs(prog) {
     const name = prog.toString('utf8', o, o + len); o += len;
     names.push([name, u32(o)]); o += 4;
   }
-  return { nWires: u32(8), names };
+  // a remapped program (wtns.remapProgram) writes witnesses of its wire map's length
+  const mapped = o + 8 <= prog.length && prog.toString('latin1', o, o + 4) === 'wmap';
+  return { nWires: mapped ? u32(o + 4) : u32(8), names };
+}
+
+// nzcb_wprog_remap: a witness program re-indexed to the wire order of another .sym (e.g.
+// circom's nzcp_live.sym, whose zkey expects circom's order), matching signals by name
+// against the program's own .sym. Arguments: Buffers or file names.
+function remapProgram(program, ownSym, targetSym) {
+  return addon.remapWitnessProgram(readBin(program), readBin(ownSym), readBin(targetSym));
 }
 
 const programs = new Map();
@@ -395,7 +404,7 @@ module.exports = {
   plonk: { setup, prove, fullProve, verify, exportSolidityCallData },
   zKey: { exportVerificationKey, exportSolidityVerifier },
   nzcp: Object.assign({}, require('./nzcp.js'), { witness: nzcpWitness }),
-  wtns: { calculate: wtnsCalculate },
+  wtns: { calculate: wtnsCalculate, remapProgram },
   version: addon.version,
   deviceCount: addon.deviceCount,
   _addon: addon,

@@ -433,10 +433,14 @@ class Circuit:
         return base, out
 
     # ---- serialisation -----------------------------------------------------------
-    def write_r1cs(self) -> bytes:
-        """iden3 r1cs v1 (the file circom --r1cs writes; read by nzcb_plonk_setup)."""
+    def write_r1cs(self, wire_map: dict | None = None) -> bytes:
+        """iden3 r1cs v1 (the file circom --r1cs writes; read by nzcb_plonk_setup).
+        wire_map: {wire: new index} renumbering every wire but 0 (the same constraints in
+        another wire order, e.g. the order of a .sym given to nzcb_wprog_remap)."""
         def le(x):
             return (x % R).to_bytes(32, "little")
+
+        wm = (lambda k: k if k == 0 else wire_map[k]) if wire_map else (lambda k: k)  # noqa: E731
 
         hdr = struct.pack("<I", 32) + R.to_bytes(32, "little")
         hdr += struct.pack("<IIIIQI", self.n_wires, self.n_out, self.n_pub_in, self.n_prv_in, self.n_wires,
@@ -446,8 +450,8 @@ class Circuit:
         for cons in self.constraints:
             for x in cons:
                 parts.append(pack_i(len(x)))
-                for k in sorted(x):
-                    parts.append(pack_i(k) + le(x[k]))
+                for k in sorted(x, key=wm):
+                    parts.append(pack_i(wm(k)) + le(x[k]))
         body = b"".join(parts)
         labels = struct.pack(f"<{self.n_wires}Q", *range(self.n_wires))
         return _binfile(b"r1cs", 1, [(1, hdr), (2, body), (3, labels)])

@@ -142,3 +142,57 @@ def test_nzcp_live_full_prove_real_circuit():
         nzcb.free_ptr(zkey[0])
     assert res[0][0] == ref_proof and res[0][1] == ref_pub[:96]
     assert split_proof == ref_proof and split_pub == res[0][1]
+
+
+def test_remapped_programs_on_gpu():
+    """nzcb_wprog_remap on the GPU: programs re-indexed to a permuted
+    .sym (tests/test_wprog_remap.py permuted_sym) write their witnesses in the target order.
+    * NZCPPubIdentity(1, 351, 0, 4, 2, 4), all 600,560 signals of a live pass: every wire
+      equals the CPU evaluation of the original program, moved to its target index;
+    * a reference test main (skipValue5_test): the remapped GPU witness proves against a
+      zkey set up from the r1cs written in the permuted order, byte-equal to the C port's
+      proof of the CPU witness on the same zkey and blinding.
+    Parity of the names with circom's own nzcp_live.sym stays unpinned."""
+    import nzcb
+    from nzcb import nzcpgen, nzcplive
+    from oracle import cbind, synth
+    from tests.test_wprog_remap import permuted_sym
+    c = nzcpgen.nzcp_pub_identity(**nzcpgen.LIVE)
+    prog = c.write_program()
+    sym, new = permuted_sym(c, 0x5E)
+    mapped = nzcb.wprog_remap(prog, c.write_sym(), sym)
+    case = C.case("live", nz.LIVE_PARAMS, C.live_tbs(), data=bytes(range(1, 21)))
+    wp = nzcb.WitnessProgram(mapped)
+    try:
+        assert wp.n_wires == c.n_wires
+        raw, st = wp.run(C.case_input_bytes(case), 1)
+    finally:
+        wp.close()
+    assert st == [0]
+    got = _ints(raw)
+    bits, ln, data = C.case_signals(case)
+    want, fail = wvm.evaluate(prog, bits + [ln] + data)
+    assert fail is None and got[0] == 1
+    assert all(got[new[k]] == want[k] for k in range(1, c.n_wires))
+    # a small main end to end: remapped GPU witness -> proof over the permuted r1cs
+    g = nzcpgen.wrapper_circuit("skipValue5_test")
+    gsym, gnew = permuted_sym(g, 0x5F)
+    gmapped = nzcb.wprog_remap(g.write_program(), g.write_sym(), gsym)
+    zkey = nzcb.plonk_setup(g.write_r1cs(gnew), nzcb.ptau_synth(12, 0x6E7A6362746175))
+    inputs = [0x83, 0x61, 0x71, 0x17, 0x17, 0]              # [\"q\", 23, 23]: nextPos 5
+    wp = nzcb.WitnessProgram(gmapped)
+    try:
+        raw, st = wp.run(b"".join(v.to_bytes(32, "little") for v in inputs), 1)
+    finally:
+        wp.close()
+    gw, gfail = wvm.evaluate(gmapped, inputs)
+    assert st == [0] and gfail is None and _ints(raw) == gw and gw[gnew[1]] == 5
+    bl = b"".join(x.to_bytes(32, "little") for x in synth.fixed_blindings())
+    ctx = nzcb.ProverContext(zkey)
+    try:
+        proof, pub = ctx.prove_witness_raw(raw, bl)
+        assert nzcb.verify(ctx.vk, proof, pub)
+    finally:
+        ctx.close()
+    ref_proof, ref_pub, _ = cbind.prove(zkey, nzcplive.wtns_file(raw), bl, npub=1)
+    assert proof == ref_proof and pub == ref_pub[:32]

@@ -55,6 +55,33 @@ const m = require('./');
 
 
 @needs_node
+def test_node_remap_program_matches_library(tmp_path):
+    """wtns.remapProgram (nzcb_wprog_remap through N-API) gives the library's bytes; an
+    unmatched .sym fails with .unmatched set."""
+    import nzcb
+    from nzcb import nzcpgen
+    from test_wprog_remap import permuted_sym
+    c = nzcpgen.wrapper_circuit("readMapLength_test")
+    sym, _ = permuted_sym(c, 9)
+    for name, data in (("p.nzwp", c.write_program()), ("own.sym", c.write_sym()), ("t.sym", sym),
+                       ("bad.sym", sym.replace(b"main.len", b"main.nope"))):
+        (tmp_path / name).write_bytes(data)
+    script = f"""
+const m = require('./');
+const fs = require('fs');
+const out = m.wtns.remapProgram('{tmp_path}/p.nzwp', '{tmp_path}/own.sym', '{tmp_path}/t.sym');
+fs.writeFileSync('{tmp_path}/mapped.nzwp', out);
+let bad = null;
+try {{ m.wtns.remapProgram('{tmp_path}/p.nzwp', '{tmp_path}/own.sym', '{tmp_path}/bad.sym'); }}
+catch (e) {{ bad = {{unmatched: e.unmatched, code: e.code}}; }}
+console.log(JSON.stringify({{bad}}));
+"""
+    d = json.loads(run_node(script))
+    assert (tmp_path / "mapped.nzwp").read_bytes() == nzcb.wprog_remap(c.write_program(), c.write_sym(), sym)
+    assert d["bad"] == {"unmatched": 1, "code": 2}
+
+
+@needs_node
 @pytest.mark.gpu
 def test_node_plonk_prove_golden():
     meta = json.load(open(os.path.join(GOLD, "p8.json")))
