@@ -60,7 +60,7 @@ def acc_pmc(src):
     """SQ / GRBM counters of the isolated accumulation (tools/acc_probe.py, two passes)."""
     vals, lines = {}, ["# rocprofv3 --pmc (two passes) -- python3 nzcb-circom_amd/tools/acc_probe.py",
                        "# fixed-base MSM alone, 2^21 + 6 points of random scalars, c = 17; "
-                       "msm_accumulate29_kernel<3, false>, averages over each pass's launches"]
+                       "msm_accumulate29_kernel<3, false, true, true>, averages over each pass's launches"]
     for d in ("pmcA", "pmcB"):
         agg = {}
         for f in glob.glob(os.path.join(src, d, "**", "*counter_collection.csv"), recursive=True):
@@ -116,8 +116,9 @@ def main():
     nw, write_kb = pmc_avg(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     fetch_raw = fetch_kb * 1024
     traffic = {
-        "kernel": "msm_accumulate29_kernel<3> (fixed-base bucket accumulation, 2^21+6-point MSM of random scalars, "
-                  "c=17: bench.py's probe, the last 10 launches of each pass)",
+        "kernel": "msm_accumulate29_kernel<3, false, true, true> (fixed-base bucket accumulation: LDS-staged "
+                  "indices, paired products; 2^21+6-point MSM of random scalars, c=17: bench.py's probe, the last 10 "
+                  "launches of each pass)",
         "command": "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate passes) -- python3 bench.py "
                    "--no-cpu-baseline --steps 8",
         "counters_kb_per_launch": {"FETCH_SIZE": {"launches": nf, "avg_kb_per_launch": round(fetch_kb, 1)},
@@ -142,6 +143,14 @@ def main():
     mb = os.path.join(src, "microbench.log")
     if os.path.exists(mb):
         shutil.copy(mb, os.path.join(out, f"{a.prefix}_microbench.txt"))
+    lane1 = os.path.join(src, "lane1")
+    if os.path.isdir(lane1):   # single-lane kernel breakdown per roctx phase (tools/phase_kernels.py)
+        txt = subprocess.run([sys.executable, os.path.join(HERE, "phase_kernels.py"), lane1, "--proofs", "4"],
+                             check=True, capture_output=True, text=True).stdout
+        with open(os.path.join(out, f"{a.prefix}_single_lane_phases.txt"), "w") as f:
+            f.write("# rocprofv3 --kernel-trace --marker-trace -- python3 bench.py --lanes 1 --steps 6 --warmup 2 "
+                    "--no-cpu-baseline --no-probe
+" + txt)
     print(psumm + summ)
 
 
