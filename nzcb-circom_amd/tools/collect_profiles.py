@@ -149,8 +149,7 @@ def main():
                              check=True, capture_output=True, text=True).stdout
         with open(os.path.join(out, f"{a.prefix}_single_lane_phases.txt"), "w") as f:
             f.write("# rocprofv3 --kernel-trace --marker-trace -- python3 bench.py --lanes 1 --steps 6 --warmup 2 "
-                    "--no-cpu-baseline --no-probe
-" + txt)
+                    "--no-cpu-baseline --no-probe\n" + txt)
     print(psumm + summ)
 
 
