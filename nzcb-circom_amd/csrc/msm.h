@@ -21,6 +21,9 @@ struct MsmBaseTable {
 // Window size of the table-based (fixed-base) MSM: 16..20 bits (NZCB_FB_WINDOW
 // overrides the default), i.e. 16..13 table rows and 2^15..2^19 buckets.
 int fixed_base_window();
+// Window of the Lagrange-basis table (A, B, C commitments of small witness values:
+// NZCB_LB_WINDOW, default 17): their few entries do not pay for a larger bucket set.
+int lagrange_window();
 
 struct MsmScratch {
   size_t max_points = 0;

@@ -41,6 +41,7 @@
 #include "f29.h"
 
 #include <atomic>
+#include <type_traits>
 #include <cstdlib>
 #include <rocprim/rocprim.hpp>
 
@@ -117,6 +118,7 @@ static constexpr int kSumPer = 4;        // level-1 sums: sequential adds per th
 static constexpr int kPartThreads = 64;  // level-2 sums: block size
 static constexpr uint32_t kSeqSpan = 64;  // finalize: longest carry run summed by one thread
 static constexpr int kLargeBlocks = 32;  // finalize: workgroups for the longer runs
+static constexpr int kFbWindow = 17;     // fixed-base window of the PTau tables (NZCB_FB_WINDOW)
 static constexpr int kLargePieceBlocks = 512;  // fixed base: workgroups over the pieces of the longer runs
 
 // LDS-staged bucket indices in the accumulation (msm_accumulate29_kernel kLdsIdx);
@@ -150,6 +152,15 @@ static bool large_pieces() {
 int fixed_base_window() {
   static const int c = [] {
     const char* e = std::getenv("NZCB_FB_WINDOW");
+    const int v = e ? std::atoi(e) : kFbWindow;
+    return (v >= 16 && v <= 20) ? v : kFbWindow;
+  }();
+  return c;
+}
+
+int lagrange_window() {
+  static const int c = [] {
+    const char* e = std::getenv("NZCB_LB_WINDOW");
     const int v = e ? std::atoi(e) : 17;
     return (v >= 16 && v <= 20) ? v : 17;
   }();
@@ -305,11 +316,20 @@ __device__ __forceinline__ uint32_t bin_entries(const Fr* __restrict__ scalars, 
   return live;
 }
 
+// bucket index bits below the high byte: 8 for c <= 17 (16-bit indices), c - 9 above
+// (c = 20: 19-bit indices, 256 high-byte regions of 2048 buckets)
+template <int C> struct BinKeys {
+  static constexpr int LO = C - 9 > 8 ? C - 9 : 8;
+  using Lo = typename std::conditional<LO <= 8, uint8_t, uint16_t>::type;      // low part, per entry
+  using Full = typename std::conditional<C <= 17, uint16_t, uint32_t>::type;   // whole index, in LDS
+};
+
 template <int C>
 __global__ void __launch_bounds__(kBinThreads)
 msm_bin_hist_kernel(const Fr* __restrict__ scalars, size_t n, int mont, uint32_t* __restrict__ counts,
                     uint32_t ntiles) {
   constexpr int NW = (255 + C - 1) / C;
+  constexpr int LO = BinKeys<C>::LO;
   __shared__ uint32_t h[256];
   h[threadIdx.x] = 0;
   __syncthreads();
@@ -321,7 +341,7 @@ msm_bin_hist_kernel(const Fr* __restrict__ scalars, size_t n, int mont, uint32_t
       const uint32_t live = bin_entries<C, NW>(scalars, i, mont, 0, kk, vv);
 #pragma unroll
       for (int w = 0; w < NW; w++)
-        if ((live >> w) & 1u) atomicAdd(&h[kk[w] >> 8], 1u);
+        if ((live >> w) & 1u) atomicAdd(&h[kk[w] >> LO], 1u);
     }
   }
   __syncthreads();
@@ -374,13 +394,14 @@ msm_bin_rowscan_kernel(uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t*
 template <int C>
 __global__ void __launch_bounds__(kBinThreads)
 msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t stride,
-                       const uint32_t* __restrict__ counts, uint32_t ntiles, uint8_t* __restrict__ lo2,
+                       const uint32_t* __restrict__ counts, uint32_t ntiles, typename BinKeys<C>::Lo* __restrict__ lo2,
                        uint32_t* __restrict__ vals2) {
   constexpr int NW = (255 + C - 1) / C;
   constexpr int TE = kTileScalars * NW;  // entries per tile, at most
+  constexpr int LO = BinKeys<C>::LO;
   __shared__ uint32_t lcount[256], lstart[256], gbase[256];
   __shared__ uint32_t lval[TE];
-  __shared__ uint16_t lkey[TE];
+  __shared__ typename BinKeys<C>::Full lkey[TE];
   __shared__ uint32_t wsum[4];
   const uint32_t* tail = counts + (size_t)256 * ntiles;  // row totals
   {
@@ -399,7 +420,7 @@ msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_
       live[j] = bin_entries<C, NW>(scalars, i, mont, stride, kk[j], vv[j]);
 #pragma unroll
       for (int w = 0; w < NW; w++)
-        if ((live[j] >> w) & 1u) rk[j][w] = atomicAdd(&lcount[kk[j][w] >> 8], 1u);
+        if ((live[j] >> w) & 1u) rk[j][w] = atomicAdd(&lcount[kk[j][w] >> LO], 1u);
     }
   }
   __syncthreads();
@@ -413,102 +434,121 @@ msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_
 #pragma unroll
     for (int w = 0; w < NW; w++) {
       if ((live[j] >> w) & 1u) {
-        const uint32_t q = lstart[kk[j][w] >> 8] + rk[j][w];
-        lkey[q] = (uint16_t)kk[j][w];
+        const uint32_t q = lstart[kk[j][w] >> LO] + rk[j][w];
+        lkey[q] = (typename BinKeys<C>::Full)kk[j][w];
         lval[q] = vv[j][w];
       }
     }
   }
   __syncthreads();
   for (uint32_t q = threadIdx.x; q < total; q += kBinThreads) {  // runs of one high byte: coalesced
-    const uint32_t key = lkey[q], hb = key >> 8;
+    const uint32_t key = lkey[q], hb = key >> LO;
     const uint32_t pos = gbase[hb] + (q - lstart[hb]);
-    lo2[pos] = (uint8_t)key;
+    lo2[pos] = (typename BinKeys<C>::Lo)(key & ((1u << LO) - 1u));
     vals2[pos] = lval[q];
   }
 }
 
+// exclusive scan in place of a[0..count) by an NT-thread workgroup (every thread calls it,
+// after a barrier that completes a[]); returns the total. wsum: NT / 64 words of LDS.
+template <int NT>
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t* a, uint32_t count, uint32_t* wsum) {
+  const uint32_t per = (count + NT - 1) / NT;
+  const uint32_t b = threadIdx.x * per;
+  uint32_t loc = 0;
+  for (uint32_t i = 0; i < per; i++)
+    if (b + i < count) loc += a[b + i];
+  const uint32_t inc = wave_incl_scan(loc);
+  if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; w++) {
+    if (w < (int)(threadIdx.x >> 6)) off += wsum[w];
+    tot += wsum[w];
+  }
+  uint32_t run = off + inc - loc;
+  for (uint32_t i = 0; i < per; i++)
+    if (b + i < count) {
+      const uint32_t v = a[b + i];
+      a[b + i] = run;
+      run += v;
+    }
+  __syncthreads();
+  return tot;
+}
+
+template <int LO>
 __global__ void __launch_bounds__(kLoThreads)
-msm_bucket_lo_kernel(const uint8_t* __restrict__ lo2, const uint32_t* __restrict__ vals2,
-                     const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t nkeys,
-                     uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted, uint32_t* __restrict__ large) {
+msm_bucket_lo_kernel(const typename std::conditional<LO <= 8, uint8_t, uint16_t>::type* __restrict__ lo2,
+                     const uint32_t* __restrict__ vals2, const uint32_t* __restrict__ counts, uint32_t ntiles,
+                     uint32_t nkeys, uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted,
+                     uint32_t* __restrict__ large) {
+  using Lo = typename std::conditional<LO <= 8, uint8_t, uint16_t>::type;
+  constexpr uint32_t NL = 1u << LO;  // buckets per high-byte region
   constexpr uint32_t U = 8;
-  __shared__ uint32_t h[256], lcnt[256], lst[256];  // lst[0] first holds the region start
-  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t h[NL], lcnt[NL], lst[NL];
+  __shared__ uint32_t wsum[kLoThreads / 64], reg[1];
   __shared__ uint32_t lv[U * kLoThreads];
-  __shared__ uint8_t lk[U * kLoThreads];
+  __shared__ Lo lk[U * kLoThreads];
   const uint32_t hb = blockIdx.x;
   const uint32_t* tail = counts + (size_t)256 * ntiles;  // row totals
   {
     uint32_t tot;
     const uint32_t st = scan256_excl(threadIdx.x < 256 ? tail[threadIdx.x] : 0u, wsum, tot);
-    if (threadIdx.x == hb) lst[0] = st;  // this region's start
-    if (threadIdx.x < 256) h[threadIdx.x] = 0;
+    if (threadIdx.x == hb) reg[0] = st;  // this region's start
   }
+  for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) h[i] = 0;
   __syncthreads();
-  const uint32_t s = lst[0];
+  const uint32_t s = reg[0];
   const uint32_t e = s + tail[hb];
-  __syncthreads();
   // 8 independent loads in flight per thread before their atomics (the loop is
-  // latency-bound otherwise: one workgroup per CU walks ~n*15/256 entries)
+  // latency-bound otherwise: one workgroup per CU walks ~entries/256 entries)
   for (uint32_t p0 = s; p0 < e; p0 += U * kLoThreads) {
     uint32_t k8[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; u++) {
       const uint32_t p = p0 + u * kLoThreads + threadIdx.x;
-      k8[u] = p < e ? (uint32_t)lo2[p] : 256u;
+      k8[u] = p < e ? (uint32_t)lo2[p] : NL;
     }
 #pragma unroll
     for (uint32_t u = 0; u < U; u++)
-      if (k8[u] < 256u) atomicAdd(&h[k8[u]], 1u);
+      if (k8[u] < NL) atomicAdd(&h[k8[u]], 1u);
   }
   __syncthreads();
-  // exclusive scan of the 256 low-byte counts -> bucket offsets (waves 0-3)
-  const uint32_t v = threadIdx.x < 256 ? h[threadIdx.x] : 0u;
-  const uint32_t inc = wave_incl_scan(v);
-  if (threadIdx.x < 256 && (threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = inc;
-  __syncthreads();
-  if (threadIdx.x < 256) {
-    uint32_t off = s;
-    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) off += wsum[w];
-    h[threadIdx.x] = off + inc - v;
-    const uint32_t key = (hb << 8) | threadIdx.x;
-    if (key < nkeys) offsets[key] = off + inc - v;
+  block_scan_excl<kLoThreads>(h, NL, wsum);  // low-index counts -> bucket offsets in the region
+  for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) {
+    h[i] += s;
+    const uint32_t key = (hb << LO) | i;
+    if (key < nkeys) offsets[key] = h[i];
   }
   if (hb == 255 && threadIdx.x == 0) offsets[nkeys] = e;  // entries in all: the last region's end
   if (hb == 0 && threadIdx.x == 0) large[0] = 0;          // the finalize's count of long bucket runs
   __syncthreads();
-  // scatter in chunks of U * kLoThreads entries, each ranked by low byte in LDS first and
+  // scatter in chunks of U * kLoThreads entries, each ranked by low index in LDS first and
   // written out run by run (coalesced)
   for (uint32_t p0 = s; p0 < e; p0 += U * kLoThreads) {
     uint32_t k8[U], v8[U], r8[U];
-    if (threadIdx.x < 256) lcnt[threadIdx.x] = 0;
+    for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) lcnt[i] = 0;
     __syncthreads();
 #pragma unroll
     for (uint32_t u = 0; u < U; u++) {
       const uint32_t p = p0 + u * kLoThreads + threadIdx.x;
-      k8[u] = p < e ? (uint32_t)lo2[p] : 256u;
+      k8[u] = p < e ? (uint32_t)lo2[p] : NL;
       v8[u] = p < e ? vals2[p] : 0u;
     }
 #pragma unroll
     for (uint32_t u = 0; u < U; u++)
-      if (k8[u] < 256u) r8[u] = atomicAdd(&lcnt[k8[u]], 1u);
+      if (k8[u] < NL) r8[u] = atomicAdd(&lcnt[k8[u]], 1u);
     __syncthreads();
-    const uint32_t c = threadIdx.x < 256 ? lcnt[threadIdx.x] : 0u;
-    const uint32_t ci = wave_incl_scan(c);
-    if (threadIdx.x < 256 && (threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = ci;
+    for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) lst[i] = lcnt[i];
     __syncthreads();
-    if (threadIdx.x < 256) {
-      uint32_t off = 0;
-      for (int w = 0; w < (int)(threadIdx.x >> 6); w++) off += wsum[w];
-      lst[threadIdx.x] = off + ci - c;
-    }
-    __syncthreads();
+    block_scan_excl<kLoThreads>(lst, NL, wsum);
 #pragma unroll
     for (uint32_t u = 0; u < U; u++)
-      if (k8[u] < 256u) {
+      if (k8[u] < NL) {
         const uint32_t q = lst[k8[u]] + r8[u];
-        lk[q] = (uint8_t)k8[u];
+        lk[q] = (Lo)k8[u];
         lv[q] = v8[u];
       }
     __syncthreads();
@@ -518,7 +558,7 @@ msm_bucket_lo_kernel(const uint8_t* __restrict__ lo2, const uint32_t* __restrict
       sorted[h[k] + (q - lst[k])] = lv[q];
     }
     __syncthreads();
-    if (threadIdx.x < 256) h[threadIdx.x] += c;
+    for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) h[i] += lcnt[i];
   }
 }
 
@@ -1295,9 +1335,11 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
     fit(make_plan(m, nullptr));
     if (m == maxp) break;
   }
-  if (fixed_base) {
+  if (fixed_base) {  // the PTau tables' window and the Lagrange table's
     MsmBaseTable t;
     t.c = fixed_base_window();
+    fit(make_plan(maxp, &t));
+    t.c = lagrange_window();
     fit(make_plan(maxp, &t));
   }
   offsets.alloc(max_keys + 1);
@@ -1319,12 +1361,15 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
   if (fixed_base) {
     MsmBaseTable t;
     t.c = fixed_base_window();
-    const MsmPlan fp = make_plan(maxp, &t);
-    const size_t b1 = pair_bound(fp.entries, fp.nkeys), b2 = pair_bound(b1, fp.nkeys);
+    MsmPlan fp = make_plan(maxp, &t);
+    t.c = lagrange_window();
+    const MsmPlan lp = make_plan(maxp, &t);
+    if (lp.entries > fp.entries) fp = lp;
+    const size_t b1 = pair_bound(fp.entries, std::min(fp.nkeys, lp.nkeys)), b2 = pair_bound(b1, std::min(fp.nkeys, lp.nkeys));
     pair_pts[0].alloc(b1 ? b1 : 1);
     pair_pts[1].alloc(b2 ? b2 : 1);
-    pair_off[0].alloc((size_t)fp.nkeys + 1);
-    pair_off[1].alloc((size_t)fp.nkeys + 1);
+    pair_off[0].alloc((size_t)max_keys + 1);
+    pair_off[1].alloc((size_t)max_keys + 1);
     pair_pre.alloc(pair_grid(b1) * kPairThreads * kPairPer * 9);
     buckets29.alloc(max_keys);
     large_off.alloc(max_keys + 2);
@@ -1414,32 +1459,36 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     if (phases) NZ_HIP(hipEventRecord(sc.ev[i], st));
   };
   mark(0);
-  const bool bins = table && (p.c == 16 || p.c == 17) && !use_library_sort() && sc.bin_counts.p;
+  const bool bins = table && p.c >= 16 && p.c <= 20 && !use_library_sort() && sc.bin_counts.p;
   if (bins) {  // hand-written bucketing (see msm_bin_hist_kernel)
     const uint32_t ntiles = (uint32_t)((n + kTileScalars - 1) / kTileScalars);
-    uint8_t* lo2 = (uint8_t*)sc.keys_out.p;
     uint32_t* tail = sc.bin_counts.p + (size_t)256 * ntiles;
     const int m = mont ? 1 : 0;
-    if (p.c == 17)
-      hipLaunchKernelGGL(msm_bin_hist_kernel<17>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
+    auto run_bins = [&](auto cc) {
+      constexpr int C = decltype(cc)::value;
+      using Lo = typename BinKeys<C>::Lo;
+      Lo* lo2 = (Lo*)sc.keys_out.p;
+      hipLaunchKernelGGL(msm_bin_hist_kernel<C>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
                          sc.bin_counts.p, ntiles);
-    else
-      hipLaunchKernelGGL(msm_bin_hist_kernel<16>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
-                         sc.bin_counts.p, ntiles);
-    NZ_HIP(hipGetLastError());
-    mark(1);
-    hipLaunchKernelGGL(msm_bin_rowscan_kernel, dim3(256), dim3(256), 0, st, sc.bin_counts.p, ntiles, tail);
-    if (p.c == 17)
-      hipLaunchKernelGGL(msm_bin_scatter_kernel<17>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
+      NZ_HIP(hipGetLastError());
+      mark(1);
+      hipLaunchKernelGGL(msm_bin_rowscan_kernel, dim3(256), dim3(256), 0, st, sc.bin_counts.p, ntiles, tail);
+      hipLaunchKernelGGL(msm_bin_scatter_kernel<C>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
                          table->stride, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
-    else
-      hipLaunchKernelGGL(msm_bin_scatter_kernel<16>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, m,
-                         table->stride, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
-    NZ_HIP(hipGetLastError());
-    mark(2);
-    hipLaunchKernelGGL(msm_bucket_lo_kernel, dim3(256), dim3(kLoThreads), 0, st, lo2, sc.vals_mid.p,
-                       sc.bin_counts.p, ntiles, p.nkeys, sc.offsets.p, sc.sorted.p, sc.large.p);
-    NZ_HIP(hipGetLastError());
+      NZ_HIP(hipGetLastError());
+      mark(2);
+      hipLaunchKernelGGL(msm_bucket_lo_kernel<BinKeys<C>::LO>, dim3(256), dim3(kLoThreads), 0, st,
+                         (const Lo*)lo2, sc.vals_mid.p, sc.bin_counts.p, ntiles, p.nkeys, sc.offsets.p,
+                         sc.sorted.p, sc.large.p);
+      NZ_HIP(hipGetLastError());
+    };
+    switch (p.c) {
+      case 16: run_bins(std::integral_constant<int, 16>()); break;
+      case 17: run_bins(std::integral_constant<int, 17>()); break;
+      case 18: run_bins(std::integral_constant<int, 18>()); break;
+      case 19: run_bins(std::integral_constant<int, 19>()); break;
+      default: run_bins(std::integral_constant<int, 20>()); break;
+    }
   } else {
     keys_dispatch(p.c, scalars, n, mont ? 1 : 0, table, sc, st);
     mark(1);

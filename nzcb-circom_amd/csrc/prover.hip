@@ -579,7 +579,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   if (lcommit) {  // one elliptic-curve iNTT per context (csrc/lagrange.hip)
     ltau.alloc((size_t)n + 2);
     lagrange_basis(ptau.p, ptau.n, power, ltau.p, s);
-    ltab.build(ltau.p, ltau.n, fixed_base_window(), s);
+    ltab.build(ltau.p, ltau.n, lagrange_window(), s);
   }
   up(qm, z.qm);
   up(ql, z.ql);

@@ -61,6 +61,24 @@ def build(params: dict = nzcpgen.LIVE, cache: bool = True):
     return r1cs, prog, c
 
 
+def write_artifacts(out_dir: str, params: dict = nzcpgen.LIVE, name: str = "nzcp_live") -> dict:
+    """The compiler outputs circom would write for the circuit, from this build's generator:
+    <name>.r1cs (circom --r1cs), <name>.nzwp (the GPU witness program, in place of
+    <name>.wasm) and <name>.nzwp.sym (circom --sym layout: "label,wire,component,name"),
+    the own .sym that nzcb_wprog_remap / wtns.remapProgram match against circom's
+    <name>.sym. Returns {kind: path}."""
+    c = nzcpgen.nzcp_pub_identity(**params)
+    os.makedirs(out_dir, exist_ok=True)
+    out = {}
+    for kind, ext, data in (("r1cs", ".r1cs", c.write_r1cs()), ("program", ".nzwp", c.write_program()),
+                            ("sym", ".nzwp.sym", c.write_sym())):
+        path = os.path.join(out_dir, name + ext)
+        with open(path, "wb") as f:
+            f.write(data)
+        out[kind] = path
+    return out
+
+
 PTAU_POWER = 21                 # powersOfTau28_hez_final_21.ptau (/root/reference/README.md:40)
 
 

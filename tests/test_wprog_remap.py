@@ -98,3 +98,16 @@ def test_remap_subset_target():
     base, _ = wvm.evaluate(prog, [1, 2, 3, 2])
     got, _ = wvm.evaluate(mapped, [1, 2, 3, 2])
     assert len(got) == len(keep) + 1 and got[1:] == [base[w] for w in keep]
+
+
+def test_write_artifacts(tmp_path):
+    """nzcplive.write_artifacts: r1cs, program and its .sym for a circuit, consistent with
+    each other (the remap of the program onto its own .sym is the identity)."""
+    from nzcb import nzcplive
+    from oracle import r1cs as r1
+    out = nzcplive.write_artifacts(str(tmp_path), params=dict(nzcpgen.EXAMPLE), name="nzcp_example")
+    prog, sym = open(out["program"], "rb").read(), open(out["sym"], "rb").read()
+    rd = r1.read_r1cs(open(out["r1cs"], "rb").read())
+    assert rd["nWires"] == wvm.parse(prog)["n_wires"] == len(sym.splitlines()) + 1
+    same = nzcb.wprog_remap(prog, sym, sym)
+    assert wvm.parse(same)["wmap"] == list(range(rd["nWires"]))
