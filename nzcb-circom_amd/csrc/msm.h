@@ -35,6 +35,7 @@ struct MsmScratch {
   // fixed-base bucketing (msm.hip msm_keys_hist_kernel): per (high key byte, tile)
   // counts, scanned in place, and the values grouped by high byte
   DevBuf<uint32_t> bin_counts, vals_mid;
+  DevBuf<uint32_t> lo_seg;    // per (bucket_lo work item, low index): count, then its first position
   DevBuf<G1xyzz> buckets;     // buckets whose entries lie in one accumulation chunk
   DevBuf<G1xyzz> carry_own;   // per chunk: partial sum of a bucket that starts in the chunk and spills over
   DevBuf<G1xyzz> carry_cont;  // per chunk: partial sum of a bucket that began in an earlier chunk
@@ -49,6 +50,8 @@ struct MsmScratch {
   DevBuf<uint32_t> large;     // [count, bucket ids...] of buckets with long carry runs
   DevBuf<uint32_t> large_off;  // fixed base: piece offsets of the listed buckets (msm_large_scan_kernel)
   DevBuf<Xyzz29> large_part;   // fixed base: one partial sum per piece
+  DevBuf<Xyzz29> parts29;      // fixed base: per (sum slot, part) partial sums (msm_seg29 / msm_bitsums29)
+  DevBuf<Xyzz29> seg_tot29, seg_run29;  // fixed base: per kSeg29-bucket segment (msm_seg29_kernel)
   DevBuf<G1xyzz> seg_tot;     // per (bucket set, segment): sum_j (j+1) * bucket_j
   DevBuf<G1xyzz> seg_run;     // per (bucket set, segment): sum_j bucket_j
   DevBuf<G1xyzz> parts;       // per (set, sum slot, part): partial plain sums
@@ -57,6 +60,7 @@ struct MsmScratch {
   size_t host_win_cap = 0;
   // shape of the MSM in flight (set by msm_enqueue, used by msm_finish)
   int cur_c = 0, cur_nsets = 0, cur_nbits = 0, cur_seglen = 0;
+  bool cur_bitsums = false;
   size_t cur_n = 0;
   uint32_t cur_nkeys = 0;
   // optional HIP-event timing: accumulation kernel (bench.py roofline) and, with

@@ -117,9 +117,19 @@ static constexpr int kSumThreads = 256;  // level-1 sums: block size
 static constexpr int kSumPer = 4;        // level-1 sums: sequential adds per thread
 static constexpr int kPartThreads = 64;  // level-2 sums: block size
 static constexpr uint32_t kSeqSpan = 64;  // finalize: longest carry run summed by one thread
+// the same for the fixed-base (radix 2^29) carries: at 2^21 random scalars a bucket spans
+// ~11 chunks; the Lagrange-basis commitments' skewed digits leave a few hundred buckets
+// with 17..1000s of carries, and a thread walking 64 of them sequentially was the
+// finalize's long pole (0.8 ms per launch, profiles/r3_single_lane_phases.txt)
+static constexpr uint32_t kSeqSpan29 = 16;
 static constexpr int kLargeBlocks = 32;  // finalize: workgroups for the longer runs
 static constexpr int kFbWindow = 17;     // fixed-base window of the PTau tables (NZCB_FB_WINDOW)
-static constexpr int kLargePieceBlocks = 512;  // fixed base: workgroups over the pieces of the longer runs
+// fixed base: workgroups over the pieces of the longer runs, and over their buckets (grid-
+// stride; random scalars list none, and under 5 proof lanes every launched workgroup waits
+// for a CU slot first, so the grids are kept small)
+static constexpr int kLargePieceBlocks = 128;
+static constexpr int kLargeFinalBlocks = 128;
+static constexpr int kLargeFinalThreads = 64;
 
 // LDS-staged bucket indices in the accumulation (msm_accumulate29_kernel kLdsIdx);
 // NZCB_ACC_LDS=0 reads them from HBM as before (A/B runs)
@@ -140,13 +150,27 @@ static bool paired_products() {
   }();
   return on;
 }
-// long carry runs summed in pieces (msm_large_piece29_kernel); NZCB_LARGE_PIECES=0 for A/B
-static bool large_pieces() {
+// fixed base, the window sum sum_k (k + 1) B_k (NZCB_FB_SUMS, for A/B runs):
+//   2 (default) segments of kSeg29 buckets + bit-slot sums, radix 2^29 (msm_seg29_kernel)
+//   1           bit slots over the buckets themselves (msm_bitsums29_kernel)
+//   0           the generic schedule's 8x32 segment reduce + slot sums
+// Same box (profiles/r3_fb_sums_ab.txt): 1 cut the isolated MSM 3.48 -> 3.08 ms but moved
+// 4x the additions of 0 (every bucket in ~8 slots) and the 5-lane bench lost 2 %.
+static bool lo_agg() {  // NZCB_LO_AGG=1: wave-aggregated LDS atomics in msm_lo_* (A/B runs)
   static const bool on = [] {
-    const char* e = std::getenv("NZCB_LARGE_PIECES");
-    return !(e && e[0] == '0');
+    const char* e = std::getenv("NZCB_LO_AGG");
+    return e && e[0] == '1';
   }();
   return on;
+}
+
+static int fb_sums() {
+  static const int v = [] {
+    const char* e = std::getenv("NZCB_FB_SUMS");
+    const int x = e ? std::atoi(e) : 2;
+    return x >= 0 && x <= 2 ? x : 2;
+  }();
+  return v;
 }
 
 int fixed_base_window() {
@@ -282,7 +306,7 @@ msm_keys_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t strid
 //                             the 15 entries), ranked in LDS by high byte, then written
 //                             out run by run (coalesced) into the high-byte regions: the
 //                             value and the key's low byte
-//   4. msm_bucket_lo_kernel   one workgroup per high byte: low-byte histogram of its
+//   4. msm_lo_*_kernel        per high byte (split into segments, see below): low-byte histogram of its
 //                             region, local scan -> the 256 bucket offsets, scatter
 // Order inside a bucket is whatever the LDS atomics give: the accumulation adds the
 // bucket's points in any order and the sum is the same point.
@@ -293,6 +317,28 @@ static constexpr int kBinThreads = 256;
 static constexpr int kBinPer = 2;                                  // scalars per thread and tile
 static constexpr uint32_t kTileScalars = kBinThreads * kBinPer;    // 512
 static constexpr int kLoThreads = 512;
+
+// old = atomicAdd(&cnt[k], 1) for the lanes with `active`, where the lanes sharing the
+// first active lane's key are served by ONE atomic of their count (each gets the old
+// count plus its rank among them, an order the plain atomics could have given too).
+// Same-address LDS atomics serialize: the Lagrange-basis commitments of 0/1-heavy witness
+// columns put ~all of a region's entries in one bucket, and a workgroup walking 2^21 of
+// them paid 64 cycles per wave-instruction (1.7 ms per launch, profiles/r3_single_lane_
+// phases.txt). Every active lane of the wave calls it at the same point.
+__device__ __forceinline__ uint32_t wave_agg_inc(uint32_t* cnt, uint32_t k, bool active) {
+  const uint64_t act = __ballot(active);
+  if (act == 0) return 0u;
+  const int lead = __builtin_ctzll(act);
+  const uint32_t k0 = __builtin_amdgcn_readlane(k, lead);
+  const bool same = active && k == k0;
+  const uint64_t m = __ballot(same);
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  uint32_t base = 0;
+  if ((int)__lane_id() == lead) base = atomicAdd(&cnt[k0], (uint32_t)__popcll(m));
+  base = __builtin_amdgcn_readlane(base, lead);
+  if (same) return base + below;
+  return active ? atomicAdd(&cnt[k], 1u) : 0u;
+}
 
 // the (key, value) of every window of scalar i; bit w of the result is set for the
 // windows with a nonzero digit (zero digits make no entry: a scalar of b bits costs about
@@ -478,82 +524,161 @@ __device__ __forceinline__ uint32_t block_scan_excl(uint32_t* a, uint32_t count,
   return tot;
 }
 
-template <int LO>
-__global__ void __launch_bounds__(kLoThreads)
-msm_bucket_lo_kernel(const typename std::conditional<LO <= 8, uint8_t, uint16_t>::type* __restrict__ lo2,
-                     const uint32_t* __restrict__ vals2, const uint32_t* __restrict__ counts, uint32_t ntiles,
-                     uint32_t nkeys, uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted,
-                     uint32_t* __restrict__ large) {
-  using Lo = typename std::conditional<LO <= 8, uint8_t, uint16_t>::type;
-  constexpr uint32_t NL = 1u << LO;  // buckets per high-byte region
-  constexpr uint32_t U = 8;
-  __shared__ uint32_t h[NL], lcnt[NL], lst[NL];
-  __shared__ uint32_t wsum[kLoThreads / 64], reg[1];
-  __shared__ uint32_t lv[U * kLoThreads];
-  __shared__ Lo lk[U * kLoThreads];
-  const uint32_t hb = blockIdx.x;
-  const uint32_t* tail = counts + (size_t)256 * ntiles;  // row totals
-  {
-    uint32_t tot;
-    const uint32_t st = scan256_excl(threadIdx.x < 256 ? tail[threadIdx.x] : 0u, wsum, tot);
-    if (threadIdx.x == hb) reg[0] = st;  // this region's start
+// Step 4 runs over work items of at most kLoSeg entries (the segments of the high-byte
+// regions, in region order), so a region holding most of the entries (the Lagrange-basis
+// commitments of 0/1-heavy witness columns: ~all 2^21 entries in bucket 0's region) is
+// spread over many workgroups instead of one (1.2 ms for that region's single workgroup
+// even with aggregated atomics; 0.1 ms for random scalars):
+//   a. msm_lo_count_kernel   per item: low-index histogram of its segment -> segoff[item][.]
+//   b. msm_lo_scan_kernel    per region: exclusive scan over its items per bucket, the
+//                            bucket offsets (scan over the buckets), segoff += bucket offset
+//   c. msm_lo_scatter_kernel per item: ranked in LDS chunk by chunk, written run by run
+static constexpr uint32_t kLoSeg = 32768;
+static constexpr uint32_t kLoU = 8;  // entries per thread and chunk
+
+// kAgg (NZCB_LO_AGG=1): the lanes sharing a key served by one LDS atomic (wave_agg_inc);
+// by default plain atomics: with regions cut into kLoSeg segments a hot bucket's
+// same-address conflicts cost ~15 us per workgroup, and the aggregation's ~10 extra
+// instructions per entry ran on every entry of every MSM
+template <bool kAgg>
+__device__ __forceinline__ uint32_t lo_inc(uint32_t* cnt, uint32_t k, bool active) {
+  if (kAgg) return wave_agg_inc(cnt, k, active);
+  return active ? atomicAdd(&cnt[k], 1u) : 0u;
+}
+
+// rs[r] = first entry of high-byte region r, rf[r] = its first work item (rf[256] = all
+// items). Every thread of the workgroup calls it (barriers inside).
+__device__ __forceinline__ void lo_regions(const uint32_t* __restrict__ tail, uint32_t* wsum, uint32_t* rs,
+                                           uint32_t* rf) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t cnt = t < 256 ? tail[t] : 0u;
+  uint32_t tot, nitems;
+  const uint32_t st = scan256_excl(cnt, wsum, tot);
+  const uint32_t f = scan256_excl((cnt + kLoSeg - 1) / kLoSeg, wsum, nitems);
+  if (t < 256) {
+    rs[t] = st;
+    rf[t] = f;
   }
+  if (t == 0) rf[256] = nitems;
+  __syncthreads();
+}
+
+// the region of work item `item` (< rf[256]): the largest r with rf[r] <= item
+__device__ __forceinline__ uint32_t lo_region_of(const uint32_t* rf, uint32_t item) {
+  uint32_t lo = 0, hi = 256;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (rf[mid] <= item) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+template <int LO, bool kAgg>
+__global__ void __launch_bounds__(kLoThreads)
+msm_lo_count_kernel(const typename std::conditional<LO <= 8, uint8_t, uint16_t>::type* __restrict__ lo2,
+                    const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* __restrict__ segoff) {
+  constexpr uint32_t NL = 1u << LO;
+  __shared__ uint32_t h[NL], wsum[kLoThreads / 64], rs[256], rf[257];
+  lo_regions(counts + (size_t)256 * ntiles, wsum, rs, rf);
+  const uint32_t item = blockIdx.x;
+  if (item >= rf[256]) return;
+  const uint32_t r = lo_region_of(rf, item);
+  const uint32_t* tail = counts + (size_t)256 * ntiles;
+  const uint32_t s = rs[r] + (item - rf[r]) * kLoSeg;
+  const uint32_t e = min(rs[r] + tail[r], s + kLoSeg);
   for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) h[i] = 0;
   __syncthreads();
-  const uint32_t s = reg[0];
-  const uint32_t e = s + tail[hb];
-  // 8 independent loads in flight per thread before their atomics (the loop is
-  // latency-bound otherwise: one workgroup per CU walks ~entries/256 entries)
-  for (uint32_t p0 = s; p0 < e; p0 += U * kLoThreads) {
-    uint32_t k8[U];
+  for (uint32_t p0 = s; p0 < e; p0 += kLoU * kLoThreads) {
+    uint32_t k8[kLoU];
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
-      const uint32_t p = p0 + u * kLoThreads + threadIdx.x;
-      k8[u] = p < e ? (uint32_t)lo2[p] : NL;
+    for (uint32_t u = 0; u < kLoU; u++) {  // independent loads in flight before the atomics
+      const uint32_t q = p0 + u * kLoThreads + threadIdx.x;
+      k8[u] = q < e ? (uint32_t)lo2[q] : NL;
     }
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++)
-      if (k8[u] < NL) atomicAdd(&h[k8[u]], 1u);
+    for (uint32_t u = 0; u < kLoU; u++) lo_inc<kAgg>(h, k8[u], k8[u] < NL);
   }
   __syncthreads();
-  block_scan_excl<kLoThreads>(h, NL, wsum);  // low-index counts -> bucket offsets in the region
+  for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) segoff[(size_t)item * NL + i] = h[i];
+}
+
+template <int LO>
+__global__ void __launch_bounds__(kLoThreads)
+msm_lo_scan_kernel(const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t* __restrict__ segoff,
+                   uint32_t nkeys, uint32_t* __restrict__ offsets, uint32_t* __restrict__ large) {
+  constexpr uint32_t NL = 1u << LO;
+  __shared__ uint32_t h[NL], wsum[kLoThreads / 64], rs[256], rf[257];
+  const uint32_t* tail = counts + (size_t)256 * ntiles;
+  lo_regions(tail, wsum, rs, rf);
+  const uint32_t hb = blockIdx.x;
+  const uint32_t f0 = rf[hb], ns = rf[hb + 1] - f0, s = rs[hb];
+  for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) {  // bucket i: its items' counts -> exclusive
+    uint32_t run = 0;
+    for (uint32_t g = 0; g < ns; g++) {
+      uint32_t* c = segoff + (size_t)(f0 + g) * NL + i;
+      const uint32_t v = *c;
+      *c = run;
+      run += v;
+    }
+    h[i] = run;
+  }
+  __syncthreads();
+  block_scan_excl<kLoThreads>(h, NL, wsum);  // bucket totals -> offsets in the region
   for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) {
-    h[i] += s;
+    const uint32_t base = s + h[i];
     const uint32_t key = (hb << LO) | i;
-    if (key < nkeys) offsets[key] = h[i];
+    if (key < nkeys) offsets[key] = base;
+    for (uint32_t g = 0; g < ns; g++) segoff[(size_t)(f0 + g) * NL + i] += base;
   }
-  if (hb == 255 && threadIdx.x == 0) offsets[nkeys] = e;  // entries in all: the last region's end
-  if (hb == 0 && threadIdx.x == 0) large[0] = 0;          // the finalize's count of long bucket runs
-  __syncthreads();
-  // scatter in chunks of U * kLoThreads entries, each ranked by low index in LDS first and
-  // written out run by run (coalesced)
-  for (uint32_t p0 = s; p0 < e; p0 += U * kLoThreads) {
-    uint32_t k8[U], v8[U], r8[U];
+  if (hb == 255 && threadIdx.x == 0) offsets[nkeys] = s + tail[255];  // entries in all
+  if (hb == 0 && threadIdx.x == 0) large[0] = 0;                     // the finalize's count of long runs
+}
+
+template <int LO, bool kAgg>
+__global__ void __launch_bounds__(kLoThreads)
+msm_lo_scatter_kernel(const typename std::conditional<LO <= 8, uint8_t, uint16_t>::type* __restrict__ lo2,
+                      const uint32_t* __restrict__ vals2, const uint32_t* __restrict__ counts, uint32_t ntiles,
+                      const uint32_t* __restrict__ segoff, uint32_t* __restrict__ sorted) {
+  using Lo = typename std::conditional<LO <= 8, uint8_t, uint16_t>::type;
+  constexpr uint32_t NL = 1u << LO;
+  __shared__ uint32_t h[NL], lcnt[NL], lst[NL];
+  __shared__ uint32_t wsum[kLoThreads / 64], rs[256], rf[257];
+  __shared__ uint32_t lv[kLoU * kLoThreads];
+  __shared__ Lo lk[kLoU * kLoThreads];
+  lo_regions(counts + (size_t)256 * ntiles, wsum, rs, rf);
+  const uint32_t item = blockIdx.x;
+  if (item >= rf[256]) return;
+  const uint32_t r = lo_region_of(rf, item);
+  const uint32_t* tail = counts + (size_t)256 * ntiles;
+  const uint32_t s = rs[r] + (item - rf[r]) * kLoSeg;
+  const uint32_t e = min(rs[r] + tail[r], s + kLoSeg);
+  for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) h[i] = segoff[(size_t)item * NL + i];
+  for (uint32_t p0 = s; p0 < e; p0 += kLoU * kLoThreads) {
+    uint32_t k8[kLoU], v8[kLoU], r8[kLoU];
     for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) lcnt[i] = 0;
     __syncthreads();
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
-      const uint32_t p = p0 + u * kLoThreads + threadIdx.x;
-      k8[u] = p < e ? (uint32_t)lo2[p] : NL;
-      v8[u] = p < e ? vals2[p] : 0u;
+    for (uint32_t u = 0; u < kLoU; u++) {
+      const uint32_t q = p0 + u * kLoThreads + threadIdx.x;
+      k8[u] = q < e ? (uint32_t)lo2[q] : NL;
+      v8[u] = q < e ? vals2[q] : 0u;
     }
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++)
-      if (k8[u] < NL) r8[u] = atomicAdd(&lcnt[k8[u]], 1u);
+    for (uint32_t u = 0; u < kLoU; u++) r8[u] = lo_inc<kAgg>(lcnt, k8[u], k8[u] < NL);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) lst[i] = lcnt[i];
     __syncthreads();
     block_scan_excl<kLoThreads>(lst, NL, wsum);
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++)
+    for (uint32_t u = 0; u < kLoU; u++)
       if (k8[u] < NL) {
         const uint32_t q = lst[k8[u]] + r8[u];
         lk[q] = (Lo)k8[u];
         lv[q] = v8[u];
       }
     __syncthreads();
-    const uint32_t cnt = e - p0 < U * kLoThreads ? e - p0 : U * kLoThreads;
-    for (uint32_t q = threadIdx.x; q < cnt; q += kLoThreads) {
+    const uint32_t cnt = e - p0 < kLoU * kLoThreads ? e - p0 : kLoU * kLoThreads;
+    for (uint32_t q = threadIdx.x; q < cnt; q += kLoThreads) {  // runs of one bucket: coalesced
       const uint32_t k = lk[q];
       sorted[h[k] + (q - lst[k])] = lv[q];
     }
@@ -1020,25 +1145,36 @@ __device__ __forceinline__ G1xyzz sum_run(const Xyzz29* carry_own, const Xyzz29*
 }
 
 // P = G1xyzz: the generic accumulation already wrote single-chunk buckets in place;
-// P = Xyzz29: every bucket is converted here (single-chunk ones from `single`).
+// P = Xyzz29: with out29 the multi-chunk buckets are summed into out29 (= the
+// accumulation's bucket array, single-chunk buckets stay where it wrote them, nothing is
+// converted: msm_bitsums29_kernel reads radix 2^29); without, every bucket is converted
+// into `buckets` (single-chunk ones from `single`).
 template <class P>
 __global__ void __launch_bounds__(kMsmThreads)
 msm_bucket_finalize_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys,
                            const P* __restrict__ single,
                            const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
-                           G1xyzz* __restrict__ buckets, uint32_t* __restrict__ large) {
+                           G1xyzz* __restrict__ buckets, uint32_t* __restrict__ large, Xyzz29* __restrict__ out29) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nkeys) return;
   const uint32_t s = offsets[k], e = offsets[k + 1];
   if (e == s) return;
   const uint32_t c0 = s / chunk, c1 = (e - 1) / chunk;
   if (c0 == c1) {  // stored by the accumulation
-    if (single) buckets[k] = load_point(single[k]);
+    if (single && !out29) buckets[k] = load_point(single[k]);
     return;
   }
-  if (c1 - c0 > kSeqSpan) {  // long run of carries (skewed digits): a workgroup sums it
+  if (c1 - c0 > (std::is_same<P, Xyzz29>::value ? kSeqSpan29 : kSeqSpan)) {  // long run (skewed digits)
     large[1 + atomicAdd(&large[0], 1u)] = (uint32_t)k;
     return;
+  }
+  if constexpr (std::is_same<P, Xyzz29>::value) {
+    if (out29) {
+      Xyzz29 v = carry_own[c0];
+      for (uint32_t u = c0 + 1; u <= c1; u++) v = add29(v, carry_cont[u]);
+      out29[k] = v;
+      return;
+    }
   }
   buckets[k] = sum_run(carry_own, carry_cont, c0, c1);
 }
@@ -1197,7 +1333,8 @@ msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, c
     const uint32_t span = carry_span(chunk, offsets, large[1 + lo], &c0);
     const uint32_t first = (item - off[lo]) * kPieceCarries;
     const uint32_t n = span - first < kPieceCarries ? span - first : kPieceCarries;
-    const Xyzz29 r = block_sum<kSumThreads>(kSumPer, sh, [&](int step, Xyzz29& rhs) {
+    const int per = (int)((n + kSumThreads - 1) / kSumThreads);  // <= kSumPer
+    const Xyzz29 r = block_sum<kSumThreads>(per, sh, [&](int step, Xyzz29& rhs) {
       const uint32_t u = (uint32_t)step * kSumThreads + threadIdx.x;
       if (u >= n) return false;
       rhs = first + u ? carry_cont[c0 + first + u] : carry_own[c0];
@@ -1208,14 +1345,35 @@ msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, c
   }
 }
 
-__global__ void __launch_bounds__(kMsmThreads)
+// a listed bucket's pieces: one wave per bucket, a tree over up to 64 pieces at a time
+// (the hottest Lagrange bucket has ~40 pieces: 6 levels instead of 40 sequential adds)
+__global__ void __launch_bounds__(kLargeFinalThreads)
 msm_large_final29_kernel(const uint32_t* __restrict__ large, const uint32_t* __restrict__ off,
-                         const Xyzz29* __restrict__ part, G1xyzz* __restrict__ buckets) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= large[0]) return;
-  Xyzz29 v = part[off[i]];
-  for (uint32_t j = off[i] + 1; j < off[i + 1]; j++) v = add29(v, part[j]);
-  buckets[large[1 + i]] = load_point(v);
+                         const Xyzz29* __restrict__ part, G1xyzz* __restrict__ buckets, Xyzz29* __restrict__ out29) {
+  __shared__ Xyzz29 sh[kLargeFinalThreads];
+  const uint32_t count = large[0];
+  for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
+    const uint32_t p0 = off[i], np = off[i + 1] - p0;
+    if (np == 1) {
+      if (threadIdx.x == 0) {
+        if (out29) out29[large[1 + i]] = part[p0];
+        else buckets[large[1 + i]] = load_point(part[p0]);
+      }
+      continue;
+    }
+    const int per = (int)((np + kLargeFinalThreads - 1) / kLargeFinalThreads);
+    const Xyzz29 r = block_sum<kLargeFinalThreads>(per, sh, [&](int step, Xyzz29& rhs) {
+      const uint32_t u = (uint32_t)step * kLargeFinalThreads + threadIdx.x;
+      if (u >= np) return false;
+      rhs = part[p0 + u];
+      return true;
+    });
+    if (threadIdx.x == 0) {
+      if (out29) out29[large[1 + i]] = r;
+      else buckets[large[1 + i]] = load_point(r);
+    }
+    __syncthreads();
+  }
 }
 
 // level 1: block (set w, slot j, part p). Slot 0 sums seg_tot[w][g] over all g; slot b+1
@@ -1255,6 +1413,94 @@ msm_parts_kernel(const G1xyzz* __restrict__ parts, int nparts, G1xyzz* __restric
     return true;
   });
   if (threadIdx.x == 0) out[blockIdx.x] = r;
+}
+
+// Fixed base (one bucket set of nb = 2^lb buckets, bucket k of weight k + 1): the window
+// sum sum_k (k + 1) B_k = sum_b 2^b S_b with S_b = sum of the buckets whose weight has
+// bit b set (b = 0..lb; slot lb holds bucket nb - 1 alone). Block (slot b, part p) sums
+// kSumPer * kSumThreads of slot b's terms: 4 sequential additions + an 8-level tree, in
+// radix 2^29 on the accumulation's own bucket array. The segment reduce of the generic
+// schedule (msm_bucket_reduce_kernel: 16 dependent 8x32 additions per thread, 2^13
+// threads, then msm_sums_kernel) did 1/4 of the additions in a 3x longer dependency
+// chain; both are latency-bound at this size (profiles/r3_single_lane_phases.txt).
+__global__ void __launch_bounds__(kSumThreads)
+msm_bitsums29_kernel(const Xyzz29* __restrict__ buckets, const uint32_t* __restrict__ offsets, int lb, int nparts,
+                     Xyzz29* __restrict__ parts) {
+  __shared__ Xyzz29 sh[kSumThreads];
+  const int p = blockIdx.x % nparts;
+  const int b = blockIdx.x / nparts;
+  const uint32_t count = b < lb ? 1u << (lb - 1) : 1u;
+  const Xyzz29 r = block_sum<kSumThreads>(kSumPer, sh, [&](int step, Xyzz29& rhs) {
+    const uint32_t q = (uint32_t)(p * kSumPer + step) * kSumThreads + threadIdx.x;
+    if (q >= count) return false;
+    const uint32_t v = b < lb ? (((q >> b) << (b + 1)) | (1u << b) | (q & ((1u << b) - 1u))) : 1u << lb;
+    const uint32_t k = v - 1u;  // weight v
+    if (offsets[k + 1] == offsets[k]) return false;
+    rhs = buckets[k];
+    return true;
+  });
+  if (threadIdx.x == 0) parts[blockIdx.x] = r;
+}
+
+// Default fixed-base sums, two levels in radix 2^29. Level 1, thread per segment g of
+// kSeg29 buckets: run_g = sum_j B_{g L + j}, tot_g = sum_j (j + 1) B_{g L + j} (running
+// sums from the top: 2 L dependent additions). Level 2 (msm_segsums29_kernel): slot 0 =
+// sum_g tot_g, slot 1 + b = sum of run_g over the g with bit b set, so that the window sum
+// is slot 0 + L sum_b 2^b slot_{1+b} (msm_finish). Each bucket is added twice and each
+// segment ~log2(nseg) / 2 + 1 times: ~2.0 additions per bucket against ~8 for the bit slots
+// over the buckets, with a dependency chain of 2 L + 4 + 8 (+ 7 in msm_parts29_kernel).
+static constexpr int kSeg29 = 4;
+
+__global__ void __launch_bounds__(kMsmThreads)
+msm_seg29_kernel(const Xyzz29* __restrict__ buckets, const uint32_t* __restrict__ offsets, uint32_t nseg,
+                 Xyzz29* __restrict__ seg_tot, Xyzz29* __restrict__ seg_run) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nseg) return;
+  Xyzz29 run = pinf<Xyzz29>(), tot = pinf<Xyzz29>();
+  for (int j = kSeg29 - 1; j >= 0; j--) {  // two addition sites per step
+    const uint32_t k = g * kSeg29 + (uint32_t)j;
+    if (offsets[k + 1] != offsets[k]) run = add29(run, buckets[k]);
+    tot = add29(tot, run);
+  }
+  seg_tot[g] = tot;
+  seg_run[g] = run;
+}
+
+// block (slot j, part p): slot 0 sums seg_tot[0..nseg), slot b + 1 the seg_run[g] with
+// bit b of g set; part p covers kSumPer * kSumThreads terms
+__global__ void __launch_bounds__(kSumThreads)
+msm_segsums29_kernel(const Xyzz29* __restrict__ seg_tot, const Xyzz29* __restrict__ seg_run, int nseg, int nparts,
+                     Xyzz29* __restrict__ parts) {
+  __shared__ Xyzz29 sh[kSumThreads];
+  const int p = blockIdx.x % nparts;
+  const int j = blockIdx.x / nparts;
+  const int count = j == 0 ? nseg : nseg >> 1;
+  const Xyzz29 r = block_sum<kSumThreads>(kSumPer, sh, [&](int step, Xyzz29& rhs) {
+    const int q = (p * kSumPer + step) * kSumThreads + (int)threadIdx.x;
+    if (q >= count) return false;
+    if (j == 0) {
+      rhs = seg_tot[q];
+    } else {
+      const int b = j - 1;
+      rhs = seg_run[((q >> b) << (b + 1)) | (1 << b) | (q & ((1 << b) - 1))];
+    }
+    return true;
+  });
+  if (threadIdx.x == 0) parts[blockIdx.x] = r;
+}
+
+// block per slot: its nparts partials, converted to the 8x32 layout once
+__global__ void __launch_bounds__(kPartThreads)
+msm_parts29_kernel(const Xyzz29* __restrict__ parts, int nparts, G1xyzz* __restrict__ out) {
+  __shared__ Xyzz29 sh[kPartThreads];
+  const int per = (nparts + kPartThreads - 1) / kPartThreads;
+  const Xyzz29 r = block_sum<kPartThreads>(per, sh, [&](int step, Xyzz29& rhs) {
+    const int q = step * kPartThreads + (int)threadIdx.x;
+    if (q >= nparts) return false;
+    rhs = parts[(size_t)blockIdx.x * nparts + q];
+    return true;
+  });
+  if (threadIdx.x == 0) out[blockIdx.x] = load_point(r);
 }
 
 // Shifted-base table: row w = 2^(c*w) * B_i, thread per base (c doublings per row,
@@ -1297,8 +1543,13 @@ void MsmBaseTable::build(const G1Affine* bases, size_t npts, int cbits, hipStrea
   NZ_HIP(hipGetLastError());
 }
 
+// work items of the bucket_lo steps: at most one partial segment per region + entries / kLoSeg
+static size_t lo_items_bound(size_t entries) { return 256 + entries / kLoSeg + 1; }
+
 struct MsmPlan {
   int c, nw, nsets, seglen, nseg, nbits, nslots, nparts;
+  int lb, bparts;  // fixed base, bit-slot sums: log2(nb) (slots lb + 1), parts per slot
+  int nseg29, nslots29, sparts29;  // fixed base, segment sums: segments, slots, parts per slot
   uint32_t nb, nkeys;
   size_t entries;
 };
@@ -1316,19 +1567,30 @@ static MsmPlan make_plan(size_t n, const MsmBaseTable* t) {
   while ((1 << p.nbits) < p.nseg) p.nbits++;
   p.nslots = p.nbits + 1;
   p.nparts = (p.nseg + kSumThreads * kSumPer - 1) / (kSumThreads * kSumPer);
+  p.lb = p.c - 1;
+  p.bparts = (int)(((p.nb >> 1) + kSumThreads * kSumPer - 1) / (kSumThreads * kSumPer));
+  p.nseg29 = (int)(p.nb >= (uint32_t)kSeg29 ? p.nb / kSeg29 : 1);
+  p.nslots29 = 1;
+  while ((1 << (p.nslots29 - 1)) < p.nseg29) p.nslots29++;
+  p.sparts29 = (p.nseg29 + kSumThreads * kSumPer - 1) / (kSumThreads * kSumPer);
   p.entries = n * (size_t)p.nw;
   return p;
 }
 
 void MsmScratch::init(size_t maxp, bool fixed_base) {
   max_points = maxp;
-  size_t max_entries = 0, max_keys = 0, max_seg = 0, max_slots = 0, max_parts = 0;
+  size_t max_entries = 0, max_keys = 0, max_seg = 0, max_slots = 0, max_parts = 0, max_parts29 = 0, max_seg29 = 0;
   auto fit = [&](const MsmPlan& p) {
     max_entries = std::max(max_entries, p.entries);
     max_keys = std::max(max_keys, (size_t)p.nkeys);
     max_seg = std::max(max_seg, (size_t)p.nseg * p.nsets);
     max_slots = std::max(max_slots, (size_t)p.nslots * p.nsets);
     max_parts = std::max(max_parts, (size_t)p.nslots * p.nsets * p.nparts);
+    if (p.nsets == 1) {  // fixed base: the bit-slot sums
+      max_slots = std::max(max_slots, (size_t)std::max(p.lb + 1, p.nslots29));
+      max_parts29 = std::max(max_parts29, (size_t)std::max((p.lb + 1) * p.bparts, p.nslots29 * p.sparts29));
+      max_seg29 = std::max(max_seg29, (size_t)p.nseg29);
+    }
   };
   for (size_t n = 1;; n <<= 1) {
     size_t m = n < maxp ? n : maxp;
@@ -1377,8 +1639,12 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
     large_part.alloc(nthreads / kPieceCarries + max_keys + 1);
     carry_own29.alloc(nthreads);
     carry_cont29.alloc(nthreads);
+    parts29.alloc(max_parts29);
+    seg_tot29.alloc(max_seg29);
+    seg_run29.alloc(max_seg29);
     bin_counts.alloc((size_t)256 * ((maxp + kTileScalars - 1) / kTileScalars) + 256);  // + row totals
     vals_mid.alloc(max_entries);
+    lo_seg.alloc(lo_items_bound(max_entries) * ((size_t)1 << BinKeys<20>::LO));  // the widest low index
   }
   carry_cont.alloc(nthreads);
   seg_tot.alloc(max_seg);
@@ -1452,6 +1718,13 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   sc.cur_nbits = p.nbits;
   sc.cur_seglen = p.seglen;
   sc.cur_nkeys = p.nkeys;
+  const int fsums = table ? fb_sums() : 0;  // 0: the generic 8x32 sums
+  const bool bsums = fsums == 1;
+  sc.cur_bitsums = bsums;
+  if (fsums == 2) {  // msm_finish: slot 0 + kSeg29 * sum_b 2^b slot_{1+b}
+    sc.cur_nbits = p.nslots29 - 1;
+    sc.cur_seglen = kSeg29;
+  }
   const bool phases = sc.prof && sc.prof_phases;
   if (sc.prof && !sc.ev[0])
     for (auto& e : sc.ev) NZ_HIP(hipEventCreate(&e));
@@ -1477,9 +1750,17 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                          table->stride, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
       NZ_HIP(hipGetLastError());
       mark(2);
-      hipLaunchKernelGGL(msm_bucket_lo_kernel<BinKeys<C>::LO>, dim3(256), dim3(kLoThreads), 0, st,
-                         (const Lo*)lo2, sc.vals_mid.p, sc.bin_counts.p, ntiles, p.nkeys, sc.offsets.p,
-                         sc.sorted.p, sc.large.p);
+      constexpr int LO = BinKeys<C>::LO;
+      const dim3 igrid((unsigned)lo_items_bound(p.entries));
+      hipLaunchKernelGGL((lo_agg() ? msm_lo_count_kernel<LO, true> : msm_lo_count_kernel<LO, false>), igrid,
+                         dim3(kLoThreads), 0, st, (const Lo*)lo2, sc.bin_counts.p, ntiles, sc.lo_seg.p);
+      NZ_HIP(hipGetLastError());
+      hipLaunchKernelGGL(msm_lo_scan_kernel<LO>, dim3(256), dim3(kLoThreads), 0, st, sc.bin_counts.p, ntiles,
+                         sc.lo_seg.p, p.nkeys, sc.offsets.p, sc.large.p);
+      NZ_HIP(hipGetLastError());
+      hipLaunchKernelGGL((lo_agg() ? msm_lo_scatter_kernel<LO, true> : msm_lo_scatter_kernel<LO, false>), igrid,
+                         dim3(kLoThreads), 0, st, (const Lo*)lo2, sc.vals_mid.p, sc.bin_counts.p, ntiles,
+                         (const uint32_t*)sc.lo_seg.p, sc.sorted.p);
       NZ_HIP(hipGetLastError());
     };
     switch (p.c) {
@@ -1496,7 +1777,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   size_t tmp = sc.sort_tmp_bytes;
   const dim3 ogrid(grid_for((size_t)p.nkeys + 1, kMsmThreads, 1u << 30));
   if (bins) {
-    // offsets written by msm_bucket_lo_kernel
+    // offsets written by msm_lo_scan_kernel
   } else if (table && p.nkeys <= 65536) {  // 16-bit keys, no sentinel (see msm_keys_kernel)
     int end_bit = 0;
     while ((1u << end_bit) < p.nkeys) end_bit++;
@@ -1575,18 +1856,14 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   }
   NZ_HIP(hipGetLastError());
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[4], st));
-  if (!bins) NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));  // bins: zeroed by msm_bucket_lo_kernel
+  if (!bins) NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));  // bins: zeroed by msm_lo_scan_kernel
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
   if (table) {
+    Xyzz29* out29 = fsums ? sc.buckets29.p : nullptr;
     hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, acc_off, p.nkeys,
                        (const Xyzz29*)sc.buckets29.p, (const Xyzz29*)sc.carry_own29.p,
-                       (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p, sc.large.p);
+                       (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p, sc.large.p, out29);
     NZ_HIP(hipGetLastError());
-    if (!large_pieces()) {  // NZCB_LARGE_PIECES=0: one workgroup per long run (A/B runs)
-      hipLaunchKernelGGL(msm_bucket_large_kernel<Xyzz29>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, chunk,
-                         acc_off, sc.large.p, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p,
-                         sc.buckets.p);
-    } else {
     hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, acc_off, sc.large.p,
                        sc.large_off.p);
     NZ_HIP(hipGetLastError());
@@ -1594,13 +1871,12 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                        sc.large.p, sc.large_off.p, (const Xyzz29*)sc.carry_own29.p,
                        (const Xyzz29*)sc.carry_cont29.p, sc.large_part.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_large_final29_kernel, dim3(grid_for(p.nkeys, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0,
-                       st, sc.large.p, sc.large_off.p, sc.large_part.p, sc.buckets.p);
-    }
+    hipLaunchKernelGGL(msm_large_final29_kernel, dim3(kLargeFinalBlocks), dim3(kLargeFinalThreads), 0, st, sc.large.p,
+                       sc.large_off.p, sc.large_part.p, sc.buckets.p, out29);
   } else {
     hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
                        (const G1xyzz*)nullptr, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p,
-                       sc.buckets.p, sc.large.p);
+                       sc.buckets.p, sc.large.p, (Xyzz29*)nullptr);
     NZ_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_bucket_large_kernel<G1xyzz>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, chunk,
                        sc.offsets.p,
@@ -1608,6 +1884,35 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   }
   NZ_HIP(hipGetLastError());
   mark(5);
+  if (fsums == 2) {
+    hipLaunchKernelGGL(msm_seg29_kernel, dim3(grid_for((size_t)p.nseg29, kMsmThreads, 1u << 30)), dim3(kMsmThreads),
+                       0, st, (const Xyzz29*)sc.buckets29.p, acc_off, (uint32_t)p.nseg29, sc.seg_tot29.p,
+                       sc.seg_run29.p);
+    NZ_HIP(hipGetLastError());
+    mark(6);
+    hipLaunchKernelGGL(msm_segsums29_kernel, dim3(p.nslots29 * p.sparts29), dim3(kSumThreads), 0, st,
+                       (const Xyzz29*)sc.seg_tot29.p, (const Xyzz29*)sc.seg_run29.p, p.nseg29, p.sparts29,
+                       sc.parts29.p);
+    NZ_HIP(hipGetLastError());
+    hipLaunchKernelGGL(msm_parts29_kernel, dim3(p.nslots29), dim3(kPartThreads), 0, st, (const Xyzz29*)sc.parts29.p,
+                       p.sparts29, sc.win.p);
+    NZ_HIP(hipGetLastError());
+    mark(7);
+    NZ_HIP(hipMemcpyAsync(sc.host_win, sc.win.p, (size_t)p.nslots29 * sizeof(G1xyzz), hipMemcpyDeviceToHost, st));
+    return;
+  }
+  if (bsums) {
+    mark(6);
+    hipLaunchKernelGGL(msm_bitsums29_kernel, dim3((p.lb + 1) * p.bparts), dim3(kSumThreads), 0, st,
+                       (const Xyzz29*)sc.buckets29.p, acc_off, p.lb, p.bparts, sc.parts29.p);
+    NZ_HIP(hipGetLastError());
+    hipLaunchKernelGGL(msm_parts29_kernel, dim3(p.lb + 1), dim3(kPartThreads), 0, st, (const Xyzz29*)sc.parts29.p,
+                       p.bparts, sc.win.p);
+    NZ_HIP(hipGetLastError());
+    mark(7);
+    NZ_HIP(hipMemcpyAsync(sc.host_win, sc.win.p, (size_t)(p.lb + 1) * sizeof(G1xyzz), hipMemcpyDeviceToHost, st));
+    return;
+  }
   hipLaunchKernelGGL(msm_bucket_reduce_kernel, dim3(grid_for((size_t)p.nsets * p.nseg, kMsmThreads, 1u << 30)),
                      dim3(kMsmThreads), 0, st, sc.buckets.p, sc.offsets.p, (int)p.nb, p.seglen, p.nseg, p.nsets,
                      sc.seg_tot.p, sc.seg_run.p);
@@ -1646,6 +1951,14 @@ G1xyzz msm_finish(MsmScratch& sc, hipStream_t st) {
         sc.phase_ms[i] += ms;
       }
     }
+  }
+  if (sc.cur_bitsums) {  // sum_b 2^b S_b over the lb + 1 = c bit slots (msm_bitsums29_kernel)
+    G1xyzz acc = G1xyzz::inf();
+    for (int b = c - 1; b >= 0; b--) {
+      acc = xyzz_dbl(acc);
+      acc = xyzz_add(acc, sc.host_win[b]);
+    }
+    return acc;
   }
   int lg_seg = 0;
   while ((1 << lg_seg) < sc.cur_seglen) lg_seg++;

@@ -263,15 +263,28 @@ ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s,
 //    joined directly.
 static constexpr int kTile29 = 2048;   // elements per tile: 9 x 8 KiB of limbs = 72 KiB LDS
 
-__device__ __forceinline__ F29 tile_ld(const uint32_t* sl, int e) {
+// LDS slot of tile element e: bits 0-4 XORed with a function of bits 5-7, a bijection on
+// every 32-element block. ds_read_b32 / ds_write_b32 bank by (address / 4) mod 32 per
+// 32-lane half, and with 8-column tiles (logC = 3) the first pass's transposed store
+// (element stride 8) hit 4 banks (8-way) and the radix-4 step at stage 0 (row stride 4,
+// element stride 32) 8 banks (4-way); swizzled, every access pattern of the kernel
+// (row-major loads/stores, all radix-4 operand sets at each stage, the odd radix-2
+// stage, the sparse copy) is conflict-free (checked exhaustively for q = 6, 7, 8).
+// swz = ~0 (default) or 0 (NZCB_NTT_SWIZZLE=0: the linear layout, for A/B runs)
+__device__ __forceinline__ int tile_slot(int e, int swz) {
+  return e ^ (swz & ((((e >> 5) & 3) << 3) | ((e >> 5) & 7)));
+}
+__device__ __forceinline__ F29 tile_ld(const uint32_t* sl, int e, int swz) {
+  const int p = tile_slot(e, swz);
   F29 x;
 #pragma unroll
-  for (int l = 0; l < 9; l++) x.v[l] = sl[l * kTile29 + e];
+  for (int l = 0; l < 9; l++) x.v[l] = sl[l * kTile29 + p];
   return x;
 }
-__device__ __forceinline__ void tile_st(uint32_t* sl, int e, const F29& x) {
+__device__ __forceinline__ void tile_st(uint32_t* sl, int e, const F29& x, int swz) {
+  const int p = tile_slot(e, swz);
 #pragma unroll
-  for (int l = 0; l < 9; l++) sl[l * kTile29 + e] = x.v[l];
+  for (int l = 0; l < 9; l++) sl[l * kTile29 + p] = x.v[l];
 }
 __device__ __forceinline__ F29 add_nn29(const F29& a, const F29& b) {
   F29 r;
@@ -304,7 +317,7 @@ __device__ __forceinline__ Fr canon_fr29(const F29& x) {  // normalized x < 64 r
 template <bool IN29, bool OUT29>
 __global__ void __launch_bounds__(kNttThreads)
 ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29* __restrict__ tw, int L, int s,
-                  int q, int logC, F29 scale29, int do_scale, NttIo io, int sparse4) {
+                  int q, int logC, F29 scale29, int do_scale, NttIo io, int sparse4, int swz) {
   __shared__ uint32_t sl[9 * kTile29];
   const int C = 1 << logC;
   const int rows = 1 << q;
@@ -325,7 +338,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
         if (io.in_f) x = mul29<Fr29>(x, io.in_f[src]);
         if (do_scale) x = mul29<Fr29>(x, scale29);
       }
-      tile_st(sl, e, x);
+      tile_st(sl, e, x, swz);
     }
   } else {
     const size_t groups_lo = ((size_t)1 << s) >> logC;
@@ -334,7 +347,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
     base = (hi << (s + q)) + lo0;
     for (int e = tid; e < n_el; e += kNttThreads) {
       const int j = e >> logC, c = e & (C - 1);
-      tile_st(sl, e, in29[base + ((size_t)j << s) + c]);
+      tile_st(sl, e, in29[base + ((size_t)j << s) + c], swz);
     }
   }
   __syncthreads();
@@ -347,7 +360,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
     // is a copy
     for (int e = tid; e < n_el; e += kNttThreads) {
       const int j = e >> logC;
-      if (j & 3) tile_st(sl, e, tile_ld(sl, ((j & ~3) << logC) + (e & (C - 1))));
+      if (j & 3) tile_st(sl, e, tile_ld(sl, ((j & ~3) << logC) + (e & (C - 1)), swz), swz);
     }
     __syncthreads();
     st = 2;
@@ -362,14 +375,14 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       const int j0 = b >> logC;
       const int i0 = ((2 * j0) << logC) + c, i1 = ((2 * j0 + 1) << logC) + c;
       const size_t k = first ? 0 : (lo0 + c);
-      const F29 x0 = tile_ld(sl, i0);
-      const F29 x1 = tile_ld(sl, i1);
+      const F29 x0 = tile_ld(sl, i0, swz);
+      const F29 x1 = tile_ld(sl, i1, swz);
       const F29 tt = g ? mul29<Fr29>(x1, twg[k]) : x1;
       F29 y0 = add_nn29(x0, tt), y1 = sub2r_nn29(x0, tt);
       norm29(y0);
       norm29(y1);
-      tile_st(sl, i0, y0);
-      tile_st(sl, i1, y1);
+      tile_st(sl, i0, y0, swz);
+      tile_st(sl, i1, y1, swz);
     }
     __syncthreads();
     st = 1;
@@ -391,7 +404,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       const size_t kc = first ? (size_t)(low + h) : (((size_t)(low + h) << s) + lo0 + c);
       const int i0 = (j << logC) + c, i1 = ((j + h) << logC) + c, i2 = ((j + 2 * h) << logC) + c,
                 i3 = ((j + 3 * h) << logC) + c;
-      F29 t1 = tile_ld(sl, i1), t3 = tile_ld(sl, i3);
+      F29 t1 = tile_ld(sl, i1, swz), t3 = tile_ld(sl, i3, swz);
       if (g) {
         const F29 wa = twa[ka];
         F29 p1, p3;
@@ -399,7 +412,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
         t1 = p1;
         t3 = p3;
       }
-      const F29 x0 = tile_ld(sl, i0), x2 = tile_ld(sl, i2);
+      const F29 x0 = tile_ld(sl, i0, swz), x2 = tile_ld(sl, i2, swz);
       const F29 y0 = add_nn29(x0, t1), y1 = sub2r_nn29(x0, t1);
       const F29 y2 = add_nn29(x2, t3), y3 = sub2r_nn29(x2, t3);
       F29 u2, u3;
@@ -409,10 +422,10 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       norm29(z1);
       norm29(z2);
       norm29(z3);
-      tile_st(sl, i0, z0);
-      tile_st(sl, i1, z1);
-      tile_st(sl, i2, z2);
-      tile_st(sl, i3, z3);
+      tile_st(sl, i0, z0, swz);
+      tile_st(sl, i1, z1, swz);
+      tile_st(sl, i2, z2, swz);
+      tile_st(sl, i3, z3, swz);
     }
     __syncthreads();
   }
@@ -429,14 +442,22 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
     for (int e = tid; e < n_el; e += kNttThreads) {
       const int j = e & (rows - 1), c = e >> q;
       const size_t dst = ((size_t)bit_rev((uint32_t)(c0 + c), L - q) << q) + j;
-      store(dst, tile_ld(sl, (j << logC) + c));
+      store(dst, tile_ld(sl, (j << logC) + c, swz));
     }
   } else {
     for (int e = tid; e < n_el; e += kNttThreads) {
       const int j = e >> logC, c = e & (C - 1);
-      store(base + ((size_t)j << s) + c, tile_ld(sl, e));
+      store(base + ((size_t)j << s) + c, tile_ld(sl, e, swz));
     }
   }
+}
+
+static int ntt29_swizzle() {  // NZCB_NTT_SWIZZLE=0: linear LDS tiles (A/B runs)
+  static const int m = [] {
+    const char* e = std::getenv("NZCB_NTT_SWIZZLE");
+    return (e && e[0] == '0') ? 0 : ~0;
+  }();
+  return m;
 }
 
 static bool ntt29_enabled() {  // NZCB_NTT29=0: the 8x32 pipeline (ntt_pass_kernel) for A/B runs
@@ -488,14 +509,15 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
                       io.in_len <= ((size_t)1 << (L - 2)) + ((size_t)1 << logC1);
   if (ntt29_enabled() && (q1 == L || t.scratch29.n >= ((size_t)9 << L))) {
     F29* scr = (F29*)t.scratch29.p;
+    const int swz = ntt29_swizzle();
     if (q1 == L) {
       hipLaunchKernelGGL((ntt29_pass_kernel<false, false>), dim3((unsigned)tiles), dim3(kNttThreads), 0, st, in,
-                         (const F29*)nullptr, out, (F29*)nullptr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4);
+                         (const F29*)nullptr, out, (F29*)nullptr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4, swz);
       NZ_HIP(hipGetLastError());
       return;
     }
     hipLaunchKernelGGL((ntt29_pass_kernel<false, true>), dim3((unsigned)tiles), dim3(kNttThreads), 0, st, in,
-                       (const F29*)nullptr, (Fr*)nullptr, scr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4);
+                       (const F29*)nullptr, (Fr*)nullptr, scr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4, swz);
     NZ_HIP(hipGetLastError());
     int s = q1;
     while (s < L) {
@@ -505,10 +527,10 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
       const size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
       if (s + q == L)
         hipLaunchKernelGGL((ntt29_pass_kernel<true, false>), dim3((unsigned)ntiles), dim3(kNttThreads), 0, st,
-                           (const Fr*)nullptr, (const F29*)scr, out, (F29*)nullptr, tw, L, s, q, logC, sc29, 0, io, 0);
+                           (const Fr*)nullptr, (const F29*)scr, out, (F29*)nullptr, tw, L, s, q, logC, sc29, 0, io, 0, swz);
       else
         hipLaunchKernelGGL((ntt29_pass_kernel<true, true>), dim3((unsigned)ntiles), dim3(kNttThreads), 0, st,
-                           (const Fr*)nullptr, (const F29*)scr, (Fr*)nullptr, scr, tw, L, s, q, logC, sc29, 0, io, 0);
+                           (const Fr*)nullptr, (const F29*)scr, (Fr*)nullptr, scr, tw, L, s, q, logC, sc29, 0, io, 0, swz);
       NZ_HIP(hipGetLastError());
       s += q;
     }
