@@ -164,6 +164,14 @@ static bool lo_agg() {  // NZCB_LO_AGG=1: wave-aggregated LDS atomics in msm_lo_
   return on;
 }
 
+static int fin_lanes() {  // NZCB_FIN_LANES=4: msm_finalize29_kernel (latency), else sequential
+  static const int v = [] {
+    const char* e = std::getenv("NZCB_FIN_LANES");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
 static int fb_sums() {
   static const int v = [] {
     const char* e = std::getenv("NZCB_FB_SUMS");
@@ -1247,6 +1255,57 @@ __device__ __forceinline__ Pt block_sum(int per, Pt* sh, Load&& load) {
   return sh[0];
 }
 
+// Fixed base with radix-2^29 sums (out29), opt-in (NZCB_FIN_LANES=4): four lanes per
+// bucket, lane r adds the carries c0 + r, c0 + r + 4, ..., then two xor-shuffle levels join
+// the lanes: ~span / 4 + 2 dependent additions instead of span - 1 (isolated finalize
+// 0.185 -> 0.152 ms at 2^21), but every lane of a wave issues each addition: 55.9 M VALU
+// instructions per launch against 36.5 M sequential (profiles/r3_fin_valu.txt), and the
+// 5-lane bench is VALU-bound, so the sequential sum stays the default. Single-chunk
+// buckets are already in place; runs longer than kSeqSpan29 carries go to the large list.
+__device__ __forceinline__ Xyzz29 shfl_xor29(const Xyzz29& v, int m) {
+  Xyzz29 o;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    o.X.v[i] = __shfl_xor(v.X.v[i], m);
+    o.Y.v[i] = __shfl_xor(v.Y.v[i], m);
+    o.ZZ.v[i] = __shfl_xor(v.ZZ.v[i], m);
+    o.ZZZ.v[i] = __shfl_xor(v.ZZZ.v[i], m);
+  }
+  return o;
+}
+
+__global__ void __launch_bounds__(kMsmThreads)
+msm_finalize29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys,
+                      const Xyzz29* __restrict__ carry_own, const Xyzz29* __restrict__ carry_cont,
+                      uint32_t* __restrict__ large, Xyzz29* __restrict__ out29) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t k = t >> 2;
+  const uint32_t r = (uint32_t)t & 3u;
+  bool multi = false;  // the same for the bucket's four lanes
+  uint32_t c0 = 0, c1 = 0;
+  if (k < nkeys) {
+    const uint32_t s = offsets[k], e = offsets[k + 1];
+    if (e != s) {
+      c0 = s / chunk;
+      c1 = (e - 1) / chunk;
+      if (c1 - c0 > kSeqSpan29) {
+        if (r == 0) large[1 + atomicAdd(&large[0], 1u)] = (uint32_t)k;
+      } else {
+        multi = c1 > c0;
+      }
+    }
+  }
+  Xyzz29 v = pinf<Xyzz29>();
+  if (multi)
+    for (uint32_t u = c0 + r; u <= c1; u += 4) v = add29(v, u == c0 ? carry_own[c0] : carry_cont[u]);
+#pragma unroll 1
+  for (int m = 1; m <= 2; m <<= 1) {  // every lane shuffles (no divergence around the exchange)
+    const Xyzz29 o = shfl_xor29(v, m);
+    if (multi) v = add29(v, o);
+  }
+  if (multi && r == 0) out29[k] = v;
+}
+
 // Buckets listed by the finalize kernel (more than kSeqSpan carries, e.g. many equal
 // digits): one workgroup per bucket, kSumThreads-way partial sums + LDS tree.
 template <class P>
@@ -1860,9 +1919,14 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
   if (table) {
     Xyzz29* out29 = fsums ? sc.buckets29.p : nullptr;
-    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, acc_off, p.nkeys,
-                       (const Xyzz29*)sc.buckets29.p, (const Xyzz29*)sc.carry_own29.p,
-                       (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p, sc.large.p, out29);
+    if (out29 && fin_lanes() == 4)
+      hipLaunchKernelGGL(msm_finalize29_kernel, dim3(grid_for((size_t)p.nkeys * 4, kMsmThreads, 1u << 30)),
+                         dim3(kMsmThreads), 0, st, chunk, acc_off, p.nkeys, (const Xyzz29*)sc.carry_own29.p,
+                         (const Xyzz29*)sc.carry_cont29.p, sc.large.p, out29);
+    else
+      hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, acc_off,
+                         p.nkeys, (const Xyzz29*)sc.buckets29.p, (const Xyzz29*)sc.carry_own29.p,
+                         (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p, sc.large.p, out29);
     NZ_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, acc_off, sc.large.p,
                        sc.large_off.p);

@@ -47,6 +47,9 @@ struct Prover {
   hipStream_t aux[kSlots] = {nullptr, nullptr, nullptr};
   hipEvent_t ready[kSlots] = {nullptr, nullptr, nullptr};
   bool slot_local[kSlots] = {false, false, false};  // slot's MSM stays on this device (Lagrange basis)
+  // round 1's interpolations of A, B, C run here (overlapping round 2's grand product)
+  hipStream_t side = nullptr;
+  hipEvent_t side_ready = nullptr, side_done = nullptr;
   ~Prover();
   // resident zkey data (LEM, as in the file)
   DevBuf<G1Affine> ptau;
@@ -110,11 +113,12 @@ struct Prover {
   hipStream_t st() const { return eng->stream; }
   void init_slots();
   void alloc_workspace();
-  void to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb);
+  void to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb, hipStream_t s = nullptr);
   void commit_start(int slot, const Fr* scalars, size_t len, const MsmBaseTable* tab = nullptr,
                     const G1Affine* bases = nullptr);
   G1Affine commit_finish(int slot);
-  Fr eval_poly(const Fr* p, size_t len, const Fr& x);
+  // np <= 8 evaluations p_j(x_j) (two launches, one host round trip)
+  void eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out);
   void prefix_product(Fr* x, size_t m, Fr* level_tmp);
   void suffix_linear(Fr* x, size_t m, const Fr& d, Fr* level_tmp);
   void div_pol1(const Fr* src, size_t m, const Fr& d, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit);

@@ -31,7 +31,6 @@ namespace nzcb {
 static constexpr int kT = 256;
 static constexpr uint32_t kZeroRef = 0xffffffffu;
 static constexpr int kScanChunk = 32;
-static constexpr int kEvalChunk = 64;
 
 // ----------------------------------------------------------------------------
 // kernels
@@ -369,25 +368,99 @@ static F29 f29_exp(Fr v, int extra) {  // split29 of v * 2^extra (host)
   return split29(v);
 }
 
-// chunked Horner: partial[block] = sum over the block's chunks of p(chunk) * x^(chunk start)
-__global__ void __launch_bounds__(kT)
-k_eval(const Fr* __restrict__ p, size_t len, Fr x, Fr xK, Fr* __restrict__ partial) {
-  __shared__ Fr sh[kT];
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t s = t * kEvalChunk;
-  Fr acc = Fr::zero();
-  if (s < len) {
-    size_t e = s + kEvalChunk < len ? s + kEvalChunk : len;
-    for (size_t i = e; i-- > s;) acc = acc * x + p[i];
-    acc = acc * pow_u64(xK, (uint64_t)t);
+// Round 4, all evaluations of one point set in two launches and one host round trip
+// (eight separately synchronised Horner launches took 1.05 ms + 8 syncs per proof,
+// profiles/r3_single_lane_phases.txt). Block b, thread i: Horner over coefficients
+// [K t, K t + K) (t = b kT + i) in radix 2^29 products, then a tree over the block's
+// threads with level factors y^(2^l), y = x^K (sum_i h_i y^i); k_eval_comb folds the
+// block sums the same way in z = x^(K kT).
+static constexpr int kEvalMax = 8;
+struct EvalSet {
+  const Fr* p[kEvalMax];
+  uint64_t len[kEvalMax];
+  Fr x[kEvalMax];
+  F29 x29[kEvalMax];  // x as the mul_fr29 operand
+  int np;
+};
+
+__device__ __forceinline__ F29 fr29_operand_dev(Fr c) {
+#pragma unroll
+  for (int k = 0; k < 5; k++) c = c + c;
+  return split29(c);
+}
+
+// NP interleaved evaluations per thread (independent Horner chains side by side), a
+// chunk of kEvalChunk2 coefficients each
+static constexpr int kEvalChunk2 = 16;
+static constexpr int kEvalLogChunk2 = 4;
+
+template <int NP>
+__global__ void __launch_bounds__(kT) k_eval_multi(EvalSet es, Fr* __restrict__ partial, int nblocks) {
+  __shared__ Fr sh[kT];      // one evaluation's tree at a time (8 KB: many workgroups per CU)
+  __shared__ F29 yl[NP][8];  // kT = 2^8 threads: y^(2^l), l < 8
+  if (threadIdx.x < NP) {
+    Fr y = es.x[threadIdx.x];
+    for (int k = 0; k < kEvalLogChunk2; k++) y = y * y;
+    for (int l = 0; l < 8; l++) {
+      yl[threadIdx.x][l] = fr29_operand_dev(y);
+      y = y * y;
+    }
   }
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int stride = kT / 2; stride > 0; stride >>= 1) {
-    if ((int)threadIdx.x < stride) sh[threadIdx.x] = sh[threadIdx.x] + sh[threadIdx.x + stride];
+  const size_t s = ((size_t)blockIdx.x * kT + threadIdx.x) * kEvalChunk2;
+  Fr acc[NP];
+#pragma unroll
+  for (int j = 0; j < NP; j++) acc[j] = Fr::zero();
+  for (int i = kEvalChunk2 - 1; i >= 0; i--) {
+#pragma unroll
+    for (int j = 0; j < NP; j++)
+      if (s + i < es.len[j]) acc[j] = mul_fr29(acc[j], es.x29[j]) + es.p[j][s + i];
+  }
+#pragma unroll
+  for (int j = 0; j < NP; j++) {
+    sh[threadIdx.x] = acc[j];
+    __syncthreads();
+    for (int l = 0; l < 8; l++) {
+      const unsigned st = 1u << l;
+      if ((threadIdx.x & (2 * st - 1)) == 0) sh[threadIdx.x] = sh[threadIdx.x] + mul_fr29(sh[threadIdx.x + st], yl[j][l]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[(size_t)j * nblocks + blockIdx.x] = sh[0];
     __syncthreads();
   }
-  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+
+// block per evaluation: sum_b partial_b z^b (z = x^(kEvalChunk2 kT) = x^(2^12)), each of the
+// 1024 threads Horner over q consecutive block sums, then a tree with factors (z^q)^(2^l)
+__global__ void __launch_bounds__(1024) k_eval_comb(EvalSet es, const Fr* __restrict__ partial, int nblocks,
+                                                    Fr* __restrict__ out) {
+  __shared__ Fr sh[1024];
+  __shared__ F29 zl[11];  // [0] = z, [1 + l] = w^(2^l), w = z^q, l < 10
+  const int j = blockIdx.x;
+  const int q = (nblocks + 1023) / 1024;
+  if (threadIdx.x == 0) {
+    Fr z = es.x[j];
+    for (int k = 0; k < kEvalLogChunk2 + 8; k++) z = z * z;
+    zl[0] = fr29_operand_dev(z);
+    Fr w = Fr::one();
+    for (int k = 0; k < q; k++) w = w * z;
+    for (int l = 0; l < 10; l++) {
+      zl[1 + l] = fr29_operand_dev(w);
+      w = w * w;
+    }
+  }
+  __syncthreads();
+  Fr acc = Fr::zero();
+  const int b0 = (int)threadIdx.x * q;
+  for (int b = b0 + q; b-- > b0;)
+    if (b < nblocks) acc = mul_fr29(acc, zl[0]) + partial[(size_t)j * nblocks + b];
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int l = 0; l < 10; l++) {
+    const unsigned st = 1u << l;
+    if ((threadIdx.x & (2 * st - 1)) == 0) sh[threadIdx.x] = sh[threadIdx.x] + mul_fr29(sh[threadIdx.x + st], zl[1 + l]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[j] = sh[0];
 }
 
 struct RArgs {
@@ -499,6 +572,12 @@ Prover::~Prover() {
     }
     if (ready[i]) (void)hipEventDestroy(ready[i]);
   }
+  if (side) {
+    (void)hipStreamSynchronize(side);
+    (void)hipStreamDestroy(side);
+  }
+  if (side_ready) (void)hipEventDestroy(side_ready);
+  if (side_done) (void)hipEventDestroy(side_done);
 }
 
 MsmShard::~MsmShard() {
@@ -707,6 +786,9 @@ void Prover::init_slots() {
     NZ_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
     NZ_HIP(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
   }
+  NZ_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+  NZ_HIP(hipEventCreateWithFlags(&side_ready, hipEventDisableTiming));
+  NZ_HIP(hipEventCreateWithFlags(&side_done, hipEventDisableTiming));
 }
 
 // per-proof working set (one per lane)
@@ -722,9 +804,9 @@ void Prover::alloc_workspace() {
   size_t lv = 0, m = n4;
   while (m > 1024) { m = (m + kScanChunk - 1) / kScanChunk; lv += m; }
   scan_tmp.alloc(lv + 2048);
-  size_t nblocks = ((size_t)3 * n + 6 + (size_t)kT * kEvalChunk - 1) / ((size_t)kT * kEvalChunk) + 1;
-  eval_part.alloc(nblocks);
-  host_part.resize(nblocks);
+  size_t nblocks = ((size_t)3 * n + 6 + (size_t)kT * kEvalChunk2 - 1) / ((size_t)kT * kEvalChunk2) + 1;
+  eval_part.alloc((size_t)kEvalMax * nblocks + kEvalMax);  // eval_many: kEvalMax rows + results
+  host_part.resize(std::max<size_t>(nblocks, kEvalMax));
   flags.p = (uint32_t*)(blind.p + 12);  // a view: the blinding upload also clears the flags
   flags.n = 1;
   flags.owned = false;
@@ -763,8 +845,8 @@ Prover::Prover(const Prover& pk, int) {
 // ----------------------------------------------------------------------------
 // building blocks
 // ----------------------------------------------------------------------------
-void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb) {
-  hipStream_t s = st();
+void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb, hipStream_t s) {
+  if (!s) s = st();
   auto t0 = std::chrono::steady_clock::now();
   ntt(eng->ntt_tables, evals, coefs, power, true, s);
   BlindIdx bi;
@@ -878,19 +960,34 @@ void Prover::set_msm_split(int world, size_t own_points, nzcb_msm_send_fn send, 
   split_own = own_points;
 }
 
-Fr Prover::eval_poly(const Fr* p, size_t len, const Fr& x) {
+void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out) {
+  if (np < 1 || np > kEvalMax) throw Error(NZCB_ERR_INTERNAL, "eval_many: bad count");
   hipStream_t s = st();
-  size_t nthreads = (len + kEvalChunk - 1) / kEvalChunk;
-  size_t nblocks = (nthreads + kT - 1) / kT;
-  if (nblocks > host_part.size()) throw Error(NZCB_ERR_INTERNAL, "eval partial buffer too small");
-  Fr xK = pow_u64(x, kEvalChunk);
-  hipLaunchKernelGGL(k_eval, dim3((unsigned)nblocks), dim3(kT), 0, s, p, len, x, xK, eval_part.p);
+  EvalSet es{};
+  size_t maxlen = 0;
+  for (int j = 0; j < np; j++) {
+    es.p[j] = polys[j];
+    es.len[j] = lens[j];
+    es.x[j] = xs[j];
+    es.x29[j] = fr29_operand(xs[j]);
+    maxlen = std::max(maxlen, lens[j]);
+  }
+  es.np = np;
+  const size_t nblocks = (maxlen + (size_t)kT * kEvalChunk2 - 1) / ((size_t)kT * kEvalChunk2);
+  if ((size_t)np * nblocks + kEvalMax > eval_part.n) throw Error(NZCB_ERR_INTERNAL, "eval partial buffer too small");
+  Fr* res = eval_part.p + (size_t)np * nblocks;
+  if (np == 7)
+    hipLaunchKernelGGL(k_eval_multi<7>, dim3((unsigned)nblocks), dim3(kT), 0, s, es, eval_part.p, (int)nblocks);
+  else if (np == 1)
+    hipLaunchKernelGGL(k_eval_multi<1>, dim3((unsigned)nblocks), dim3(kT), 0, s, es, eval_part.p, (int)nblocks);
+  else
+    throw Error(NZCB_ERR_INTERNAL, "eval_many: 1 or 7 evaluations");
   NZ_HIP(hipGetLastError());
-  NZ_HIP(hipMemcpyAsync(host_part.data(), eval_part.p, nblocks * sizeof(Fr), hipMemcpyDeviceToHost, s));
+  hipLaunchKernelGGL(k_eval_comb, dim3(np), dim3(1024), 0, s, es, (const Fr*)eval_part.p, (int)nblocks, res);
+  NZ_HIP(hipGetLastError());
+  NZ_HIP(hipMemcpyAsync(host_part.data(), res, np * sizeof(Fr), hipMemcpyDeviceToHost, s));
   NZ_HIP(hipStreamSynchronize(s));
-  Fr acc = Fr::zero();
-  for (size_t b = 0; b < nblocks; b++) acc = acc + host_part[b];
-  return acc;
+  for (int j = 0; j < np; j++) out[j] = host_part[j];
 }
 
 void Prover::prefix_product(Fr* x, size_t m, Fr* level_tmp) {
@@ -984,6 +1081,9 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   NZ_HIP(hipSetDevice(eng->device));
   hipStream_t s = st();
   msm_ms = ntt_ms = 0;
+  // a previous proof that failed in round 2 may have left the side stream's NTTs running
+  // on this lane's buffers (blind, A, B, C)
+  if (side_done) NZ_HIP(hipEventSynchronize(side_done));
   RoctxPhases ranges("plonk_prove");
   ranges.next("witness: calculateAdditions + buildABC");
   auto T0 = std::chrono::steady_clock::now();
@@ -1043,9 +1143,16 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       commit_start(1, B.p, n + 2, &ltab, ltau.p);
       lg("multiexp C");
       commit_start(2, C.p, n + 2, &ltab, ltau.p);
-      to4t(A.p, pol_a.p, A4.p, ba, 2);
-      to4t(B.p, pol_b.p, B4.p, bb, 2);
-      to4t(C.p, pol_c.p, C4.p, bc, 2);
+      // the interpolations and 4n coset evaluations of A, B, C are only needed by round
+      // 3's quotient (and round 4): on the side stream they overlap the commitments AND
+      // round 2's grand product, which reads the evaluations only (round 2 waits for them
+      // before Z's own NTTs, which share the NTT scratch)
+      NZ_HIP(hipEventRecord(side_ready, s));
+      NZ_HIP(hipStreamWaitEvent(side, side_ready, 0));
+      to4t(A.p, pol_a.p, A4.p, ba, 2, side);
+      to4t(B.p, pol_b.p, B4.p, bb, 2, side);
+      to4t(C.p, pol_c.p, C4.p, bc, 2, side);
+      NZ_HIP(hipEventRecord(side_done, side));
     } else {
       to4t(A.p, pol_a.p, A4.p, ba, 2);
       lg("multiexp A");
@@ -1109,6 +1216,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     NZ_HIP(hipStreamSynchronize(s));
     if (last_pref * last_ratio != Fr::one()) throw Error(NZCB_ERR_COPY, "Copy constraints does not match");
     const int bz[3] = {9, 8, 7};
+    NZ_HIP(hipStreamWaitEvent(s, side_done, 0));  // A, B, C's NTTs (same scratch) are done
     to4t(Z.p, pol_z.p, Z4.p, bz, 3);
     lg("multiexp Z");
     commit_start(0, pol_z.p, n + 3);
@@ -1189,13 +1297,20 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     g1_uncompressed(pT3, tr.data() + 128);
     xi = hash_to_fr(tr);
     lg("xi: " + fr_dec(xi));
-    ea = eval_poly(pol_a.p, n + 2, xi);
-    eb = eval_poly(pol_b.p, n + 2, xi);
-    ec = eval_poly(pol_c.p, n + 2, xi);
-    es1 = eval_poly(sigma.p, n, xi);
-    es2 = eval_poly(sigma.p + 5 * (size_t)n, n, xi);
-    et = eval_poly(t.p, 3 * (size_t)n + 6, xi);
-    ezw = eval_poly(pol_z.p, n + 3, xi * wn);
+    {
+      const Fr* polys[7] = {pol_a.p, pol_b.p, pol_c.p, sigma.p, sigma.p + 5 * (size_t)n, t.p, pol_z.p};
+      const size_t lens[7] = {n + 2, n + 2, n + 2, n, n, 3 * (size_t)n + 6, n + 3};
+      const Fr xs[7] = {xi, xi, xi, xi, xi, xi, xi * wn};
+      Fr ev[7];
+      eval_many(7, polys, lens, xs, ev);
+      ea = ev[0];
+      eb = ev[1];
+      ec = ev[2];
+      es1 = ev[3];
+      es2 = ev[4];
+      et = ev[5];
+      ezw = ev[6];
+    }
     Fr coef_ab = ea * eb;
     Fr betaxi = beta * xi;
     Fr e2 = (ea + betaxi + gamma) * (eb + betaxi * k1 + gamma);
@@ -1210,7 +1325,11 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     hipLaunchKernelGGL(k_pol_r, dim3(grid_for(n + 3, kT, 1u << 30)), dim3(kT), 0, s, pol_z.p, qm.p, ql.p, qr.p,
                        qo.p, qc.p, sigma.p + 10 * (size_t)n, (size_t)n, ra, pol_r.p);
     NZ_HIP(hipGetLastError());
-    er = eval_poly(pol_r.p, n + 3, xi);
+    {
+      const Fr* polys[1] = {pol_r.p};
+      const size_t lens[1] = {n + 3};
+      eval_many(1, polys, lens, &xi, &er);
+    }
   }
   tm[5] = ms_since(t4);
 
