@@ -15,7 +15,10 @@ struct MsmBaseTable {
   DevBuf<G1Affine> q;  // affine, coordinates x * 2^261 mod p (Montgomery-261, csrc/f29.h)
   size_t n = 0, stride = 0;
   int c = 0, nw = 0;
-  void build(const G1Affine* bases, size_t n, int c, hipStream_t st);
+  // rows of 2^-256 B_i: the MSM then takes Montgomery-256 scalars as they are (mont = true
+  // is required; msm.hip msm_table_kernel)
+  bool mont_folded = false;
+  void build(const G1Affine* bases, size_t n, int c, hipStream_t st, bool fold_mont = false);
 };
 
 // Window size of the table-based (fixed-base) MSM: 16..20 bits (NZCB_FB_WINDOW
@@ -70,6 +73,7 @@ struct MsmScratch {
   double phase_ms[7] = {0, 0, 0, 0, 0, 0, 0};
   uint64_t prof_launches = 0, prof_points = 0, prof_entries = 0;
   hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t done = nullptr;  // recorded after the window sums' copy to host_win (msm_finish waits on it)
   void init(size_t max_points, bool fixed_base = false);
   ~MsmScratch();
 };

@@ -156,6 +156,23 @@ static bool paired_products() {
 //   0           the generic schedule's 8x32 segment reduce + slot sums
 // Same box (profiles/r3_fb_sums_ab.txt): 1 cut the isolated MSM 3.48 -> 3.08 ms but moved
 // 4x the additions of 0 (every bucket in ~8 slots) and the 5-lane bench lost 2 %.
+static uint32_t seq_span29() {  // NZCB_SEQ_SPAN29: longest carry run a finalize thread sums (A/B)
+  static const uint32_t v = [] {
+    const char* e = std::getenv("NZCB_SEQ_SPAN29");
+    const int x = e ? std::atoi(e) : (int)kSeqSpan29;
+    return (uint32_t)(x >= 1 ? x : kSeqSpan29);
+  }();
+  return v;
+}
+
+static bool lo_split() {  // NZCB_LO_SPLIT=0: one workgroup per high-byte region (A/B runs)
+  static const bool on = [] {
+    const char* e = std::getenv("NZCB_LO_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static bool lo_agg() {  // NZCB_LO_AGG=1: wave-aggregated LDS atomics in msm_lo_* (A/B runs)
   static const bool on = [] {
     const char* e = std::getenv("NZCB_LO_AGG");
@@ -695,6 +712,91 @@ msm_lo_scatter_kernel(const typename std::conditional<LO <= 8, uint8_t, uint16_t
   }
 }
 
+// Round-2 step 4 (NZCB_LO_SPLIT=0, A/B runs): one workgroup per high-byte region.
+template <int LO>
+__global__ void __launch_bounds__(kLoThreads)
+msm_bucket_lo_kernel(const typename std::conditional<LO <= 8, uint8_t, uint16_t>::type* __restrict__ lo2,
+                     const uint32_t* __restrict__ vals2, const uint32_t* __restrict__ counts, uint32_t ntiles,
+                     uint32_t nkeys, uint32_t* __restrict__ offsets, uint32_t* __restrict__ sorted,
+                     uint32_t* __restrict__ large) {
+  using Lo = typename std::conditional<LO <= 8, uint8_t, uint16_t>::type;
+  constexpr uint32_t NL = 1u << LO;  // buckets per high-byte region
+  constexpr uint32_t U = 8;
+  __shared__ uint32_t h[NL], lcnt[NL], lst[NL];
+  __shared__ uint32_t wsum[kLoThreads / 64], reg[1];
+  __shared__ uint32_t lv[U * kLoThreads];
+  __shared__ Lo lk[U * kLoThreads];
+  const uint32_t hb = blockIdx.x;
+  const uint32_t* tail = counts + (size_t)256 * ntiles;  // row totals
+  {
+    uint32_t tot;
+    const uint32_t st = scan256_excl(threadIdx.x < 256 ? tail[threadIdx.x] : 0u, wsum, tot);
+    if (threadIdx.x == hb) reg[0] = st;  // this region's start
+  }
+  for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) h[i] = 0;
+  __syncthreads();
+  const uint32_t s = reg[0];
+  const uint32_t e = s + tail[hb];
+  // 8 independent loads in flight per thread before their atomics (the loop is
+  // latency-bound otherwise: one workgroup per CU walks ~entries/256 entries)
+  for (uint32_t p0 = s; p0 < e; p0 += U * kLoThreads) {
+    uint32_t k8[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t p = p0 + u * kLoThreads + threadIdx.x;
+      k8[u] = p < e ? (uint32_t)lo2[p] : NL;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (k8[u] < NL) atomicAdd(&h[k8[u]], 1u);
+  }
+  __syncthreads();
+  block_scan_excl<kLoThreads>(h, NL, wsum);  // low-index counts -> bucket offsets in the region
+  for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) {
+    h[i] += s;
+    const uint32_t key = (hb << LO) | i;
+    if (key < nkeys) offsets[key] = h[i];
+  }
+  if (hb == 255 && threadIdx.x == 0) offsets[nkeys] = e;  // entries in all: the last region's end
+  if (hb == 0 && threadIdx.x == 0) large[0] = 0;          // the finalize's count of long bucket runs
+  __syncthreads();
+  // scatter in chunks of U * kLoThreads entries, each ranked by low index in LDS first and
+  // written out run by run (coalesced)
+  for (uint32_t p0 = s; p0 < e; p0 += U * kLoThreads) {
+    uint32_t k8[U], v8[U], r8[U];
+    for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) lcnt[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t p = p0 + u * kLoThreads + threadIdx.x;
+      k8[u] = p < e ? (uint32_t)lo2[p] : NL;
+      v8[u] = p < e ? vals2[p] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (k8[u] < NL) r8[u] = atomicAdd(&lcnt[k8[u]], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) lst[i] = lcnt[i];
+    __syncthreads();
+    block_scan_excl<kLoThreads>(lst, NL, wsum);
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (k8[u] < NL) {
+        const uint32_t q = lst[k8[u]] + r8[u];
+        lk[q] = (Lo)k8[u];
+        lv[q] = v8[u];
+      }
+    __syncthreads();
+    const uint32_t cnt = e - p0 < U * kLoThreads ? e - p0 : U * kLoThreads;
+    for (uint32_t q = threadIdx.x; q < cnt; q += kLoThreads) {
+      const uint32_t k = lk[q];
+      sorted[h[k] + (q - lst[k])] = lv[q];
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < NL; i += kLoThreads) h[i] += lcnt[i];
+  }
+}
+
 static bool use_library_sort() {
   static const bool v = [] {
     const char* e = std::getenv("NZCB_ROCPRIM_SORT");
@@ -1159,7 +1261,7 @@ __device__ __forceinline__ G1xyzz sum_run(const Xyzz29* carry_own, const Xyzz29*
 // into `buckets` (single-chunk ones from `single`).
 template <class P>
 __global__ void __launch_bounds__(kMsmThreads)
-msm_bucket_finalize_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys,
+msm_bucket_finalize_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys, uint32_t seq_span29,
                            const P* __restrict__ single,
                            const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
                            G1xyzz* __restrict__ buckets, uint32_t* __restrict__ large, Xyzz29* __restrict__ out29) {
@@ -1172,7 +1274,7 @@ msm_bucket_finalize_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets,
     if (single && !out29) buckets[k] = load_point(single[k]);
     return;
   }
-  if (c1 - c0 > (std::is_same<P, Xyzz29>::value ? kSeqSpan29 : kSeqSpan)) {  // long run (skewed digits)
+  if (c1 - c0 > (std::is_same<P, Xyzz29>::value ? seq_span29 : kSeqSpan)) {  // long run (skewed digits)
     large[1 + atomicAdd(&large[0], 1u)] = (uint32_t)k;
     return;
   }
@@ -1563,10 +1665,13 @@ msm_parts29_kernel(const Xyzz29* __restrict__ parts, int nparts, G1xyzz* __restr
 }
 
 // Shifted-base table: row w = 2^(c*w) * B_i, thread per base (c doublings per row,
-// one Fermat inversion per stored affine point).
+// one Fermat inversion per stored affine point). fold: the rows of 2^-256 B_i instead
+// (kinv = 2^-256 mod r as an integer), so that the Montgomery-256 form m = s 2^256 of a
+// scalar is itself the digit source: sum m_i (2^-256 B_i) = sum s_i B_i, and the MSM's
+// two digit passes skip their from_mont_fr29 product per scalar.
 __global__ void __launch_bounds__(kMsmThreads)
-msm_table_kernel(const G1Affine* __restrict__ bases, size_t n, size_t stride, int c, int nw, Fq k261,
-                 G1Affine* __restrict__ q) {
+msm_table_kernel(const G1Affine* __restrict__ bases, size_t n, size_t stride, int c, int nw, Fq k261, int fold,
+                 Fr kinv, G1Affine* __restrict__ q) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const G1Affine P = bases[i];
@@ -1575,6 +1680,13 @@ msm_table_kernel(const G1Affine* __restrict__ bases, size_t n, size_t stride, in
     return;
   }
   G1xyzz acc = xyzz_from_affine(P);
+  if (fold) {  // 2^-256 P, left-to-right double-and-add (kinv < r < 2^254, uniform bits)
+    acc = G1xyzz::inf();
+    for (int b = 253; b >= 0; b--) {
+      acc = xyzz_dbl(acc);
+      if ((kinv.v[b >> 5] >> (b & 31)) & 1u) acc = xyzz_add_affine(acc, P.x, P.y);
+    }
+  }
   for (int w = 0; w < nw; w++) {
     if (w)
       for (int k = 0; k < c; k++) acc = xyzz_dbl(acc);
@@ -1586,8 +1698,9 @@ msm_table_kernel(const G1Affine* __restrict__ bases, size_t n, size_t stride, in
   }
 }
 
-void MsmBaseTable::build(const G1Affine* bases, size_t npts, int cbits, hipStream_t st) {
+void MsmBaseTable::build(const G1Affine* bases, size_t npts, int cbits, hipStream_t st, bool fold_mont) {
   n = npts;
+  mont_folded = fold_mont;
   stride = npts;
   c = cbits;
   nw = num_windows(c);
@@ -1597,8 +1710,11 @@ void MsmBaseTable::build(const G1Affine* bases, size_t npts, int cbits, hipStrea
   Fq thirty_two = Fq::zero();
   thirty_two.v[0] = 32;
   const Fq k261 = to_mont(thirty_two);  // 2^261 mod p
+  Fr one_raw = Fr::zero();
+  one_raw.v[0] = 1;
+  const Fr kinv = from_mont(one_raw);  // the integer 2^-256 mod r
   hipLaunchKernelGGL(msm_table_kernel, dim3(grid_for(n, kMsmThreads, 1u << 30)), dim3(kMsmThreads), 0, st, bases, n,
-                     stride, c, nw, k261, q.p);
+                     stride, c, nw, k261, fold_mont ? 1 : 0, kinv, q.p);
   NZ_HIP(hipGetLastError());
 }
 
@@ -1716,6 +1832,7 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
 
 MsmScratch::~MsmScratch() {
   if (host_win) (void)hipHostFree(host_win);
+  if (done) (void)hipEventDestroy(done);
   for (auto& e : ev)
     if (e) (void)hipEventDestroy(e);
 }
@@ -1766,8 +1883,12 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                  const MsmBaseTable* table) {
   sc.cur_n = n;
   if (n == 0) return;
+  if (!sc.done) NZ_HIP(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming));
   if (n > sc.max_points) throw Error(NZCB_ERR_ARG, "msm larger than scratch");
   if (table && n > table->n) throw Error(NZCB_ERR_ARG, "msm larger than its base table");
+  if (table && table->mont_folded && !mont) throw Error(NZCB_ERR_ARG, "2^-256-folded table needs Montgomery scalars");
+  // a folded table takes the Montgomery form's integer as the scalar (msm_table_kernel)
+  const int mdig = (mont && !(table && table->mont_folded)) ? 1 : 0;
   const MsmPlan p = make_plan(n, table);
   if (p.entries > sc.sorted.n || p.nkeys + 1 > sc.offsets.n)
     throw Error(NZCB_ERR_ARG, "msm scratch was not sized for this schedule");
@@ -1795,7 +1916,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   if (bins) {  // hand-written bucketing (see msm_bin_hist_kernel)
     const uint32_t ntiles = (uint32_t)((n + kTileScalars - 1) / kTileScalars);
     uint32_t* tail = sc.bin_counts.p + (size_t)256 * ntiles;
-    const int m = mont ? 1 : 0;
+    const int m = mdig;
     auto run_bins = [&](auto cc) {
       constexpr int C = decltype(cc)::value;
       using Lo = typename BinKeys<C>::Lo;
@@ -1810,6 +1931,12 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
       NZ_HIP(hipGetLastError());
       mark(2);
       constexpr int LO = BinKeys<C>::LO;
+      if (!lo_split()) {
+        hipLaunchKernelGGL(msm_bucket_lo_kernel<LO>, dim3(256), dim3(kLoThreads), 0, st, (const Lo*)lo2,
+                           sc.vals_mid.p, sc.bin_counts.p, ntiles, p.nkeys, sc.offsets.p, sc.sorted.p, sc.large.p);
+        NZ_HIP(hipGetLastError());
+        return;
+      }
       const dim3 igrid((unsigned)lo_items_bound(p.entries));
       hipLaunchKernelGGL((lo_agg() ? msm_lo_count_kernel<LO, true> : msm_lo_count_kernel<LO, false>), igrid,
                          dim3(kLoThreads), 0, st, (const Lo*)lo2, sc.bin_counts.p, ntiles, sc.lo_seg.p);
@@ -1830,7 +1957,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
       default: run_bins(std::integral_constant<int, 20>()); break;
     }
   } else {
-    keys_dispatch(p.c, scalars, n, mont ? 1 : 0, table, sc, st);
+    keys_dispatch(p.c, scalars, n, mdig, table, sc, st);
     mark(1);
   }
   size_t tmp = sc.sort_tmp_bytes;
@@ -1925,7 +2052,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                          (const Xyzz29*)sc.carry_cont29.p, sc.large.p, out29);
     else
       hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, acc_off,
-                         p.nkeys, (const Xyzz29*)sc.buckets29.p, (const Xyzz29*)sc.carry_own29.p,
+                         p.nkeys, seq_span29(), (const Xyzz29*)sc.buckets29.p, (const Xyzz29*)sc.carry_own29.p,
                          (const Xyzz29*)sc.carry_cont29.p, sc.buckets.p, sc.large.p, out29);
     NZ_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, acc_off, sc.large.p,
@@ -1939,7 +2066,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                        sc.large_off.p, sc.large_part.p, sc.buckets.p, out29);
   } else {
     hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
-                       (const G1xyzz*)nullptr, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p,
+                       kSeqSpan29, (const G1xyzz*)nullptr, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p,
                        sc.buckets.p, sc.large.p, (Xyzz29*)nullptr);
     NZ_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_bucket_large_kernel<G1xyzz>, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, chunk,
@@ -1963,6 +2090,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     NZ_HIP(hipGetLastError());
     mark(7);
     NZ_HIP(hipMemcpyAsync(sc.host_win, sc.win.p, (size_t)p.nslots29 * sizeof(G1xyzz), hipMemcpyDeviceToHost, st));
+    NZ_HIP(hipEventRecord(sc.done, st));
     return;
   }
   if (bsums) {
@@ -1975,6 +2103,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     NZ_HIP(hipGetLastError());
     mark(7);
     NZ_HIP(hipMemcpyAsync(sc.host_win, sc.win.p, (size_t)(p.lb + 1) * sizeof(G1xyzz), hipMemcpyDeviceToHost, st));
+    NZ_HIP(hipEventRecord(sc.done, st));
     return;
   }
   hipLaunchKernelGGL(msm_bucket_reduce_kernel, dim3(grid_for((size_t)p.nsets * p.nseg, kMsmThreads, 1u << 30)),
@@ -1991,11 +2120,14 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   mark(7);
   NZ_HIP(hipMemcpyAsync(sc.host_win, sc.win.p, (size_t)p.nsets * p.nslots * sizeof(G1xyzz), hipMemcpyDeviceToHost,
                         st));
+  NZ_HIP(hipEventRecord(sc.done, st));
 }
 
 G1xyzz msm_finish(MsmScratch& sc, hipStream_t st) {
   if (sc.cur_n == 0) return G1xyzz::inf();
-  NZ_HIP(hipStreamSynchronize(st));
+  // the window sums' copy, not the whole stream: work queued on the stream after the MSM
+  // (the prover's A/B/C interpolations follow C's commitment on its stream) runs on
+  NZ_HIP(hipEventSynchronize(sc.done));
   const int c = sc.cur_c, nsets = sc.cur_nsets, nslots = sc.cur_nbits + 1;
   if (sc.prof) {
     float t = 0;

@@ -114,12 +114,14 @@ struct Prover {
   void init_slots();
   void alloc_workspace();
   void to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb, hipStream_t s = nullptr);
+  void to4t_coefs(const Fr* evals, Fr* coefs, const int* bidx, int nb, hipStream_t s);
+  void to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s);
   void commit_start(int slot, const Fr* scalars, size_t len, const MsmBaseTable* tab = nullptr,
-                    const G1Affine* bases = nullptr);
+                    const G1Affine* bases = nullptr, bool on_main = false);
   G1Affine commit_finish(int slot);
   // np <= 8 evaluations p_j(x_j) (two launches, one host round trip)
   void eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out);
-  void prefix_product(Fr* x, size_t m, Fr* level_tmp);
+  void prefix_product(Fr* x, size_t m, Fr* level_tmp, bool have_totals = false);
   void suffix_linear(Fr* x, size_t m, const Fr& d, Fr* level_tmp);
   void div_pol1(const Fr* src, size_t m, const Fr& d, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit);
   double ms_since(std::chrono::steady_clock::time_point t0);

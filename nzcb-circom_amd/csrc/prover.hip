@@ -121,9 +121,74 @@ static F29 fr29_operand(Fr c) {
   return split29(c);
 }
 
-// Round 2: num_i / den_i with chunked Montgomery batch inversion.
+// Round 2: num_i / den_i with Montgomery batch inversion: each thread's chunk of
+// kScanChunk denominators by prefix products, then ONE Fermat inversion per workgroup
+// over a product tree of the threads' chunk totals in LDS (one inversion per chunk was
+// ~12 of the ~24 products per element, and a 1.1 ms launch on round 2's path).
 __global__ void __launch_bounds__(kT)
 k_perm_ratio(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
+             const Fr* __restrict__ sigma, size_t n, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi,
+             PermArgs pa, Fr* __restrict__ ratio, Fr* __restrict__ den_s, Fr* __restrict__ pre_s,
+             Fr* __restrict__ chunk_tot) {
+  __shared__ Fr tree[2 * kT];
+  const int tid = threadIdx.x;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + tid;
+  const size_t s = t * kScanChunk;
+  const size_t e = s >= n ? s : (s + kScanChunk < n ? s + kScanChunk : n);  // empty past n
+  const Fr* s1 = sigma + n;  // sigma1 evals (4n), read at stride 4
+  const Fr* s2 = sigma + 5 * n + n;
+  const Fr* s3 = sigma + 10 * n + n;
+  Fr pre = Fr::one();
+  for (size_t i = s; i < e; i++) {
+    Fr w = root4(rlo, rhi, 4 * i);
+    Fr a = A[i], b = B[i], c = C[i];
+    const Fr bw = mul_fr29(w, pa.beta29);
+    const Fr k1bw = pa.k23 ? bw + bw : mul_fr29(w, pa.k1beta29);
+    const Fr k2bw = pa.k23 ? k1bw + bw : mul_fr29(w, pa.k2beta29);
+    Fr num = (a + bw + pa.gamma) * (b + k1bw + pa.gamma);
+    num = num * (c + k2bw + pa.gamma);
+    Fr den = (a + mul_fr29(s1[4 * i], pa.beta29) + pa.gamma) * (b + mul_fr29(s2[4 * i], pa.beta29) + pa.gamma);
+    den = den * (c + mul_fr29(s3[4 * i], pa.beta29) + pa.gamma);
+    ratio[i] = num;
+    den_s[i] = den;
+    pre = pre * den;
+    pre_s[i] = pre;
+  }
+  // one inversion for the workgroup: product tree over the chunk totals, inverted at the
+  // root, unwound to each thread's 1 / (its chunk's product)
+  tree[kT + tid] = pre;
+  __syncthreads();
+  for (int w = kT / 2; w >= 1; w >>= 1) {
+    if (tid < w) tree[w + tid] = tree[2 * (w + tid)] * tree[2 * (w + tid) + 1];
+    __syncthreads();
+  }
+  if (tid == 0) tree[1] = inverse(tree[1]);
+  __syncthreads();
+  for (int w = 1; w < kT; w <<= 1) {
+    if (tid < w) {
+      const int nd = w + tid;
+      const Fr iv = tree[nd], l = tree[2 * nd], r = tree[2 * nd + 1];
+      tree[2 * nd] = iv * r;
+      tree[2 * nd + 1] = iv * l;
+    }
+    __syncthreads();
+  }
+  Fr inv = tree[kT + tid];
+  Fr prod = Fr::one();  // the chunk's product of ratios: level 0 of Z's prefix-product scan
+  for (size_t i = e; i-- > s;) {
+    Fr before = (i > s) ? pre_s[i - 1] : Fr::one();
+    Fr dinv = inv * before;
+    inv = inv * den_s[i];
+    const Fr r = ratio[i] * dinv;
+    ratio[i] = r;
+    prod = prod * r;
+  }
+  if (s < n) chunk_tot[t] = prod;
+}
+
+// Round 2 as in round 2 (NZCB_PERM_TREE=0, A/B runs): one inversion per thread's chunk.
+__global__ void __launch_bounds__(kT)
+k_perm_ratio_chunk(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
              const Fr* __restrict__ sigma, size_t n, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi,
              PermArgs pa, Fr* __restrict__ ratio, Fr* __restrict__ den_s, Fr* __restrict__ pre_s) {
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -366,6 +431,29 @@ __global__ void k_dbl_pow(Fr* __restrict__ x, size_t m, int e) {
 static F29 f29_exp(Fr v, int extra) {  // split29 of v * 2^extra (host)
   for (int k = 0; k < extra; k++) v = v + v;
   return split29(v);
+}
+
+// One evaluation per launch (NZCB_EVAL_MANY=0, A/B runs): chunked Horner, partial[block]
+// = sum over the block's chunks of p(chunk) * x^(chunk start), summed on the host
+static constexpr int kEvalChunk = 64;
+__global__ void __launch_bounds__(kT)
+k_eval(const Fr* __restrict__ p, size_t len, Fr x, Fr xK, Fr* __restrict__ partial) {
+  __shared__ Fr sh[kT];
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t s = t * kEvalChunk;
+  Fr acc = Fr::zero();
+  if (s < len) {
+    size_t e = s + kEvalChunk < len ? s + kEvalChunk : len;
+    for (size_t i = e; i-- > s;) acc = acc * x + p[i];
+    acc = acc * pow_u64(xK, (uint64_t)t);
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int stride = kT / 2; stride > 0; stride >>= 1) {
+    if ((int)threadIdx.x < stride) sh[threadIdx.x] = sh[threadIdx.x] + sh[threadIdx.x + stride];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
 }
 
 // Round 4, all evaluations of one point set in two launches and one host round trip
@@ -653,7 +741,14 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     if (sec.len) NZ_HIP(hipMemcpyAsync(buf.p, sec.p, sec.len, hipMemcpyHostToDevice, s));
   };
   up(ptau, z.ptau);
-  ptab.build(ptau.p, ptau.n, fixed_base_window(), s);
+  // rows of 2^-256 PTau: the commitments' Montgomery-form scalars are digit sources as
+  // they are (every ptab MSM is enqueued with mont = true; split ranges and devices keep
+  // plain tables)
+  static const bool fold = [] {  // NZCB_FOLD=0: a plain PTau table (A/B runs)
+    const char* e = std::getenv("NZCB_FOLD");
+    return !(e && e[0] == '0');
+  }();
+  ptab.build(ptau.p, ptau.n, fixed_base_window(), s, fold);
   lcommit = lagrange_commit_enabled() && ptau.n >= (size_t)n + 2;
   if (lcommit) {  // one elliptic-curve iNTT per context (csrc/lagrange.hip)
     ltau.alloc((size_t)n + 2);
@@ -786,7 +881,11 @@ void Prover::init_slots() {
     NZ_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
     NZ_HIP(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
   }
-  NZ_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+  static const bool use_side = [] {  // NZCB_SIDE_STREAM=1: a stream of their own (A/B runs)
+    const char* e = std::getenv("NZCB_SIDE_STREAM");
+    return e && e[0] == '1';
+  }();
+  if (use_side) NZ_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
   NZ_HIP(hipEventCreateWithFlags(&side_ready, hipEventDisableTiming));
   NZ_HIP(hipEventCreateWithFlags(&side_done, hipEventDisableTiming));
 }
@@ -828,6 +927,7 @@ Prover::Prover(const Prover& pk, int) {
   ptau.alias(pk.ptau);
   ptab.q.alias(pk.ptab.q);
   ptab.n = pk.ptab.n; ptab.stride = pk.ptab.stride; ptab.c = pk.ptab.c; ptab.nw = pk.ptab.nw;
+  ptab.mont_folded = pk.ptab.mont_folded;
   lcommit = pk.lcommit;
   ltau.alias(pk.ltau);
   ltab.q.alias(pk.ltab.q);
@@ -847,12 +947,25 @@ Prover::Prover(const Prover& pk, int) {
 // ----------------------------------------------------------------------------
 void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb, hipStream_t s) {
   if (!s) s = st();
+  to4t_coefs(evals, coefs, bidx, nb, s);
+  to4t_evals4(coefs, evals4, nb, s);
+}
+
+// the blinded coefficients (what the commitment needs) ...
+void Prover::to4t_coefs(const Fr* evals, Fr* coefs, const int* bidx, int nb, hipStream_t s) {
   auto t0 = std::chrono::steady_clock::now();
   ntt(eng->ntt_tables, evals, coefs, power, true, s);
   BlindIdx bi;
   bi.count = nb;
   for (int k = 0; k < nb; k++) bi.idx[k] = bidx[k];
   hipLaunchKernelGGL(k_blind, dim3(1), dim3(64), 0, s, coefs, (size_t)n, blind.p, bi);
+  NZ_HIP(hipGetLastError());
+  ntt_ms += ms_since(t0);  // host enqueue time only (kernels run asynchronously)
+}
+
+// ... and their 4n coset evaluations (what round 3's quotient needs)
+void Prover::to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s) {
+  auto t0 = std::chrono::steady_clock::now();
   // evaluations of the *blinded* polynomial on the coset g*<w4> (round-3 quotient input)
   NttIo io;  // coset shift g^j and the zero padding fused into the NTT's first pass
   io.in_len = (size_t)n + nb;
@@ -865,9 +978,11 @@ void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int n
 // Commitments run on their own streams: the MSM of one polynomial overlaps the NTTs
 // of the next and the other MSMs of the same round (their sort / reduction kernels are
 // latency-bound and fill the gaps of the compute-bound bucket accumulation).
-void Prover::commit_start(int slot, const Fr* coefs, size_t len, const MsmBaseTable* tab, const G1Affine* bases) {
+void Prover::commit_start(int slot, const Fr* coefs, size_t len, const MsmBaseTable* tab, const G1Affine* bases,
+                          bool on_main) {
   NZ_HIP(hipEventRecord(ready[slot], st()));
-  NZ_HIP(hipStreamWaitEvent(aux[slot], ready[slot], 0));
+  hipStream_t ms = on_main ? st() : aux[slot];  // the stream this slot's MSM runs on
+  if (!on_main) NZ_HIP(hipStreamWaitEvent(ms, ready[slot], 0));
   // the Lagrange-basis commitments (A, B, C: mostly small scalars) are not split: the
   // devices and ranks of a split hold PTau ranges
   const bool local = tab != nullptr && tab != &ptab;
@@ -892,9 +1007,9 @@ void Prover::commit_start(int slot, const Fr* coefs, size_t len, const MsmBaseTa
       throw Error(NZCB_ERR_INTERNAL, "msm split: sending the scalars to the other ranks failed");
     len = std::min(len, split_own);
   }
-  msm_enqueue(*msc[slot], bases ? bases : ptau.p, coefs, len, true, aux[slot], tab ? tab : &ptab);
+  msm_enqueue(*msc[slot], bases ? bases : ptau.p, coefs, len, true, ms, tab ? tab : &ptab);
   static const bool serial = std::getenv("NZCB_SERIAL") != nullptr;  // profiling: one kernel at a time
-  if (serial) NZ_HIP(hipStreamSynchronize(aux[slot]));
+  if (serial) NZ_HIP(hipStreamSynchronize(ms));
 }
 
 namespace {
@@ -963,6 +1078,24 @@ void Prover::set_msm_split(int world, size_t own_points, nzcb_msm_send_fn send, 
 void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out) {
   if (np < 1 || np > kEvalMax) throw Error(NZCB_ERR_INTERNAL, "eval_many: bad count");
   hipStream_t s = st();
+  static const bool many = [] {
+    const char* e = std::getenv("NZCB_EVAL_MANY");
+    return !(e && e[0] == '0');
+  }();
+  if (!many) {
+    for (int j = 0; j < np; j++) {
+      const size_t nb1 = ((lens[j] + kEvalChunk - 1) / kEvalChunk + kT - 1) / kT;
+      hipLaunchKernelGGL(k_eval, dim3((unsigned)nb1), dim3(kT), 0, s, polys[j], lens[j], xs[j],
+                         pow_u64(xs[j], kEvalChunk), eval_part.p);
+      NZ_HIP(hipGetLastError());
+      NZ_HIP(hipMemcpyAsync(host_part.data(), eval_part.p, nb1 * sizeof(Fr), hipMemcpyDeviceToHost, s));
+      NZ_HIP(hipStreamSynchronize(s));
+      Fr acc = Fr::zero();
+      for (size_t b = 0; b < nb1; b++) acc = acc + host_part[b];
+      out[j] = acc;
+    }
+    return;
+  }
   EvalSet es{};
   size_t maxlen = 0;
   for (int j = 0; j < np; j++) {
@@ -990,15 +1123,16 @@ void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const
   for (int j = 0; j < np; j++) out[j] = host_part[j];
 }
 
-void Prover::prefix_product(Fr* x, size_t m, Fr* level_tmp) {
+void Prover::prefix_product(Fr* x, size_t m, Fr* level_tmp, bool have_totals) {
   hipStream_t s = st();
-  if (m <= 1024) {
+  if (m <= 1024 && !have_totals) {
     hipLaunchKernelGGL(k_scan_mul_small, dim3(1), dim3(1024), 0, s, x, (int)m, level_tmp + 1024);
     NZ_HIP(hipGetLastError());
     return;
   }
   size_t nc = (m + kScanChunk - 1) / kScanChunk;
-  hipLaunchKernelGGL(k_chunk_prod, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, level_tmp);
+  if (!have_totals)  // else level_tmp[0..nc) holds the chunk products already (k_perm_ratio)
+    hipLaunchKernelGGL(k_chunk_prod, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, level_tmp);
   prefix_product(level_tmp, nc, level_tmp + nc);
   hipLaunchKernelGGL(k_apply_prod, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, level_tmp);
   NZ_HIP(hipGetLastError());
@@ -1142,17 +1276,22 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       lg("multiexp B");
       commit_start(1, B.p, n + 2, &ltab, ltau.p);
       lg("multiexp C");
-      commit_start(2, C.p, n + 2, &ltab, ltau.p);
-      // the interpolations and 4n coset evaluations of A, B, C are only needed by round
-      // 3's quotient (and round 4): on the side stream they overlap the commitments AND
-      // round 2's grand product, which reads the evaluations only (round 2 waits for them
-      // before Z's own NTTs, which share the NTT scratch)
-      NZ_HIP(hipEventRecord(side_ready, s));
-      NZ_HIP(hipStreamWaitEvent(side, side_ready, 0));
-      to4t(A.p, pol_a.p, A4.p, ba, 2, side);
-      to4t(B.p, pol_b.p, B4.p, bb, 2, side);
-      to4t(C.p, pol_c.p, C4.p, bc, 2, side);
-      NZ_HIP(hipEventRecord(side_done, side));
+      // The interpolations and 4n coset evaluations of A, B, C are only needed by round 3's
+      // quotient (and round 4), so they overlap the commitments AND round 2's grand product,
+      // which reads the evaluations only (round 2 waits for them before Z's own NTTs, which
+      // share the NTT scratch). They run on C's commitment stream, and C's MSM takes the
+      // main stream: a stream of their own per lane cost 2.5 % of the 5-lane bench
+      // (NZCB_SIDE_STREAM=1, profiles/r3_side_stream_ab.txt). msm_finish waits on the
+      // MSM's own event, not on its stream.
+      const bool own_side = side != nullptr;
+      hipStream_t ss = own_side ? side : aux[2];
+      NZ_HIP(hipEventRecord(side_ready, s));  // A, B, C final (k_abc_tail), before C's MSM
+      commit_start(2, C.p, n + 2, &ltab, ltau.p, !own_side);
+      NZ_HIP(hipStreamWaitEvent(ss, side_ready, 0));
+      to4t(A.p, pol_a.p, A4.p, ba, 2, ss);
+      to4t(B.p, pol_b.p, B4.p, bb, 2, ss);
+      to4t(C.p, pol_c.p, C4.p, bc, 2, ss);
+      NZ_HIP(hipEventRecord(side_done, ss));
     } else {
       to4t(A.p, pol_a.p, A4.p, ba, 2);
       lg("multiexp A");
@@ -1204,22 +1343,33 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     PermArgs pa{beta, gamma, k1, k2, fr29_operand(beta), fr29_operand(k1 * beta), fr29_operand(k2 * beta),
                 k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0};
     size_t nchunks = (n + kScanChunk - 1) / kScanChunk;
-    hipLaunchKernelGGL(k_perm_ratio, dim3(grid_for(nchunks, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, sigma.p,
-                       (size_t)n, root_lo.p, root_hi.p, pa, Z.p, T.p, Tz.p);
+    static const bool perm_tree = [] {  // NZCB_PERM_TREE=0: one inversion per chunk (A/B runs)
+      const char* e = std::getenv("NZCB_PERM_TREE");
+      return !(e && e[0] == '0');
+    }();
+    if (perm_tree)
+      hipLaunchKernelGGL(k_perm_ratio, dim3(grid_for(nchunks, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, sigma.p,
+                         (size_t)n, root_lo.p, root_hi.p, pa, Z.p, T.p, Tz.p, scan_tmp.p);
+    else
+      hipLaunchKernelGGL(k_perm_ratio_chunk, dim3(grid_for(nchunks, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p,
+                         sigma.p, (size_t)n, root_lo.p, root_hi.p, pa, Z.p, T.p, Tz.p);
     NZ_HIP(hipGetLastError());
     // keep the last ratio to form the total product Z[n] = prod of all ratios
     Fr last_ratio;
     NZ_HIP(hipMemcpyAsync(&last_ratio, Z.p + (n - 1), sizeof(Fr), hipMemcpyDeviceToHost, s));
-    prefix_product(Z.p, n, scan_tmp.p);
+    prefix_product(Z.p, n, scan_tmp.p, perm_tree);
     Fr last_pref;
     NZ_HIP(hipMemcpyAsync(&last_pref, Z.p + (n - 1), sizeof(Fr), hipMemcpyDeviceToHost, s));
     NZ_HIP(hipStreamSynchronize(s));
     if (last_pref * last_ratio != Fr::one()) throw Error(NZCB_ERR_COPY, "Copy constraints does not match");
     const int bz[3] = {9, 8, 7};
     NZ_HIP(hipStreamWaitEvent(s, side_done, 0));  // A, B, C's NTTs (same scratch) are done
-    to4t(Z.p, pol_z.p, Z4.p, bz, 3);
+    // Z's commitment needs only its coefficients: its MSM starts before the 4n coset NTT,
+    // which runs beside it on the main stream (single-proof round 2: -1 ms)
+    to4t_coefs(Z.p, pol_z.p, bz, 3, s);
     lg("multiexp Z");
     commit_start(0, pol_z.p, n + 3);
+    to4t_evals4(pol_z.p, Z4.p, 3, s);
     pZ = commit_finish(0);
   }
   tm[3] = ms_since(t2);
