@@ -261,7 +261,10 @@ ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s,
 //    (v_8 = the top limb, bits 232..), v - q r < r + (q + 1) 2^232 < 2r, then one
 //    conditional subtraction (join_fr29); with an output factor the product < 1.4 r is
 //    joined directly.
-static constexpr int kTile29 = 2048;   // elements per tile: 9 x 8 KiB of limbs = 72 KiB LDS
+// elements per tile: 1024 (9 x 4 KiB of limbs = 36 KiB LDS, 256 threads, 4 tiles per CU) or
+// 2048 (72 KiB, 512 threads, 2 tiles per CU; NZCB_NTT_TILE=2048): the same 4 waves per SIMD,
+// in twice as many independent barrier domains with the smaller tile; one radix-4 group per
+// thread either way
 
 // LDS slot of tile element e: bits 0-4 XORed with a function of bits 5-7, a bijection on
 // every 32-element block. ds_read_b32 / ds_write_b32 bank by (address / 4) mod 32 per
@@ -274,17 +277,19 @@ static constexpr int kTile29 = 2048;   // elements per tile: 9 x 8 KiB of limbs 
 __device__ __forceinline__ int tile_slot(int e, int swz) {
   return e ^ (swz & ((((e >> 5) & 3) << 3) | ((e >> 5) & 7)));
 }
+template <int TILE>
 __device__ __forceinline__ F29 tile_ld(const uint32_t* sl, int e, int swz) {
   const int p = tile_slot(e, swz);
   F29 x;
 #pragma unroll
-  for (int l = 0; l < 9; l++) x.v[l] = sl[l * kTile29 + p];
+  for (int l = 0; l < 9; l++) x.v[l] = sl[l * TILE + p];
   return x;
 }
+template <int TILE>
 __device__ __forceinline__ void tile_st(uint32_t* sl, int e, const F29& x, int swz) {
   const int p = tile_slot(e, swz);
 #pragma unroll
-  for (int l = 0; l < 9; l++) sl[l * kTile29 + p] = x.v[l];
+  for (int l = 0; l < 9; l++) sl[l * TILE + p] = x.v[l];
 }
 __device__ __forceinline__ F29 add_nn29(const F29& a, const F29& b) {
   F29 r;
@@ -314,11 +319,12 @@ __device__ __forceinline__ Fr canon_fr29(const F29& x) {  // normalized x < 64 r
 // One pass of stages [s, s+q) on tiles of (2^q rows) x (2^logC columns). IN29: values from
 // the F29 scratch (else the Fr input, first pass only); OUT29: values to the F29 scratch
 // (else canonical Fr to `out`, last pass only).
-template <bool IN29, bool OUT29>
-__global__ void __launch_bounds__(kNttThreads)
+template <bool IN29, bool OUT29, int TILE>
+__global__ void __launch_bounds__(TILE / 4)
 ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29* __restrict__ tw, int L, int s,
                   int q, int logC, F29 scale29, int do_scale, NttIo io, int sparse4, int swz) {
-  __shared__ uint32_t sl[9 * kTile29];
+  constexpr int T = TILE / 4;  // threads
+  __shared__ uint32_t sl[9 * TILE];
   const int C = 1 << logC;
   const int rows = 1 << q;
   const int n_el = rows << logC;
@@ -327,7 +333,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
   size_t base = 0, c0 = 0, lo0 = 0;
   if (!IN29) {  // first pass: bit-reversed gather of the Fr input, prologue factors
     c0 = t << logC;
-    for (int e = tid; e < n_el; e += kNttThreads) {
+    for (int e = tid; e < n_el; e += T) {
       const int j = e >> logC, c = e & (C - 1);
       const size_t src = ((size_t)bit_rev((uint32_t)j, q) << (L - q)) + c0 + c;
       F29 x;
@@ -338,16 +344,16 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
         if (io.in_f) x = mul29<Fr29>(x, io.in_f[src]);
         if (do_scale) x = mul29<Fr29>(x, scale29);
       }
-      tile_st(sl, e, x, swz);
+      tile_st<TILE>(sl, e, x, swz);
     }
   } else {
     const size_t groups_lo = ((size_t)1 << s) >> logC;
     const size_t hi = t / groups_lo;
     lo0 = (t % groups_lo) << logC;
     base = (hi << (s + q)) + lo0;
-    for (int e = tid; e < n_el; e += kNttThreads) {
+    for (int e = tid; e < n_el; e += T) {
       const int j = e >> logC, c = e & (C - 1);
-      tile_st(sl, e, in29[base + ((size_t)j << s) + c], swz);
+      tile_st<TILE>(sl, e, in29[base + ((size_t)j << s) + c], swz);
     }
   }
   __syncthreads();
@@ -358,9 +364,9 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
     // zero-padded input past tile 0: of every four bit-reversed rows 4m..4m+3 only row 4m
     // is nonzero, and stages 0-1 map (x, 0, 0, 0) to (x, x, x, x): the first radix-4 step
     // is a copy
-    for (int e = tid; e < n_el; e += kNttThreads) {
+    for (int e = tid; e < n_el; e += T) {
       const int j = e >> logC;
-      if (j & 3) tile_st(sl, e, tile_ld(sl, ((j & ~3) << logC) + (e & (C - 1)), swz), swz);
+      if (j & 3) tile_st<TILE>(sl, e, tile_ld<TILE>(sl, ((j & ~3) << logC) + (e & (C - 1)), swz), swz);
     }
     __syncthreads();
     st = 2;
@@ -368,21 +374,21 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
     const int g = s;
     const F29* __restrict__ twg = tw + (((size_t)1 << g) - 1);
 #pragma unroll
-    for (int u = 0; u < kBfPerThread; u++) {
-      const int b = tid + u * kNttThreads;
+    for (int u = 0; u < 2; u++) {
+      const int b = tid + u * T;
       if (b >= nbf) continue;
       const int c = b & (C - 1);
       const int j0 = b >> logC;
       const int i0 = ((2 * j0) << logC) + c, i1 = ((2 * j0 + 1) << logC) + c;
       const size_t k = first ? 0 : (lo0 + c);
-      const F29 x0 = tile_ld(sl, i0, swz);
-      const F29 x1 = tile_ld(sl, i1, swz);
+      const F29 x0 = tile_ld<TILE>(sl, i0, swz);
+      const F29 x1 = tile_ld<TILE>(sl, i1, swz);
       const F29 tt = g ? mul29<Fr29>(x1, twg[k]) : x1;
       F29 y0 = add_nn29(x0, tt), y1 = sub2r_nn29(x0, tt);
       norm29(y0);
       norm29(y1);
-      tile_st(sl, i0, y0, swz);
-      tile_st(sl, i1, y1, swz);
+      tile_st<TILE>(sl, i0, y0, swz);
+      tile_st<TILE>(sl, i1, y1, swz);
     }
     __syncthreads();
     st = 1;
@@ -404,7 +410,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       const size_t kc = first ? (size_t)(low + h) : (((size_t)(low + h) << s) + lo0 + c);
       const int i0 = (j << logC) + c, i1 = ((j + h) << logC) + c, i2 = ((j + 2 * h) << logC) + c,
                 i3 = ((j + 3 * h) << logC) + c;
-      F29 t1 = tile_ld(sl, i1, swz), t3 = tile_ld(sl, i3, swz);
+      F29 t1 = tile_ld<TILE>(sl, i1, swz), t3 = tile_ld<TILE>(sl, i3, swz);
       if (g) {
         const F29 wa = twa[ka];
         F29 p1, p3;
@@ -412,7 +418,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
         t1 = p1;
         t3 = p3;
       }
-      const F29 x0 = tile_ld(sl, i0, swz), x2 = tile_ld(sl, i2, swz);
+      const F29 x0 = tile_ld<TILE>(sl, i0, swz), x2 = tile_ld<TILE>(sl, i2, swz);
       const F29 y0 = add_nn29(x0, t1), y1 = sub2r_nn29(x0, t1);
       const F29 y2 = add_nn29(x2, t3), y3 = sub2r_nn29(x2, t3);
       F29 u2, u3;
@@ -422,10 +428,10 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       norm29(z1);
       norm29(z2);
       norm29(z3);
-      tile_st(sl, i0, z0, swz);
-      tile_st(sl, i1, z1, swz);
-      tile_st(sl, i2, z2, swz);
-      tile_st(sl, i3, z3, swz);
+      tile_st<TILE>(sl, i0, z0, swz);
+      tile_st<TILE>(sl, i1, z1, swz);
+      tile_st<TILE>(sl, i2, z2, swz);
+      tile_st<TILE>(sl, i3, z3, swz);
     }
     __syncthreads();
   }
@@ -439,15 +445,15 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
     }
   };
   if (first) {
-    for (int e = tid; e < n_el; e += kNttThreads) {
+    for (int e = tid; e < n_el; e += T) {
       const int j = e & (rows - 1), c = e >> q;
       const size_t dst = ((size_t)bit_rev((uint32_t)(c0 + c), L - q) << q) + j;
-      store(dst, tile_ld(sl, (j << logC) + c, swz));
+      store(dst, tile_ld<TILE>(sl, (j << logC) + c, swz));
     }
   } else {
-    for (int e = tid; e < n_el; e += kNttThreads) {
+    for (int e = tid; e < n_el; e += T) {
       const int j = e >> logC, c = e & (C - 1);
-      store(base + ((size_t)j << s) + c, tile_ld(sl, e, swz));
+      store(base + ((size_t)j << s) + c, tile_ld<TILE>(sl, e, swz));
     }
   }
 }
@@ -466,6 +472,58 @@ static bool ntt29_enabled() {  // NZCB_NTT29=0: the 8x32 pipeline (ntt_pass_kern
     return !(e && e[0] == '0');
   }();
   return on;
+}
+
+// 1024-element tiles by default: 2^23 forward 1.074 -> 1.054 ms, 2^21 0.282 -> 0.275 ms on
+// one box (profiles/r3_ntt_tile_ab.txt); NZCB_NTT_TILE=2048 restores 72 KiB tiles (A/B runs)
+static int ntt29_tile() {
+  static const int v = [] {
+    const char* e = std::getenv("NZCB_NTT_TILE");
+    return (e && std::atoi(e) == 2048) ? 2048 : 1024;
+  }();
+  return v;
+}
+
+// The 9x29 pipeline's passes: stages [0, q1) with the bit-reversed gather, then <= 8
+// stages per pass through the F29 scratch; the last pass writes canonical Fr.
+template <int TILE>
+static void ntt29_passes(const NttTables& t, const Fr* in, Fr* out, const F29* tw, int L, const F29& sc29,
+                         int do_scale, const NttIo& io, bool sparse_ok, int swz, hipStream_t st) {
+  constexpr int T = TILE / 4;
+  const int q1 = L < 8 ? L : 8;
+  const int cols = 1 << (L - q1);
+  int logC1 = 0;
+  while ((1 << (logC1 + 1)) <= cols && ((1 << (q1 + logC1 + 1)) <= TILE)) logC1++;
+  const size_t tiles = (size_t)cols >> logC1;
+  // inputs nonzero only below N/4 (+ a few in tile 0's columns: the blinding terms):
+  // tiles past the first skip stages 0-1 (a 4n coset NTT of an n+3-term polynomial)
+  const int sparse4 = sparse_ok && L >= 2 && q1 >= 2 && !(q1 & 1) &&
+                      io.in_len <= ((size_t)1 << (L - 2)) + ((size_t)1 << logC1);
+  F29* scr = (F29*)t.scratch29.p;
+  if (q1 == L) {
+    hipLaunchKernelGGL((ntt29_pass_kernel<false, false, TILE>), dim3((unsigned)tiles), dim3(T), 0, st, in,
+                       (const F29*)nullptr, out, (F29*)nullptr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4, swz);
+    NZ_HIP(hipGetLastError());
+    return;
+  }
+  hipLaunchKernelGGL((ntt29_pass_kernel<false, true, TILE>), dim3((unsigned)tiles), dim3(T), 0, st, in,
+                     (const F29*)nullptr, (Fr*)nullptr, scr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4, swz);
+  NZ_HIP(hipGetLastError());
+  int s = q1;
+  while (s < L) {
+    const int q = (L - s) < 8 ? (L - s) : 8;
+    int logC = 0;
+    while (logC + 1 <= s && (1 << (q + logC + 1)) <= TILE) logC++;
+    const size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
+    if (s + q == L)
+      hipLaunchKernelGGL((ntt29_pass_kernel<true, false, TILE>), dim3((unsigned)ntiles), dim3(T), 0, st,
+                         (const Fr*)nullptr, (const F29*)scr, out, (F29*)nullptr, tw, L, s, q, logC, sc29, 0, io, 0, swz);
+    else
+      hipLaunchKernelGGL((ntt29_pass_kernel<true, true, TILE>), dim3((unsigned)ntiles), dim3(T), 0, st,
+                         (const Fr*)nullptr, (const F29*)scr, (Fr*)nullptr, scr, tw, L, s, q, logC, sc29, 0, io, 0, swz);
+    NZ_HIP(hipGetLastError());
+    s += q;
+  }
 }
 
 void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hipStream_t st, const Fr* scale,
@@ -508,32 +566,11 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   const int sparse4 = sparse_ok && L >= 2 && q1 >= 2 && !(q1 & 1) &&
                       io.in_len <= ((size_t)1 << (L - 2)) + ((size_t)1 << logC1);
   if (ntt29_enabled() && (q1 == L || t.scratch29.n >= ((size_t)9 << L))) {
-    F29* scr = (F29*)t.scratch29.p;
     const int swz = ntt29_swizzle();
-    if (q1 == L) {
-      hipLaunchKernelGGL((ntt29_pass_kernel<false, false>), dim3((unsigned)tiles), dim3(kNttThreads), 0, st, in,
-                         (const F29*)nullptr, out, (F29*)nullptr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4, swz);
-      NZ_HIP(hipGetLastError());
-      return;
-    }
-    hipLaunchKernelGGL((ntt29_pass_kernel<false, true>), dim3((unsigned)tiles), dim3(kNttThreads), 0, st, in,
-                       (const F29*)nullptr, (Fr*)nullptr, scr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4, swz);
-    NZ_HIP(hipGetLastError());
-    int s = q1;
-    while (s < L) {
-      const int q = (L - s) < 8 ? (L - s) : 8;
-      int logC = 0;
-      while (logC + 1 <= s && (1 << (q + logC + 1)) <= kTile29) logC++;
-      const size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
-      if (s + q == L)
-        hipLaunchKernelGGL((ntt29_pass_kernel<true, false>), dim3((unsigned)ntiles), dim3(kNttThreads), 0, st,
-                           (const Fr*)nullptr, (const F29*)scr, out, (F29*)nullptr, tw, L, s, q, logC, sc29, 0, io, 0, swz);
-      else
-        hipLaunchKernelGGL((ntt29_pass_kernel<true, true>), dim3((unsigned)ntiles), dim3(kNttThreads), 0, st,
-                           (const Fr*)nullptr, (const F29*)scr, (Fr*)nullptr, scr, tw, L, s, q, logC, sc29, 0, io, 0, swz);
-      NZ_HIP(hipGetLastError());
-      s += q;
-    }
+    if (ntt29_tile() == 1024)
+      ntt29_passes<1024>(t, in, out, tw, L, sc29, do_scale, io, sparse_ok, swz, st);
+    else
+      ntt29_passes<2048>(t, in, out, tw, L, sc29, do_scale, io, sparse_ok, swz, st);
     return;
   }
   hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)tiles), dim3(kNttThreads), lds, st, in, out, tw, L, 0, q1, logC1,
