@@ -141,6 +141,16 @@ static bool lds_indices() {
   return on;
 }
 
+// the 4-wave accumulation with LDS-DMA point prefetch (msm_accumulate29_dma_kernel);
+// NZCB_ACC_DMA=1 for A/B runs
+static bool acc_dma() {
+  static const bool on = [] {
+    const char* e = std::getenv("NZCB_ACC_DMA");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // interleaved product pairs in the accumulation (kPair); NZCB_ACC_PAIR=0 for A/B runs
 // (same box: isolated accumulation 2.295 -> 2.254 ms, bench +1.3 %)
 static bool paired_products() {
@@ -1028,6 +1038,145 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
     ent = ent_n;
     ent_n = ent_nn;
     P = Pn;
+  }
+}
+
+// 4 waves per SIMD (NZCB_ACC_DMA=1, A/B runs). At 4 waves (<= 128 VGPRs) the register-
+// prefetched next point of msm_accumulate29_kernel spilled to scratch; here the next
+// entry's table point goes HBM -> LDS by global_load_lds_dwordx4 (four 16-byte quarters
+// per lane, no VGPRs held while it is in flight) and is read back at the top of the next
+// iteration. The indices are staged kDmaGroup slots at a time (two barriers per group; every
+// thread of the workgroup runs the same kChunk iterations, finished or not), so one
+// workgroup needs 16 x 257 x 4 B of indices + 256 x 64 B of points = 32.4 KB and four fit
+// a CU (16 waves). Same additions, same results as the 3-wave kernel.
+static constexpr uint32_t kDmaGroup = 16;
+static_assert(kChunk % kDmaGroup == 0, "index groups tile the chunk");
+
+// x, y die after the first product pair: the rare doubling reloads its point from the
+// table (`pt`, `neg`) instead of keeping 18 VGPRs live through the whole addition
+__device__ __forceinline__ void acc_madd29(Xyzz29& acc, bool& inf, const F29& x, F29 y,
+                                           const G1Affine* __restrict__ pt, bool neg) {
+  if (inf) {
+    norm29(y);
+    acc.X = x;
+    acc.Y = y;
+    acc.ZZ = f29_const(Fq29::ONE);
+    acc.ZZZ = f29_const(Fq29::ONE);
+    inf = false;
+    return;
+  }
+  // madd-2008-s with the products paired (as msm_accumulate29_kernel kPair)
+  F29 U2, S2, PP, RR;
+  mul29x2<Fq29>(x, acc.ZZ, y, acc.ZZZ, U2, S2);
+  const F29 Pd = sub29(U2, acc.X, Fq29::K8);   // < 10p
+  const F29 R = sub29(S2, acc.Y, Fq29::K4);    // < 6p
+  sqr29x2(Pd, R, PP, RR);
+  if (is0p29_fast(PP)) {  // same abscissa: doubling (equal points) or infinity (opposite)
+    if (is0p29(RR)) {
+      const G1Affine P = *pt;
+      const F29 x2 = split29(P.x);
+      F29 y2 = split29(P.y);
+      if (neg) y2 = neg29_nn(y2);
+      norm29(y2);
+      mdbl29_rare(x2, y2, &acc);
+    } else {
+      inf = true;
+    }
+    return;
+  }
+  F29 PPP, Q, ZZ3, ZZZ3;
+  mul29x2<Fq29>(Pd, PP, acc.X, PP, PPP, Q);
+  const F29 X3 = sub2x29(RR, PPP, Q);  // RR + 6p - PPP - 2Q < 8p
+  mul29x2<Fq29>(acc.ZZ, PP, acc.ZZZ, PPP, ZZ3, ZZZ3);
+  acc.Y = mul2sum29(R, sub29_nn(Q, X3, Fq29W::K10), neg4p29_nn(acc.Y), PPP);
+  acc.ZZ = ZZ3;
+  acc.ZZZ = ZZZ3;
+  acc.X = X3;
+}
+
+__global__ void __launch_bounds__(kMsmThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
+msm_accumulate29_dma_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
+                            const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
+                            Xyzz29* __restrict__ buckets, Xyzz29* __restrict__ carry_own,
+                            Xyzz29* __restrict__ carry_cont) {
+  __shared__ uint32_t sidx[kDmaGroup * kLdsStride];
+  __shared__ uint4 spt[4 * kMsmThreads];  // [wave][quarter][lane], 16 B each
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t M = offsets[nkeys];
+  const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * kChunk;
+  const uint32_t s = (uint32_t)t * kChunk;
+  const bool live = t < nthreads && s < M;
+  const uint32_t e = live ? (s + kChunk < M ? s + kChunk : M) : s;
+  const uint32_t lane = threadIdx.x & 63;
+  uint4* wpt = spt + (threadIdx.x >> 6) * 256;
+  auto stage = [&](uint32_t g) {  // slots [g kDmaGroup, (g + 1) kDmaGroup) of every thread's chunk
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < kMsmThreads * kDmaGroup; j += kMsmThreads) {
+      const uint32_t thr = j / kDmaGroup, slot = j - thr * kDmaGroup;
+      const uint32_t q = wg0 + thr * kChunk + g * kDmaGroup + slot;
+      sidx[slot * kLdsStride + thr] = q < M ? sorted[q] : 0u;
+    }
+    __syncthreads();
+  };
+  auto dma = [&](uint32_t ent) {  // table point of `ent` -> this lane's four LDS quarters
+    const uint4* src = (const uint4*)(bases + (ent & 0x7fffffffu));
+#pragma unroll
+    for (int qq = 0; qq < 4; qq++)
+      __builtin_amdgcn_global_load_lds((const void*)(src + qq),
+                                       (__attribute__((address_space(3))) void*)(wpt + qq * 64), 16, 0, 0);
+  };
+  stage(0);
+  uint32_t k = 0, kstart = 0, kend = 0;
+  if (live) {
+    k = find_key(offsets, nkeys, s);
+    kstart = offsets[k];
+    kend = offsets[k + 1];
+  }
+  uint32_t ent = sidx[threadIdx.x];
+  dma(ent);
+  Xyzz29 acc;
+  bool inf = true;
+  for (uint32_t j = 0; j < kChunk; j++) {
+    const uint32_t pos = s + j;
+    const uint4 q0 = wpt[lane], q1 = wpt[64 + lane], q2 = wpt[128 + lane], q3 = wpt[192 + lane];
+    G1Affine P;
+    P.x.v[0] = q0.x; P.x.v[1] = q0.y; P.x.v[2] = q0.z; P.x.v[3] = q0.w;
+    P.x.v[4] = q1.x; P.x.v[5] = q1.y; P.x.v[6] = q1.z; P.x.v[7] = q1.w;
+    P.y.v[0] = q2.x; P.y.v[1] = q2.y; P.y.v[2] = q2.z; P.y.v[3] = q2.w;
+    P.y.v[4] = q3.x; P.y.v[5] = q3.y; P.y.v[6] = q3.z; P.y.v[7] = q3.w;
+    const bool use = pos < e && !P.is_inf();
+    const uint32_t ent_cur = ent;
+    const F29 x = split29(P.x);
+    F29 y = split29(P.y);
+    if (ent >> 31) y = neg29_nn(y);  // 2p - y, limbs < 2^30: only S2's product reads it
+    // the point is in registers before the next one overwrites its LDS quarters
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (j + 1 < kChunk) {
+      if ((j + 1) % kDmaGroup == 0) stage((j + 1) / kDmaGroup);
+      ent = sidx[((j + 1) % kDmaGroup) * kLdsStride + threadIdx.x];
+      dma(ent);
+    }
+    if (pos < e) {
+      if (use) acc_madd29(acc, inf, x, y, bases + (ent_cur & 0x7fffffffu), (ent_cur >> 31) != 0);
+      const uint32_t p1 = pos + 1;
+      if (p1 == kend || p1 == e) {
+        const bool starts = kstart >= s;
+        const bool ends = kend <= e;
+        Xyzz29 out = acc;
+        if (inf)
+#pragma unroll
+          for (int i = 0; i < 9; i++) out.ZZ.v[i] = 0;
+        if (starts && ends) buckets[k] = out;
+        else if (!starts) carry_cont[t] = out;
+        else carry_own[t] = out;
+        inf = true;
+        while (p1 < e && kend <= p1) {
+          k++;
+          kstart = kend;
+          kend = offsets[k + 1];
+        }
+      }
+    }
   }
 }
 
@@ -2025,6 +2174,9 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
       hipLaunchKernelGGL((msm_accumulate29_kernel<3, true>), agrid, dim3(kMsmThreads), 0, st, chunk, acc_src,
                          sc.sorted.p, acc_off, p.nkeys, nthreads, sc.buckets29.p, sc.carry_own29.p,
                          sc.carry_cont29.p);
+    else if (chunk == kChunk && acc_dma())
+      hipLaunchKernelGGL(msm_accumulate29_dma_kernel, agrid, dim3(kMsmThreads), 0, st, gather, sc.sorted.p,
+                         sc.offsets.p, p.nkeys, nthreads, sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
     else if (chunk == kChunk && acc_waves == 3 && lds_indices())
       hipLaunchKernelGGL((paired_products() ? msm_accumulate29_kernel<3, false, true, true>
                                             : msm_accumulate29_kernel<3, false, true, false>),
