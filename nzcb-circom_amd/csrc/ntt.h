@@ -31,9 +31,13 @@ struct NttTables {
 //   output j: out[j] * out_f[j]; sets *out_flags if an output at j >= out_limit is
 //             nonzero. out_f_has_scale: out_f already holds the inverse transform's
 //             1/N (the first pass then skips it).
+//   fold (a polynomial of degree < n + fold_len evaluated where x^n = d): input j <
+//             fold_len also adds in[j + fold_n] * d, before in_f (fold_f: d's operand)
 struct NttIo {
   size_t in_len = ~size_t(0);
   const F29* in_f = nullptr;
+  size_t fold_len = 0, fold_n = 0;
+  F29 fold_f = {};
   const F29* out_f = nullptr;
   bool out_f_has_scale = false;
   size_t out_limit = ~size_t(0);

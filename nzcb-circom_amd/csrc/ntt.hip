@@ -125,6 +125,7 @@ ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s,
       Fr v = Fr::zero();
       if (src < io.in_len) {
         v = in[src];
+        if (src < io.fold_len) v = v + mul_fr29(in[src + io.fold_n], io.fold_f);
         if (io.in_f) v = mul_fr29(v, io.in_f[src]);
         if (do_scale) v = mul_fr29(v, scale29);
       }
@@ -341,6 +342,15 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       for (int l = 0; l < 9; l++) x.v[l] = 0;
       if (src < io.in_len) {
         x = split29(in[src]);
+        if (src < io.fold_len) {  // + in[src + n] d: limbs < 2^30, value < 2.4 r (mul29 inputs)
+          const F29 hi = mul29<Fr29>(split29(in[src + io.fold_n]), io.fold_f);
+#pragma unroll
+          for (int l = 0; l < 9; l++) x.v[l] += hi.v[l];
+          if (!io.in_f) {
+            norm29(x);
+            x = split29(canon_fr29(x));
+          }
+        }
         if (io.in_f) x = mul29<Fr29>(x, io.in_f[src]);
         if (do_scale) x = mul29<Fr29>(x, scale29);
       }

@@ -71,6 +71,14 @@ struct Prover {
   DevBuf<F29> g29, gi29;                 // g^j (j < n + 8) and g^-j / 4n (j < 4n), mul_fr29 operands
   Fr zh_inv[4];
   DevBuf<Fr> cq, cs, cl;          // coset evaluations: Qm..Qc (5 x 4n), sigma1..3 (3 x 4n), L_j (nl x 4n)
+  // Three-coset quotient (quot3): the quotient is evaluated on cosets c_j H, c_j = g w4^j,
+  // j < 3 (3n points, coset-major [j][m]) and t's top six coefficients come from the top
+  // coefficients of A, B, C, Z and sigma (prove(), round 3)
+  bool quot3 = false;
+  DevBuf<Fr> cq3, cs3, cl3;       // Qm..Qc (5 x 3n), sigma1..3 (3 x 3n), L_j (nl x 3n)
+  DevBuf<F29> tw3, itw3;          // c_j^k and c_j^-k / 4n (3 x n each), mul_fr29 operands
+  Fr d3[3];                       // c_j^n = g^n w4^(j n)
+  Fr sig_top[3][4];               // sigma_k coefficients n-4 .. n-1
   // per-proof working set
   DevBuf<Fr> wit;                 // nVars (witness + internal), Montgomery
   DevBuf<Fr> wtns_in;             // raw witness upload (normal form)
@@ -116,6 +124,7 @@ struct Prover {
   void to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb, hipStream_t s = nullptr);
   void to4t_coefs(const Fr* evals, Fr* coefs, const int* bidx, int nb, hipStream_t s);
   void to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s);
+  void round3_quot3(const Fr& beta, const Fr& gamma, const Fr& alpha, hipStream_t s);
   void commit_start(int slot, const Fr* scalars, size_t len, const MsmBaseTable* tab = nullptr,
                     const G1Affine* bases = nullptr, bool on_main = false);
   G1Affine commit_finish(int slot);

@@ -352,6 +352,15 @@ k_quotient_coset(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* _
 // the final sum S < 9r < 2^257 (mul29's input limit), so T is canonical after one
 // conditional subtraction. Used for nPublic <= 8 (two PI chunks at most).
 constexpr uint32_t kQ29MaxPub = 8;
+
+// NZCB_QUOT3=1: the three-coset quotient (Prover::quot3)
+static bool quot3_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("NZCB_QUOT3");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 struct QArgs29 {
   F29 beta, bk1, bk2, alpha2, zhinv[4];  // exponent 261
   F29 gamma, negone;                     // exponent 256 (negone = r - 1)
@@ -381,14 +390,32 @@ __device__ __forceinline__ F29 q29_pi(const Fr* __restrict__ cl, const Fr* __res
   }
 }
 
+// THREE (three-coset quotient): the points are c_j w^m, j < 3, stored coset-major at
+// i = j n + m (x = g w4^(4m + j), Z(w x) at j n + (m + 1) mod n, 1/Z_H by j); otherwise
+// the 4n coset g<w4> in natural order (x_i = g w4^i, Z(w x) at i + 4, 1/Z_H by i mod 4).
+// Every array holds npts = 3n or 4n points per polynomial.
+template <bool THREE>
 __global__ void __launch_bounds__(kT)
 k_quotient_coset29(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
                    const Fr* __restrict__ Z, const Fr* __restrict__ cq, const Fr* __restrict__ cs,
                    const Fr* __restrict__ cl, uint32_t npub, const Fr* __restrict__ Apub, size_t n,
                    const Fr* __restrict__ xlo, const Fr* __restrict__ xhi, QArgs29 q, Fr* __restrict__ T) {
-  const size_t n4 = 4 * n;
+  const size_t n4 = (THREE ? 3 : 4) * n;  // points per array
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
+  size_t ix, izw;
+  int cj;
+  if (THREE) {
+    const int lg = __ffsll((long long)n) - 1;
+    const size_t j = i >> lg, m = i & (n - 1);
+    ix = 4 * m + j;
+    izw = j * n + ((m + 1) & (n - 1));
+    cj = (int)j;
+  } else {
+    ix = i;
+    izw = (i + 4) & (n4 - 1);
+    cj = (int)(i & 3);
+  }
   const F29 a = split29(A[i]), b = split29(B[i]), c = split29(C[i]), z = split29(Z[i]);
   // gate: qm a b + ql a + qr b + qo c + qc - sum_j L_j Apub_j
   F29 gate;
@@ -400,7 +427,7 @@ k_quotient_coset29(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr*
   if (npub > 0) gate = add29(gate, q29_pi(cl, Apub, 0, npub < 4 ? npub : 4, n4, i));
   if (npub > 4) gate = add29(gate, q29_pi(cl, Apub, 4, npub - 4, n4, i));  // < 7r
   // permutation: (a + b x + g)(b + b k1 x + g)(c + b k2 x + g) z - (a + b s1 + g)(..)(..) z(w x)
-  const F29 x = mul29<Fr29>(split29(xlo[i & 4095]), split29(xhi[i >> 12]));
+  const F29 x = mul29<Fr29>(split29(xlo[ix & 4095]), split29(xhi[ix >> 12]));
   const F29 bx = mul29<Fr29>(q.beta, x);                   // < 2r
   const F29 bx2 = q.k23 ? add29(bx, bx) : mul29<Fr29>(q.bk1, x);  // < 4r
   const F29 bx3 = q.k23 ? add29(bx2, bx) : mul29<Fr29>(q.bk2, x);  // < 6r
@@ -411,12 +438,54 @@ k_quotient_coset29(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr*
   const F29 g1 = add29(add29(a, mul29<Fr29>(q.beta, split29(cs[i]))), q.gamma);
   const F29 g2 = add29(add29(b, mul29<Fr29>(q.beta, split29(cs[n4 + i]))), q.gamma);
   const F29 g3 = add29(add29(c, mul29<Fr29>(q.beta, split29(cs[2 * n4 + i]))), q.gamma);
-  const F29 den = mul29<Fr29>(mul29<Fr29>(mul29<Fr29>(g1, g2), g3), split29(Z[(i + 4) & (n4 - 1)]));
+  const F29 den = mul29<Fr29>(mul29<Fr29>(mul29<Fr29>(g1, g2), g3), split29(Z[izw]));
   // alpha (num - den) + alpha^2 (z - 1) L1, one reduction
   const F29 pa[2] = {q.alpha, q.alpha2};
   const F29 pb[2] = {sub29(num, den, Fr29::K2), mul29<Fr29>(add29(z, q.negone), split29(cl[i]))};
   const F29 S = add29(gate, mulsum29<Fr29, 2>(pa, pb));  // < 9r
-  T[i] = join_fr29(mul29<Fr29>(S, q.zhinv[i & 3]));
+  T[i] = join_fr29(mul29<Fr29>(S, q.zhinv[cj]));
+}
+
+// The three-coset quotient's divisibility check: N vanishes on H iff every gate holds
+// there (the permutation part vanishes on H once round 2's copy check passed, z(1) = 1 by
+// construction), i.e. qm a b + ql a + qr b + qo c + qc - PI = 0 at every w^m; the zkey's
+// 4n evaluations (plain domain) hold the selectors on H at stride 4
+__global__ void __launch_bounds__(kT)
+k_gate_h(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C, const Fr* __restrict__ qm,
+         const Fr* __restrict__ ql, const Fr* __restrict__ qr, const Fr* __restrict__ qo, const Fr* __restrict__ qc,
+         size_t n, uint32_t npub, uint32_t* __restrict__ flags) {
+  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n) return;
+  const size_t e = n + 4 * m;
+  const Fr a = A[m], b = B[m], c = C[m];
+  Fr g = qm[e] * a * b + ql[e] * a + qr[e] * b + qo[e] * c + qc[e];
+  if (m < npub) g = g - a;  // PI(w^m) = -pub_m, pub_m = A(w^m)
+  if (!g.is_zero()) atomicOr(flags, 1u);
+}
+
+// t from its remainders v_j = (t mod (X^n - d_j)) / 4, j < 3, d_j = D w4^(j n) (w4^n = i,
+// a 4th root of unity: d = D, iD, -D) and its top coefficients q3 = t[3n..3n+6):
+// with w_j = v_j - d_j^3 q3 / 4 (c_j below), Q0 = w0 + w2 + 2 w1 - i (w0 - w2),
+// Q1 = (w0 - w2) 2 / D, Q2 = (w0 + w2 - 2 w1 + i (w0 - w2)) / D^2; t = Q0 | Q1 | Q2 | q3
+struct T3Args {
+  Fr c0[6], c1[6], c2[6], q3[6];
+  Fr i4, two_over_d, inv_d2;
+};
+__global__ void __launch_bounds__(kT)
+k_t_combine(const Fr* __restrict__ V, size_t n, T3Args a, Fr* __restrict__ t) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  Fr v0 = V[k], v1 = V[n + k], v2 = V[2 * n + k];
+  if (k < 6) {
+    v0 = v0 - a.c0[k];
+    v1 = v1 - a.c1[k];
+    v2 = v2 - a.c2[k];
+  }
+  const Fr sm = v0 + v2, dl = v0 - v2, im = dl * a.i4, v12 = v1 + v1;
+  t[k] = sm + v12 - im;
+  t[n + k] = dl * a.two_over_d;
+  t[2 * n + k] = (sm - v12 + im) * a.inv_d2;
+  t[3 * n + k] = k < 6 ? a.q3[k] : Fr::zero();
 }
 
 // x <- x * 2^e (mod r), canonical in and out: the exponent pre-scaling of kQ29
@@ -842,9 +911,61 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
       p = p * w4n;
     }
   }
+  quot3 = quot3_enabled() && nPublic <= kQ29MaxPub && power >= 6;
   alloc_workspace();
+  if (quot3) {  // three-coset quotient: per-coset twists c_j^k and untwists c_j^-k / 4n, j < 3
+    const size_t nhi3 = (n + 4095) / 4096;
+    tw3.alloc((size_t)3 * n);
+    itw3.alloc((size_t)3 * n);
+    const Fr inv4n = inverse(fr_small(n4));
+    DevBuf<Fr> lo, hi;
+    for (int j = 0; j < 3; j++) {
+      const Fr cj = g * pow_u64(w4, (uint64_t)j), cji = inverse(cj);
+      d3[j] = pow_u64(cj, n);
+      table(lo, nlo, cj, one);
+      table(hi, nhi3, pow_u64(cj, 4096), one);
+      hipLaunchKernelGGL(k_factor29_table, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, tw3.p + (size_t)j * n,
+                         lo.p, hi.p, one, (size_t)n);
+      NZ_HIP(hipStreamSynchronize(s));  // lo / hi are reallocated below
+      table(lo, nlo, cji, one);
+      table(hi, nhi3, pow_u64(cji, 4096), one);
+      hipLaunchKernelGGL(k_factor29_table, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, itw3.p + (size_t)j * n,
+                         lo.p, hi.p, inv4n, (size_t)n);
+      NZ_HIP(hipGetLastError());
+      NZ_HIP(hipStreamSynchronize(s));
+    }
+    for (int k = 0; k < 3; k++)
+      NZ_HIP(hipMemcpy(sig_top[k], sigma.p + (size_t)k * 5 * n + (n - 4), 4 * sizeof(Fr), hipMemcpyDeviceToHost));
+  }
   // coset evaluations of the fixed polynomials from the zkey coefficients (once per context)
-  {
+  if (quot3) {
+    const uint32_t nl = nPublic > 0 ? nPublic : 1;
+    const size_t n3 = (size_t)3 * n;
+    cq3.alloc(5 * n3);
+    cs3.alloc(3 * n3);
+    cl3.alloc(nl * n3);
+    auto coset3 = [&](const Fr* coefs, Fr* out) {  // Q(c_j w^m) at [j n + m]
+      for (int j = 0; j < 3; j++) {
+        NttIo io;
+        io.in_len = n;
+        io.in_f = tw3.p + (size_t)j * n;
+        ntt(eng->ntt_tables, coefs, out + (size_t)j * n, power, false, s, nullptr, &io);
+      }
+    };
+    const DevBuf<Fr>* qs[5] = {&qm, &ql, &qr, &qo, &qc};
+    for (int k = 0; k < 5; k++) coset3(qs[k]->p, cq3.p + (size_t)k * n3);
+    for (int k = 0; k < 3; k++) coset3(sigma.p + (size_t)k * 5 * n, cs3.p + (size_t)k * n3);
+    for (uint32_t j = 0; j < nl; j++) coset3(lagrange.p + (size_t)j * 5 * n, cl3.p + (size_t)j * n3);
+    NZ_HIP(hipGetLastError());
+    auto scale = [&](Fr* p, size_t m, int e) {
+      hipLaunchKernelGGL(k_dbl_pow, dim3(grid_for(m, kT, 1u << 30)), dim3(kT), 0, s, p, m, e);
+    };
+    scale(cq3.p, n3, 10);             // qm
+    scale(cq3.p + n3, 3 * n3, 5);     // ql, qr, qo
+    scale(cl3.p, (size_t)nl * n3, 5); // L_j
+    scale(x_lo.p, nlo, 5);            // g w4^j
+    NZ_HIP(hipGetLastError());
+  } else {
     const uint32_t nl = nPublic > 0 ? nPublic : 1;
     cq.alloc((size_t)5 * n4);
     cs.alloc((size_t)3 * n4);
@@ -939,12 +1060,102 @@ Prover::Prover(const Prover& pk, int) {
   g_lo.alias(pk.g_lo); g_hi.alias(pk.g_hi); gi_lo.alias(pk.gi_lo); gi_hi.alias(pk.gi_hi);
   g29.alias(pk.g29); gi29.alias(pk.gi29);
   cq.alias(pk.cq); cs.alias(pk.cs); cl.alias(pk.cl);
+  quot3 = pk.quot3;
+  cq3.alias(pk.cq3); cs3.alias(pk.cs3); cl3.alias(pk.cl3);
+  tw3.alias(pk.tw3); itw3.alias(pk.itw3);
+  for (int j = 0; j < 3; j++) d3[j] = pk.d3[j];
+  std::memcpy(sig_top, pk.sig_top, sizeof(sig_top));
   alloc_workspace();
 }
 
 // ----------------------------------------------------------------------------
 // building blocks
 // ----------------------------------------------------------------------------
+// Round 3 with the quotient on three cosets c_j H (c_j = g w4^j, j < 3) instead of the
+// whole 4n coset: deg t <= 3n + 5, so 3n evaluations fix t mod prod_j (X^n - d_j) and the
+// six coefficients t[3n..3n+6) come from elsewhere: N = t Z_H gives t[3n + k] = N[4n + k],
+// and only the permutation products reach degree 4n, so they are alpha times the top
+// coefficients of A B C Z - (A + beta S1)(B + beta S2)(C + beta S3) Z(wX), a convolution of
+// the six top coefficients of each factor (host). Per coset one n-point iNTT gives
+// t mod (X^n - d_j); k_t_combine solves for the quarters of t. The divisibility check of
+// the 4n path (coefficients >= 3n + 6 of the 4n iNTT) becomes the gate check on H.
+// Same t, bit for bit: t is unique.
+void Prover::round3_quot3(const Fr& beta, const Fr& gamma, const Fr& alpha, hipStream_t s) {
+  const size_t n3 = (size_t)3 * n;
+  QArgs29 q29;
+  q29.beta = f29_exp(beta, 5);
+  q29.k23 = k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0;
+  q29.bk1 = f29_exp(beta * k1, 5);
+  q29.bk2 = f29_exp(beta * k2, 5);
+  q29.alpha2 = f29_exp(alpha * alpha, 5);
+  for (int k = 0; k < 4; k++) q29.zhinv[k] = f29_exp(zh_inv[k], 5);
+  q29.gamma = f29_exp(gamma, 0);
+  q29.negone = f29_exp(neg(Fr::one()), 0);
+  q29.alpha = f29_exp(alpha, 20);
+  hipLaunchKernelGGL((k_quotient_coset29<true>), dim3(grid_for(n3, kT, 1u << 30)), dim3(kT), 0, s, A4.p, B4.p, C4.p,
+                     Z4.p, cq3.p, cs3.p, cl3.p, nPublic, A.p, (size_t)n, x_lo.p, root_hi.p, q29, T.p);
+  hipLaunchKernelGGL(k_gate_h, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, qm.p, ql.p, qr.p,
+                     qo.p, qc.p, (size_t)n, nPublic, flags.p);
+  NZ_HIP(hipGetLastError());
+  for (int j = 0; j < 3; j++) {  // v_j = (t mod (X^n - d_j)) / 4
+    NttIo io;
+    io.out_f = itw3.p + (size_t)j * n;
+    io.out_f_has_scale = true;
+    ntt(eng->ntt_tables, T.p + (size_t)j * n, Tz.p + (size_t)j * n, power, true, s, nullptr, &io);
+  }
+  NZ_HIP(hipGetLastError());
+  Fr top[4][6];  // coefficients n-4 .. n+1 of A, B, C and n-3 .. n+2 of Z
+  uint32_t f = 0;
+  NZ_HIP(hipMemcpyAsync(top[0], pol_a.p + (n - 4), 6 * sizeof(Fr), hipMemcpyDeviceToHost, s));
+  NZ_HIP(hipMemcpyAsync(top[1], pol_b.p + (n - 4), 6 * sizeof(Fr), hipMemcpyDeviceToHost, s));
+  NZ_HIP(hipMemcpyAsync(top[2], pol_c.p + (n - 4), 6 * sizeof(Fr), hipMemcpyDeviceToHost, s));
+  NZ_HIP(hipMemcpyAsync(top[3], pol_z.p + (n - 3), 6 * sizeof(Fr), hipMemcpyDeviceToHost, s));
+  NZ_HIP(hipMemcpyAsync(&f, flags.p, 4, hipMemcpyDeviceToHost, s));
+  NZ_HIP(hipStreamSynchronize(s));
+  if (f & 1u) throw Error(NZCB_ERR_T_DIV, "T Polynomial is not divisible");
+  // factor coefficients by offset u from the top degree (A, B, C: n + 1; Z: n + 2)
+  Fr p1[4][6], p2[4][6];
+  const Fr w = wn, wi = inverse(wn);
+  const Fr wpow[6] = {w * w, w, Fr::one(), wi, wi * wi, wi * wi * wi};  // w^(2 - u)
+  for (int u = 0; u < 6; u++) {
+    for (int f3 = 0; f3 < 3; f3++) {
+      p1[f3][u] = top[f3][5 - u];
+      p2[f3][u] = top[f3][5 - u];
+      if (u >= 2) p2[f3][u] = p2[f3][u] + beta * sig_top[f3][5 - u];  // S index n + 1 - u <= n - 1
+    }
+    p1[3][u] = top[3][5 - u];
+    p2[3][u] = top[3][5 - u] * wpow[u];  // Z(wX): coefficient j times w^j
+  }
+  auto conv = [](const Fr (&x)[6], const Fr (&y)[6], Fr (&out)[6]) {
+    for (int s2 = 0; s2 < 6; s2++) {
+      Fr acc = Fr::zero();
+      for (int u = 0; u <= s2; u++) acc = acc + x[u] * y[s2 - u];
+      out[s2] = acc;
+    }
+  };
+  Fr e1[6], e2[6], e3[6], h1[6], h2[6], h3[6];
+  conv(p1[0], p1[1], e1);
+  conv(e1, p1[2], e2);
+  conv(e2, p1[3], e3);
+  conv(p2[0], p2[1], h1);
+  conv(h1, p2[2], h2);
+  conv(h2, p2[3], h3);
+  T3Args ta;
+  const Fr D = d3[0], D3 = D * D * D, i4 = d3[1] * inverse(D), quarter = inverse(fr_small(4));
+  for (int k = 0; k < 6; k++) {
+    ta.q3[k] = alpha * (e3[5 - k] - h3[5 - k]);  // t[3n + k] = N[4n + k]
+    const Fr c = D3 * ta.q3[k] * quarter;
+    ta.c0[k] = c;
+    ta.c1[k] = neg(i4 * c);  // (i D)^3 = -i D^3
+    ta.c2[k] = neg(c);       // (-D)^3
+  }
+  ta.i4 = i4;
+  ta.two_over_d = fr_small(2) * inverse(D);
+  ta.inv_d2 = inverse(D * D);
+  hipLaunchKernelGGL(k_t_combine, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, Tz.p, (size_t)n, ta, t.p);
+  NZ_HIP(hipGetLastError());
+}
+
 void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb, hipStream_t s) {
   if (!s) s = st();
   to4t_coefs(evals, coefs, bidx, nb, s);
@@ -967,6 +1178,20 @@ void Prover::to4t_coefs(const Fr* evals, Fr* coefs, const int* bidx, int nb, hip
 void Prover::to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s) {
   auto t0 = std::chrono::steady_clock::now();
   // evaluations of the *blinded* polynomial on the coset g*<w4> (round-3 quotient input)
+  if (quot3) {  // on c_j H, j < 3: the nb top coefficients folded in (x^n = d_j there)
+    for (int j = 0; j < 3; j++) {
+      NttIo io;
+      io.in_len = n;
+      io.in_f = tw3.p + (size_t)j * n;
+      io.fold_len = (size_t)nb;
+      io.fold_n = n;
+      io.fold_f = fr29_operand(d3[j]);
+      ntt(eng->ntt_tables, coefs, evals4 + (size_t)j * n, power, false, s, nullptr, &io);
+    }
+    NZ_HIP(hipGetLastError());
+    ntt_ms += ms_since(t0);
+    return;
+  }
   NttIo io;  // coset shift g^j and the zero padding fused into the NTT's first pass
   io.in_len = (size_t)n + nb;
   io.in_f = g29.p;
@@ -1394,7 +1619,9 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     q.bk2 = beta * k2;
     for (int k = 0; k < 4; k++) q.zhinv[k] = zh_inv[k];
     auto tq = std::chrono::steady_clock::now();
-    if (nPublic <= kQ29MaxPub) {
+    if (quot3) {
+      round3_quot3(beta, gamma, alpha, s);
+    } else if (nPublic <= kQ29MaxPub) {
       QArgs29 q29;
       q29.beta = f29_exp(beta, 5);
       q29.k23 = k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0;
@@ -1405,25 +1632,27 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       q29.gamma = f29_exp(gamma, 0);
       q29.negone = f29_exp(neg(Fr::one()), 0);
       q29.alpha = f29_exp(alpha, 20);
-      hipLaunchKernelGGL(k_quotient_coset29, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, A4.p, B4.p, C4.p,
-                         Z4.p, cq.p, cs.p, cl.p, nPublic, A.p, (size_t)n, x_lo.p, root_hi.p, q29, T.p);
+      hipLaunchKernelGGL((k_quotient_coset29<false>), dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, A4.p, B4.p,
+                         C4.p, Z4.p, cq.p, cs.p, cl.p, nPublic, A.p, (size_t)n, x_lo.p, root_hi.p, q29, T.p);
     } else {
       hipLaunchKernelGGL(k_quotient_coset, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, A4.p, B4.p, C4.p,
                          Z4.p, cq.p, cs.p, cl.p, nPublic, A.p, (size_t)n, x_lo.p, root_hi.p, q, T.p);
     }
     NZ_HIP(hipGetLastError());
-    NttIo io;  // 1/4n, the coset unscale g^-j and the degree check fused into the iNTT's last pass
-    io.out_f = gi29.p;
-    io.out_f_has_scale = true;
-    io.out_limit = (size_t)3 * n + 6;
-    io.out_flags = flags.p;
-    ntt(eng->ntt_tables, T.p, t.p, power + 2, true, s, nullptr, &io);
-    NZ_HIP(hipGetLastError());
-    uint32_t f = 0;
-    NZ_HIP(hipMemcpyAsync(&f, flags.p, 4, hipMemcpyDeviceToHost, s));
-    NZ_HIP(hipStreamSynchronize(s));
+    if (!quot3) {
+      NttIo io;  // 1/4n, the coset unscale g^-j and the degree check fused into the iNTT's last pass
+      io.out_f = gi29.p;
+      io.out_f_has_scale = true;
+      io.out_limit = (size_t)3 * n + 6;
+      io.out_flags = flags.p;
+      ntt(eng->ntt_tables, T.p, t.p, power + 2, true, s, nullptr, &io);
+      NZ_HIP(hipGetLastError());
+      uint32_t f = 0;
+      NZ_HIP(hipMemcpyAsync(&f, flags.p, 4, hipMemcpyDeviceToHost, s));
+      NZ_HIP(hipStreamSynchronize(s));
+      if (f & 1u) throw Error(NZCB_ERR_T_DIV, "T Polynomial is not divisible");
+    }
     ntt_ms += ms_since(tq);
-    if (f & 1u) throw Error(NZCB_ERR_T_DIV, "T Polynomial is not divisible");
     lg("multiexp T1");
     commit_start(0, t.p, n);
     lg("multiexp T2");
