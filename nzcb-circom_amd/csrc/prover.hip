@@ -353,11 +353,12 @@ k_quotient_coset(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* _
 // conditional subtraction. Used for nPublic <= 8 (two PI chunks at most).
 constexpr uint32_t kQ29MaxPub = 8;
 
-// NZCB_QUOT3=1: the three-coset quotient (Prover::quot3)
+// the three-coset quotient (Prover::quot3, default; same box: bench 37.5 -> 38.9 proofs/s,
+// profiles/r3_quot3_ab.txt); NZCB_QUOT3=0 restores the 4n coset (A/B runs)
 static bool quot3_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("NZCB_QUOT3");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on;
 }
