@@ -230,3 +230,32 @@ def test_msm_split_live_oracle():
     ctx.set_msm_devices([0, 0, 0, 0])
     got, _ = ctx.prove_raw(binfmt.write_wtns(c["witness"]), b"".join(x.to_bytes(32, "little") for x in bl))
     assert got == plonk.proof_to_bytes(proof)
+
+
+@pytest.mark.parametrize("quot3", ["0", "1"])
+def test_quotient_schedules_same_proof(quot3):
+    """The three-coset quotient (default, n >= 64) and the 4n coset one (NZCB_QUOT3=0; also
+    every n < 64, e.g. p5 above) prove p8 bit for bit, and both report a broken gate as
+    snarkjs's "T Polynomial is not divisible" (a fresh process: the switch is read once)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = (
+        "import sys, json; sys.path[:0] = [%r, %r]\n"
+        "import nzcb\n"
+        "from oracle import binfmt\n"
+        "g = %r\n"
+        "meta = json.load(open(g + '/p8.json')); exp = meta['proofs']['fixed']\n"
+        "zkey = open(g + '/p8.zkey', 'rb').read(); wtns = open(g + '/p8.wtns', 'rb').read()\n"
+        "ctx = nzcb.ProverContext(zkey)\n"
+        "proof, _ = ctx.prove_raw(wtns, bytes.fromhex(exp['blinding']))\n"
+        "assert proof.hex() == exp['proof_bin'], 'proof differs'\n"
+        "w = binfmt.read_wtns(wtns)['witness']; w[20] = w[20] + 1\n"
+        "try:\n"
+        "    ctx.prove_raw(binfmt.write_wtns(w)); raise SystemExit('no error')\n"
+        "except nzcb.NzcbError as e:\n"
+        "    assert str(e) == 'T Polynomial is not divisible', str(e)\n"
+        "print('ok')\n" % (os.path.join(root, "nzcb-circom_amd"), root, GOLD))
+    env = dict(os.environ, NZCB_QUOT3=quot3)
+    p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stdout + p.stderr
