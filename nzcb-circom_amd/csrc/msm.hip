@@ -151,6 +151,15 @@ static bool acc_dma() {
   return on;
 }
 
+// the run's second addition without the products by ZZ1 = ZZZ1 = 1 (kAff); NZCB_ACC_AFF=1
+static bool acc_aff() {
+  static const bool on = [] {
+    const char* e = std::getenv("NZCB_ACC_AFF");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // interleaved product pairs in the accumulation (kPair); NZCB_ACC_PAIR=0 for A/B runs
 // (same box: isolated accumulation 2.295 -> 2.254 ms, bench +1.3 %)
 static bool paired_products() {
@@ -911,7 +920,10 @@ __device__ __forceinline__ G1xyzz load_point(const Xyzz29& a) {
 static constexpr uint32_t kLdsStride = kMsmThreads + 1;  // slot-major rows, +1: conflict-free fill
 // kPair: the addition's independent products in interleaved pairs (mul29x2 / sqr29x2:
 // U2 | S2, PP | RR, PPP | Q, ZZ3 | ZZZ3), two v_mad_u64_u32 chains per asm statement
-template <int WAVES, bool kDirect = false, bool kLdsIdx = false, bool kPair = false>
+// kAff: the addition right after a run's first entry (acc = (x, y, 1, 1), every lane of a
+// wave at once at step 1 of the chunks) skips the products by ZZ1 = ZZZ1 = 1: U2 = x, S2 = y,
+// ZZ3 = PP, ZZZ3 = PPP (a wave-uniform branch around two product pairs, one addition site)
+template <int WAVES, bool kDirect = false, bool kLdsIdx = false, bool kPair = false, bool kAff = false>
 __global__ void __launch_bounds__(kMsmThreads) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
 msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
                         const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
@@ -939,7 +951,7 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
   uint32_t k = find_key(offsets, nkeys, s);
   uint32_t kstart = offsets[k], kend = offsets[k + 1];
   Xyzz29 acc;
-  bool inf = true;
+  bool inf = true, aff = false;
   // software pipeline: the next entry's table point is loaded before this entry's
   // addition, so the gather's latency hides behind ~8k cycles of arithmetic, and the
   // entry after it is read one step earlier still, so that gather's address is in a
@@ -963,10 +975,16 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
         acc.ZZ = f29_const(Fq29::ONE);
         acc.ZZZ = f29_const(Fq29::ONE);
         inf = false;
+        aff = kAff;
       } else if (kPair) {
         // madd-2008-s as above, products paired
         F29 U2, S2, PP, RR;
-        mul29x2<Fq29>(x, acc.ZZ, y, acc.ZZZ, U2, S2);
+        if (kAff && aff) {  // x ZZ1 = x, y ZZZ1 = y (ONE is the Montgomery-261 1)
+          U2 = x;
+          S2 = y;  // 2p - y for a negated digit: limbs < 2^30, sub29 normalizes R
+        } else {
+          mul29x2<Fq29>(x, acc.ZZ, y, acc.ZZZ, U2, S2);
+        }
         const F29 Pd = sub29(U2, acc.X, Fq29::K8);   // < 10p
         const F29 R = sub29(S2, acc.Y, Fq29::K4);    // < 6p
         sqr29x2(Pd, R, PP, RR);
@@ -981,12 +999,18 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
           F29 PPP, Q, ZZ3, ZZZ3;
           mul29x2<Fq29>(Pd, PP, acc.X, PP, PPP, Q);
           const F29 X3 = sub2x29(RR, PPP, Q);  // RR + 6p - PPP - 2Q < 8p
-          mul29x2<Fq29>(acc.ZZ, PP, acc.ZZZ, PPP, ZZ3, ZZZ3);
+          if (kAff && aff) {
+            ZZ3 = PP;
+            ZZZ3 = PPP;
+          } else {
+            mul29x2<Fq29>(acc.ZZ, PP, acc.ZZZ, PPP, ZZ3, ZZZ3);
+          }
           acc.Y = mul2sum29(R, sub29_nn(Q, X3, Fq29W::K10), neg4p29_nn(acc.Y), PPP);
           acc.ZZ = ZZ3;
           acc.ZZZ = ZZZ3;
           acc.X = X3;
         }
+        aff = false;
       } else {
         // madd-2008-s (XYZZ + affine): 8 products + 2 squares
         const F29 U2 = mul29(x, acc.ZZ);
@@ -2178,8 +2202,9 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
       hipLaunchKernelGGL(msm_accumulate29_dma_kernel, agrid, dim3(kMsmThreads), 0, st, gather, sc.sorted.p,
                          sc.offsets.p, p.nkeys, nthreads, sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
     else if (chunk == kChunk && acc_waves == 3 && lds_indices())
-      hipLaunchKernelGGL((paired_products() ? msm_accumulate29_kernel<3, false, true, true>
-                                            : msm_accumulate29_kernel<3, false, true, false>),
+      hipLaunchKernelGGL((!paired_products() ? msm_accumulate29_kernel<3, false, true, false>
+                          : acc_aff()        ? msm_accumulate29_kernel<3, false, true, true, true>
+                                             : msm_accumulate29_kernel<3, false, true, true>),
                          agrid, dim3(kMsmThreads), 0, st, chunk, gather, sc.sorted.p, sc.offsets.p, p.nkeys, nthreads,
                          sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
     else
