@@ -108,6 +108,20 @@ int nzcb_prove_witness(nzcb_ctx* ctx, const uint8_t* witness, size_t n_witness, 
 int nzcb_prove_device(nzcb_ctx* ctx, const void* dev_witness, size_t n_witness, const uint8_t* blinding,
                       uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_err* err);
 
+/* One proof with its own logger (NULL: the context's, nzcb_ctx_set_logger), the witness in
+ * any of the three forms above: NZCB_WITNESS_WTNS (.wtns bytes, n = byte length),
+ * NZCB_WITNESS_HOST (n x 32-byte LE values in host memory), NZCB_WITNESS_DEVICE (the same
+ * in HBM). Concurrent calls on one context (several host threads; the N-API addon's
+ * in-flight promises) each take a free lane and run at the same time; a call waits while
+ * every lane is proving. nzcb_prove, nzcb_prove_witness and nzcb_prove_device are this
+ * with the context's logger. */
+#define NZCB_WITNESS_WTNS 0
+#define NZCB_WITNESS_HOST 1
+#define NZCB_WITNESS_DEVICE 2
+int nzcb_prove_logged(nzcb_ctx* ctx, const void* witness, size_t n, int kind, const uint8_t* blinding,
+                      uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_log_fn log, void* log_user,
+                      nzcb_err* err);
+
 /* Proof lanes (default 1): each extra lane is a per-proof working set + streams on
  * the context's device (~6.5 GB at n = 2^21) sharing the HBM-resident proving key,
  * so nzcb_prove_batch keeps `lanes` proofs in flight and one proof's latency-bound

@@ -63,15 +63,10 @@ int nzcb_engine_lagrange_basis(nzcb_engine* e, const void* dev_ptau, size_t ptau
 int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont, int reps,
                          double* ms, double* acc_ms, nzcb_err* err);
 /* Fixed-base schedule (the prover's): builds the shifted-base table of the first
- * n_table bases (c = 17: 2^(17w) multiples, 15 rows), then runs the MSM of the first n.
+ * n_table bases (c = 20 by default: 2^(20w) multiples, 13 rows), then runs the MSM of the first n.
  * One-shot (table and scratch freed on return); for parity tests. */
 int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
                               int scalars_mont, uint8_t* out_affine, nzcb_err* err);
-/* Batch-affine pairing rounds ahead of the fixed-base bucket accumulation (each halves
- * every bucket's run): rounds >= 0 forces that many (at most 6; 0 = XYZZ accumulation
- * only), rounds < 0 restores the automatic choice (NZCB_PAIR_ROUNDS, default 0, while
- * the average run is >= 8 entries). Process-wide; for tests and tuning. */
-int nzcb_msm_set_pair_rounds(int rounds);
 /* Per-phase MSM timing (HIP events, average over reps after one warm-up):
  * out[0] wall ms, out[1..7] keys, sort, offsets, accumulate, finalize, reduce, sums,
  * out[8] table build ms (fixed_base only), out[9] bucket entries per MSM (nonzero digits). */

@@ -251,11 +251,6 @@ int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars,
   NZ_GUARD_END(err)
 }
 
-int nzcb_msm_set_pair_rounds(int rounds) {
-  msm_set_pair_rounds(rounds);
-  return 0;
-}
-
 int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
                               int scalars_mont, uint8_t* out_affine, nzcb_err* err) {
   NZ_GUARD_BEGIN

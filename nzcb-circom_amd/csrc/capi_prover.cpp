@@ -4,9 +4,12 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -48,7 +51,15 @@ struct nzcb_ctx {
   std::vector<std::vector<std::unique_ptr<Prover>>> dev_extra;
   nzcb_log_fn log_fn = nullptr;
   void* log_user = nullptr;
-  std::mutex mu;  // calls on one context are serialized (SURVEY.md §8b "Threading")
+  // Concurrency (SURVEY.md §8b "Threading"): proofs hold `cfg` shared and take a lane from
+  // the pool for their duration, so concurrent callers (the N-API addon's in-flight
+  // promises, several host threads) run on different lanes at once; configuration calls
+  // (lanes, logger, splits, transcript) hold `cfg` exclusively, after in-flight proofs.
+  std::shared_mutex cfg;
+  std::mutex pool_mu;
+  std::condition_variable pool_cv;
+  std::vector<Prover*> idle;  // lanes not proving; rebuilt by reset_pool (cfg held exclusively)
+  double last_tm[9] = {0};    // phases of the last finished proof (nzcb_ctx_last_timings)
   Prover* lane(size_t i) { return i == 0 ? p.get() : extra[i - 1].get(); }
   size_t lanes() const { return 1 + extra.size(); }  // per device
   // every lane of every device (batch workers), device-interleaved so that a short batch
@@ -60,6 +71,44 @@ struct nzcb_ctx {
       for (size_t d = 0; d < dev_p.size(); d++) v.push_back(l == 0 ? dev_p[d].get() : dev_extra[d][l - 1].get());
     }
     return v;
+  }
+  // the lanes proofs may use: lane 0 of device 0 alone while a split covers it (the split's
+  // commitments are lane 0's), else all of them
+  std::vector<Prover*> usable() {
+    if (p->split_send || !p->shards.empty()) return {p.get()};
+    return all();
+  }
+  void reset_pool() {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    idle = usable();
+    std::reverse(idle.begin(), idle.end());  // lane 0 of device 0 is taken first
+  }
+  // a lane for one proof (blocks while all are proving), logging to `fn` or the context's logger
+  Prover* acquire(nzcb_log_fn fn, void* user) {
+    Prover* q;
+    {
+      std::unique_lock<std::mutex> lk(pool_mu);
+      pool_cv.wait(lk, [&] { return !idle.empty(); });
+      q = idle.back();
+      idle.pop_back();
+    }
+    if (!fn) {
+      fn = log_fn;
+      user = log_user;
+    }
+    if (fn)
+      q->log = [fn, user](const std::string& m) { fn(user, m.c_str()); };
+    else
+      q->log = nullptr;
+    return q;
+  }
+  void release(Prover* q) {
+    {
+      std::lock_guard<std::mutex> lk(pool_mu);
+      std::memcpy(last_tm, q->tm, sizeof(last_tm));
+      idle.push_back(q);
+    }
+    pool_cv.notify_one();
   }
 };
 
@@ -95,6 +144,7 @@ nzcb_ctx* nzcb_ctx_create(const uint8_t* zkey, size_t zkey_len, int device, nzcb
   try {
     auto* c = new nzcb_ctx();
     c->p.reset(new Prover(zkey, zkey_len, device));
+    c->reset_pool();
     if (err) err->code = 0;
     return c;
   } catch (const Error& e) {
@@ -123,6 +173,7 @@ nzcb_ctx* nzcb_ctx_create_devices(const uint8_t* zkey, size_t zkey_len, const in
       c->dev_p.emplace_back(new Prover(zkey, zkey_len, devices[i]));
       c->dev_extra.emplace_back();
     }
+    c->reset_pool();
     NZ_HIP(hipSetDevice(devices[0]));
     if (err) err->code = 0;
     return c;
@@ -171,27 +222,21 @@ void nzcb_ctx_destroy(nzcb_ctx* ctx) { delete ctx; }
 
 void nzcb_ctx_set_logger(nzcb_ctx* ctx, nzcb_log_fn fn, void* user) {
   if (!ctx) return;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::unique_lock<std::shared_mutex> lk(ctx->cfg);
   ctx->log_fn = fn;
   ctx->log_user = user;
-  for (Prover* q : ctx->all()) {
-    if (fn)
-      q->log = [ctx](const std::string& m) { ctx->log_fn(ctx->log_user, m.c_str()); };
-    else
-      q->log = nullptr;
-  }
 }
 
 void nzcb_ctx_set_transcript_public(nzcb_ctx* ctx, int on) {
   if (!ctx) return;
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::unique_lock<std::shared_mutex> lk(ctx->cfg);
   for (Prover* q : ctx->all()) q->transcript_public = on != 0;
 }
 
 int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err) {
   if (!ctx || lanes < 1 || lanes > 16) return fail(err, NZCB_ERR_ARG, "lanes must be in 1..16");
   try {
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::unique_lock<std::shared_mutex> lk(ctx->cfg);
     while (ctx->lanes() > (size_t)lanes) {
       ctx->extra.pop_back();
       for (auto& de : ctx->dev_extra) de.pop_back();
@@ -199,12 +244,9 @@ int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err) {
     while (ctx->lanes() < (size_t)lanes) {
       const int l = (int)ctx->lanes();
       ctx->extra.emplace_back(new Prover(*ctx->p, l));
-      ctx->extra.back()->log = ctx->p->log;
-      for (size_t d = 0; d < ctx->dev_p.size(); d++) {
-        ctx->dev_extra[d].emplace_back(new Prover(*ctx->dev_p[d], l));
-        ctx->dev_extra[d].back()->log = ctx->p->log;
-      }
+      for (size_t d = 0; d < ctx->dev_p.size(); d++) ctx->dev_extra[d].emplace_back(new Prover(*ctx->dev_p[d], l));
     }
+    ctx->reset_pool();
     NZ_HIP(hipSetDevice(ctx->p->eng->device));
     if (err) err->code = 0;
     return 0;
@@ -220,8 +262,9 @@ int nzcb_ctx_lanes(const nzcb_ctx* ctx) { return ctx ? (int)ctx->lanes() : 0; }
 int nzcb_ctx_set_msm_devices(nzcb_ctx* ctx, const int* devices, int ndev, nzcb_err* err) {
   if (!ctx || !devices || ndev < 1 || ndev > 64) return fail(err, NZCB_ERR_ARG, "devices: 1..64 ids");
   try {
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::unique_lock<std::shared_mutex> lk(ctx->cfg);
     ctx->p->set_msm_devices(std::vector<int>(devices, devices + ndev));
+    ctx->reset_pool();
     if (err) err->code = 0;
     return 0;
   } catch (const Error& e) {
@@ -235,8 +278,9 @@ int nzcb_ctx_set_msm_split(nzcb_ctx* ctx, int world, size_t own_points, nzcb_msm
                            nzcb_msm_gather_fn gather, void* user, nzcb_err* err) {
   if (!ctx || world < 1 || world > 1024) return fail(err, NZCB_ERR_ARG, "msm split: world must be in 1..1024");
   try {
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::unique_lock<std::shared_mutex> lk(ctx->cfg);
     ctx->p->set_msm_split(world, own_points, send, gather, user);
+    ctx->reset_pool();
     if (err) err->code = 0;
     return 0;
   } catch (const Error& e) {
@@ -255,15 +299,19 @@ static int prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_wit
   if (!ctx || count < 0 || (count && (!witnesses || !proofs_out))) return fail(err, NZCB_ERR_ARG, "null argument");
   const size_t npub = ctx->p->nPublic;
   if (npub && (!pubs_out || pub_stride < 32 * npub)) return fail(err, NZCB_ERR_ARG, "public output buffer too small");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+  std::shared_lock<std::shared_mutex> lk(ctx->cfg);
   std::atomic<int> next(0);
   std::atomic<int> first_bad(count);
   std::vector<int> codes(count, 0);
   std::vector<std::string> msgs(count);
-  auto worker = [&](Prover* pr) {
+  // one worker per lane: each takes a lane from the pool (shared with concurrent single
+  // proofs), proves items until the batch is drained, and returns it
+  auto worker = [&]() {
+    Prover* pr = nullptr;
     for (;;) {
       const int i = next.fetch_add(1);
-      if (i >= count || (!keep_going && i > first_bad.load())) return;
+      if (i >= count || (!keep_going && i > first_bad.load())) break;
+      if (!pr) pr = ctx->acquire(nullptr, nullptr);
       try {
         pr->prove((const uint8_t*)witnesses[i], n_witness,
                   blindings ? blindings + (size_t)i * NZCB_BLINDING_BYTES : nullptr,
@@ -286,15 +334,12 @@ static int prove_batch(nzcb_ctx* ctx, const void* const* witnesses, size_t n_wit
         }
       }
     }
+    if (pr) ctx->release(pr);
   };
-  // lane 0 of device 0 is the only lane whose commitments a split (nzcb_ctx_set_msm_devices /
-  // nzcb_ctx_set_msm_split) covers, so a split context proves its batch on lane 0 alone
-  std::vector<Prover*> ws = ctx->p->split_send || !ctx->p->shards.empty() ? std::vector<Prover*>{ctx->p.get()}
-                                                                         : ctx->all();
-  const size_t nl = std::min(ws.size(), (size_t)(count > 0 ? count : 1));
+  const size_t nl = std::min(ctx->usable().size(), (size_t)(count > 0 ? count : 1));
   std::vector<std::thread> th;
-  for (size_t l = 1; l < nl; l++) th.emplace_back(worker, ws[l]);
-  worker(ws[0]);
+  for (size_t l = 1; l < nl; l++) th.emplace_back(worker);
+  worker();
   for (auto& t : th) t.join();
   if (status_out)
     for (int i = 0; i < count; i++) status_out[i] = codes[i];
@@ -333,14 +378,36 @@ int nzcb_ctx_info(const nzcb_ctx* ctx, uint32_t out[5]) {
   return 0;
 }
 
-int nzcb_prove_witness(nzcb_ctx* ctx, const uint8_t* witness, size_t n_witness, const uint8_t* blinding,
-                       uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_err* err) {
+namespace {
+// one proof on a lane of the pool; kind: NZCB_WITNESS_WTNS / _HOST / _DEVICE
+int prove_one(nzcb_ctx* ctx, const void* witness, size_t n, int kind, const uint8_t* blinding, uint8_t* proof_out,
+              uint8_t* pub_out, size_t pub_cap, nzcb_log_fn log, void* log_user, nzcb_err* err) {
   if (!ctx || !witness || !proof_out) return fail(err, NZCB_ERR_ARG, "null argument");
+  if (kind != NZCB_WITNESS_WTNS && kind != NZCB_WITNESS_HOST && kind != NZCB_WITNESS_DEVICE)
+    return fail(err, NZCB_ERR_ARG, "unknown witness kind");
   if (pub_cap < 32 * (size_t)ctx->p->nPublic || (!pub_out && ctx->p->nPublic))
     return fail(err, NZCB_ERR_ARG, "public output buffer too small");
   try {
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->p->prove(witness, n_witness, blinding, proof_out, pub_out);
+    const uint8_t* values = (const uint8_t*)witness;
+    size_t nw = n;
+    if (kind == NZCB_WITNESS_WTNS) {
+      Wtns w = parse_wtns(values, n);
+      if (!w.q_is_r)
+        return fail(err, NZCB_ERR_CURVE, "Curve of the witness does not match the curve of the proving key");
+      values = w.values;
+      nw = w.nWitness;
+    }
+    std::shared_lock<std::shared_mutex> lk(ctx->cfg);
+    Prover* pr = ctx->acquire(log, log_user);
+    try {
+      pr->prove(values, nw, blinding, proof_out, pub_out, kind == NZCB_WITNESS_DEVICE);
+    } catch (...) {
+      pr->log = nullptr;
+      ctx->release(pr);
+      throw;
+    }
+    pr->log = nullptr;
+    ctx->release(pr);
     if (err) err->code = 0;
     return 0;
   } catch (const Error& e) {
@@ -348,42 +415,38 @@ int nzcb_prove_witness(nzcb_ctx* ctx, const uint8_t* witness, size_t n_witness, 
   } catch (const std::exception& e) {
     return fail(err, NZCB_ERR_INTERNAL, e.what());
   }
+}
+}  // namespace
+
+int nzcb_prove_witness(nzcb_ctx* ctx, const uint8_t* witness, size_t n_witness, const uint8_t* blinding,
+                       uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_err* err) {
+  return prove_one(ctx, witness, n_witness, NZCB_WITNESS_HOST, blinding, proof_out, pub_out, pub_cap, nullptr, nullptr,
+                   err);
 }
 
 int nzcb_prove_device(nzcb_ctx* ctx, const void* dev_witness, size_t n_witness, const uint8_t* blinding,
                       uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_err* err) {
-  if (!ctx || !dev_witness || !proof_out) return fail(err, NZCB_ERR_ARG, "null argument");
-  if (pub_cap < 32 * (size_t)ctx->p->nPublic || (!pub_out && ctx->p->nPublic))
-    return fail(err, NZCB_ERR_ARG, "public output buffer too small");
-  try {
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    ctx->p->prove((const uint8_t*)dev_witness, n_witness, blinding, proof_out, pub_out, true);
-    if (err) err->code = 0;
-    return 0;
-  } catch (const Error& e) {
-    return fail(err, e.code, e.what());
-  } catch (const std::exception& e) {
-    return fail(err, NZCB_ERR_INTERNAL, e.what());
-  }
+  return prove_one(ctx, dev_witness, n_witness, NZCB_WITNESS_DEVICE, blinding, proof_out, pub_out, pub_cap, nullptr,
+                   nullptr, err);
 }
 
 int nzcb_prove(nzcb_ctx* ctx, const uint8_t* wtns, size_t wtns_len, const uint8_t* blinding, uint8_t* proof_out,
                uint8_t* pub_out, size_t pub_cap, nzcb_err* err) {
-  if (!ctx || !wtns) return fail(err, NZCB_ERR_ARG, "null argument");
-  try {
-    Wtns w = parse_wtns(wtns, wtns_len);
-    if (!w.q_is_r)
-      return fail(err, NZCB_ERR_CURVE, "Curve of the witness does not match the curve of the proving key");
-    return nzcb_prove_witness(ctx, w.values, w.nWitness, blinding, proof_out, pub_out, pub_cap, err);
-  } catch (const Error& e) {
-    return fail(err, e.code, e.what());
-  }
+  return prove_one(ctx, wtns, wtns_len, NZCB_WITNESS_WTNS, blinding, proof_out, pub_out, pub_cap, nullptr, nullptr,
+                   err);
+}
+
+int nzcb_prove_logged(nzcb_ctx* ctx, const void* witness, size_t n, int kind, const uint8_t* blinding,
+                      uint8_t* proof_out, uint8_t* pub_out, size_t pub_cap, nzcb_log_fn log, void* log_user,
+                      nzcb_err* err) {
+  return prove_one(ctx, witness, n, kind, blinding, proof_out, pub_out, pub_cap, log, log_user, err);
 }
 
 int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap) {
   if (!ctx || !ms) return 0;
   int k = cap < 9 ? cap : 9;
-  for (int i = 0; i < k; i++) ms[i] = ctx->p->tm[i];
+  std::lock_guard<std::mutex> lk(const_cast<nzcb_ctx*>(ctx)->pool_mu);
+  for (int i = 0; i < k; i++) ms[i] = ctx->last_tm[i];
   return k;
 }
 

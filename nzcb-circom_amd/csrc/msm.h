@@ -21,11 +21,11 @@ struct MsmBaseTable {
   void build(const G1Affine* bases, size_t n, int c, hipStream_t st, bool fold_mont = false);
 };
 
-// Window size of the table-based (fixed-base) MSM: 16..20 bits (NZCB_FB_WINDOW
-// overrides the default), i.e. 16..13 table rows and 2^15..2^19 buckets.
+// Window size of the table-based (fixed-base) MSM: 20 bits by default (13 table rows,
+// 2^19 buckets); NZCB_FB_WINDOW = 16..20 overrides it.
 int fixed_base_window();
-// Window of the Lagrange-basis table (A, B, C commitments of small witness values:
-// NZCB_LB_WINDOW, default 17): their few entries do not pay for a larger bucket set.
+// Window of the Lagrange-basis table (A, B, C commitments of small witness values: 17):
+// their few entries do not pay for a larger bucket set.
 int lagrange_window();
 
 struct MsmScratch {
@@ -35,35 +35,30 @@ struct MsmScratch {
   DevBuf<uint32_t> keys_in, keys_out, vals_in;
   DevBuf<uint8_t> sort_tmp;
   size_t sort_tmp_bytes = 0;
-  // fixed-base bucketing (msm.hip msm_keys_hist_kernel): per (high key byte, tile)
+  // fixed-base bucketing (msm.hip msm_bin_hist_kernel): per (high key byte, tile)
   // counts, scanned in place, and the values grouped by high byte
   DevBuf<uint32_t> bin_counts, vals_mid;
   DevBuf<uint32_t> lo_seg;    // per (bucket_lo work item, low index): count, then its first position
-  DevBuf<G1xyzz> buckets;     // buckets whose entries lie in one accumulation chunk
+  DevBuf<G1xyzz> buckets;     // generic: buckets whose entries lie in one accumulation chunk
   DevBuf<G1xyzz> carry_own;   // per chunk: partial sum of a bucket that starts in the chunk and spills over
   DevBuf<G1xyzz> carry_cont;  // per chunk: partial sum of a bucket that began in an earlier chunk
-  // fixed-base schedule: the accumulation stores its results unconverted (radix 2^29,
-  // Montgomery-261); the finalize kernel converts them into buckets
+  // fixed-base schedule: buckets and carries stay in radix 2^29 (Montgomery-261)
   DevBuf<Xyzz29> buckets29, carry_own29, carry_cont29;
-  // fixed-base pairing rounds (msm.hip msm_pair29_kernel): ping-pong affine sums and
-  // bucket offsets, and the exclusive prefix products of the slope denominators
-  DevBuf<G1Affine> pair_pts[2];
-  DevBuf<uint32_t> pair_off[2];
-  DevBuf<uint32_t> pair_pre;
   DevBuf<uint32_t> large;     // [count, bucket ids...] of buckets with long carry runs
   DevBuf<uint32_t> large_off;  // fixed base: piece offsets of the listed buckets (msm_large_scan_kernel)
   DevBuf<Xyzz29> large_part;   // fixed base: one partial sum per piece
-  DevBuf<Xyzz29> parts29;      // fixed base: per (sum slot, part) partial sums (msm_seg29 / msm_bitsums29)
-  DevBuf<Xyzz29> seg_tot29, seg_run29;  // fixed base: per kSeg29-bucket segment (msm_seg29_kernel)
-  DevBuf<G1xyzz> seg_tot;     // per (bucket set, segment): sum_j (j+1) * bucket_j
-  DevBuf<G1xyzz> seg_run;     // per (bucket set, segment): sum_j bucket_j
-  DevBuf<G1xyzz> parts;       // per (set, sum slot, part): partial plain sums
-  DevBuf<G1xyzz> win;         // per (set, sum slot): see msm_sums_kernel
+  // fixed-base window sum (msm.hip msm_tile29_kernel): row / column partials per tile, lines
+  DevBuf<Xyzz29> rowp29, colp29, lines29;
+  DevBuf<G1xyzz> seg_tot;     // generic: per (bucket set, segment): sum_j (j+1) * bucket_j
+  DevBuf<G1xyzz> seg_run;     // generic: per (bucket set, segment): sum_j bucket_j
+  DevBuf<G1xyzz> parts;       // generic: per (set, sum slot, part): partial plain sums
+  DevBuf<G1xyzz> win;         // per (set, sum slot): see msm_sums_kernel / msm_slots29_kernel
   G1xyzz* host_win = nullptr;  // pinned
   size_t host_win_cap = 0;
   // shape of the MSM in flight (set by msm_enqueue, used by msm_finish)
   int cur_c = 0, cur_nsets = 0, cur_nbits = 0, cur_seglen = 0;
-  bool cur_bitsums = false;
+  bool cur_fixed = false;
+  int cur_a = 0, cur_hb = 0;  // fixed base: column / row bits of the window sum
   size_t cur_n = 0;
   uint32_t cur_nkeys = 0;
   // optional HIP-event timing: accumulation kernel (bench.py roofline) and, with
@@ -77,10 +72,6 @@ struct MsmScratch {
   void init(size_t max_points, bool fixed_base = false);
   ~MsmScratch();
 };
-
-// Batch-affine pairing rounds before the fixed-base accumulation: r >= 0 forces r rounds
-// (at most 6), r < 0 restores the automatic choice. Process-wide.
-void msm_set_pair_rounds(int r);
 
 // Window size of the generic (variable-base) MSM of n points.
 int msm_window_bits(size_t n);

@@ -47,8 +47,7 @@ struct Prover {
   hipStream_t aux[kSlots] = {nullptr, nullptr, nullptr};
   hipEvent_t ready[kSlots] = {nullptr, nullptr, nullptr};
   bool slot_local[kSlots] = {false, false, false};  // slot's MSM stays on this device (Lagrange basis)
-  // round 1's interpolations of A, B, C run here (overlapping round 2's grand product)
-  hipStream_t side = nullptr;
+  // round 1's interpolations of A, B, C run on aux[2] (overlapping round 2's grand product)
   hipEvent_t side_ready = nullptr, side_done = nullptr;
   ~Prover();
   // resident zkey data (LEM, as in the file)
@@ -62,6 +61,7 @@ struct Prover {
   bool lcommit = false;
   DevBuf<Fr> qm, ql, qr, qo, qc;  // [n coefs | 4n evals]
   DevBuf<Fr> sigma;               // 3 x [n | 4n]
+  DevBuf<Fr> sig_h;               // 3 x n: sigma_k(w^i), contiguous (round 2)
   DevBuf<Fr> lagrange;            // nLagrange x [n | 4n]
   DevBuf<uint32_t> amap, bmap, cmap;
   DevBuf<AddRec> adds;
@@ -87,7 +87,7 @@ struct Prover {
   DevBuf<Fr> A4, B4, C4, Z4, T, Tz, t;  // 4n (A4..Z4: coset evaluations)
   DevBuf<Fr> pol_r, pol_wxi, pol_wxiw;    // n+3, n+6, n+3
   DevBuf<Fr> blind;               // 12 (index 0 unused)
-  DevBuf<Fr> scan_tmp;            // recursive scan levels
+  DevBuf<Fr> scan_tmp;            // tile totals / heads of the round-2 and round-5 scans, and their levels
   DevBuf<Fr> eval_part;           // partial sums of polynomial evaluations
   DevBuf<uint32_t> flags;
   std::vector<Fr> host_part;
@@ -130,7 +130,7 @@ struct Prover {
   G1Affine commit_finish(int slot);
   // np <= 8 evaluations p_j(x_j) (two launches, one host round trip)
   void eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out);
-  void prefix_product(Fr* x, size_t m, Fr* level_tmp, bool have_totals = false);
+  void prefix_product(Fr* x, size_t m, Fr* level_tmp);
   void suffix_linear(Fr* x, size_t m, const Fr& d, Fr* level_tmp);
   void div_pol1(const Fr* src, size_t m, const Fr& d, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit);
   double ms_since(std::chrono::steady_clock::time_point t0);

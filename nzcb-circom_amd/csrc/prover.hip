@@ -121,106 +121,311 @@ static F29 fr29_operand(Fr c) {
   return split29(c);
 }
 
-// Round 2: num_i / den_i with Montgomery batch inversion: each thread's chunk of
-// kScanChunk denominators by prefix products, then ONE Fermat inversion per workgroup
-// over a product tree of the threads' chunk totals in LDS (one inversion per chunk was
-// ~12 of the ~24 products per element, and a 1.1 ms launch on round 2's path).
-__global__ void __launch_bounds__(kT)
-k_perm_ratio(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
-             const Fr* __restrict__ sigma, size_t n, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi,
-             PermArgs pa, Fr* __restrict__ ratio, Fr* __restrict__ den_s, Fr* __restrict__ pre_s,
-             Fr* __restrict__ chunk_tot) {
-  __shared__ Fr tree[2 * kT];
-  const int tid = threadIdx.x;
-  const size_t t = (size_t)blockIdx.x * blockDim.x + tid;
-  const size_t s = t * kScanChunk;
-  const size_t e = s >= n ? s : (s + kScanChunk < n ? s + kScanChunk : n);  // empty past n
-  const Fr* s1 = sigma + n;  // sigma1 evals (4n), read at stride 4
-  const Fr* s2 = sigma + 5 * n + n;
-  const Fr* s3 = sigma + 10 * n + n;
-  Fr pre = Fr::one();
-  for (size_t i = s; i < e; i++) {
-    Fr w = root4(rlo, rhi, 4 * i);
-    Fr a = A[i], b = B[i], c = C[i];
-    const Fr bw = mul_fr29(w, pa.beta29);
-    const Fr k1bw = pa.k23 ? bw + bw : mul_fr29(w, pa.k1beta29);
-    const Fr k2bw = pa.k23 ? k1bw + bw : mul_fr29(w, pa.k2beta29);
-    Fr num = (a + bw + pa.gamma) * (b + k1bw + pa.gamma);
-    num = num * (c + k2bw + pa.gamma);
-    Fr den = (a + mul_fr29(s1[4 * i], pa.beta29) + pa.gamma) * (b + mul_fr29(s2[4 * i], pa.beta29) + pa.gamma);
-    den = den * (c + mul_fr29(s3[4 * i], pa.beta29) + pa.gamma);
-    ratio[i] = num;
-    den_s[i] = den;
-    pre = pre * den;
-    pre_s[i] = pre;
+// ---- coalesced tile scans (round 2's grand product, round 5's divPol1) --------------
+// A workgroup owns a tile of kTileN consecutive elements and thread t the kPer consecutive
+// elements [kPer t, kPer t + kPer) of it, so the sequential part of a scan runs in
+// registers. Loads and stores go through LDS: coalesced (consecutive lanes, consecutive
+// 32-byte elements) on the HBM side, and with one word of padding per 4 elements (word
+// 8 e + e / 4 + w) both the coalesced pass and the per-thread pass hit 32 distinct banks per
+// 32-lane half for kPer = 2 and 4 (ds_read_b32 / ds_write_b32 bank by (a / 4) mod 32).
+// The chunk-per-thread scans these replace (kScanChunk = 32 elements per thread read
+// straight from HBM, 1 KB apart per lane) ran at 0.06-0.3 of the HBM rate.
+#ifndef NZ_KPER
+#define NZ_KPER 2
+#endif
+static constexpr int kPer = NZ_KPER;  // elements per thread in the tile scans (A/B: -DNZ_KPER=4)
+static constexpr int kTileN = kT * kPer;                // 1024
+static constexpr int kStageWords = kTileN * 8 + kTileN / 4;
+
+__device__ __forceinline__ int stage_word(int e) { return e * 8 + e / 4; }
+
+// elements [base, base + kTileN) of f(g) (g < len; zero past it) -> use(j, x) for this
+// thread's kPer elements j (consumed as they leave LDS: no array of them stays live)
+template <class F, class U>
+__device__ __forceinline__ void stage_use(F&& f, size_t base, size_t len, uint32_t* lds, U&& use) {
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const int e = k * kT + (int)threadIdx.x;
+    const size_t g = base + (size_t)e;
+    const Fr v = g < len ? f(g) : Fr::zero();
+#pragma unroll
+    for (int w = 0; w < 8; w++) lds[stage_word(e) + w] = v.v[w];
   }
-  // one inversion for the workgroup: product tree over the chunk totals, inverted at the
-  // root, unwound to each thread's 1 / (its chunk's product)
-  tree[kT + tid] = pre;
   __syncthreads();
-  for (int w = kT / 2; w >= 1; w >>= 1) {
-    if (tid < w) tree[w + tid] = tree[2 * (w + tid)] * tree[2 * (w + tid) + 1];
-    __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int e = kPer * (int)threadIdx.x + j;
+    Fr x;
+#pragma unroll
+    for (int w = 0; w < 8; w++) x.v[w] = lds[stage_word(e) + w];
+    use(j, x);
   }
-  if (tid == 0) tree[1] = inverse(tree[1]);
   __syncthreads();
-  for (int w = 1; w < kT; w <<= 1) {
-    if (tid < w) {
-      const int nd = w + tid;
-      const Fr iv = tree[nd], l = tree[2 * nd], r = tree[2 * nd + 1];
-      tree[2 * nd] = iv * r;
-      tree[2 * nd + 1] = iv * l;
-    }
-    __syncthreads();
-  }
-  Fr inv = tree[kT + tid];
-  Fr prod = Fr::one();  // the chunk's product of ratios: level 0 of Z's prefix-product scan
-  for (size_t i = e; i-- > s;) {
-    Fr before = (i > s) ? pre_s[i - 1] : Fr::one();
-    Fr dinv = inv * before;
-    inv = inv * den_s[i];
-    const Fr r = ratio[i] * dinv;
-    ratio[i] = r;
-    prod = prod * r;
-  }
-  if (s < n) chunk_tot[t] = prod;
+}
+template <class F>
+__device__ __forceinline__ void stage_in(F&& f, size_t base, size_t len, uint32_t* lds, Fr (&out)[kPer]) {
+  stage_use(f, base, len, lds, [&](int j, const Fr& x) { out[j] = x; });
 }
 
-// Round 2 as in round 2 (NZCB_PERM_TREE=0, A/B runs): one inversion per thread's chunk.
+// this thread's kPer elements -> dst[base + e] for base + e < len (coalesced)
+__device__ __forceinline__ void stage_out(const Fr (&v)[kPer], size_t base, size_t len, uint32_t* lds, Fr* dst) {
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int e = kPer * (int)threadIdx.x + j;
+#pragma unroll
+    for (int w = 0; w < 8; w++) lds[stage_word(e) + w] = v[j].v[w];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const int e = k * kT + (int)threadIdx.x;
+    const size_t g = base + (size_t)e;
+    Fr x;
+#pragma unroll
+    for (int w = 0; w < 8; w++) x.v[w] = lds[stage_word(e) + w];
+    if (g < len) dst[g] = x;
+  }
+  __syncthreads();
+}
+
+// exclusive product scan of v over the workgroup's threads (Kogge-Stone in LDS, 8 steps);
+// total = the product of all kT values
+__device__ __forceinline__ Fr block_prod_excl(const Fr& v, Fr* sh, Fr& total) {
+  const int tid = threadIdx.x;
+  sh[tid] = v;
+  __syncthreads();
+  Fr acc = v;
+#pragma unroll 1
+  for (int d = 1; d < kT; d <<= 1) {
+    const Fr o = tid >= d ? sh[tid - d] : Fr::one();
+    __syncthreads();
+    acc = acc * o;
+    sh[tid] = acc;
+    __syncthreads();
+  }
+  total = sh[kT - 1];
+  const Fr ex = tid ? sh[tid - 1] : Fr::one();
+  __syncthreads();
+  return ex;
+}
+
+// exclusive suffix product scan of v over the workgroup's threads (Kogge-Stone in LDS)
+__device__ __forceinline__ Fr block_prod_excl_suffix(const Fr& v, Fr* sh) {
+  const int tid = threadIdx.x;
+  sh[tid] = v;
+  __syncthreads();
+  Fr acc = v;
+#pragma unroll 1
+  for (int d = 1; d < kT; d <<= 1) {
+    const Fr o = tid + d < kT ? sh[tid + d] : Fr::one();
+    __syncthreads();
+    acc = acc * o;
+    sh[tid] = acc;
+    __syncthreads();
+  }
+  const Fr ex = tid + 1 < kT ? sh[tid + 1] : Fr::one();
+  __syncthreads();
+  return ex;
+}
+
+// Round 2 without a single inversion per element or per workgroup:
+//   Z_i = prod_{k<i} num_k / den_k = (prod_{k<i} num_k) (prod_{k>=i} den_k) / prod_k den_k,
+// with num_i = (a + b w^i + g)(b + k1 b w^i + g)(c + k2 b w^i + g) and
+//      den_i = (a + b s1_i + g)(b + b s2_i + g)(c + b s3_i + g):
+// an exclusive prefix product of the numerators, an inclusive suffix product of the
+// denominators and ONE inversion per proof (of prod den, which the copy-constraint check
+// compares with prod num anyway). A workgroup computes its tile's num / den, the tile-local
+// scans (thread-local over kPer elements, Kogge-Stone over the threads) and writes
+// Zloc_i = Nloc_excl_i * Dloc_suffix_i and the tile totals; k_perm_factors and
+// k_apply_tiles multiply in the other tiles' totals and the inverse. The sigma evaluations
+// come from contiguous copies (Prover::sig_h), not at stride 4 from the 4n evaluations.
+// Round 3 ran a batch inversion per 32-element chunk per thread (1.24 ms at 2^21, the
+// chunks 1 KB apart per lane, den / prefix arrays written and read back through HBM).
+__device__ __forceinline__ Fr perm_bw(const Fr* rlo, const Fr* rhi, size_t e, size_t n, const F29& op) {
+  return e < n ? mul_fr29(root4(rlo, rhi, 4 * e), op) : Fr::zero();
+}
+
 __global__ void __launch_bounds__(kT)
-k_perm_ratio_chunk(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
-             const Fr* __restrict__ sigma, size_t n, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi,
-             PermArgs pa, Fr* __restrict__ ratio, Fr* __restrict__ den_s, Fr* __restrict__ pre_s) {
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t s = t * kScanChunk;
-  if (s >= n) return;
-  size_t e = s + kScanChunk < n ? s + kScanChunk : n;
-  const Fr* s1 = sigma + n;           // sigma1 evals (4n), read at stride 4
-  const Fr* s2 = sigma + 5 * n + n;
-  const Fr* s3 = sigma + 10 * n + n;
-  Fr pre = Fr::one();
-  for (size_t i = s; i < e; i++) {
-    Fr w = root4(rlo, rhi, 4 * i);
-    Fr a = A[i], b = B[i], c = C[i];
-    const Fr bw = mul_fr29(w, pa.beta29);
-    const Fr k1bw = pa.k23 ? bw + bw : mul_fr29(w, pa.k1beta29);
-    const Fr k2bw = pa.k23 ? k1bw + bw : mul_fr29(w, pa.k2beta29);
-    Fr num = (a + bw + pa.gamma) * (b + k1bw + pa.gamma);
-    num = num * (c + k2bw + pa.gamma);
-    Fr den = (a + mul_fr29(s1[4 * i], pa.beta29) + pa.gamma) * (b + mul_fr29(s2[4 * i], pa.beta29) + pa.gamma);
-    den = den * (c + mul_fr29(s3[4 * i], pa.beta29) + pa.gamma);
-    ratio[i] = num;
-    den_s[i] = den;
-    pre = pre * den;
-    pre_s[i] = pre;
+k_perm_tile(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
+            const Fr* __restrict__ sig_h, size_t n, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi,
+            PermArgs pa, Fr* __restrict__ Z, Fr* __restrict__ ntot, Fr* __restrict__ dtot) {
+  __shared__ uint32_t stg[kStageWords];
+  __shared__ Fr sh[kT];
+  const int tid = threadIdx.x;
+  const size_t base = (size_t)blockIdx.x * kTileN;
+  const size_t e0 = base + (size_t)kPer * tid;
+  const F29 beta29 = pa.beta29, k1beta29 = pa.k1beta29, k2beta29 = pa.k2beta29;  // no byval copy in scratch
+  const Fr gamma = pa.gamma;
+  const bool k23 = pa.k23 != 0;
+  Fr num[kPer], den[kPer], v[kPer], u[kPer];
+#pragma unroll 1
+  for (int k = 0; k < 3; k++) {
+    // witness column: num *= x + k b w + g (k b w: b w, 2 b w, 3 b w when k1, k2 = 2, 3, what
+    // snarkjs getK1K2 finds for BN254); the value stays for the denominator
+    const F29 op = k23 || k == 0 ? beta29 : (k == 1 ? k1beta29 : k2beta29);
+    const Fr* col = k == 0 ? A : B;
+    if (k == 2) col = C;
+    stage_use([&](size_t g) { return col[g]; }, base, n, stg,
+              [&](int j, const Fr& x) {
+                Fr kbw = perm_bw(rlo, rhi, e0 + j, n, op);
+                if (k23 && k) kbw = k == 1 ? kbw + kbw : kbw + kbw + kbw;
+                const Fr f = x + kbw + gamma;
+                num[j] = k ? num[j] * f : f;
+                u[j] = x + gamma;
+              });
+    // sigma_k: den *= x + b s_k + g
+    stage_use([&](size_t g) { return sig_h[(size_t)k * n + g]; }, base, n, stg, [&](int j, const Fr& x) {
+      const Fr g = u[j] + mul_fr29(x, beta29);
+      den[j] = k ? den[j] * g : g;
+    });
   }
-  Fr inv = inverse(pre);
-  for (size_t i = e; i-- > s;) {
-    Fr before = (i > s) ? pre_s[i - 1] : Fr::one();
-    Fr dinv = inv * before;
-    inv = inv * den_s[i];
-    ratio[i] = ratio[i] * dinv;
+#pragma unroll
+  for (int j = 0; j < kPer; j++)  // past n: factor 1
+    if (e0 + j >= n) num[j] = den[j] = Fr::one();
+  // thread-local: v = exclusive prefix of num, u = inclusive suffix of den
+  v[0] = Fr::one();
+#pragma unroll
+  for (int j = 1; j < kPer; j++) v[j] = v[j - 1] * num[j - 1];
+  u[kPer - 1] = den[kPer - 1];
+#pragma unroll
+  for (int j = kPer - 2; j >= 0; j--) u[j] = u[j + 1] * den[j];
+  Fr nt;
+  const Fr np = block_prod_excl(v[kPer - 1] * num[kPer - 1], sh, nt);
+  const Fr ds = block_prod_excl_suffix(u[0], sh);
+  const Fr c = np * ds;
+#pragma unroll
+  for (int j = 0; j < kPer; j++) v[j] = v[j] * u[j] * c;
+  stage_out(v, base, n, stg, Z);
+  if (tid == 0) {
+    ntot[blockIdx.x] = nt;
+    dtot[blockIdx.x] = ds * u[0];  // thread 0: its own suffix times the others'
   }
+}
+
+// F_T = (prod_{T'<T} N_T') (prod_{T'>T} D_T') / prod D (one workgroup; each thread a run of
+// consecutive tiles); totals[0] = prod N, totals[1] = prod D (round 2's copy-constraint check)
+__global__ void __launch_bounds__(1024)
+k_perm_factors(const Fr* __restrict__ ntot, const Fr* __restrict__ dtot, int ntiles, Fr* __restrict__ F,
+               Fr* __restrict__ totals) {
+  __shared__ Fr sh[1024];
+  __shared__ Fr inv_d;
+  const int tid = threadIdx.x;
+  const int per = (ntiles + 1023) / 1024;
+  const int t0 = min(tid * per, ntiles), t1 = min(t0 + per, ntiles);
+  Fr pn = Fr::one(), pd = Fr::one();
+  for (int t = t0; t < t1; t++) {
+    pn = pn * ntot[t];
+    pd = pd * dtot[t];
+  }
+  // exclusive prefix of pn, exclusive suffix of pd over the 1024 threads
+  Fr an = pn, ad = pd;
+  sh[tid] = an;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const Fr o = tid >= d ? sh[tid - d] : Fr::one();
+    __syncthreads();
+    an = an * o;
+    sh[tid] = an;
+    __syncthreads();
+  }
+  const Fr nall = sh[1023];
+  const Fr npre = tid ? sh[tid - 1] : Fr::one();
+  __syncthreads();
+  sh[tid] = ad;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const Fr o = tid + d < 1024 ? sh[tid + d] : Fr::one();
+    __syncthreads();
+    ad = ad * o;
+    sh[tid] = ad;
+    __syncthreads();
+  }
+  const Fr dall = sh[0];
+  const Fr dsuf = tid + 1 < 1024 ? sh[tid + 1] : Fr::one();
+  if (tid == 0) {
+    inv_d = inverse(dall);
+    totals[0] = nall;
+    totals[1] = dall;
+  }
+  __syncthreads();
+  // within the run: prefix of N (forward), suffix of D (backward)
+  Fr run = npre * inv_d;
+  for (int t = t0; t < t1; t++) {
+    F[t] = run;
+    run = run * ntot[t];
+  }
+  Fr sd = dsuf;
+  for (int t = t1 - 1; t >= t0; t--) {
+    F[t] = F[t] * sd;
+    sd = sd * dtot[t];
+  }
+}
+
+// Z[i] *= F[i / kTileN] (coalesced)
+__global__ void __launch_bounds__(kT)
+k_apply_tiles(Fr* __restrict__ x, size_t m, const Fr* __restrict__ F) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  x[i] = x[i] * F[i / kTileN];
+}
+
+// Round 5's divPol1: y_i = x_i + d y_{i+1} over i < m, x_i =
+// src[i + 1] (x_{m-1} = 0), y_m = 0, by tiles. Each thread runs the recurrence over its
+// kPer elements, the workgroup combines the thread heads h_t by a Kogge-Stone suffix scan
+// Y_t += D^(2^s) Y_(t+2^s) (D = d^kPer), and the tile's carry-in Y (the true y at the next
+// tile's first element) seeds the last thread. Two passes: kWrite = false writes only the
+// tile heads (carry-in 0), which a small scan turns into the true carries; kWrite = true
+// recomputes the tile with its carry and writes y (x is read twice instead of y written,
+// read and written again by a fix-up pass).
+template <bool kWrite>
+__global__ void __launch_bounds__(kT)
+k_lin_tile(const Fr* __restrict__ src, size_t m, Fr d, const Fr* __restrict__ carry, Fr* __restrict__ out) {
+  __shared__ uint32_t stg[kStageWords];
+  __shared__ Fr sh[kT];
+  const int tid = threadIdx.x;
+  const size_t base = (size_t)blockIdx.x * kTileN;
+  Fr x[kPer];
+  stage_in([&](size_t g) { return src[g + 1]; }, base, m - 1, stg, x);
+  Fr dp[kPer + 1];  // d^0 .. d^kPer
+  dp[0] = Fr::one();
+#pragma unroll
+  for (int j = 1; j <= kPer; j++) dp[j] = dp[j - 1] * d;
+  Fr y = Fr::zero();
+  if (kWrite && tid == kT - 1 && carry) y = carry[blockIdx.x + 1];
+#pragma unroll
+  for (int j = kPer - 1; j >= 0; j--) {
+    y = x[j] + d * y;
+    x[j] = y;
+  }
+  // suffix scan of the heads: Y_t = h_t + D Y_(t+1)
+  Fr D = dp[kPer];
+  sh[tid] = y;
+  __syncthreads();
+#pragma unroll 1
+  for (int s = 1; s < kT; s <<= 1) {
+    const Fr o = tid + s < kT ? sh[tid + s] : Fr::zero();
+    __syncthreads();
+    y = y + D * o;
+    sh[tid] = y;
+    __syncthreads();
+    D = sqr(D);
+  }
+  if (!kWrite) {
+    if (tid == 0) out[blockIdx.x] = y;
+    return;
+  }
+  // the true y of this thread's elements: local + d^(kPer - j) Y_(t+1)
+  const Fr next = tid + 1 < kT ? sh[tid + 1] : Fr::zero();
+#pragma unroll
+  for (int j = 0; j < kPer; j++) x[j] = x[j] + dp[kPer - j] * next;
+  __syncthreads();
+  stage_out(x, base, m, stg, out);
+}
+
+// contiguous sigma_k(w^i) = the 4n evaluation at 4 i (once per context)
+__global__ void k_stride4(const Fr* __restrict__ src, size_t n, Fr* __restrict__ dst) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[4 * i];
 }
 
 // exclusive prefix products: chunk products, small single-block scan, apply
@@ -503,29 +708,6 @@ static F29 f29_exp(Fr v, int extra) {  // split29 of v * 2^extra (host)
   return split29(v);
 }
 
-// One evaluation per launch (NZCB_EVAL_MANY=0, A/B runs): chunked Horner, partial[block]
-// = sum over the block's chunks of p(chunk) * x^(chunk start), summed on the host
-static constexpr int kEvalChunk = 64;
-__global__ void __launch_bounds__(kT)
-k_eval(const Fr* __restrict__ p, size_t len, Fr x, Fr xK, Fr* __restrict__ partial) {
-  __shared__ Fr sh[kT];
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t s = t * kEvalChunk;
-  Fr acc = Fr::zero();
-  if (s < len) {
-    size_t e = s + kEvalChunk < len ? s + kEvalChunk : len;
-    for (size_t i = e; i-- > s;) acc = acc * x + p[i];
-    acc = acc * pow_u64(xK, (uint64_t)t);
-  }
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int stride = kT / 2; stride > 0; stride >>= 1) {
-    if ((int)threadIdx.x < stride) sh[threadIdx.x] = sh[threadIdx.x] + sh[threadIdx.x + stride];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
-}
-
 // Round 4, all evaluations of one point set in two launches and one host round trip
 // (eight separately synchronised Horner launches took 1.05 ms + 8 syncs per proof,
 // profiles/r3_single_lane_phases.txt). Block b, thread i: Horner over coefficients
@@ -658,13 +840,6 @@ __global__ void k_pol_wxi(const Fr* __restrict__ t, const Fr* __restrict__ pr, c
   out[i] = w;
 }
 
-// dst[i] = src[i+1] (i < m-1), dst[m-1] = 0: divPol1 input for the suffix recurrence
-__global__ void k_shift_down(const Fr* __restrict__ src, size_t m, Fr* __restrict__ dst) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  dst[i] = (i + 1 < m) ? src[i + 1] : Fr::zero();
-}
-
 // "Polinomial does not divide": P0 == -d * q0
 __global__ void k_div_check(const Fr* __restrict__ src, Fr p0_adjust, const Fr* __restrict__ q, Fr d,
                             uint32_t* flags, uint32_t bit) {
@@ -729,10 +904,6 @@ Prover::~Prover() {
       (void)hipStreamDestroy(aux[i]);
     }
     if (ready[i]) (void)hipEventDestroy(ready[i]);
-  }
-  if (side) {
-    (void)hipStreamSynchronize(side);
-    (void)hipStreamDestroy(side);
   }
   if (side_ready) (void)hipEventDestroy(side_ready);
   if (side_done) (void)hipEventDestroy(side_done);
@@ -814,11 +985,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   // rows of 2^-256 PTau: the commitments' Montgomery-form scalars are digit sources as
   // they are (every ptab MSM is enqueued with mont = true; split ranges and devices keep
   // plain tables)
-  static const bool fold = [] {  // NZCB_FOLD=0: a plain PTau table (A/B runs)
-    const char* e = std::getenv("NZCB_FOLD");
-    return !(e && e[0] == '0');
-  }();
-  ptab.build(ptau.p, ptau.n, fixed_base_window(), s, fold);
+  ptab.build(ptau.p, ptau.n, fixed_base_window(), s, true);
   lcommit = lagrange_commit_enabled() && ptau.n >= (size_t)n + 2;
   if (lcommit) {  // one elliptic-curve iNTT per context (csrc/lagrange.hip)
     ltau.alloc((size_t)n + 2);
@@ -831,6 +998,11 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   up(qo, z.qo);
   up(qc, z.qc);
   up(sigma, z.sigma);
+  sig_h.alloc((size_t)3 * n);  // sigma_k on H, contiguous (round 2's grand product)
+  for (int k = 0; k < 3; k++)
+    hipLaunchKernelGGL(k_stride4, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, sigma.p + (size_t)k * 5 * n + n,
+                       (size_t)n, sig_h.p + (size_t)k * n);
+  NZ_HIP(hipGetLastError());
   up(lagrange, z.lagrange);
   up(amap, z.amap);
   up(bmap, z.bmap);
@@ -1003,11 +1175,6 @@ void Prover::init_slots() {
     NZ_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
     NZ_HIP(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
   }
-  static const bool use_side = [] {  // NZCB_SIDE_STREAM=1: a stream of their own (A/B runs)
-    const char* e = std::getenv("NZCB_SIDE_STREAM");
-    return e && e[0] == '1';
-  }();
-  if (use_side) NZ_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
   NZ_HIP(hipEventCreateWithFlags(&side_ready, hipEventDisableTiming));
   NZ_HIP(hipEventCreateWithFlags(&side_done, hipEventDisableTiming));
 }
@@ -1022,9 +1189,8 @@ void Prover::alloc_workspace() {
   T.alloc(n4); Tz.alloc(n4); t.alloc(n4);
   pol_r.alloc(n + 3); pol_wxi.alloc(n + 6); pol_wxiw.alloc(n + 3);
   blind.alloc(13);  // b1..b11 (index 0 unused), then the 32-bit check flags in slot 12
-  size_t lv = 0, m = n4;
-  while (m > 1024) { m = (m + kScanChunk - 1) / kScanChunk; lv += m; }
-  scan_tmp.alloc(lv + 2048);
+  // tile totals / heads (n / kTileN + 2) and the small scans' levels over them
+  scan_tmp.alloc(3 * ((size_t)n / kTileN + 2) + 4096);
   size_t nblocks = ((size_t)3 * n + 6 + (size_t)kT * kEvalChunk2 - 1) / ((size_t)kT * kEvalChunk2) + 1;
   eval_part.alloc((size_t)kEvalMax * nblocks + kEvalMax);  // eval_many: kEvalMax rows + results
   host_part.resize(std::max<size_t>(nblocks, kEvalMax));
@@ -1055,7 +1221,7 @@ Prover::Prover(const Prover& pk, int) {
   ltab.q.alias(pk.ltab.q);
   ltab.n = pk.ltab.n; ltab.stride = pk.ltab.stride; ltab.c = pk.ltab.c; ltab.nw = pk.ltab.nw;
   qm.alias(pk.qm); ql.alias(pk.ql); qr.alias(pk.qr); qo.alias(pk.qo); qc.alias(pk.qc);
-  sigma.alias(pk.sigma); lagrange.alias(pk.lagrange);
+  sigma.alias(pk.sigma); sig_h.alias(pk.sig_h); lagrange.alias(pk.lagrange);
   amap.alias(pk.amap); bmap.alias(pk.bmap); cmap.alias(pk.cmap); adds.alias(pk.adds);
   root_lo.alias(pk.root_lo); root_hi.alias(pk.root_hi); x_lo.alias(pk.x_lo);
   g_lo.alias(pk.g_lo); g_hi.alias(pk.g_hi); gi_lo.alias(pk.gi_lo); gi_hi.alias(pk.gi_hi);
@@ -1304,24 +1470,6 @@ void Prover::set_msm_split(int world, size_t own_points, nzcb_msm_send_fn send, 
 void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out) {
   if (np < 1 || np > kEvalMax) throw Error(NZCB_ERR_INTERNAL, "eval_many: bad count");
   hipStream_t s = st();
-  static const bool many = [] {
-    const char* e = std::getenv("NZCB_EVAL_MANY");
-    return !(e && e[0] == '0');
-  }();
-  if (!many) {
-    for (int j = 0; j < np; j++) {
-      const size_t nb1 = ((lens[j] + kEvalChunk - 1) / kEvalChunk + kT - 1) / kT;
-      hipLaunchKernelGGL(k_eval, dim3((unsigned)nb1), dim3(kT), 0, s, polys[j], lens[j], xs[j],
-                         pow_u64(xs[j], kEvalChunk), eval_part.p);
-      NZ_HIP(hipGetLastError());
-      NZ_HIP(hipMemcpyAsync(host_part.data(), eval_part.p, nb1 * sizeof(Fr), hipMemcpyDeviceToHost, s));
-      NZ_HIP(hipStreamSynchronize(s));
-      Fr acc = Fr::zero();
-      for (size_t b = 0; b < nb1; b++) acc = acc + host_part[b];
-      out[j] = acc;
-    }
-    return;
-  }
   EvalSet es{};
   size_t maxlen = 0;
   for (int j = 0; j < np; j++) {
@@ -1349,16 +1497,15 @@ void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const
   for (int j = 0; j < np; j++) out[j] = host_part[j];
 }
 
-void Prover::prefix_product(Fr* x, size_t m, Fr* level_tmp, bool have_totals) {
+void Prover::prefix_product(Fr* x, size_t m, Fr* level_tmp) {
   hipStream_t s = st();
-  if (m <= 1024 && !have_totals) {
+  if (m <= 1024) {
     hipLaunchKernelGGL(k_scan_mul_small, dim3(1), dim3(1024), 0, s, x, (int)m, level_tmp + 1024);
     NZ_HIP(hipGetLastError());
     return;
   }
   size_t nc = (m + kScanChunk - 1) / kScanChunk;
-  if (!have_totals)  // else level_tmp[0..nc) holds the chunk products already (k_perm_ratio)
-    hipLaunchKernelGGL(k_chunk_prod, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, level_tmp);
+  hipLaunchKernelGGL(k_chunk_prod, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, level_tmp);
   prefix_product(level_tmp, nc, level_tmp + nc);
   hipLaunchKernelGGL(k_apply_prod, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, level_tmp);
   NZ_HIP(hipGetLastError());
@@ -1381,8 +1528,13 @@ void Prover::suffix_linear(Fr* x, size_t m, const Fr& d, Fr* level_tmp) {
 
 void Prover::div_pol1(const Fr* src, size_t m, const Fr& d, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit) {
   hipStream_t s = st();
-  hipLaunchKernelGGL(k_shift_down, dim3(grid_for(m, kT, 1u << 30)), dim3(kT), 0, s, src, m, dst);
-  suffix_linear(dst, m, d, scan_tmp.p);
+  const size_t ntiles = (m + kTileN - 1) / kTileN;
+  Fr* heads = scan_tmp.p;  // ntiles + 1 (the last one 0: the carry into the last tile)
+  NZ_HIP(hipMemsetAsync(heads + ntiles, 0, sizeof(Fr), s));
+  hipLaunchKernelGGL(k_lin_tile<false>, dim3((unsigned)ntiles), dim3(kT), 0, s, src, m, d, (const Fr*)nullptr, heads);
+  NZ_HIP(hipGetLastError());
+  suffix_linear(heads, ntiles, pow_u64(d, kTileN), heads + ntiles + 1);  // true heads: H_T = h_T + d^N H_(T+1)
+  hipLaunchKernelGGL(k_lin_tile<true>, dim3((unsigned)ntiles), dim3(kT), 0, s, src, m, d, (const Fr*)heads, dst);
   hipLaunchKernelGGL(k_div_check, dim3(1), dim3(64), 0, s, src, p0_adjust, dst, d, flags.p, flag_bit);
   NZ_HIP(hipGetLastError());
 }
@@ -1507,12 +1659,11 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       // which reads the evaluations only (round 2 waits for them before Z's own NTTs, which
       // share the NTT scratch). They run on C's commitment stream, and C's MSM takes the
       // main stream: a stream of their own per lane cost 2.5 % of the 5-lane bench
-      // (NZCB_SIDE_STREAM=1, profiles/r3_side_stream_ab.txt). msm_finish waits on the
-      // MSM's own event, not on its stream.
-      const bool own_side = side != nullptr;
-      hipStream_t ss = own_side ? side : aux[2];
+      // (round 3, profiles/r3_side_stream_ab.txt). msm_finish waits on the MSM's own event,
+      // not on its stream.
+      hipStream_t ss = aux[2];
       NZ_HIP(hipEventRecord(side_ready, s));  // A, B, C final (k_abc_tail), before C's MSM
-      commit_start(2, C.p, n + 2, &ltab, ltau.p, !own_side);
+      commit_start(2, C.p, n + 2, &ltab, ltau.p, true);
       NZ_HIP(hipStreamWaitEvent(ss, side_ready, 0));
       to4t(A.p, pol_a.p, A4.p, ba, 2, ss);
       to4t(B.p, pol_b.p, B4.p, bb, 2, ss);
@@ -1568,26 +1719,24 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   {
     PermArgs pa{beta, gamma, k1, k2, fr29_operand(beta), fr29_operand(k1 * beta), fr29_operand(k2 * beta),
                 k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0};
-    size_t nchunks = (n + kScanChunk - 1) / kScanChunk;
-    static const bool perm_tree = [] {  // NZCB_PERM_TREE=0: one inversion per chunk (A/B runs)
-      const char* e = std::getenv("NZCB_PERM_TREE");
-      return !(e && e[0] == '0');
-    }();
-    if (perm_tree)
-      hipLaunchKernelGGL(k_perm_ratio, dim3(grid_for(nchunks, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, sigma.p,
-                         (size_t)n, root_lo.p, root_hi.p, pa, Z.p, T.p, Tz.p, scan_tmp.p);
-    else
-      hipLaunchKernelGGL(k_perm_ratio_chunk, dim3(grid_for(nchunks, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p,
-                         sigma.p, (size_t)n, root_lo.p, root_hi.p, pa, Z.p, T.p, Tz.p);
+    const size_t ntiles = (n + kTileN - 1) / kTileN;
+    if (ntiles > 1024 * 64) throw Error(NZCB_ERR_INTERNAL, "round 2: domain too large for the tile factors");
+    Fr* ntot = scan_tmp.p;  // per tile: numerator / denominator totals, then the factors F_T
+    Fr* dtot = ntot + ntiles;
+    Fr* fac = dtot + ntiles;
+    Fr* totals = fac + ntiles;
+    hipLaunchKernelGGL(k_perm_tile, dim3((unsigned)ntiles), dim3(kT), 0, s, A.p, B.p, C.p, sig_h.p, (size_t)n,
+                       root_lo.p, root_hi.p, pa, Z.p, ntot, dtot);
+    hipLaunchKernelGGL(k_perm_factors, dim3(1), dim3(1024), 0, s, (const Fr*)ntot, (const Fr*)dtot, (int)ntiles,
+                       fac, totals);
+    hipLaunchKernelGGL(k_apply_tiles, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, Z.p, (size_t)n,
+                       (const Fr*)fac);
     NZ_HIP(hipGetLastError());
-    // keep the last ratio to form the total product Z[n] = prod of all ratios
-    Fr last_ratio;
-    NZ_HIP(hipMemcpyAsync(&last_ratio, Z.p + (n - 1), sizeof(Fr), hipMemcpyDeviceToHost, s));
-    prefix_product(Z.p, n, scan_tmp.p, perm_tree);
-    Fr last_pref;
-    NZ_HIP(hipMemcpyAsync(&last_pref, Z.p + (n - 1), sizeof(Fr), hipMemcpyDeviceToHost, s));
+    // Z[n] = prod num / prod den must be 1
+    Fr tt[2];
+    NZ_HIP(hipMemcpyAsync(tt, totals, sizeof(tt), hipMemcpyDeviceToHost, s));
     NZ_HIP(hipStreamSynchronize(s));
-    if (last_pref * last_ratio != Fr::one()) throw Error(NZCB_ERR_COPY, "Copy constraints does not match");
+    if (tt[0] != tt[1]) throw Error(NZCB_ERR_COPY, "Copy constraints does not match");
     const int bz[3] = {9, 8, 7};
     NZ_HIP(hipStreamWaitEvent(s, side_done, 0));  // A, B, C's NTTs (same scratch) are done
     // Z's commitment needs only its coefficients: its MSM starts before the 4n coset NTT,
@@ -1709,6 +1858,23 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       const Fr* polys[1] = {pol_r.p};
       const size_t lens[1] = {n + 3};
       eval_many(1, polys, lens, &xi, &er);
+    }
+    // The quotient checked at xi before it is committed to: the three-coset t
+    // is never inverse-transformed over 4n, so nothing else would catch an error in its
+    // coset evaluations, t's recombination or the round-3 stream ordering. From the round-4
+    // evaluations (what plonk_verify recomputes): t(xi) Z_H(xi) = r(xi) + PI(xi)
+    //   - alpha (a + b s1 + g)(b + b s2 + g)(c + g) z(w xi) - alpha^2 L1(xi)
+    // with PI(xi) = -sum_j pub_j L_j(xi), L_j(xi) = w^j (xi^n - 1) / (n (xi - w^j)).
+    {
+      const Fr zh = xim - Fr::one(), nf = fr_small(n);
+      Fr pi = Fr::zero(), wj = Fr::one();
+      for (uint32_t j = 0; j < nPublic; j++) {
+        pi = pi - Apub[j] * wj * zh * inverse(nf * (xi - wj));
+        wj = wj * wn;
+      }
+      const Fr perm = alpha * (ea + beta * es1 + gamma) * (eb + beta * es2 + gamma) * (ec + gamma) * ezw;
+      if (et * zh != er + pi - perm - e4)
+        throw Error(NZCB_ERR_INTERNAL, "quotient check failed: t(xi) Z_H(xi) differs from the numerator at xi");
     }
   }
   tm[5] = ms_since(t4);

@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -1009,6 +1010,9 @@ using namespace nzcb;
 
 struct nzcb_wprog {
   wvm::Program* p;
+  // runs share the program's status / scratch buffers: concurrent callers (the N-API
+  // addon's in-flight fullProve promises) take turns; one run of a batch is one launch
+  std::mutex mu;
 };
 
 extern "C" {
@@ -1054,6 +1058,7 @@ int nzcb_wprog_run_dev(nzcb_wprog* h, const void* dev_inputs, int count, void* d
                        int32_t* status_out, void* stream, nzcb_err* err) {
   try {
     if (!h) throw Error(NZCB_ERR_ARG, "witness program: null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
     wvm::run(h->p, dev_inputs, count, dev_witness, witness_stride, status_out, (hipStream_t)stream);
     return NZCB_OK;
   } catch (const Error& e) {
@@ -1076,6 +1081,7 @@ int nzcb_wprog_run(nzcb_wprog* h, const uint8_t* inputs, int count, uint8_t* wit
     const size_t nw = (size_t)h->p->out_wires() * 32;
     DevBuf<uint8_t> din(nin ? nin : 1), dw(nw * count);
     if (nin) NZ_HIP(hipMemcpy(din.p, inputs, nin, hipMemcpyHostToDevice));
+    std::lock_guard<std::mutex> lk(h->mu);
     wvm::run(h->p, din.p, count, dw.p, nw, status_out, nullptr);
     NZ_HIP(hipMemcpy(witness_out, dw.p, nw * count, hipMemcpyDeviceToHost));
     return NZCB_OK;

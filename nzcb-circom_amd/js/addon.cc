@@ -3,16 +3,20 @@
 // The reference's host is Node.js: its proofs come from snarkjs.plonk.prove /
 // plonk.fullProve [EXT] (snarkjs 0.4.12, /root/reference/package.json:18). This
 // addon binds the C-ABI in include/nzcb.h one-to-one; index.js wraps it in the
-// snarkjs-compatible Promise API. Proving runs in napi_async_work on the libuv
-// pool so the event loop is never blocked; the optional logger is called back on
-// the main thread through a thread-safe function.
+// snarkjs-compatible Promise API. Every prove / fullProveDevice call runs on a thread of
+// its own and takes a free lane of the context (nzcb_prove_logged), so concurrent promises
+// on one context are proved at the same time, up to the context's lanes (setLanes); the
+// result and the optional logger come back to the main thread through thread-safe
+// functions, and the event loop is never blocked.
 #define NAPI_VERSION 6
 #include <node_api.h>
 
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/nzcb.h"
@@ -29,9 +33,6 @@ namespace {
 
 struct Ctx {
   nzcb_ctx* ctx = nullptr;
-  // held across set_logger + prove + clear, so two in-flight prove() promises on one
-  // context never swap or drop each other's logger
-  std::mutex prove_mu;
 };
 
 void ctx_finalize(napi_env, void* data, void*) {
@@ -110,20 +111,25 @@ napi_value CreateContextFile(napi_env env, napi_callback_info info) {
   return ext;
 }
 
+struct Wprog;
+
+// one prove / fullProveDevice call: runs on its own thread, completes on the main thread
 struct ProveWork {
-  napi_async_work work = nullptr;
   napi_deferred deferred = nullptr;
-  napi_ref ctx_ref = nullptr, wtns_ref = nullptr;
-  napi_threadsafe_function tsfn = nullptr;
+  napi_ref ctx_ref = nullptr, in_ref = nullptr, prog_ref = nullptr;
+  napi_threadsafe_function done = nullptr;  // completion (no JS function: prove_complete)
+  napi_threadsafe_function tsfn = nullptr;  // the logger, if any
   Ctx* c = nullptr;
-  const uint8_t* wtns = nullptr;
-  size_t wtns_len = 0;
+  Wprog* prog = nullptr;                    // fullProveDevice: the witness program
+  const uint8_t* in = nullptr;              // .wtns bytes (prove) or input signals (fullProveDevice)
+  size_t in_len = 0;
   bool has_blinding = false;
   uint8_t blinding[NZCB_BLINDING_BYTES];
   uint8_t proof[NZCB_PROOF_BYTES];
   uint8_t pub[32 * 64];
   uint32_t npub = 0;
   int rc = 0;
+  int32_t status = 0;  // fullProveDevice: the witness program's failed check, if any
   nzcb_err err{};
 };
 
@@ -145,44 +151,77 @@ void call_logger(napi_env env, napi_value fn, void*, void* data) {
   free(msg);
 }
 
-void prove_execute(napi_env, void* data) {
+void prove_complete(napi_env env, napi_value, void*, void* data) {
   ProveWork* w = static_cast<ProveWork*>(data);
+  if (env) {
+    if (w->rc) {
+      napi_reject_deferred(env, w->deferred, make_error(env, w->rc, w->err.msg));
+    } else if (w->status) {
+      napi_reject_deferred(env, w->deferred, make_error(env, w->status, "Assert Failed (witness calculation)"));
+    } else {
+      std::string pj(8192, '\0'), uj(96 * 64 + 8, '\0');
+      nzcb_proof_to_json(w->proof, &pj[0], pj.size());
+      nzcb_public_to_json(w->pub, (int)w->npub, &uj[0], uj.size());
+      napi_value obj, a, b;
+      napi_create_object(env, &obj);
+      napi_create_string_utf8(env, pj.c_str(), NAPI_AUTO_LENGTH, &a);
+      napi_create_string_utf8(env, uj.c_str(), NAPI_AUTO_LENGTH, &b);
+      napi_set_named_property(env, obj, "proof", a);
+      napi_set_named_property(env, obj, "publicSignals", b);
+      napi_resolve_deferred(env, w->deferred, obj);
+    }
+    napi_delete_reference(env, w->ctx_ref);
+    napi_delete_reference(env, w->in_ref);
+    if (w->prog_ref) napi_delete_reference(env, w->prog_ref);
+  }
+  if (w->tsfn) napi_release_threadsafe_function(w->tsfn, napi_tsfn_release);
+  napi_release_threadsafe_function(w->done, napi_tsfn_release);
+  delete w;
+}
+
+void run_fullprove_device(ProveWork* w);
+
+void prove_thread(ProveWork* w) {
   uint32_t info[5];
   nzcb_ctx_info(w->c->ctx, info);
   w->npub = info[1];
   if (w->npub > 64) {
     w->rc = NZCB_ERR_ARG;
     std::snprintf(w->err.msg, sizeof(w->err.msg), "too many public signals for the addon buffer");
-    return;
+  } else if (w->prog) {
+    run_fullprove_device(w);
+  } else {
+    w->rc = nzcb_prove_logged(w->c->ctx, w->in, w->in_len, NZCB_WITNESS_WTNS, w->has_blinding ? w->blinding : nullptr,
+                              w->proof, w->pub, sizeof(w->pub), w->tsfn ? log_trampoline : nullptr, w, &w->err);
   }
-  std::lock_guard<std::mutex> lk(w->c->prove_mu);
-  nzcb_ctx_set_logger(w->c->ctx, w->tsfn ? log_trampoline : nullptr, w);
-  w->rc = nzcb_prove(w->c->ctx, w->wtns, w->wtns_len, w->has_blinding ? w->blinding : nullptr, w->proof, w->pub,
-                     sizeof(w->pub), &w->err);
-  nzcb_ctx_set_logger(w->c->ctx, nullptr, nullptr);
+  napi_call_threadsafe_function(w->done, w, napi_tsfn_blocking);
 }
 
-void prove_complete(napi_env env, napi_status, void* data) {
-  ProveWork* w = static_cast<ProveWork*>(data);
-  if (w->rc) {
-    napi_reject_deferred(env, w->deferred, make_error(env, w->rc, w->err.msg));
-  } else {
-    std::string pj(8192, '\0'), uj(96 * 64 + 8, '\0');
-    nzcb_proof_to_json(w->proof, &pj[0], pj.size());
-    nzcb_public_to_json(w->pub, (int)w->npub, &uj[0], uj.size());
-    napi_value obj, a, b;
-    napi_create_object(env, &obj);
-    napi_create_string_utf8(env, pj.c_str(), NAPI_AUTO_LENGTH, &a);
-    napi_create_string_utf8(env, uj.c_str(), NAPI_AUTO_LENGTH, &b);
-    napi_set_named_property(env, obj, "proof", a);
-    napi_set_named_property(env, obj, "publicSignals", b);
-    napi_resolve_deferred(env, w->deferred, obj);
+// the common argument handling of prove / fullProveDevice: blinding (argv[bi]), logger
+// (argv[bi + 1]); creates the promise and starts the thread
+napi_value start_prove(napi_env env, ProveWork* w, napi_value* argv, size_t argc, size_t bi) {
+  napi_valuetype t;
+  if (argc > bi && napi_typeof(env, argv[bi], &t) == napi_ok && t == napi_object) {
+    void* bd = nullptr;
+    size_t bl = 0;
+    if (napi_get_buffer_info(env, argv[bi], &bd, &bl) == napi_ok && bl == NZCB_BLINDING_BYTES) {
+      std::memcpy(w->blinding, bd, bl);
+      w->has_blinding = true;
+    }
   }
-  if (w->tsfn) napi_release_threadsafe_function(w->tsfn, napi_tsfn_release);
-  napi_delete_reference(env, w->ctx_ref);
-  napi_delete_reference(env, w->wtns_ref);
-  napi_delete_async_work(env, w->work);
-  delete w;
+  napi_value name;
+  if (argc > bi + 1 && napi_typeof(env, argv[bi + 1], &t) == napi_ok && t == napi_function) {
+    napi_create_string_utf8(env, "nzcb-logger", NAPI_AUTO_LENGTH, &name);
+    CHECK(napi_create_threadsafe_function(env, argv[bi + 1], nullptr, name, 0, 1, nullptr, nullptr, nullptr,
+                                          call_logger, &w->tsfn));
+  }
+  napi_value promise;
+  CHECK(napi_create_promise(env, &w->deferred, &promise));
+  napi_create_string_utf8(env, "nzcb-prove", NAPI_AUTO_LENGTH, &name);
+  CHECK(napi_create_threadsafe_function(env, nullptr, nullptr, name, 0, 1, nullptr, nullptr, nullptr, prove_complete,
+                                        &w->done));
+  std::thread(prove_thread, w).detach();
+  return promise;
 }
 
 // prove(ctx, wtns: Buffer, blinding: Buffer|null, logger: Function|null) -> Promise<{proof, publicSignals}> (JSON strings)
@@ -193,37 +232,86 @@ napi_value Prove(napi_env env, napi_callback_info info) {
   ProveWork* w = new ProveWork();
   CHECK(napi_get_value_external(env, argv[0], reinterpret_cast<void**>(&w->c)));
   void* wd = nullptr;
-  CHECK(napi_get_buffer_info(env, argv[1], &wd, &w->wtns_len));
-  w->wtns = static_cast<const uint8_t*>(wd);
+  CHECK(napi_get_buffer_info(env, argv[1], &wd, &w->in_len));
+  w->in = static_cast<const uint8_t*>(wd);
   CHECK(napi_create_reference(env, argv[0], 1, &w->ctx_ref));
-  CHECK(napi_create_reference(env, argv[1], 1, &w->wtns_ref));
-  napi_valuetype t;
-  if (argc > 2 && napi_typeof(env, argv[2], &t) == napi_ok && t == napi_object) {
-    void* bd = nullptr;
-    size_t bl = 0;
-    if (napi_get_buffer_info(env, argv[2], &bd, &bl) == napi_ok && bl == NZCB_BLINDING_BYTES) {
-      std::memcpy(w->blinding, bd, bl);
-      w->has_blinding = true;
-    }
+  CHECK(napi_create_reference(env, argv[1], 1, &w->in_ref));
+  return start_prove(env, w, argv, argc, 2);
+}
+
+// setLanes(ctx, lanes) -> lanes: proofs in flight on the context (nzcb_ctx_set_lanes)
+napi_value SetLanes(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c = nullptr;
+  CHECK(napi_get_value_external(env, argv[0], reinterpret_cast<void**>(&c)));
+  int32_t lanes = 1;
+  CHECK(napi_get_value_int32(env, argv[1], &lanes));
+  nzcb_err err{};
+  if (nzcb_ctx_set_lanes(c->ctx, lanes, &err)) {
+    napi_throw(env, make_error(env, err.code, err.msg));
+    return nullptr;
   }
-  if (argc > 3 && napi_typeof(env, argv[3], &t) == napi_ok && t == napi_function) {
-    napi_value name;
-    napi_create_string_utf8(env, "nzcb-logger", NAPI_AUTO_LENGTH, &name);
-    CHECK(napi_create_threadsafe_function(env, argv[3], nullptr, name, 0, 1, nullptr, nullptr, nullptr, call_logger,
-                                          &w->tsfn));
-  }
-  napi_value promise, rname;
-  CHECK(napi_create_promise(env, &w->deferred, &promise));
-  napi_create_string_utf8(env, "nzcb-prove", NAPI_AUTO_LENGTH, &rname);
-  CHECK(napi_create_async_work(env, nullptr, rname, prove_execute, prove_complete, w, &w->work));
-  CHECK(napi_queue_async_work(env, w->work));
-  return promise;
+  napi_value v;
+  napi_create_int32(env, nzcb_ctx_lanes(c->ctx), &v);
+  return v;
 }
 
 // ---- witness programs (nzcb_wprog_*): circom's witness calculator on the GPU ----------
 struct Wprog {
   nzcb_wprog* p = nullptr;
 };
+
+// HBM buffers reused across fullProveDevice calls (a witness of nzcp_live is 19.2 MB; a
+// hipMalloc per proof would cost more than the witness program's run)
+std::mutex g_pool_mu;
+std::multimap<size_t, void*> g_pool;
+void* pool_get(size_t bytes) {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pool.find(bytes);
+    if (it != g_pool.end()) {
+      void* p = it->second;
+      g_pool.erase(it);
+      return p;
+    }
+  }
+  return nzcb_dev_alloc(bytes);
+}
+void pool_put(size_t bytes, void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool.emplace(bytes, p);
+}
+
+// plonk.fullProve with a witness program, everything in HBM: the input signals go up
+// (a few KB), the witness program writes the witness into a device buffer, and the proof
+// reads it there (nzcb_wprog_run_dev + nzcb_prove_logged NZCB_WITNESS_DEVICE); only the
+// proof and the public signals come back
+void run_fullprove_device(ProveWork* w) {
+  uint32_t pi[5];
+  nzcb_wprog_info(w->prog->p, pi);
+  const size_t nwires = pi[0], nin = (size_t)pi[2] + pi[3];
+  if (w->in_len != nin * 32) {
+    w->rc = NZCB_ERR_ARG;
+    std::snprintf(w->err.msg, sizeof(w->err.msg), "expected %zu input signals", nin);
+    return;
+  }
+  void* din = pool_get(nin * 32 ? nin * 32 : 32);
+  void* dw = pool_get(nwires * 32);
+  if (!din || !dw || nzcb_memcpy_h2d(din, w->in, w->in_len) != 0) {
+    w->rc = NZCB_ERR_HIP;
+    std::snprintf(w->err.msg, sizeof(w->err.msg), "device buffers for the witness failed");
+  } else {
+    w->rc = nzcb_wprog_run_dev(w->prog->p, din, 1, dw, nwires * 32, &w->status, nullptr, &w->err);
+    if (!w->rc && !w->status)
+      w->rc = nzcb_prove_logged(w->c->ctx, dw, nwires, NZCB_WITNESS_DEVICE, w->has_blinding ? w->blinding : nullptr,
+                                w->proof, w->pub, sizeof(w->pub), w->tsfn ? log_trampoline : nullptr, w, &w->err);
+  }
+  pool_put(nin * 32 ? nin * 32 : 32, din);
+  pool_put(nwires * 32, dw);
+}
 
 void wprog_finalize(napi_env, void* data, void*) {
   Wprog* w = static_cast<Wprog*>(data);
@@ -319,6 +407,24 @@ napi_value CalculateWitness(napi_env env, napi_callback_info info) {
   CHECK(napi_create_async_work(env, nullptr, rname, witness_execute, witness_complete, k, &k->work));
   CHECK(napi_queue_async_work(env, k->work));
   return promise;
+}
+
+// fullProveDevice(ctx, prog, inputs: Buffer (n_inputs x 32 B LE), blinding, logger)
+//   -> Promise<{proof, publicSignals}>
+napi_value FullProveDevice(napi_env env, napi_callback_info info) {
+  size_t argc = 5;
+  napi_value argv[5];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  ProveWork* w = new ProveWork();
+  CHECK(napi_get_value_external(env, argv[0], reinterpret_cast<void**>(&w->c)));
+  CHECK(napi_get_value_external(env, argv[1], reinterpret_cast<void**>(&w->prog)));
+  void* d = nullptr;
+  CHECK(napi_get_buffer_info(env, argv[2], &d, &w->in_len));
+  w->in = static_cast<const uint8_t*>(d);
+  CHECK(napi_create_reference(env, argv[0], 1, &w->ctx_ref));
+  CHECK(napi_create_reference(env, argv[1], 1, &w->prog_ref));
+  CHECK(napi_create_reference(env, argv[2], 1, &w->in_ref));
+  return start_prove(env, w, argv, argc, 3);
 }
 
 napi_value Info(napi_env env, napi_callback_info info) {
@@ -617,6 +723,8 @@ napi_value Init(napi_env env, napi_value exports) {
       {"createContextFile", nullptr, CreateContextFile, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"createWitnessProgram", nullptr, CreateWitnessProgram, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"calculateWitness", nullptr, CalculateWitness, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"fullProveDevice", nullptr, FullProveDevice, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"setLanes", nullptr, SetLanes, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

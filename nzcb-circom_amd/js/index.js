@@ -46,9 +46,12 @@ function randomBlinding() {
 
 // One HBM-resident context per (zkey, device): the zkey is uploaded once. A file name is
 // memory-mapped by the library (nzcb_ctx_create_file), so zkeys of nzcp_live size
-// (~3.9 GB, beyond a Node Buffer) work; buffers are keyed by content.
+// (~3.9 GB, beyond a Node Buffer) work; buffers are keyed by content. A context has
+// `lanes` proof lanes (options.lanes, NZCB_LANES, default 5: bench.py's measured best):
+// concurrent prove / fullProve promises on it run on different lanes at the same time.
+const DEFAULT_LANES = Number(process.env.NZCB_LANES || 5);
 const contexts = new Map();
-function contextFor(zkey, device) {
+function contextFor(zkey, device, lanes) {
   let key;
   if (typeof zkey === 'string') {
     const st = fs.statSync(zkey);
@@ -59,7 +62,10 @@ function contextFor(zkey, device) {
   let ctx = contexts.get(key);
   if (!ctx) {
     ctx = typeof zkey === 'string' ? addon.createContextFile(zkey, device) : addon.createContext(readBin(zkey), device);
+    addon.setLanes(ctx, lanes || DEFAULT_LANES);
     contexts.set(key, ctx);
+  } else if (lanes) {
+    addon.setLanes(ctx, lanes);
   }
   return ctx;
 }
@@ -74,11 +80,15 @@ function loggerFn(logger) {
 async function prove(zkeyFileName, witnessFileName, logger, options) {
   options = options || {};
   const wtns = readBin(witnessFileName);
-  const ctx = contextFor(zkeyFileName, options.device || 0);
+  const ctx = contextFor(zkeyFileName, options.device || 0, options.lanes);
+  const res = await addon.prove(ctx, wtns, blindingFor(options), loggerFn(logger));
+  return { proof: JSON.parse(res.proof), publicSignals: JSON.parse(res.publicSignals) };
+}
+
+function blindingFor(options) {
   const blinding = options.blinding ? Buffer.from(options.blinding) : randomBlinding();
   if (blinding.length !== BLINDING_BYTES) throw new Error('blinding must be 11 x 32 bytes');
-  const res = await addon.prove(ctx, wtns, blinding, loggerFn(logger));
-  return { proof: JSON.parse(res.proof), publicSignals: JSON.parse(res.publicSignals) };
+  return blinding;
 }
 
 // ---------------------------------------------------------------------------
@@ -222,8 +232,8 @@ function programFor(progBuf, device) {
   return p;
 }
 
-async function wtnsCalculateGpu(input, progBuf, device) {
-  const { handle, meta } = programFor(progBuf, device);
+// the main's input object -> n_inputs x 32-byte LE values, by the program's input names
+function programInputBuffer(input, meta) {
   const vals = [];
   for (const [name, size] of meta.names) {
     if (!(name in input)) throw new Error(`Signal ${name} not found\n`);
@@ -241,6 +251,12 @@ async function wtnsCalculateGpu(input, progBuf, device) {
     if (v < BigInt(0)) v += R;
     for (let j = 0; j < 32; j++) { buf[32 * i + j] = Number(v & BigInt(255)); v >>= BigInt(8); }
   });
+  return buf;
+}
+
+async function wtnsCalculateGpu(input, progBuf, device) {
+  const { handle, meta } = programFor(progBuf, device);
+  const buf = programInputBuffer(input, meta);
   const wit = await addon.calculateWitness(handle, buf);
   const hdr = Buffer.alloc(12 + 12 + 4 + 32 + 4 + 12);
   let o = 0;
@@ -260,13 +276,21 @@ async function wtnsCalculateGpu(input, progBuf, device) {
 }
 
 // wasmFile: a circom 2.0.x witness .wasm (run on the host CPU, as snarkjs does) or a
-// witness program ("nzwp", run on the GPU)
+// witness program ("nzwp", run on the GPU). With a witness program the witness never
+// leaves HBM: the program writes it into a device buffer that the proof reads
+// (addon.fullProveDevice); only the input signals go up and the proof comes back.
 async function fullProve(input, wasmFile, zkeyFileName, logger, options) {
   options = options || {};
   const code = readBin(wasmFile);
-  const wtns = code.slice(0, 4).toString('latin1') === 'nzwp'
-    ? await wtnsCalculateGpu(input, code, options.device || 0)
-    : await wtnsCalculate(input, code);
+  const device = options.device || 0;
+  if (code.slice(0, 4).toString('latin1') === 'nzwp') {
+    const { handle, meta } = programFor(code, device);
+    const ctx = contextFor(zkeyFileName, device, options.lanes);
+    const res = await addon.fullProveDevice(ctx, handle, programInputBuffer(input, meta), blindingFor(options),
+      loggerFn(logger));
+    return { proof: JSON.parse(res.proof), publicSignals: JSON.parse(res.publicSignals) };
+  }
+  const wtns = await wtnsCalculate(input, code);
   return prove(zkeyFileName, { type: 'mem', data: wtns }, logger, options);
 }
 

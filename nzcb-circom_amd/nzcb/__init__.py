@@ -42,8 +42,8 @@ EXPORTED_SYMBOLS = [
     "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_from_zkey_file", "nzcb_vk_to_json", "nzcb_verify",
     "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_engine_lagrange_basis", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
-    "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d", "nzcb_msm_set_pair_rounds",
-    "nzcb_plonk_setup", "nzcb_prove_batch_status", "nzcb_wprog_remap",
+    "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d",
+    "nzcb_plonk_setup", "nzcb_prove_batch_status", "nzcb_wprog_remap", "nzcb_prove_logged",
 ]
 
 
@@ -107,6 +107,8 @@ def load(path: str | None = None):
         "nzcb_prove": (c_int, [c_void_p, u8p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
         "nzcb_prove_witness": (c_int, [c_void_p, u8p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
         "nzcb_prove_device": (c_int, [c_void_p, c_void_p, c_size_t, u8p, u8p, u8p, c_size_t, POINTER(_Err)]),
+        "nzcb_prove_logged": (c_int, [c_void_p, c_void_p, c_size_t, c_int, u8p, u8p, u8p, c_size_t, LOG_FN, c_void_p,
+                                      POINTER(_Err)]),
         "nzcb_ctx_kernel_stats": (c_int, [c_void_p, c_int, POINTER(c_double)]),
         "nzcb_ctx_set_lanes": (c_int, [c_void_p, c_int, POINTER(_Err)]),
         "nzcb_ctx_set_msm_devices": (c_int, [c_void_p, POINTER(c_int), c_int, POINTER(_Err)]),
@@ -152,7 +154,6 @@ def load(path: str | None = None):
                                          POINTER(c_double), POINTER(_Err)]),
         "nzcb_engine_msm_fixed_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_int, u8p,
                                               POINTER(_Err)]),
-        "nzcb_msm_set_pair_rounds": (c_int, [c_int]),
         "nzcb_plonk_setup": (c_int, [ctypes.c_char_p, c_size_t, ctypes.c_char_p, c_size_t, c_int, POINTER(POINTER(c_uint8)),
                                      POINTER(c_size_t), POINTER(_Err)]),
         "nzcb_nzcp_input_signals": (c_size_t, [POINTER(NzcpParams)]),
@@ -379,11 +380,6 @@ def memcpy_h2d_ptr(dst: int, src_addr: int, nbytes: int):
     rc = load().nzcb_memcpy_h2d(dst, src_addr, nbytes)
     if rc:
         raise NzcbError(rc, "h2d failed")
-
-
-def msm_set_pair_rounds(rounds: int):
-    """Force `rounds` batch-affine pairing rounds in fixed-base MSMs (< 0: automatic)."""
-    load().nzcb_msm_set_pair_rounds(int(rounds))
 
 
 def d2d(dst: int, src: int, nbytes: int):

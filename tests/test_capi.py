@@ -26,7 +26,7 @@ def test_product_header_excludes_internal_entry_points():
     product, internal = set(_declared()), set(_declared("nzcb_internal.h"))
     assert not product & internal
     assert not [s for s in product if s.startswith(("nzcb_engine_", "nzcb_synth_"))]
-    assert {"nzcb_msm_set_pair_rounds", "nzcb_ctx_kernel_stats", "nzcb_engine_msm_dev"} <= internal
+    assert {"nzcb_ctx_kernel_stats", "nzcb_engine_msm_dev"} <= internal
     assert {"nzcb_ctx_create_devices", "nzcb_prove_batch", "nzcb_msm_table_run", "nzcb_dev_alloc"} <= product
 
 

@@ -203,24 +203,14 @@ def test_msm_long_carry_runs(engine, fixed):
         assert got == want
 
 
-@pytest.fixture
-def pair_rounds():
-    """Force the fixed-base MSM's batch-affine pairing rounds (msm.hip msm_pair29_kernel),
-    which the automatic choice only enables for runs of >= 8 entries per bucket."""
-    import nzcb
-    yield nzcb.msm_set_pair_rounds
-    nzcb.msm_set_pair_rounds(-1)
-
-
-@pytest.mark.parametrize("rounds", [1, 2, 3, 6])
 @pytest.mark.parametrize("kind", ["rand", "equal", "mixed", "small"])
-def test_msm_fixed_base_pairing_rounds(engine, pair_rounds, rounds, kind):
-    """Pairing rounds on runs of every parity: equal scalars put a window's entries in one
-    bucket (long runs, odd tails), "small" scalars leave most windows zero (the infinity
-    entries of bucket 0 pair with each other and with finite points)."""
+def test_msm_fixed_base_digit_patterns(engine, kind):
+    """Bucket runs of every shape: equal scalars put a window's entries in one bucket (runs
+    spanning many accumulation chunks: the finalize's large list), "small" scalars leave
+    most windows zero (no entries), "mixed" has 0, 1, 2, r - 1 and random scalars."""
     n = 1500
-    rng = random.Random(rounds * 31 + len(kind))
-    pts = _bases(n, 900 + rounds)
+    rng = random.Random(31 + len(kind))
+    pts = _bases(n, 900 + len(kind))
     if kind == "rand":
         sc = [rng.randrange(R_MOD) for _ in range(n)]
     elif kind == "equal":
@@ -229,19 +219,17 @@ def test_msm_fixed_base_pairing_rounds(engine, pair_rounds, rounds, kind):
         sc = [rng.randrange(1 << 24) for _ in range(n)]
     else:
         sc = [rng.choice([0, 1, 2, R_MOD - 1, rng.randrange(R_MOD)]) for _ in range(n)]
-    pair_rounds(rounds)
     assert _msm_fixed(engine, pts, sc) == bn.msm(pts, sc)
 
 
-@pytest.mark.parametrize("rounds", [1, 2, 4])
-def test_msm_fixed_base_pairing_doublings_and_cancellations(engine, pair_rounds, rounds):
-    """Equal points in one bucket (the pair is a doubling), a point and its negation (the
-    pair is infinity), infinity bases, and sums that meet again in later rounds."""
+def test_msm_fixed_base_doublings_and_cancellations(engine):
+    """Equal points in one bucket (the accumulation doubles), a point and its negation (the
+    bucket sum is infinity), infinity bases, and equal partial sums meeting in the finalize
+    and the window sum's trees."""
     g = bn.g1_mul(bn.G1_GEN, 4321)
     h = bn.g1_mul(bn.G1_GEN, 99)
     pts = [g, g, bn.g1_neg(g), g, None, g, h, h, bn.g1_neg(h), None, g, g, g, g, h, bn.g1_neg(g)]
     sc = [5, 5, 5, 5, 5, R_MOD - 5, 5, 5, 5, 7, 5, 5, 5, 5, R_MOD - 5, 5]
-    pair_rounds(rounds)
     assert _msm_fixed(engine, pts, sc) == bn.msm(pts, sc)
 
 

@@ -92,7 +92,7 @@ const lines = [];
 (async () => {{
   const bl = Buffer.from('{exp['blinding']}', 'hex');
   const r = await m.plonk.prove('{GOLD}/p8.zkey', '{GOLD}/p8.wtns', {{debug: (s) => lines.push(s)}}, {{blinding: bl}});
-  // two concurrent proofs on the same (cached) context are serialized by the library
+  // two concurrent proofs on the same (cached) context run on two of its lanes
   const [a, b] = await Promise.all([
     m.plonk.prove('{GOLD}/p8.zkey', '{GOLD}/p8.wtns', null, {{blinding: bl}}),
     m.plonk.prove({{type: 'mem', data: require('fs').readFileSync('{GOLD}/p8.zkey')}}, '{GOLD}/p8.wtns', null, {{blinding: bl}})]);
@@ -265,6 +265,47 @@ const m = require('./');
     assert d["a"]["proof"] == d["g"]["proof"]
     assert d["ok"] is True
     assert d["err"].startswith("Signal b not found")
+
+
+@needs_node
+@pytest.mark.gpu
+def test_node_concurrent_full_prove_matches_sequential(tmp_path):
+    """concurrent plonk.fullProve promises on one context feed its lanes
+    (nzcb_prove_logged per call, no per-context lock) and keep the witness in HBM
+    (fullProveDevice). 8 concurrent calls with fixed blinding, over 3 lanes (so calls wait
+    for a lane), give the same proofs as the same 8 calls made one after another; each call's
+    logger sees only its own proof's lines."""
+    import nzcb
+    import wasm_tiny
+    r1cs, prog = wasm_tiny.mul_circuit()
+    zkey = nzcb.plonk_setup(r1cs, nzcb.ptau_synth(4, 0x1234567))
+    (tmp_path / "mul.zkey").write_bytes(zkey)
+    (tmp_path / "mul.wprog").write_bytes(prog)
+    bl = b"".join((7 * i + 3 + (i << 200)).to_bytes(32, "little") for i in range(11)).hex()
+    script = f"""
+const m = require('./');
+(async () => {{
+  const bl = Buffer.from('{bl}', 'hex');
+  const z = '{tmp_path}/mul.zkey', p = '{tmp_path}/mul.wprog';
+  const opts = {{blinding: bl, lanes: 3}};
+  const seq = [];
+  for (let a = 2; a < 10; a++) seq.push(await m.plonk.fullProve({{a, b: 11}}, p, z, null, opts));
+  const logs = [];
+  const con = await Promise.all([...Array(8).keys()].map((i) => {{
+    const lines = [];
+    logs.push(lines);
+    return m.plonk.fullProve({{a: i + 2, b: 11}}, p, z, {{debug: (s) => lines.push(s)}}, opts);
+  }}));
+  const vk = await m.zKey.exportVerificationKey(z);
+  const ok = await Promise.all(con.map((r) => m.plonk.verify(vk, r.publicSignals, r.proof)));
+  console.log(JSON.stringify({{seq, con, ok, logs: logs.map((l) => l.filter((x) => x === 'multiexp A').length)}}));
+}})().catch((e) => {{ console.error(e); process.exit(1); }});
+"""
+    d = json.loads(run_node(script))
+    assert d["seq"] == d["con"]
+    assert [r["publicSignals"] for r in d["con"]] == [[str(11 * a)] for a in range(2, 10)]
+    assert all(d["ok"])
+    assert d["logs"] == [1] * 8
 
 
 @needs_node
