@@ -323,6 +323,9 @@ void nzcb_dev_free(void* p);
 int nzcb_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int nzcb_memcpy_d2h(void* dst, const void* src, size_t bytes);
 int nzcb_memcpy_d2d(void* dst, const void* src, size_t bytes);
+/* The same ordered on a HIP stream (no host wait): work enqueued on `stream` afterwards
+ * sees the copy (nzcb/msmsplit.py: scalars into the scatter rows on torch's stream). */
+int nzcb_memcpy_d2d_async(void* dst, const void* src, size_t bytes, void* stream);
 
 /* ---- Serving side of nzcb_ctx_set_msm_split (one per serving rank) ---------------- */
 /* A resident fixed-base MSM table over n device bases (affine LEM, e.g. a PTau range),

@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_from_zkey_file", "nzcb_vk_to_json", "nzcb_verify",
     "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_engine_lagrange_basis", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d",
-    "nzcb_plonk_setup", "nzcb_prove_batch_status", "nzcb_wprog_remap", "nzcb_prove_logged",
+    "nzcb_plonk_setup", "nzcb_prove_batch_status", "nzcb_wprog_remap", "nzcb_prove_logged", "nzcb_memcpy_d2d_async",
 ]
 
 
@@ -143,6 +143,7 @@ def load(path: str | None = None):
         "nzcb_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_size_t]),
         "nzcb_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_size_t]),
         "nzcb_memcpy_d2d": (c_int, [c_void_p, c_void_p, c_size_t]),
+        "nzcb_memcpy_d2d_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
         "nzcb_engine_ntt_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, POINTER(_Err)]),
         "nzcb_engine_msm_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, u8p, POINTER(_Err)]),
         "nzcb_engine_time_ntt": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, POINTER(c_double),
@@ -385,6 +386,12 @@ def memcpy_h2d_ptr(dst: int, src_addr: int, nbytes: int):
 def d2d(dst: int, src: int, nbytes: int):
     if load().nzcb_memcpy_d2d(dst, src, nbytes) != 0:
         raise NzcbError(10, "hipMemcpy D2D failed")
+
+
+def d2d_async(dst: int, src: int, nbytes: int, stream: int):
+    """Device copy ordered on HIP stream `stream` (no host wait)."""
+    if load().nzcb_memcpy_d2d_async(dst, src, nbytes, stream) != 0:
+        raise NzcbError(10, "hipMemcpyAsync D2D failed")
 
 
 def d2h(src: int, nbytes: int) -> bytes:

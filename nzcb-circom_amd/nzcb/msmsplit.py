@@ -81,14 +81,17 @@ class Comm:
         self.dist.broadcast(t, 0)
         return tuple(int(x) for x in t.cpu().tolist())   # .cpu() waits for the broadcast
 
+    def stream(self) -> int:
+        """torch's current HIP stream (the one collectives are ordered after), 0 on CPU."""
+        return self.torch.cuda.current_stream().cuda_stream if self.device.startswith("cuda") else 0
+
     def scatter_rows(self, rows, out):
         """rows: rank 0's [world, row_bytes] tensor (None elsewhere); out: this rank's row.
-        Returns the collective's work handle (wait on it before rows are rewritten)."""
-        work = self.dist.scatter(out, list(rows.unbind(0)) if rows is not None else None, src=0,
-                                 async_op=True)
-        if not self.device.startswith("cuda"):   # gloo: complete in submission order
-            work.wait()
-        return work
+        Asynchronous on every backend: returns the collective's work handle, which rank 0
+        waits on before it rewrites the rows (the slot's next send) and a serving rank before
+        its GPU reads `out`. On RCCL the scatter is ordered after the work already on torch's
+        current stream, the row copies included (SplitRoot._device_copy)."""
+        return self.dist.scatter(out, list(rows.unbind(0)) if rows is not None else None, src=0, async_op=True)
 
     def gather64(self, own: bytes) -> bytes | None:
         """Every rank's 64-byte partial to rank 0 (None on the other ranks)."""
@@ -124,7 +127,10 @@ class SplitRoot:
     def _device_copy(self, src, lo: int, cnt: int, row):
         import nzcb
         if self.comm.device.startswith("cuda"):
-            nzcb.d2d(row.data_ptr(), src + 32 * lo, 32 * cnt)
+            # ordered on torch's current stream, which the scatter issued next waits for: the
+            # rows are complete when RCCL reads them, with no host wait (the prover's scalars
+            # at `src` are final: csrc/prover.hip commit_start synchronizes their event first)
+            nzcb.d2d_async(row.data_ptr(), src + 32 * lo, 32 * cnt, self.comm.stream())
         else:
             row[:32 * cnt].copy_(self.comm.torch.frombuffer(bytearray(nzcb.d2h(src + 32 * lo, 32 * cnt)),
                                                             dtype=self.comm.torch.uint8))
@@ -135,8 +141,8 @@ class SplitRoot:
             rows = self.comm.torch.empty((self.comm.world, max(self.row, 1)), dtype=self.comm.torch.uint8,
                                          device=self.comm.device)
         elif work is not None:   # the slot's previous scatter must have read its rows
-            work.wait()
-            self.comm.sync()
+            work.wait()         # RCCL: torch's stream waits for it; gloo: the host does
+            self.comm.sync()    # and the host waits for torch's stream before refilling
         # fill first: if the source fails, no header is out and the servers stay in step
         for r, ((lo, _), cnt) in enumerate(zip(self.ranges, slice_counts(count, self.ranges))):
             if r and cnt:
@@ -182,8 +188,8 @@ def serve(comm: Comm, partial, n_points: int) -> int:
             return served
         if kind == HDR_SCALARS:
             t = comm.empty(row)
-            comm.scatter_rows(None, t).wait()
-            comm.sync()   # the backend reads the slice on its own stream
+            comm.scatter_rows(None, t).wait()   # the slice has arrived (RCCL: on torch's stream) ...
+            comm.sync()   # ... and the host waits for that stream: the backend reads t on its own
             parts[slot] = partial(slot, t, slice_counts(count, ranges)[comm.rank])
             served += 1
         elif kind == HDR_GATHER:

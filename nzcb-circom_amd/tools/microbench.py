@@ -18,7 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--min-log", type=int, default=18)
     ap.add_argument("--max-log", type=int, default=24)
-    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=10)
     args = ap.parse_args()
     nmax = 1 << args.max_log
     eng = nzcb.Engine(0, max_log_ntt=args.max_log, max_msm_points=nmax)
@@ -39,8 +39,10 @@ def main():
             ph = eng.time_msm_phases(bases, sc, n, True, fixed, args.reps)
             ms = ph["wall"]
             gbs = 96 * n / (ms / 1e3) / 1e9
+            phases = {k: round(v, 4) for k, v in ph.items() if k not in ("wall", "entries", "table_build")}
             print(json.dumps({"kernel": "msm_fixed_base" if fixed else "msm", "log_n": lg, "ms": round(ms, 4),
-                              "phases_ms": {k: round(v, 4) for k, v in ph.items() if k not in ("wall", "entries")}, "entries": int(ph.get("entries", 0)),
+                              "phases_ms": phases, "phase_sum_ms": round(sum(phases.values()), 4),
+                              "table_build_ms": round(ph.get("table_build", 0), 2), "entries": int(ph.get("entries", 0)),
                               "points_per_s": round(n / (ms / 1e3), 1), "GBs": round(gbs, 1),
                               "frac": round(gbs / PEAK, 5)}), flush=True)
     for p in (sc, out, bases):

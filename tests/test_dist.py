@@ -155,6 +155,80 @@ def _split_worker(rank, world, port, n, jobs, fail, out):
     dist.destroy_process_group()
 
 
+def _split_order_worker(rank, world, port, n, jobs, out):
+    """Back-to-back commitments on ONE slot with a slow scalar source: every scatter is
+    asynchronous (msmsplit.Comm.scatter_rows), so rank 0's next send must wait for the
+    slot's previous scatter before it refills the rows, and a serving rank must wait for
+    its slice before reading it; a send that skipped either wait would fold stale or torn
+    scalars into the partials."""
+    import time
+    import torch.distributed as dist
+    from nzcb import msmsplit
+    from oracle import cbind
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    comm = msmsplit.Comm(dist, "cpu")
+    pts = _split_points(n)
+    ranges = msmsplit.point_ranges(n, world)
+    lo, _ = ranges[rank]
+
+    def cpu_partial(own_slice: bytes, cnt):
+        return cbind.msm(b"".join(pts[lo:lo + cnt]), own_slice[:32 * cnt], threads=1) if cnt else bytes(64)
+
+    if rank == 0:
+        def slow_source(src, first, cnt, row):
+            import torch
+            time.sleep(0.05)   # a slow producer of the scalars (a long device copy)
+            row[:32 * cnt].copy_(torch.frombuffer(bytearray(src[32 * first:32 * (first + cnt)]), dtype=torch.uint8))
+
+        with msmsplit.SplitRoot(comm, n, scalar_source=slow_source) as root:
+            folded = []
+            for sc in jobs:                      # the same slot again and again, no gather between
+                root.send(0, sc, len(sc) // 32)
+                folded.append(root.gather(0, cpu_partial(sc, msmsplit.slice_counts(len(sc) // 32, ranges)[0])))
+            # two sends on one slot before any gather: the second waits for the first scatter
+            root.send(1, jobs[0], len(jobs[0]) // 32)
+            root.send(1, jobs[1], len(jobs[1]) // 32)
+            folded.append(root.gather(1, cpu_partial(jobs[1], msmsplit.slice_counts(len(jobs[1]) // 32,
+                                                                                     ranges)[0])))
+        out[0] = folded
+    else:
+        def slow_partial(slot, t, cnt):
+            time.sleep(0.02)
+            return cpu_partial(bytes(t.tolist()), cnt)
+        out[rank] = msmsplit.serve(comm, slow_partial, n)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_msm_split_async_scatter_ordering_gloo():
+    """the split's scatters are asynchronous on every backend; the waits
+    that order them (rank 0 before refilling a slot's rows, serving ranks before reading a
+    slice) keep every folded commitment equal to the unsplit MSM under a slow source."""
+    import random
+    from oracle import bn254 as bn
+    from oracle import cbind
+    n, world = 70, 2
+    rng = random.Random(77)
+    jobs = [b"".join(bn.to_lem(rng.randrange(bn.R_MOD), bn.R_MOD) for _ in range(k)) for k in (66, 70, 40, 66)]
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_split_order_worker, args=(world, _free_port(), n, jobs, out), nprocs=world, join=True)
+        res = dict(out)
+    pts = _split_points(n)
+    want_jobs = jobs + [jobs[1]]
+    assert res[1] == len(jobs) + 2   # the serving rank answered every send, the overwritten one included
+    assert len(res[0]) == len(want_jobs)
+    for sc, parts in zip(want_jobs, res[0]):
+        count = len(sc) // 32
+        acc = None
+        for r in range(world):
+            p = parts[64 * r:64 * r + 64]
+            x, y = bn.from_le(p[:32]), bn.from_le(p[32:])
+            acc = bn.g1_add(acc, None if x == 0 and y == 0 else (x, y))
+        want = cbind.msm(b"".join(pts[:count]), sc, threads=1)
+        assert acc == (bn.from_le(want[:32]), bn.from_le(want[32:]))
+
+
 @pytest.mark.parametrize("world,fail", [(2, False), (3, False), (2, True)])
 def test_msm_split_across_ranks_gloo(world, fail):
     """Every commitment's folded partials equal the unsplit MSM (C port), for MSM lengths
