@@ -63,7 +63,7 @@ int nzcb_engine_lagrange_basis(nzcb_engine* e, const void* dev_ptau, size_t ptau
 int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont, int reps,
                          double* ms, double* acc_ms, nzcb_err* err);
 /* Fixed-base schedule (the prover's): builds the shifted-base table of the first
- * n_table bases (c = 20 by default: 2^(20w) multiples, 13 rows), then runs the MSM of the first n.
+ * n_table bases (c = 17 by default: 2^(17w) multiples, 15 rows), then runs the MSM of the first n.
  * One-shot (table and scratch freed on return); for parity tests. */
 int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
                               int scalars_mont, uint8_t* out_affine, nzcb_err* err);

@@ -21,8 +21,8 @@ struct MsmBaseTable {
   void build(const G1Affine* bases, size_t n, int c, hipStream_t st, bool fold_mont = false);
 };
 
-// Window size of the table-based (fixed-base) MSM: 20 bits by default (13 table rows,
-// 2^19 buckets); NZCB_FB_WINDOW = 16..20 overrides it.
+// Window size of the table-based (fixed-base) MSM: 17 bits by default (15 table rows,
+// 2^16 buckets); NZCB_FB_WINDOW = 16..20 overrides it.
 int fixed_base_window();
 // Window of the Lagrange-basis table (A, B, C commitments of small witness values: 17):
 // their few entries do not pay for a larger bucket set.

@@ -82,9 +82,11 @@ static constexpr int kLargePieceBlocks = 128;
 static constexpr int kLargeFinalBlocks = 128;
 static constexpr int kLargeFinalThreads = 64;
 
-// Fixed-base window of the PTau tables: c = 20 bits (13 table rows, 2^19 buckets, 13
-// entries per random scalar); NZCB_FB_WINDOW = 16..20 overrides it for A/B runs.
-static constexpr int kFbWindow = 20;
+// Fixed-base window of the PTau tables: c = 17 bits (15 table rows, 2^16 buckets, 15
+// entries per random scalar). c = 20 (13 rows, 2^19 buckets) accumulates 9 % faster but its
+// bucketing and window sum cost more than that (profiles/r4_window_ab.txt);
+// NZCB_FB_WINDOW = 16..20 selects another for A/B runs.
+static constexpr int kFbWindow = 17;
 int fixed_base_window() {
   static const int c = [] {
     const char* e = std::getenv("NZCB_FB_WINDOW");

@@ -2,6 +2,7 @@
 
 Bit-exact: every output is a unique field / affine-curve element.
 """
+import os
 import random
 
 import pytest
@@ -289,3 +290,17 @@ def test_lagrange_basis_vs_oracle(engine, log_n):
     got = [bn.g1_from_lem(out[64 * k:64 * k + 64]) for k in range(n + 2)]
     assert got == want
 
+
+
+@pytest.mark.parametrize("window", ["16", "19", "20"])
+def test_msm_fixed_base_other_windows(window):
+    """The fixed-base tests above under the windows NZCB_FB_WINDOW selects besides the default
+    c = 17 (c = 19, 20: 2^18 / 2^19 buckets, the tile and line kernels' larger grids; a fresh
+    process, the switch is read once)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, NZCB_FB_WINDOW=window)
+    p = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", "-m", "gpu",
+                        os.path.abspath(__file__), "-k", "fixed_base and not other_windows"],
+                       capture_output=True, text=True, timeout=110, env=env)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
