@@ -67,9 +67,11 @@ int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars,
  * One-shot (table and scratch freed on return); for parity tests. */
 int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
                               int scalars_mont, uint8_t* out_affine, nzcb_err* err);
-/* Per-phase MSM timing (HIP events, average over reps after one warm-up):
+/* Per-phase MSM timing (HIP events, average over reps after three warm-up runs):
  * out[0] wall ms, out[1..7] keys, sort, offsets, accumulate, finalize, reduce, sums,
- * out[8] table build ms (fixed_base only), out[9] bucket entries per MSM (nonzero digits). */
+ * out[8] table build ms (fixed_base only), out[9] bucket entries per MSM (nonzero digits),
+ * out[10] host ms per MSM from the device results' arrival to the affine result (the
+ * window combination on the CPU: the Horner over the window slots). out holds 11 doubles. */
 int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
                           int fixed_base, int reps, double* out, nzcb_err* err);
 /* Field self-test helpers: out[i] = a[i] * b[i] (Montgomery, device), n elements. */

@@ -302,6 +302,7 @@ int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars
   sc->prof_launches = 0;
   sc->prof_entries = 0;
   for (double& x : sc->phase_ms) x = 0;
+  sc->host_ms = 0;
   auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < reps; i++)
     (void)msm(*sc, (const G1Affine*)bases, (const Fr*)scalars, n, scalars_mont != 0, g.stream, t.get());
@@ -310,6 +311,7 @@ int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars
   for (int i = 0; i < 7; i++) out[1 + i] = sc->phase_ms[i] / r;
   out[8] = table_ms;
   out[9] = (double)sc->prof_entries / r;
+  out[10] = sc->host_ms / r;
   sc->prof = sc->prof_phases = false;
   return 0;
   NZ_GUARD_END(err)

@@ -236,6 +236,13 @@ void nzcb_ctx_set_transcript_public(nzcb_ctx* ctx, int on) {
 int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err) {
   if (!ctx || lanes < 1 || lanes > 16) return fail(err, NZCB_ERR_ARG, "lanes must be in 1..16");
   try {
+    {  // unchanged: no exclusive lock, which would wait for every proof in flight
+      std::shared_lock<std::shared_mutex> lk(ctx->cfg);
+      if (ctx->lanes() == (size_t)lanes) {
+        if (err) err->code = 0;
+        return 0;
+      }
+    }
     std::unique_lock<std::shared_mutex> lk(ctx->cfg);
     while (ctx->lanes() > (size_t)lanes) {
       ctx->extra.pop_back();

@@ -66,6 +66,7 @@ struct MsmScratch {
   bool prof = false, prof_phases = false;
   double prof_ms = 0;
   double phase_ms[7] = {0, 0, 0, 0, 0, 0, 0};
+  double host_ms = 0;  // msm_finish's CPU part (prof_phases)
   uint64_t prof_launches = 0, prof_points = 0, prof_entries = 0;
   hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipEvent_t done = nullptr;  // recorded after the window sums' copy to host_win (msm_finish waits on it)

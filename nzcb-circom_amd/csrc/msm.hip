@@ -30,8 +30,9 @@
 
 #include "f29.h"
 
-#include <type_traits>
+#include <chrono>
 #include <cstdlib>
+#include <type_traits>
 #include <rocprim/rocprim.hpp>
 
 namespace nzcb {
@@ -1517,6 +1518,15 @@ G1xyzz msm_finish(MsmScratch& sc, hipStream_t st) {
       }
     }
   }
+  const auto t_host = std::chrono::steady_clock::now();
+  struct HostClock {  // the CPU part below, for the phase timing (nzcb_engine_time_msm2)
+    MsmScratch& sc;
+    std::chrono::steady_clock::time_point t0;
+    ~HostClock() {
+      if (sc.prof && sc.prof_phases)
+        sc.host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+  } host_clock{sc, t_host};
   if (sc.cur_fixed) {  // W = 2^a sum_b 2^b R_b + sum_b 2^b C_b + C (msm_slots29_kernel)
     const int hb = sc.cur_hb, a = sc.cur_a;
     const G1xyzz* s = sc.host_win;

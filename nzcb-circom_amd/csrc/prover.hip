@@ -130,11 +130,13 @@ static F29 fr29_operand(Fr c) {
 // 32-lane half for kPer = 2 and 4 (ds_read_b32 / ds_write_b32 bank by (a / 4) mod 32).
 // The chunk-per-thread scans these replace (kScanChunk = 32 elements per thread read
 // straight from HBM, 1 KB apart per lane) ran at 0.06-0.3 of the HBM rate.
+// kPer = 4 (175 VGPRs, no scratch, 2 waves per SIMD) against 2 (132 VGPRs, 48 B of scratch
+// in k_perm_tile): bench +0.9 % on one box (profiles/r4_window_ab.txt); -DNZ_KPER=2 for A/B
 #ifndef NZ_KPER
-#define NZ_KPER 2
+#define NZ_KPER 4
 #endif
-static constexpr int kPer = NZ_KPER;  // elements per thread in the tile scans (A/B: -DNZ_KPER=4)
-static constexpr int kTileN = kT * kPer;                // 1024
+static constexpr int kPer = NZ_KPER;  // elements per thread in the tile scans
+static constexpr int kTileN = kT * kPer;                // 2048
 static constexpr int kStageWords = kTileN * 8 + kTileN / 4;
 
 __device__ __forceinline__ int stage_word(int e) { return e * 8 + e / 4; }

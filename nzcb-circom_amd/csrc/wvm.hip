@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -725,6 +726,22 @@ __global__ void __launch_bounds__(NT) wvm_kernel(Prog P, const Fr* __restrict__ 
   }
 }
 
+// per-run buffers: concurrent runs of one program (the N-API addon's fullProve promises,
+// each on its own thread) take a slot each, so they overlap on the GPU instead of taking
+// turns; a slot's stream runs the launch when the caller passes none
+struct RunSlot {
+  DevBuf<uint32_t> status;
+  size_t status_cap = 0;
+  DevBuf<Fr> scratch;  // remapped programs: the program's own wire order
+  size_t scratch_cap = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t after_null = nullptr;  // orders the slot's stream after the null stream's work
+  ~RunSlot() {
+    if (after_null) (void)hipEventDestroy(after_null);
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
 struct Program {
   int device = 0;
   uint32_t n_wires = 0, n_out = 0, n_pub = 0, n_prv = 0, n_levels = 0;
@@ -732,15 +749,30 @@ struct Program {
   DevBuf<DTerm> terms;
   DevBuf<Op> ops;
   DevBuf<Level> levels;
-  DevBuf<uint32_t> status;
-  size_t status_cap = 0;
   // wire map of a remapped program (nzcb_wprog_remap): output wire t = program wire
-  // wmap[t]; the program runs into `scratch` and a gather writes the target order
+  // wmap[t]; the program runs into a slot's scratch and a gather writes the target order
   uint32_t n_target = 0;
   DevBuf<uint32_t> wmap;
-  DevBuf<Fr> scratch;
-  size_t scratch_cap = 0;
+  std::mutex slot_mu;
+  std::vector<std::unique_ptr<RunSlot>> slots;
+  std::vector<RunSlot*> idle;
   uint32_t out_wires() const { return n_target ? n_target : n_wires; }
+  RunSlot* acquire() {
+    std::lock_guard<std::mutex> lk(slot_mu);
+    if (idle.empty()) {
+      slots.emplace_back(new RunSlot());
+      NZ_HIP(hipStreamCreateWithFlags(&slots.back()->st, hipStreamNonBlocking));
+      NZ_HIP(hipEventCreateWithFlags(&slots.back()->after_null, hipEventDisableTiming));
+      return slots.back().get();
+    }
+    RunSlot* r = idle.back();
+    idle.pop_back();
+    return r;
+  }
+  void release(RunSlot* r) {
+    std::lock_guard<std::mutex> lk(slot_mu);
+    idle.push_back(r);
+  }
 };
 
 // witness i, target wire t = scratch witness i, program wire map[t]
@@ -941,19 +973,30 @@ void run(Program* P, const void* dev_inputs, int count, void* dev_witness, size_
   if (stride_bytes % 32 || stride_bytes < (size_t)P->out_wires() * 32)
     throw Error(NZCB_ERR_ARG, "witness program: witness stride below n_wires x 32 B");
   NZ_HIP(hipSetDevice(P->device));
+  RunSlot* R = P->acquire();
+  struct Release {
+    Program* P;
+    RunSlot* R;
+    ~Release() { P->release(R); }
+  } release{P, R};
+  if (!s) {  // no stream given: the slot's, after whatever the caller queued on the null stream
+    NZ_HIP(hipEventRecord(R->after_null, nullptr));
+    NZ_HIP(hipStreamWaitEvent(R->st, R->after_null, 0));
+    s = R->st;
+  }
   Fr* run_dst = (Fr*)dev_witness;
   size_t run_stride = stride_bytes / 32;
   if (P->n_target) {  // remapped: the program's own wire order into scratch, then the gather
-    if ((size_t)count > P->scratch_cap) {
-      P->scratch.alloc((size_t)count * P->n_wires);
-      P->scratch_cap = (size_t)count;
+    if ((size_t)count > R->scratch_cap) {
+      R->scratch.alloc((size_t)count * P->n_wires);
+      R->scratch_cap = (size_t)count;
     }
-    run_dst = P->scratch.p;
+    run_dst = R->scratch.p;
     run_stride = P->n_wires;
   }
-  if ((size_t)count > P->status_cap) {
-    P->status.alloc((size_t)count);
-    P->status_cap = (size_t)count;
+  if ((size_t)count > R->status_cap) {
+    R->status.alloc((size_t)count);
+    R->status_cap = (size_t)count;
   }
   Prog g;
   g.consts = P->consts.p;
@@ -981,7 +1024,7 @@ void run(Program* P, const void* dev_inputs, int count, void* dev_witness, size_
   }();
   auto kern = nt == 256 ? wvm_kernel<256> : (nt == 1024 ? wvm_kernel<1024> : wvm_kernel<512>);
   hipLaunchKernelGGL(kern, dim3((unsigned)count), dim3(nt), 0, s, g, (const Fr*)dev_inputs, run_dst, run_stride,
-                     P->status.p, lclk.p);
+                     R->status.p, lclk.p);
   NZ_HIP(hipGetLastError());
   if (P->n_target) {
     const unsigned gx = (unsigned)std::min<size_t>(((size_t)P->n_target + 255) / 256, 1024);
@@ -990,7 +1033,7 @@ void run(Program* P, const void* dev_inputs, int count, void* dev_witness, size_
     NZ_HIP(hipGetLastError());
   }
   std::vector<uint32_t> st((size_t)count);
-  NZ_HIP(hipMemcpyAsync(st.data(), P->status.p, (size_t)count * 4, hipMemcpyDeviceToHost, s));
+  NZ_HIP(hipMemcpyAsync(st.data(), R->status.p, (size_t)count * 4, hipMemcpyDeviceToHost, s));
   NZ_HIP(hipStreamSynchronize(s));
   if (lclk.p) {
     std::vector<uint64_t> h(((size_t)P->n_levels + 1) * kClockSlots, 0);
@@ -1009,10 +1052,7 @@ void run(Program* P, const void* dev_inputs, int count, void* dev_witness, size_
 using namespace nzcb;
 
 struct nzcb_wprog {
-  wvm::Program* p;
-  // runs share the program's status / scratch buffers: concurrent callers (the N-API
-  // addon's in-flight fullProve promises) take turns; one run of a batch is one launch
-  std::mutex mu;
+  wvm::Program* p;  // concurrent runs take a RunSlot each (no lock around a run)
 };
 
 extern "C" {
@@ -1058,7 +1098,6 @@ int nzcb_wprog_run_dev(nzcb_wprog* h, const void* dev_inputs, int count, void* d
                        int32_t* status_out, void* stream, nzcb_err* err) {
   try {
     if (!h) throw Error(NZCB_ERR_ARG, "witness program: null handle");
-    std::lock_guard<std::mutex> lk(h->mu);
     wvm::run(h->p, dev_inputs, count, dev_witness, witness_stride, status_out, (hipStream_t)stream);
     return NZCB_OK;
   } catch (const Error& e) {
@@ -1081,7 +1120,6 @@ int nzcb_wprog_run(nzcb_wprog* h, const uint8_t* inputs, int count, uint8_t* wit
     const size_t nw = (size_t)h->p->out_wires() * 32;
     DevBuf<uint8_t> din(nin ? nin : 1), dw(nw * count);
     if (nin) NZ_HIP(hipMemcpy(din.p, inputs, nin, hipMemcpyHostToDevice));
-    std::lock_guard<std::mutex> lk(h->mu);
     wvm::run(h->p, din.p, count, dw.p, nw, status_out, nullptr);
     NZ_HIP(hipMemcpy(witness_out, dw.p, nw * count, hipMemcpyDeviceToHost));
     return NZCB_OK;

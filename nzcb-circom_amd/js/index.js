@@ -21,10 +21,13 @@ const addon = require(path.join(__dirname, 'build', 'nzcb.node'));
 const R = BigInt('21888242871839275222246405745257275088548364400416034343698204186575808495617');
 const BLINDING_BYTES = 11 * 32;
 
+// File arguments: a path, {type: "mem", data}, or a Buffer / Uint8Array (used in place,
+// not copied)
 function readBin(x) {
   if (typeof x === 'string') return fs.readFileSync(x);
-  if (x && x.type === 'mem') return Buffer.from(x.data);
-  if (x instanceof Uint8Array) return Buffer.from(x);
+  if (x && x.type === 'mem') return Array.isArray(x.data) ? Buffer.from(x.data) : readBin(x.data);
+  if (Buffer.isBuffer(x)) return x;
+  if (x instanceof Uint8Array) return Buffer.from(x.buffer, x.byteOffset, x.byteLength);
   throw new Error('expected a file name, a buffer or {type: "mem", data}');
 }
 
@@ -51,23 +54,30 @@ function randomBlinding() {
 // concurrent prove / fullProve promises on it run on different lanes at the same time.
 const DEFAULT_LANES = Number(process.env.NZCB_LANES || 5);
 const contexts = new Map();
+const zkeyHashes = new WeakMap();  // zkey Buffer -> content hash (hashed once per Buffer)
 function contextFor(zkey, device, lanes) {
   let key;
   if (typeof zkey === 'string') {
     const st = fs.statSync(zkey);
     key = `file:${path.resolve(zkey)}:${st.size}:${st.mtimeMs}:${device}`;
   } else {
-    key = crypto.createHash('sha256').update(readBin(zkey)).digest('hex') + ':' + device;
+    const buf = readBin(zkey);
+    let h = zkeyHashes.get(buf);
+    if (!h) zkeyHashes.set(buf, (h = crypto.createHash('sha256').update(buf).digest('hex')));
+    key = h + ':' + device;
   }
-  let ctx = contexts.get(key);
-  if (!ctx) {
-    ctx = typeof zkey === 'string' ? addon.createContextFile(zkey, device) : addon.createContext(readBin(zkey), device);
-    addon.setLanes(ctx, lanes || DEFAULT_LANES);
-    contexts.set(key, ctx);
-  } else if (lanes) {
-    addon.setLanes(ctx, lanes);
+  let c = contexts.get(key);
+  if (!c) {
+    c = { ctx: typeof zkey === 'string' ? addon.createContextFile(zkey, device) : addon.createContext(readBin(zkey), device),
+          lanes: lanes || DEFAULT_LANES };
+    addon.setLanes(c.ctx, c.lanes);
+    contexts.set(key, c);
+  } else if (lanes && lanes !== c.lanes) {
+    // a change of lane count waits for the proofs in flight (it rebuilds the lane pool)
+    addon.setLanes(c.ctx, lanes);
+    c.lanes = lanes;
   }
-  return ctx;
+  return c.ctx;
 }
 
 function loggerFn(logger) {
@@ -221,15 +231,50 @@ function remapProgram(program, ownSym, targetSym) {
   return addon.remapWitnessProgram(readBin(program), readBin(ownSym), readBin(targetSym));
 }
 
+// fullProve's program argument: a path is read again only when its size or mtime changes (a
+// server passes the same path on every call)
+const programFiles = new Map();
+function readProgram(x) {
+  if (typeof x !== 'string') return readBin(x);
+  const st = fs.statSync(x);
+  const f = programFiles.get(x);
+  if (f && f.size === st.size && f.mtimeMs === st.mtimeMs) return f.buf;
+  const buf = fs.readFileSync(x);
+  programFiles.set(x, { size: st.size, mtimeMs: st.mtimeMs, buf });
+  return buf;
+}
+
+// loaded programs by content hash; a Buffer seen before skips the hash (a program of
+// nzcp_live's size takes tens of ms to hash: per call, that was the Node path's bottleneck)
 const programs = new Map();
+const programsByBuf = new WeakMap();
 function programFor(progBuf, device) {
+  let byDev = programsByBuf.get(progBuf);
+  if (byDev && byDev.has(device)) return byDev.get(device);
   const key = crypto.createHash('sha256').update(progBuf).digest('hex') + ':' + device;
   let p = programs.get(key);
   if (!p) {
     p = { handle: addon.createWitnessProgram(progBuf, device), meta: programInputs(progBuf) };
     programs.set(key, p);
   }
+  if (!byDev) programsByBuf.set(progBuf, (byDev = new Map()));
+  byDev.set(device, p);
   return p;
+}
+
+// one signal value -> 32-byte LE at buf[off] (buf zero-filled): small non-negative numbers
+// directly, everything else reduced mod r and written as four 64-bit words
+const M64 = (BigInt(1) << BigInt(64)) - BigInt(1);
+const B64 = BigInt(64);
+function putSignal(buf, off, x) {
+  if (typeof x === 'number' && Number.isSafeInteger(x) && x >= 0) {
+    buf.writeUIntLE(x % 0x1000000000000, off, 6);
+    if (x >= 0x1000000000000) buf.writeUInt16LE(Math.floor(x / 0x1000000000000), off + 6);
+    return;
+  }
+  let v = BigInt(x) % R;
+  if (v < BigInt(0)) v += R;
+  for (let j = 0; j < 4; j++) { buf.writeBigUInt64LE(v & M64, off + 8 * j); v >>= B64; }
 }
 
 // the main's input object -> n_inputs x 32-byte LE values, by the program's input names
@@ -246,11 +291,7 @@ function programInputBuffer(input, meta) {
     if (!meta.names.some(([n]) => n === k)) throw new Error(`Signal ${k} not found\n`);
   }
   const buf = Buffer.alloc(32 * vals.length);
-  vals.forEach((x, i) => {
-    let v = BigInt(x) % R;
-    if (v < BigInt(0)) v += R;
-    for (let j = 0; j < 32; j++) { buf[32 * i + j] = Number(v & BigInt(255)); v >>= BigInt(8); }
-  });
+  vals.forEach((x, i) => putSignal(buf, 32 * i, x));
   return buf;
 }
 
@@ -281,7 +322,7 @@ async function wtnsCalculateGpu(input, progBuf, device) {
 // (addon.fullProveDevice); only the input signals go up and the proof comes back.
 async function fullProve(input, wasmFile, zkeyFileName, logger, options) {
   options = options || {};
-  const code = readBin(wasmFile);
+  const code = readProgram(wasmFile);
   const device = options.device || 0;
   if (code.slice(0, 4).toString('latin1') === 'nzwp') {
     const { handle, meta } = programFor(code, device);

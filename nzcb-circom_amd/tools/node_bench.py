@@ -3,7 +3,7 @@
 program and K pass inputs (bench.py's passes), runs js/bench.js (N concurrent
 plonk.fullProve calls through the snarkjs-shaped API), checks the first pass's public
 signals against the independent nzcp kernel, and prints the Node line.
-  python3 tools/node_bench.py [--proofs K] [--concurrency N] [--lanes L] [--dir D]
+  python3 tools/node_bench.py [--proofs K] [--concurrency N] [--lanes L] [--dir D] [--reuse]
 The GPU work of the preparation runs in a child process (--prep), so the process that
 starts node has never initialised the GPU."""
 import argparse
@@ -27,8 +27,12 @@ def main():
     ap.add_argument("--lanes", type=int, default=5)
     ap.add_argument("--dir", default="/tmp/nzcb_node_bench")
     ap.add_argument("--prep", action="store_true")
+    ap.add_argument("--reuse", action="store_true", help="keep the files of an earlier run in --dir")
     a = ap.parse_args()
     if not a.prep:
+        if a.reuse and os.path.exists(os.path.join(a.dir, "want.json")):
+            run_node(a)
+            return
         q = subprocess.run([sys.executable, os.path.abspath(__file__), "--prep", "--proofs", str(a.proofs), "--dir",
                             a.dir], timeout=1200)
         if q.returncode:
