@@ -181,6 +181,11 @@ class Circuit:
         self.in_base = 1 + n_out
         # signal names, circom's hierarchical "main.<component>.<signal>[i]" (write_sym)
         self.names = {}
+        # further names, (name, wire or -1): signals equal to another signal's wire (a
+        # component's inputs, an output passed on) or substituted away (-1), as circom's
+        # .sym lists them (Circuit.declare)
+        self.extra_names = []
+        self._used = set()              # every name given so far (names stay unique)
         self._path = ["main"]
         self._seq = {}
         o = 1
@@ -193,7 +198,8 @@ class Circuit:
         prefix = ".".join(self._path)
         one = n == 1 if scalar is None else scalar
         for i in range(n):
-            self.names[base + i] = f"{prefix}.{sig}" if one else f"{prefix}.{sig}[{i}]"
+            self.names[base + i] = nm = f"{prefix}.{sig}" if one else f"{prefix}.{sig}[{i}]"
+            self._used.add(nm)
 
     def _next(self, kind: str) -> int:
         key = (len(self._path), ".".join(self._path), kind)
@@ -226,13 +232,47 @@ class Circuit:
             self._name(base, n, name)
         return base
 
+    def declare(self, sig: str, x):
+        """circom's signal `sig` of the current component ("valueTally.nums": a signal of a
+        sub-component) with value x: an LC or int, or a list of them for an array (nested
+        for more dimensions). For the .sym only (no wire, constraint or operation): a
+        value that is one wire still under an automatic name (_sN) takes the
+        signal's name (e.g. a product the parent computed into this component's input, as
+        circom names it); any other value adds a name, with the wire it equals (one wire,
+        coefficient 1) or -1 (a constant or a combination: circom --O2 substitutes it)."""
+        prefix = ".".join(self._path)
+
+        def put(name, v):
+            if name in self._used:      # e.g. a test main's output, named by the main itself
+                return
+            self._used.add(name)
+            if isinstance(v, dict) and len(v) == 1:
+                (wire, coef), = v.items()
+                if wire and coef == 1:
+                    cur = self.names.get(wire, "")
+                    if cur.rsplit(".", 1)[-1].startswith("_s"):   # an automatic name: take it
+                        self.names[wire] = name
+                    elif cur != name:
+                        self.extra_names.append((name, wire))
+                    return
+            self.extra_names.append((name, -1))
+
+        def walk(name, v):
+            if isinstance(v, (list, tuple)):
+                for i, y in enumerate(v):
+                    walk(f"{name}[{i}]", y)
+            else:
+                put(name, v)
+        walk(f"{prefix}.{sig}", x)
+
     def write_sym(self) -> bytes:
-        """circom's .sym text: one line per named signal, "label,wire,component,name", in
-        wire order (every allocated wire has a name; wire 0 = the constant one has none,
-        as in circom)."""
+        """circom's .sym text: one line per named signal, "label,wire,component,name": the
+        allocated wires in wire order (every one has a name; wire 0 = the constant one has
+        none, as in circom), then the declared further names (Circuit.declare), each with
+        the wire it shares or -1."""
         comps, lines = {}, []
-        for label, wire in enumerate(sorted(self.names), 1):
-            name = self.names[wire]
+        entries = [(self.names[wire], wire) for wire in sorted(self.names)] + self.extra_names
+        for label, (name, wire) in enumerate(entries, 1):
             comp = comps.setdefault(name.rsplit(".", 1)[0], len(comps))
             lines.append(f"{label},{wire},{comp},{name}\n")
         return "".join(lines).encode()
@@ -287,6 +327,7 @@ class Circuit:
         """circomlib Num2Bits(n): n bit signals, LSB first."""
         with self.component("Num2Bits", name):
             base = self.alloc(n, "out")
+            self.declare("in", lc(x))
         bits = [w(base + i) for i in range(n)]
         for b in bits:
             self.constrain(b, sub(b, 1), 0)
@@ -298,6 +339,7 @@ class Circuit:
         """circomlib IsZero: inv <-- x != 0 ? 1/x : 0; out <== -x inv + 1; x out === 0."""
         x = lc(x)
         with self.component("IsZero", name):
+            self.declare("in", x)
             inv = self.alloc(1, "inv")
             self._op(OP_INV, inv, x)
             out = self.mul(scale(x, -1), w(inv), 1, name="out")
@@ -306,12 +348,17 @@ class Circuit:
 
     def is_equal(self, a, b, name: str | None = None) -> dict:
         with self.component("IsEqual", name):
-            return self.is_zero(sub(b, a), name="isz")
+            self.declare("in", [lc(a), lc(b)])
+            out = self.is_zero(sub(b, a), name="isz")
+            self.declare("out", out)
+            return out
 
     def less_than(self, a, b, n: int, err: int, name: str | None = None) -> dict:
         """circomlib LessThan(n): Num2Bits(n+1) of a + 2^n - b, out = 1 - bit n."""
         with self.component("LessThan", name):
+            self.declare("in", [lc(a), lc(b)])
             bits = self.num2bits(add(a, 1 << n, scale(b, -1)), n + 1, err, name="n2b")
+            self.declare("out", sub(1, bits[n]))
         return sub(1, bits[n])
 
     def quin(self, n: int, in_base: int, m: int, index, err_range: int, err_select: int,
@@ -333,9 +380,19 @@ class Circuit:
             self.names[base + n + i] = f"{prefix}.eqs[{i}].inv"
         for i in range(m):
             self.names[base + 2 * n + i] = f"{prefix}.sums[{i}]"
+        self._used.update(self.names[base + i] for i in range(2 * n + m))
         eq = lambda i: w(base + i)            # noqa: E731
         inv = lambda i: w(base + n + i)       # noqa: E731
         sums = lambda i: w(base + 2 * n + i)  # noqa: E731
+        # circom's names of the inputs (in[k] = 0 past m), the output, eqs[i].in and the
+        # sums past m (equal to sums[m - 1], as in[k] = 0 there)
+        self.declare("in", [w(in_base + k) if k < m else 0 for k in range(n)])
+        self.declare("index", index)
+        self.declare("out", sums(m - 1) if m else 0)
+        for i in range(n):
+            self.declare(f"eqs[{i}].in", sub(i, index))
+        for i in range(m, n):
+            self.declare(f"sums[{i}]", sums(m - 1) if m else 0)
         for i in range(n):
             d = sub(i, index)
             self.constrain(d, inv(i), sub(1, eq(i)))

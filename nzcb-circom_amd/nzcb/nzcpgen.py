@@ -59,20 +59,41 @@ class Bytes:
     def __init__(self, base: int, n: int):
         self.base, self.n = base, n
 
+    def wires(self) -> list:
+        return [w(self.base + k) for k in range(self.n)]
+
+
+# Names: every template declares its circom signals (Circuit.declare) and passes its
+# components' names (cname / name), so the .sym names each signal as circom's does:
+# main.<component>[i].<signal>[j] (tests/test_circom_names.py against the reference's
+# declarations). Names change no wire, constraint or operation.
 
 # ---------------------------------------------------------------------------- cbortpl
 @_template("GetType")
 def get_type(c: Circuit, v):
     """GetType (cbortpl.circom:26-52): Num2Bits(8), ShR(8, 5), Bits2Num(3)."""
-    bits = c.num2bits(v, 8, ERR_RANGE)
-    return c.lin(add(*[scale(bits[5 + i], 1 << i) for i in range(3)]))
+    c.declare("v", v)
+    bits = c.num2bits(v, 8, ERR_RANGE, name="n2b")
+    t = c.lin(add(*[scale(bits[5 + i], 1 << i) for i in range(3)]))
+    c.declare("type", t)
+    c.declare("shr.in", bits)
+    c.declare("shr.out", bits[5:])
+    c.declare("b2n.in", bits[5:])
+    c.declare("b2n.out", t)
+    return t
 
 
 @_template("GetX")
 def get_x(c: Circuit, v):
     """GetX (cbortpl.circom:57-72): the 5 low bits of v."""
-    bits = c.num2bits(v, 8, ERR_RANGE)
-    return c.lin(add(*[scale(bits[i], 1 << i) for i in range(5)]))
+    c.declare("v", v)
+    bits = c.num2bits(v, 8, ERR_RANGE, name="num2Bits")
+    x = c.lin(add(*[scale(bits[i], 1 << i) for i in range(5)]))
+    c.declare("x", x)
+    c.declare("vbits", bits)
+    c.declare("b2n.in", bits[:5])
+    c.declare("b2n.out", x)
+    return x
 
 
 @_template("GetV")
@@ -80,60 +101,100 @@ def get_v(c: Circuit, b: Bytes, pos):
     """GetV (cbortpl.circom:78-90): QuinSelector(BytesLen). Both of QuinSelector's checks
     (the LessThan's Num2Bits and ``lessThan.out === 1``) report ERR_SELECT, as the
     restatement oracle/nzcp_circuit.py quin_selector classifies them."""
-    return c.quin(b.n, b.base, b.n, pos, ERR_SELECT, ERR_SELECT)
+    c.declare("pos", pos)
+    c.declare("bytes", b.wires())
+    v = c.quin(b.n, b.base, b.n, pos, ERR_SELECT, ERR_SELECT, name="quinSelector")
+    c.declare("v", v)
+    return v
+
+
+def _tally(c: Circuit, name: str, nums: list, out_name: str | None = None):
+    """CalculateTotal(n) (calculate_total.circom, not on disk) over products already
+    computed: nums[i], sum = their sum (a signal when longer than two terms)."""
+    total = c.lin(add(*nums))
+    if out_name:
+        c.declare(out_name, total)
+    c.declare(f"{name}.nums", nums)
+    c.declare(f"{name}.sum", total)
+    return total
 
 
 @_template("DecodeUint23")
 def decode_uint23(c: Circuit, v):
     """DecodeUint23 (cbortpl.circom:95-114)."""
-    x = get_x(c, v)
-    lt = c.less_than(x, 24, 8, ERR_RANGE)
+    c.declare("v", v)
+    x = get_x(c, v, cname="getX")
+    lt = c.less_than(x, 24, 8, ERR_RANGE, name="lt")
     c.check_zero(sub(lt, 1), ERR_UINT23)
+    c.declare("value", x)
     return x
 
 
 @_template("DecodeUint")
 def decode_uint(c: Circuit, v, b: Bytes, pos):
     """DecodeUint (cbortpl.circom:120-241): every branch is evaluated. Returns (value, nextPos)."""
-    x = get_x(c, v)
-    cond23 = c.less_than(x, 24, 8, ERR_RANGE)
-    cond24 = c.is_equal(x, 24)
-    cond25 = c.is_equal(x, 25)
-    cond26 = c.is_equal(x, 26)
+    c.declare("v", v)
+    c.declare("bytes", b.wires())
+    c.declare("pos", pos)
+    x = get_x(c, v, cname="getX")
+    c.declare("x", x)
+    cond23 = c.less_than(x, 24, 8, ERR_RANGE, name="lessThan")
+    cond24 = c.is_equal(x, 24, name="isEqual24")
+    cond25 = c.is_equal(x, 25, name="isEqual25")
+    cond26 = c.is_equal(x, 26, name="isEqual26")
+    c.declare("condition23", cond23)
+    c.declare("condition24", cond24)
+    c.declare("condition25", cond25)
+    c.declare("condition26", cond26)
     pos = lc(pos)
     value23, next23 = x, pos
-    value24 = get_v(c, b, c.mul(cond24, pos))
+    value24 = get_v(c, b, c.mul(cond24, pos), cname="getV_24")
     next24 = add(pos, 1)
-    v1_25 = get_v(c, b, c.mul(cond25, pos))
-    v2_25 = get_v(c, b, c.mul(cond25, add(pos, 1)))
+    v1_25 = get_v(c, b, c.mul(cond25, pos), cname="getV1_25")
+    v2_25 = get_v(c, b, c.mul(cond25, add(pos, 1)), cname="getV2_25")
     value25 = add(scale(v1_25, 256), v2_25)
     next25 = add(pos, 2)
-    v26 = [get_v(c, b, c.mul(cond26, add(pos, j))) for j in range(4)]
-    value26 = add(scale(v26[0], 1 << 24), scale(v26[1], 1 << 16), scale(v26[2], 1 << 8), v26[3])
+    v26 = [get_v(c, b, c.mul(cond26, add(pos, j)), cname=f"getV{j + 1}_26") for j in range(4)]
+    f26 = [1 << 24, 1 << 16, 1 << 8, 1]
+    value26 = add(*[scale(v26[j], f26[j]) for j in range(4)])
     next26 = add(pos, 4)
-    value = c.lin(add(c.mul(cond23, value23), c.mul(cond24, value24), c.mul(cond25, value25),
-                      c.mul(cond26, value26)))
-    next_pos = c.lin(add(c.mul(cond23, next23), c.mul(cond24, next24), c.mul(cond25, next25),
-                         c.mul(cond26, next26)))
+    for sig, val in (("value23", value23), ("nextPos23", next23), ("value24", value24), ("nextPos24", next24),
+                     ("value1_25", scale(v1_25, 256)), ("value2_25", v2_25), ("value25", value25),
+                     ("nextPos25", next25), ("value1_26", scale(v26[0], f26[0])),
+                     ("value2_26", scale(v26[1], f26[1])), ("value3_26", scale(v26[2], f26[2])),
+                     ("value4_26", v26[3]), ("value26", value26), ("nextPos26", next26)):
+        c.declare(sig, val)
+    nums = [c.mul(cond23, value23), c.mul(cond24, value24), c.mul(cond25, value25), c.mul(cond26, value26)]
+    value = _tally(c, "valueTally", nums, "value")
+    nums = [c.mul(cond23, next23), c.mul(cond24, next24), c.mul(cond25, next25), c.mul(cond26, next26)]
+    next_pos = _tally(c, "nextPosTally", nums, "nextPos")
     return value, next_pos
 
 
 @_template("ReadType")
 def read_type(c: Circuit, b: Bytes, pos):
     """ReadType (cbortpl.circom:246-261). Returns (nextPos, type, v)."""
-    v = get_v(c, b, pos)
-    typ = get_type(c, v)
+    c.declare("bytes", b.wires())
+    c.declare("pos", pos)
+    v = get_v(c, b, pos, cname="getV")
+    c.declare("v", v)
+    typ = get_type(c, v, cname="getType")
+    c.declare("type", typ)
+    c.declare("nextPos", add(pos, 1))
     return add(pos, 1), typ, v
 
 
 @_template("SkipValueScalar")
 def skip_value_scalar(c: Circuit, b: Bytes, pos):
     """SkipValueScalar (cbortpl.circom:266-297): ints and strings."""
-    nxt, typ, v = read_type(c, b, pos)
-    value, dnext = decode_uint(c, v, b, nxt)
-    is_int = c.is_equal(typ, MAJOR_INT)
-    is_string = c.is_equal(typ, MAJOR_STRING)
-    return c.lin(add(c.mul(is_int, dnext), c.mul(is_string, add(dnext, value))))
+    c.declare("bytes", b.wires())
+    c.declare("pos", pos)
+    nxt, typ, v = read_type(c, b, pos, cname="readType")
+    value, dnext = decode_uint(c, v, b, nxt, cname="decodeUint")
+    is_int = c.is_equal(typ, MAJOR_INT, name="isInt")
+    is_string = c.is_equal(typ, MAJOR_STRING, name="isString")
+    nums = [c.mul(is_int, dnext), c.mul(is_string, add(dnext, value))]
+    return _tally(c, "calculateTotal", nums, "nextPos")
 
 
 @_template("SkipValue")
@@ -143,65 +204,94 @@ def skip_value(c: Circuit, b: Bytes, pos, max_array_len: int):
     slot's end, gated by shouldConsider[i] = isArray * (i < isArray * len); a
     QuinSelector(MaxArrayLen) picks the end of element len - 1. nzcp_live has
     MaxArrayLen = 0: no loop, and QuinSelector(0) outputs 0 (quinSelector.circom:19-41)."""
-    nxt, typ, v = read_type(c, b, pos)
-    value, dnext = decode_uint(c, v, b, nxt)
-    is_int = c.is_equal(typ, MAJOR_INT)
-    is_string = c.is_equal(typ, MAJOR_STRING)
-    is_array = c.is_equal(typ, MAJOR_ARRAY)
+    c.declare("bytes", b.wires())
+    c.declare("pos", pos)
+    nxt, typ, v = read_type(c, b, pos, cname="readType")
+    value, dnext = decode_uint(c, v, b, nxt, cname="decodeUint")
+    is_int = c.is_equal(typ, MAJOR_INT, name="isInt")
+    is_string = c.is_equal(typ, MAJOR_STRING, name="isString")
+    is_array = c.is_equal(typ, MAJOR_ARRAY, name="isArray")
     arr_len = c.mul(is_array, value) if max_array_len else None     # lt[i].in[1] <== isArray.out * value
     ends = c.alloc(max_array_len)                                   # nextPosArray[i] = qs.in[i]
+    c.declare("nextPosArray", [w(ends + i) for i in range(max_array_len)])
     prev = dnext
     bits = log2(max_array_len) + 1
     for i in range(max_array_len):
-        lt = c.less_than(i, arr_len, bits, ERR_RANGE)
+        lt = c.less_than(i, arr_len, bits, ERR_RANGE, name=f"lt[{i}]")
         consider = c.mul(is_array, lt)                              # shouldConsider[i]
-        end = skip_value_scalar(c, b, c.mul(prev, consider))
+        c.declare(f"shouldConsider[{i}]", consider)
+        end = skip_value_scalar(c, b, c.mul(prev, consider), cname=f"skipValue[{i}]")
         c.lin(end, dst=ends + i)
         prev = w(ends + i)
     index = c.mul(is_array, sub(value, 1))     # qs.index <== isArray.out * (decodeUint.value - 1)
-    terms = [c.mul(is_int, dnext), c.mul(is_string, add(dnext, value))]
+    nums = [c.mul(is_int, dnext), c.mul(is_string, add(dnext, value))]
     if max_array_len:
-        terms.append(c.mul(is_array, get_v(c, Bytes(ends, max_array_len), index)))
-    return c.lin(add(*terms))
+        nums.append(c.mul(is_array, c.quin(max_array_len, ends, max_array_len, index, ERR_SELECT, ERR_SELECT,
+                                           name="qs")))
+    else:       # QuinSelector(0): no inputs, out = 0 (its LessThan is declared, not wired)
+        c.declare("qs.index", index)
+        c.declare("qs.out", 0)
+        c.declare("qs.lessThan.in", [0, 0])
+        nums.append(0)
+    return _tally(c, "calculateTotal", nums, "nextPos")
 
 
 @_template("StringEquals")
 def string_equals(c: Circuit, b: Bytes, const: list, pos, length):
     """StringEquals (cbortpl.circom:373-404)."""
-    is_same_len = c.is_equal(length, len(const))
+    c.declare("bytes", b.wires())
+    c.declare("pos", pos)
+    c.declare("len", length)
+    is_same_len = c.is_equal(length, len(const), name="isSameLen")
     cond = [is_same_len]
     for i, ch in enumerate(const):
-        cond.append(c.is_equal(ch, get_v(c, b, add(pos, i))))
-    return c.is_zero(sub(len(const) + 1, add(*cond)))
+        cond.append(c.is_equal(ch, get_v(c, b, add(pos, i), cname=f"getV[{i}]"), name=f"isEqual[{i}]"))
+    out = c.is_zero(sub(len(const) + 1, add(*cond)), name="isZero")
+    c.declare("out", out)
+    return out
 
 
 @_template("ReadStringLength")
 def read_string_length(c: Circuit, b: Bytes, pos):
     """ReadStringLength (cbortpl.circom:410-428). Returns (len, nextPos = pos + 1)."""
-    nxt, typ, v = read_type(c, b, pos)
+    c.declare("bytes", b.wires())
+    c.declare("pos", pos)
+    nxt, typ, v = read_type(c, b, pos, cname="readType")
     c.check_zero(sub(typ, MAJOR_STRING), ERR_NOT_STRING)
-    value, _ = decode_uint(c, v, b, nxt)
+    value, _ = decode_uint(c, v, b, nxt, cname="dUint")
+    c.declare("len", value)
+    c.declare("nextPos", nxt)
     return value, nxt
 
 
 @_template("ReadMapLength")
 def read_map_length(c: Circuit, b: Bytes, pos):
     """ReadMapLength (cbortpl.circom:434-453). Returns (len, nextPos)."""
-    nxt, typ, v = read_type(c, b, pos)
+    c.declare("pos", pos)
+    c.declare("bytes", b.wires())
+    nxt, typ, v = read_type(c, b, pos, cname="readType")
     c.check_zero(sub(typ, MAJOR_MAP), ERR_NOT_MAP)
-    return decode_uint23(c, v), nxt
+    length = decode_uint23(c, v, cname="dUint23")
+    c.declare("len", length)
+    c.declare("nextPos", nxt)
+    return length, nxt
 
 
 @_template("CopyString")
 def copy_string(c: Circuit, b: Bytes, pos, max_len: int, out_base: int | None = None):
     """CopyString (cbortpl.circom:460-503). Returns (outbytes, nextPos, len)."""
-    length, nxt = read_string_length(c, b, pos)
+    c.declare("bytes", b.wires())
+    c.declare("pos", pos)
+    length, nxt = read_string_length(c, b, pos, cname="readStrLen")
     bits = log2(max_len) + 1
     out = []
     for i in range(max_len):
-        v = get_v(c, b, add(nxt, i))
-        lt = c.less_than(i, length, bits, ERR_RANGE)
+        v = get_v(c, b, add(nxt, i), cname=f"getV[{i}]")
+        lt = c.less_than(i, length, bits, ERR_RANGE, name=f"lt[{i}]")
         out.append(c.mul(v, lt))
+    c.declare("outbytes", out)
+    c.declare("nextPos", add(nxt, length))
+    c.declare("len", length)
     return out, add(nxt, length), length
 
 
@@ -210,28 +300,38 @@ def copy_string(c: Circuit, b: Bytes, pos, max_len: int, out_base: int | None = 
 def find_cwt_claims(c: Circuit, b: Bytes, map_len, pos, max_array_len: int, max_map_len: int):
     """FindCWTClaims (nzcptpl.circom:33-145). Returns (vcPos, exp)."""
     vc = [118, 99]
+    c.declare("mapLen", map_len)
+    c.declare("bytes", b.wires())
+    c.declare("pos", pos)
     found, exp_pos = [], []
     for k in range(max_map_len):
-        nxt, typ, v = read_type(c, b, pos)
-        value, dnext = decode_uint(c, v, b, nxt)
-        is_string = c.is_equal(typ, MAJOR_STRING)
-        is_int = c.is_equal(typ, MAJOR_INT)
+        nxt, typ, v = read_type(c, b, pos, cname=f"readType[{k}]")
+        c.declare(f"v[{k}]", v)
+        c.declare(f"type[{k}]", typ)
+        value, dnext = decode_uint(c, v, b, nxt, cname=f"decodeUint[{k}]")
+        c.declare(f"value[{k}]", value)
+        is_string = c.is_equal(typ, MAJOR_STRING, name=f"isString[{k}]")
+        is_int = c.is_equal(typ, MAJOR_INT, name=f"isInt[{k}]")
         skip_pos = c.mul(value, is_string, dnext)
-        next_pos = skip_value(c, b, skip_pos, max_array_len)     # runs once its inputs are set
-        needle = string_equals(c, b, vc, dnext, value)
-        is4 = c.is_equal(4, value)
-        within = c.less_than(k, map_len, 8, ERR_RANGE)
+        next_pos = skip_value(c, b, skip_pos, max_array_len, cname=f"skipValue[{k}]")   # runs once its inputs are set
+        needle = string_equals(c, b, vc, dnext, value, cname=f"isNeedleString[{k}]")
+        is4 = c.is_equal(4, value, name=f"is4Int[{k}]")
+        within = c.less_than(k, map_len, 8, ERR_RANGE, name=f"withinMapLen[{k}]")
         is_needle = c.mul(is_string, needle)
         is_exp = c.mul(is_int, is4)
         accepted = c.mul(is_needle, within)
         exp_accepted = c.mul(is_exp, within)
+        for sig, val in (("isNeedle", is_needle), ("isExp", is_exp), ("isAccepted", accepted),
+                         ("isExpAccepted", exp_accepted)):
+            c.declare(f"{sig}[{k}]", val)
         found.append(c.mul(accepted, add(dnext, value)))
         exp_pos.append(c.mul(exp_accepted, dnext))
         pos = next_pos
-    vc_pos = c.lin(add(*found))
-    epos = c.lin(add(*exp_pos))
-    nxt, _, v = read_type(c, b, epos)
-    exp, _ = decode_uint(c, v, b, nxt)
+    vc_pos = _tally(c, "foundPosTally", found, "vcPos")
+    epos = _tally(c, "expPosTally", exp_pos)
+    nxt, _, v = read_type(c, b, epos, cname="expReadType")
+    exp, _ = decode_uint(c, v, b, nxt, cname="expDecodeUint")
+    c.declare("exp", exp)
     return vc_pos, exp
 
 
@@ -241,19 +341,27 @@ def find_cred_subj(c: Circuit, b: Bytes, map_len, pos, max_array_len: int, max_m
     reference at test/nzcp.js:144-215). Returns needlePos, the position of the
     "credentialSubject" key's value."""
     needle_str = [99, 114, 101, 100, 101, 110, 116, 105, 97, 108, 83, 117, 98, 106, 101, 99, 116]
+    c.declare("mapLen", map_len)
+    c.declare("bytes", b.wires())
+    c.declare("pos", pos)
     found = []
     for k in range(max_map_len):
-        nxt, typ, v = read_type(c, b, pos)
-        value, dnext = decode_uint(c, v, b, nxt)
-        is_string = c.is_equal(typ, MAJOR_STRING)
-        next_pos = skip_value(c, b, c.mul(value, is_string, dnext), max_array_len)
-        needle = string_equals(c, b, needle_str, dnext, value)
-        within = c.less_than(k, map_len, 8, ERR_RANGE)
+        nxt, typ, v = read_type(c, b, pos, cname=f"readType[{k}]")
+        c.declare(f"v[{k}]", v)
+        c.declare(f"type[{k}]", typ)
+        value, dnext = decode_uint(c, v, b, nxt, cname=f"decodeUint[{k}]")
+        c.declare(f"value[{k}]", value)
+        is_string = c.is_equal(typ, MAJOR_STRING, name=f"isString[{k}]")
+        next_pos = skip_value(c, b, c.mul(value, is_string, dnext), max_array_len, cname=f"skipValue[{k}]")
+        needle = string_equals(c, b, needle_str, dnext, value, cname=f"isNeedleString[{k}]")
+        within = c.less_than(k, map_len, 8, ERR_RANGE, name=f"withinMapLen[{k}]")
         is_needle = c.mul(is_string, needle)
         accepted = c.mul(is_needle, within)
+        c.declare(f"isNeedle[{k}]", is_needle)
+        c.declare(f"isAccepted[{k}]", accepted)
         found.append(c.mul(accepted, add(dnext, value)))
         pos = next_pos
-    return c.lin(add(*found))
+    return _tally(c, "foundPosTally", found, "needlePos")
 
 
 @_template("ReadCredSubj")
@@ -263,6 +371,9 @@ def read_cred_subj(c: Circuit, b: Bytes, pos, max_buffer_len: int, map_len=None)
     map_len: the mapLen input, checked against 3 (``hardcore_assert``, :261); NZCPPubIdentity
     passes the constant 3 (:552), which leaves no constraint."""
     n_map = 3
+    c.declare("mapLen", n_map if map_len is None else map_len)
+    c.declare("bytes", b.wires())
+    c.declare("pos", pos)
     if map_len is not None:
         c.check_zero(sub(map_len, n_map), ERR_RANGE)
     max_str = max_buffer_len // n_map
@@ -271,19 +382,23 @@ def read_cred_subj(c: Circuit, b: Bytes, pos, max_buffer_len: int, map_len=None)
     dob = [100, 111, 98]
     is_g, is_f, is_d, copies = [], [], [], []
     for k in range(n_map):
-        length, nxt = read_string_length(c, b, pos)
-        is_g.append(string_equals(c, b, given, nxt, length))
-        is_f.append(string_equals(c, b, family, nxt, length))
-        is_d.append(string_equals(c, b, dob, nxt, length))
-        out, pos, ln = copy_string(c, b, add(nxt, length), max_str)
+        length, nxt = read_string_length(c, b, pos, cname=f"readStringLength[{k}]")
+        is_g.append(string_equals(c, b, given, nxt, length, cname=f"isGivenName[{k}]"))
+        is_f.append(string_equals(c, b, family, nxt, length, cname=f"isFamilyName[{k}]"))
+        is_d.append(string_equals(c, b, dob, nxt, length, cname=f"isDOB[{k}]"))
+        out, pos, ln = copy_string(c, b, add(nxt, length), max_str, cname=f"copyString[{k}]")
         copies.append((out, ln))
     res = []
-    for sel in (is_g, is_f, is_d):
+    for sel, nm in ((is_g, "givenName"), (is_f, "familyName"), (is_d, "dob")):
         base = c.alloc(max_str)
         prods = [[c.mul(sel[i], copies[i][0][h]) for i in range(n_map)] for h in range(max_str)]
         for h in range(max_str):
             c.lin(add(*prods[h]), dst=base + h)
-        ln = c.lin(add(*[c.mul(sel[i], copies[i][1]) for i in range(n_map)]))
+        c.declare(nm, [w(base + h) for h in range(max_str)] + [0] * (max_buffer_len - max_str))
+        for h in range(max_str):
+            c.declare(f"{nm}CharTally[{h}].nums", prods[h])
+            c.declare(f"{nm}CharTally[{h}].sum", w(base + h))
+        ln = _tally(c, f"{nm}LenTally", [c.mul(sel[i], copies[i][1]) for i in range(n_map)], f"{nm}Len")
         res.append((base, ln))
     return res, max_str
 
@@ -294,15 +409,20 @@ def construct_nullifier(c: Circuit, names, max_str: int, max_buffer_len: int):
     comma = 44
     bits = log2(max_buffer_len) + 1
     (gb, gl), (fb, fl), (db, dl) = names
+    for nm, base, ln in (("givenName", gb, gl), ("familyName", fb, fl), ("dob", db, dl)):
+        c.declare(nm, [w(base + h) if h < max_str else 0 for h in range(max_buffer_len)])
+        c.declare(f"{nm}Len", ln)
     result = []
     for k in range(max_buffer_len):
-        is_given = c.less_than(k, gl, bits, ERR_RANGE)
-        under_sep1 = c.less_than(k, add(gl, 1), bits, ERR_RANGE)
-        under_family = c.less_than(k, add(gl, 1, fl), bits, ERR_RANGE)
-        under_sep2 = c.less_than(k, add(gl, 1, fl, 1), bits, ERR_RANGE)
-        g_sel = c.quin(max_buffer_len, gb, max_str, k, ERR_SELECT, ERR_SELECT)
-        f_sel = c.quin(max_buffer_len, fb, max_str, sub(sub(k, gl), 1), ERR_SELECT, ERR_SELECT)
-        d_sel = c.quin(max_buffer_len, db, max_str, sub(sub(sub(sub(k, gl), 1), fl), 1), ERR_SELECT, ERR_SELECT)
+        is_given = c.less_than(k, gl, bits, ERR_RANGE, name=f"isGivenName[{k}]")
+        under_sep1 = c.less_than(k, add(gl, 1), bits, ERR_RANGE, name=f"isUnderSep1[{k}]")
+        under_family = c.less_than(k, add(gl, 1, fl), bits, ERR_RANGE, name=f"isUnderFamilyName[{k}]")
+        under_sep2 = c.less_than(k, add(gl, 1, fl, 1), bits, ERR_RANGE, name=f"isUnderSep2[{k}]")
+        g_sel = c.quin(max_buffer_len, gb, max_str, k, ERR_SELECT, ERR_SELECT, name=f"givenNameSelector[{k}]")
+        f_sel = c.quin(max_buffer_len, fb, max_str, sub(sub(k, gl), 1), ERR_SELECT, ERR_SELECT,
+                       name=f"familyNameSelector[{k}]")
+        d_sel = c.quin(max_buffer_len, db, max_str, sub(sub(sub(sub(k, gl), 1), fl), 1), ERR_SELECT, ERR_SELECT,
+                       name=f"dobSelector[{k}]")
         not_given = sub(1, is_given)
         is_sep1 = c.mul(under_sep1, not_given)
         is_family = c.mul(under_family, sub(1, under_sep1))
@@ -313,6 +433,12 @@ def construct_nullifier(c: Circuit, names, max_str: int, max_buffer_len: int):
         dob_char = c.mul(is_dob, d_sel)
         result.append(c.lin(add(given_char, scale(is_sep1, comma), family_char, scale(is_sep2, comma), dob_char),
                             force=True))
+        for sig, val in (("notGivenName", not_given), ("isSep1", is_sep1), ("isFamilyName", is_family),
+                         ("isSep2", is_sep2), ("isDOB", is_dob), ("givenNameChar", given_char),
+                         ("sep1Char", scale(is_sep1, comma)), ("familyNameChar", family_char),
+                         ("sep2Char", scale(is_sep2, comma)), ("dobChar", dob_char), ("result", result[-1])):
+            c.declare(f"{sig}[{k}]", val)
+    c.declare("resultLen", add(gl, 1, fl, 1, dl))
     return result
 
 
@@ -427,6 +553,8 @@ def nzcp_pub_identity(is_live: int, max_tbs_bytes: int, max_array_len_vc: int, m
     bits = log2(max_tbs_bytes) + 1
     for k in range(max_tbs_bytes):
         b2n = add(*[scale(tbs[8 * k + 7 - i], 1 << i) for i in range(8)])
+        c.declare(f"b2n[{k}].in", [tbs[8 * k + 7 - i] for i in range(8)])
+        c.declare(f"b2n[{k}].out", b2n)
         lt = c.less_than(k, tbs_len, bits, ERR_RANGE, name=f"ltLen[{k}]")
         c.mul(b2n, lt, dst=tb + k)
     tbytes = Bytes(tb, max_tbs_bytes)
@@ -437,6 +565,8 @@ def nzcp_pub_identity(is_live: int, max_tbs_bytes: int, max_array_len_vc: int, m
     nb = [c.num2bits(result[k], 8, ERR_RANGE, name=f"n2bNullifier[{k}]") for k in range(null_bytes)]
     nbase = next(iter(nb[0][0]))            # byte wires: nbase + 8k + j (LSB-first bits)
     sha512 = sha512_64(c, nbase, cname="nullifierSha512")
+    c.declare("exp", exp)
+    c.declare("nullifierBits", sha512)
     exp_bits = c.num2bits(exp, 32, ERR_RANGE, name="n2bExp")
     ins = [[0] * chunk_bits for _ in range(3)]
     for k in range(chunk_bytes):                                   # nullifier hash part (:596-601)
@@ -469,6 +599,8 @@ def nzcp_pub_identity(is_live: int, max_tbs_bytes: int, max_array_len_vc: int, m
     for j in range(3):                                             # Bits2Num(248) -> out (:653-655)
         c.lin(add(*[scale(x, 1 << i) if isinstance(x, dict) else 0 for i, x in enumerate(ins[j])]),
               dst=c.out_wires[j])
+        c.declare(f"outB2n[{j}].in", [x if isinstance(x, dict) else 0 for x in ins[j]])
+        c.declare(f"outB2n[{j}].out", w(c.out_wires[j]))
     return c
 
 

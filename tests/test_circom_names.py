@@ -102,8 +102,6 @@ def test_golden_extraction_covers_the_reference_templates():
                                              "nullifierBits"]
 
 
-@pytest.mark.xfail(reason="nzcpgen names its inner templates' components by kind (DecodeUint[k]); renaming in progress",
-                   strict=False)
 def test_every_reference_signal_is_named(live_sym, reference_names):
     names, _ = reference_names
     assert len(names) > 100000
@@ -111,8 +109,6 @@ def test_every_reference_signal_is_named(live_sym, reference_names):
     assert not missing, f"{len(missing)} of {len(names)} missing, e.g. {missing[:10]}"
 
 
-@pytest.mark.xfail(reason="nzcpgen names its inner templates' components by kind (DecodeUint[k]); renaming in progress",
-                   strict=False)
 def test_every_library_instance_is_named(live_sym, reference_names):
     """circomlib / sha256-var / sha512 instances (internals unpinned): the instance exists."""
     _, externals = reference_names
@@ -125,10 +121,28 @@ def test_every_library_instance_is_named(live_sym, reference_names):
     assert not missing, f"{len(missing)} of {len(externals)} instances missing, e.g. {missing[:10]}"
 
 
-@pytest.mark.xfail(reason="substituted signals are not listed with -1 yet", strict=False)
 def test_io_and_substituted_signals_wires(live_sym):
-    """main's outputs and inputs keep circom's wires 1..; a signal circom substitutes away
-    (a pure alias such as ToBeSigned's bytes-to-number or nullifierBits) is listed with -1."""
+    """main's outputs and inputs keep circom's wires 1..; a signal equal to another signal
+    (a component's input, an output passed on) shares that signal's wire, and one that is a
+    constant or a combination of several wires (circom --O2 substitutes it) is listed
+    with -1, as circom writes it."""
     assert live_sym["main.out[0]"] == 1 and live_sym["main.out[2]"] == 3
     assert live_sym["main.toBeSigned[0]"] == 4 and live_sym["main.data[159]"] == 4 + 2808 + 160
-    assert live_sym["main.nullifierBits[0]"] == -1
+    # nullifierBits: the SHA-512 gadget's output bits, one wire each
+    assert live_sym["main.nullifierBits[0]"] > 0
+    # an alias: the first map-length read's byte array is main's ToBeSigned
+    assert live_sym["main.readMapLengthClaims.bytes[7]"] == live_sym["main.ToBeSigned[7]"]
+    assert live_sym["main.findVC.decodeUint[0].getV_24.quinSelector.in[3]"] == live_sym["main.ToBeSigned[3]"]
+    # combinations and constants: Bits2Num's sum, a padded name byte, QuinSelector(0)'s out
+    assert live_sym["main.b2n[0].out"] == -1
+    assert live_sym["main.readCredSubj.givenName[63]"] == -1
+    assert live_sym["main.findVC.skipValue[0].qs.out"] == -1
+
+
+def test_sym_names_are_unique_and_cover_every_wire(live_sym):
+    from nzcb import nzcpgen
+    c = nzcpgen.nzcp_pub_identity(**nzcpgen.LIVE)
+    lines = c.write_sym().decode().splitlines()
+    assert len(lines) == len(live_sym)            # no name twice
+    wires = {int(x.split(",")[1]) for x in lines}
+    assert set(range(1, c.n_wires)) <= wires and wires - set(range(1, c.n_wires)) == {-1}

@@ -6,8 +6,9 @@ order, e.g. circom's own nzcp_live.sym for the reference's nzcp_live_final.zkey
 (/root/reference/README.md:43). Checked here against a permuted self-generated .sym, on
 the CPU (the library's remap, the oracle's evaluation of the remapped program); the GPU
 run of a remapped program and a proof over a permuted r1cs are in tests/test_gpu_wvm.py.
-Whether the names equal circom's own .sym is unpinned: circom and its output are not on
-disk."""
+The names are those the reference's templates declare (tests/test_circom_names.py); which of
+two equal signals circom keeps as the wire (the other listed with -1) is unpinned: circom
+and its output are not on disk."""
 import random
 
 import pytest
@@ -36,7 +37,9 @@ def test_sym_names_every_wire_once():
     sym = c.write_sym().decode().splitlines()
     wires = [int(x.split(",")[1]) for x in sym]
     names = [x.split(",", 3)[3] for x in sym]
-    assert wires == list(range(1, c.n_wires)) and len(set(names)) == len(names)
+    # the wires in order, then the further names (signals sharing a wire, or -1)
+    assert wires[:c.n_wires - 1] == list(range(1, c.n_wires)) and len(set(names)) == len(names)
+    assert all(0 < x < c.n_wires or x == -1 for x in wires[c.n_wires - 1:])
     assert names[:2] == ["main.len", "main.nextPos"] and names[2] == "main.pos"     # circom's main order
     assert names[3:10] == [f"main.bytes[{i}]" for i in range(7)]
 
@@ -108,6 +111,8 @@ def test_write_artifacts(tmp_path):
     out = nzcplive.write_artifacts(str(tmp_path), params=dict(nzcpgen.EXAMPLE), name="nzcp_example")
     prog, sym = open(out["program"], "rb").read(), open(out["sym"], "rb").read()
     rd = r1.read_r1cs(open(out["r1cs"], "rb").read())
-    assert rd["nWires"] == wvm.parse(prog)["n_wires"] == len(sym.splitlines()) + 1
+    wires = {int(x.split(b",")[1]) for x in sym.splitlines()}
+    assert rd["nWires"] == wvm.parse(prog)["n_wires"] == max(wires) + 1
+    assert wires == set(range(1, rd["nWires"])) | {-1}     # every wire named; substituted signals -1
     same = nzcb.wprog_remap(prog, sym, sym)
     assert wvm.parse(same)["wmap"] == list(range(rd["nWires"]))
