@@ -23,9 +23,11 @@
  *                 bit-exact proofs for tests; zero blinding is NOT zero-knowledge.
  *
  * This header is the product ABI. Kernel-level entry points for tests,
- * microbenchmarks and tuning (nzcb_engine_*, the synthetic-circuit setup, kernel timing,
- * the pairing-round knob) are in nzcb_internal.h: they are exported by the same library but
- * are not part of the drop-in boundary and may change between releases.
+ * microbenchmarks and tuning (nzcb_engine_*, the synthetic-circuit setup, kernel timing)
+ * are in nzcb_internal.h: they are exported by the same library but are not part of the
+ * drop-in boundary and may change between releases. Until round 3 they were declared here;
+ * code that used them through this header compiles with -DNZCB_WITH_INTERNAL (this header
+ * then includes nzcb_internal.h) or includes nzcb_internal.h itself.
  */
 #ifndef NZCB_H
 #define NZCB_H
@@ -341,5 +343,8 @@ void nzcb_msm_table_destroy(nzcb_msm_table* t);
 
 #ifdef __cplusplus
 }
+#endif
+#ifdef NZCB_WITH_INTERNAL  /* the pre-round-4 declarations (source compatibility) */
+#include "nzcb_internal.h"
 #endif
 #endif

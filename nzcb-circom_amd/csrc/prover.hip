@@ -230,6 +230,27 @@ __device__ __forceinline__ Fr block_prod_excl_suffix(const Fr& v, Fr* sh) {
   return ex;
 }
 
+// exclusive suffix sum of v over the workgroup's threads, sum_{t' > t} v_t' (Kogge-Stone in
+// LDS, additions only); total = the sum of all kT values
+__device__ __forceinline__ Fr block_sum_excl_suffix(const Fr& v, Fr* sh, Fr& total) {
+  const int tid = threadIdx.x;
+  sh[tid] = v;
+  __syncthreads();
+  Fr acc = v;
+#pragma unroll 1
+  for (int d = 1; d < kT; d <<= 1) {
+    const Fr o = tid + d < kT ? sh[tid + d] : Fr::zero();
+    __syncthreads();
+    acc = acc + o;
+    sh[tid] = acc;
+    __syncthreads();
+  }
+  total = sh[0];
+  const Fr ex = tid + 1 < kT ? sh[tid + 1] : Fr::zero();
+  __syncthreads();
+  return ex;
+}
+
 // Round 2 without a single inversion per element or per workgroup:
 //   Z_i = prod_{k<i} num_k / den_k = (prod_{k<i} num_k) (prod_{k>=i} den_k) / prod_k den_k,
 // with num_i = (a + b w^i + g)(b + k1 b w^i + g)(c + k2 b w^i + g) and
@@ -304,13 +325,14 @@ k_perm_tile(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __rest
   }
 }
 
-// F_T = (prod_{T'<T} N_T') (prod_{T'>T} D_T') / prod D (one workgroup; each thread a run of
-// consecutive tiles); totals[0] = prod N, totals[1] = prod D (round 2's copy-constraint check)
+// F_T = (prod_{T'<T} N_T') (prod_{T'>T} D_T') (one workgroup; each thread a run of
+// consecutive tiles); totals[0] = prod N, totals[1] = prod D (round 2's copy-constraint check).
+// 1 / prod D is the host's (Prover::prove reads the totals for the check anyway): a
+// single-lane Fermat inversion here was most of this kernel's 0.6 ms.
 __global__ void __launch_bounds__(1024)
 k_perm_factors(const Fr* __restrict__ ntot, const Fr* __restrict__ dtot, int ntiles, Fr* __restrict__ F,
                Fr* __restrict__ totals) {
   __shared__ Fr sh[1024];
-  __shared__ Fr inv_d;
   const int tid = threadIdx.x;
   const int per = (ntiles + 1023) / 1024;
   const int t0 = min(tid * per, ntiles), t1 = min(t0 + per, ntiles);
@@ -345,13 +367,11 @@ k_perm_factors(const Fr* __restrict__ ntot, const Fr* __restrict__ dtot, int nti
   const Fr dall = sh[0];
   const Fr dsuf = tid + 1 < 1024 ? sh[tid + 1] : Fr::one();
   if (tid == 0) {
-    inv_d = inverse(dall);
     totals[0] = nall;
     totals[1] = dall;
   }
-  __syncthreads();
   // within the run: prefix of N (forward), suffix of D (backward)
-  Fr run = npre * inv_d;
+  Fr run = npre;
   for (int t = t0; t < t1; t++) {
     F[t] = run;
     run = run * ntot[t];
@@ -363,64 +383,59 @@ k_perm_factors(const Fr* __restrict__ ntot, const Fr* __restrict__ dtot, int nti
   }
 }
 
-// Z[i] *= F[i / kTileN] (coalesced)
+// Z[i] *= F[i / kTileN] / prod D (coalesced)
 __global__ void __launch_bounds__(kT)
-k_apply_tiles(Fr* __restrict__ x, size_t m, const Fr* __restrict__ F) {
+k_apply_tiles(Fr* __restrict__ x, size_t m, const Fr* __restrict__ F, Fr inv_d) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
-  x[i] = x[i] * F[i / kTileN];
+  x[i] = x[i] * (F[i / kTileN] * inv_d);
 }
 
 // Round 5's divPol1: y_i = x_i + d y_{i+1} over i < m, x_i =
 // src[i + 1] (x_{m-1} = 0), y_m = 0, by tiles. Each thread runs the recurrence over its
-// kPer elements, the workgroup combines the thread heads h_t by a Kogge-Stone suffix scan
-// Y_t += D^(2^s) Y_(t+2^s) (D = d^kPer), and the tile's carry-in Y (the true y at the next
-// tile's first element) seeds the last thread. Two passes: kWrite = false writes only the
-// tile heads (carry-in 0), which a small scan turns into the true carries; kWrite = true
-// recomputes the tile with its carry and writes y (x is read twice instead of y written,
-// read and written again by a fix-up pass).
+// kPer elements (head h_t = sum_j x_(kPer t + j) d^j). Across the threads the recurrence is
+// a weighted suffix sum: the true y at thread t's first element is
+//   Y_t = d^(-kPer t) (sum_(t' >= t) h_t' d^(kPer t') + c d^kTileN)
+// with c the tile's carry-in (the true y at the next tile's first element), so with the
+// tables P[t] = d^(kPer t), Pinv[t] = d^(-kPer t) (LinTab, built on the host once per d)
+// the scan is of additions: two products per thread instead of two per Kogge-Stone step
+// (round 3's multiplicative scan, 16 products per thread). Two passes: kWrite = false writes
+// the tile heads (c = 0), which a small scan turns into the true carries; kWrite = true
+// recomputes the tile with its carry and writes y. d = 0 (y = x) works with Pinv = 0.
+struct LinTab {
+  Fr P[kT + 1];     // d^(kPer t)
+  Fr Pinv[kT + 1];  // d^(-kPer t) (0 for t > 0 when d = 0)
+  Fr dp[kPer + 1];  // d^j
+};
+static_assert(sizeof(LinTab) % sizeof(Fr) == 0, "LinTab is stored as Fr words");
+
 template <bool kWrite>
 __global__ void __launch_bounds__(kT)
-k_lin_tile(const Fr* __restrict__ src, size_t m, Fr d, const Fr* __restrict__ carry, Fr* __restrict__ out) {
+k_lin_tile(const Fr* __restrict__ src, size_t m, const LinTab* __restrict__ tab, const Fr* __restrict__ carry,
+           Fr* __restrict__ out) {
   __shared__ uint32_t stg[kStageWords];
   __shared__ Fr sh[kT];
   const int tid = threadIdx.x;
   const size_t base = (size_t)blockIdx.x * kTileN;
   Fr x[kPer];
   stage_in([&](size_t g) { return src[g + 1]; }, base, m - 1, stg, x);
-  Fr dp[kPer + 1];  // d^0 .. d^kPer
-  dp[0] = Fr::one();
-#pragma unroll
-  for (int j = 1; j <= kPer; j++) dp[j] = dp[j - 1] * d;
+  const Fr d = tab->dp[1];
   Fr y = Fr::zero();
-  if (kWrite && tid == kT - 1 && carry) y = carry[blockIdx.x + 1];
 #pragma unroll
   for (int j = kPer - 1; j >= 0; j--) {
     y = x[j] + d * y;
     x[j] = y;
   }
-  // suffix scan of the heads: Y_t = h_t + D Y_(t+1)
-  Fr D = dp[kPer];
-  sh[tid] = y;
-  __syncthreads();
-#pragma unroll 1
-  for (int s = 1; s < kT; s <<= 1) {
-    const Fr o = tid + s < kT ? sh[tid + s] : Fr::zero();
-    __syncthreads();
-    y = y + D * o;
-    sh[tid] = y;
-    __syncthreads();
-    D = sqr(D);
-  }
+  Fr total;
+  Fr ex = block_sum_excl_suffix(y * tab->P[tid], sh, total);
   if (!kWrite) {
-    if (tid == 0) out[blockIdx.x] = y;
+    if (tid == 0) out[blockIdx.x] = total;
     return;
   }
-  // the true y of this thread's elements: local + d^(kPer - j) Y_(t+1)
-  const Fr next = tid + 1 < kT ? sh[tid + 1] : Fr::zero();
+  if (carry) ex = ex + carry[blockIdx.x + 1] * tab->P[kT];
+  const Fr next = ex * tab->Pinv[tid + 1];  // the true y at element kPer (t + 1) of the tile
 #pragma unroll
-  for (int j = 0; j < kPer; j++) x[j] = x[j] + dp[kPer - j] * next;
-  __syncthreads();
+  for (int j = 0; j < kPer; j++) x[j] = x[j] + tab->dp[kPer - j] * next;
   stage_out(x, base, m, stg, out);
 }
 
@@ -693,7 +708,7 @@ k_t_combine(const Fr* __restrict__ V, size_t n, T3Args a, Fr* __restrict__ t) {
   t[k] = sm + v12 - im;
   t[n + k] = dl * a.two_over_d;
   t[2 * n + k] = (sm - v12 + im) * a.inv_d2;
-  t[3 * n + k] = k < 6 ? a.q3[k] : Fr::zero();
+  if (k < 6) t[3 * n + k] = a.q3[k];  // t has 3n + 6 coefficients (its buffer no more)
 }
 
 // x <- x * 2^e (mod r), canonical in and out: the exponent pre-scaling of kQ29
@@ -1068,15 +1083,18 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   table(g_hi, nhi, pow_u64(g, 4096), one);
   table(gi_lo, nlo, gi, one);
   table(gi_hi, nhi, pow_u64(gi, 4096), one);
-  {  // full per-index coset factors for the NTT prologue (g^j, j < n + 8) and the
-     // quotient iNTT's epilogue (g^-j / 4n, j < 4n)
+  quot3 = quot3_enabled() && nPublic <= kQ29MaxPub && power >= 6;
+  {  // full per-index coset factors for the NTT prologue (g^j, j < n + 8) and the 4n
+     // quotient iNTT's epilogue (g^-j / 4n, j < 4n; not needed by the three-coset quotient)
     const Fr two = one + one;
     g29.alloc((size_t)n + 8);
-    gi29.alloc(n4);
     hipLaunchKernelGGL(k_factor29_table, dim3(grid_for((size_t)n + 8, kT, 1u << 30)), dim3(kT), 0, s, g29.p, g_lo.p,
                        g_hi.p, one, (size_t)n + 8);
-    hipLaunchKernelGGL(k_factor29_table, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, gi29.p, gi_lo.p, gi_hi.p,
-                       inverse(pow_u64(two, (uint64_t)power + 2)), (size_t)n4);
+    if (!quot3) {
+      gi29.alloc(n4);
+      hipLaunchKernelGGL(k_factor29_table, dim3(grid_for(n4, kT, 1u << 30)), dim3(kT), 0, s, gi29.p, gi_lo.p,
+                         gi_hi.p, inverse(pow_u64(two, (uint64_t)power + 2)), (size_t)n4);
+    }
     NZ_HIP(hipGetLastError());
   }
   {
@@ -1086,7 +1104,6 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
       p = p * w4n;
     }
   }
-  quot3 = quot3_enabled() && nPublic <= kQ29MaxPub && power >= 6;
   alloc_workspace();
   if (quot3) {  // three-coset quotient: per-coset twists c_j^k and untwists c_j^-k / 4n, j < 3
     const size_t nhi3 = (n + 4095) / 4096;
@@ -1187,12 +1204,17 @@ void Prover::alloc_workspace() {
   wtns_in.alloc(nWit ? nWit : 1);
   A.alloc(n + 2); B.alloc(n + 2); C.alloc(n + 2); Z.alloc(n);
   pol_a.alloc(n + 2); pol_b.alloc(n + 2); pol_c.alloc(n + 2); pol_z.alloc(n + 3);
-  A4.alloc(n4); B4.alloc(n4); C4.alloc(n4); Z4.alloc(n4);
-  T.alloc(n4); Tz.alloc(n4); t.alloc(n4);
+  // coset evaluations and the quotient: 3n under the three-coset quotient (T also holds
+  // round 5's n + 6 Wxi numerator, t the 3n + 6 quotient coefficients), 4n otherwise
+  const size_t ne = quot3 ? (size_t)3 * n : n4;
+  A4.alloc(ne); B4.alloc(ne); C4.alloc(ne); Z4.alloc(ne);
+  T.alloc(ne); Tz.alloc(ne); t.alloc(quot3 ? ne + 6 : n4);
   pol_r.alloc(n + 3); pol_wxi.alloc(n + 6); pol_wxiw.alloc(n + 3);
   blind.alloc(13);  // b1..b11 (index 0 unused), then the 32-bit check flags in slot 12
   // tile totals / heads (n / kTileN + 2) and the small scans' levels over them
   scan_tmp.alloc(3 * ((size_t)n / kTileN + 2) + 4096);
+  lin_tab.alloc(2 * sizeof(LinTab) / sizeof(Fr));  // round 5's divPol1 tables (d = xi, xi w)
+  lin_host.resize(2 * sizeof(LinTab) / sizeof(Fr));
   size_t nblocks = ((size_t)3 * n + 6 + (size_t)kT * kEvalChunk2 - 1) / ((size_t)kT * kEvalChunk2) + 1;
   eval_part.alloc((size_t)kEvalMax * nblocks + kEvalMax);  // eval_many: kEvalMax rows + results
   host_part.resize(std::max<size_t>(nblocks, kEvalMax));
@@ -1469,7 +1491,8 @@ void Prover::set_msm_split(int world, size_t own_points, nzcb_msm_send_fn send, 
   split_own = own_points;
 }
 
-void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out) {
+void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out,
+                       const std::function<void()>& overlap) {
   if (np < 1 || np > kEvalMax) throw Error(NZCB_ERR_INTERNAL, "eval_many: bad count");
   hipStream_t s = st();
   EvalSet es{};
@@ -1495,6 +1518,7 @@ void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const
   hipLaunchKernelGGL(k_eval_comb, dim3(np), dim3(1024), 0, s, es, (const Fr*)eval_part.p, (int)nblocks, res);
   NZ_HIP(hipGetLastError());
   NZ_HIP(hipMemcpyAsync(host_part.data(), res, np * sizeof(Fr), hipMemcpyDeviceToHost, s));
+  if (overlap) overlap();  // host work beside the evaluation kernels
   NZ_HIP(hipStreamSynchronize(s));
   for (int j = 0; j < np; j++) out[j] = host_part[j];
 }
@@ -1528,16 +1552,34 @@ void Prover::suffix_linear(Fr* x, size_t m, const Fr& d, Fr* level_tmp) {
   NZ_HIP(hipGetLastError());
 }
 
-void Prover::div_pol1(const Fr* src, size_t m, const Fr& d, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit) {
+// divPol1's power tables for d (k_lin_tile's LinTab) into slot k of lin_tab: host products,
+// uploaded on the prover's stream (round 4 builds both while its evaluations run)
+void Prover::lin_tables(int k, const Fr& d) {
+  LinTab& t = ((LinTab*)lin_host.data())[k];
+  t.dp[0] = Fr::one();
+  for (int j = 1; j <= kPer; j++) t.dp[j] = t.dp[j - 1] * d;
+  const Fr dk = t.dp[kPer], dki = inverse(dk);  // inverse(0) = 0: Pinv = 0 past t = 0
+  t.P[0] = t.Pinv[0] = Fr::one();
+  for (int i = 1; i <= kT; i++) {
+    t.P[i] = t.P[i - 1] * dk;
+    t.Pinv[i] = t.Pinv[i - 1] * dki;
+  }
+  NZ_HIP(hipMemcpyAsync((LinTab*)lin_tab.p + k, &t, sizeof(LinTab), hipMemcpyHostToDevice, st()));
+}
+
+void Prover::div_pol1(const Fr* src, size_t m, int tab, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit) {
   hipStream_t s = st();
   const size_t ntiles = (m + kTileN - 1) / kTileN;
+  const LinTab* lt = (const LinTab*)lin_tab.p + tab;
+  const LinTab& ht = ((const LinTab*)lin_host.data())[tab];
   Fr* heads = scan_tmp.p;  // ntiles + 1 (the last one 0: the carry into the last tile)
   NZ_HIP(hipMemsetAsync(heads + ntiles, 0, sizeof(Fr), s));
-  hipLaunchKernelGGL(k_lin_tile<false>, dim3((unsigned)ntiles), dim3(kT), 0, s, src, m, d, (const Fr*)nullptr, heads);
+  hipLaunchKernelGGL(k_lin_tile<false>, dim3((unsigned)ntiles), dim3(kT), 0, s, src, m, lt, (const Fr*)nullptr, heads);
   NZ_HIP(hipGetLastError());
-  suffix_linear(heads, ntiles, pow_u64(d, kTileN), heads + ntiles + 1);  // true heads: H_T = h_T + d^N H_(T+1)
-  hipLaunchKernelGGL(k_lin_tile<true>, dim3((unsigned)ntiles), dim3(kT), 0, s, src, m, d, (const Fr*)heads, dst);
-  hipLaunchKernelGGL(k_div_check, dim3(1), dim3(64), 0, s, src, p0_adjust, dst, d, flags.p, flag_bit);
+  // true heads: H_T = h_T + d^kTileN H_(T+1)
+  suffix_linear(heads, ntiles, ht.P[kT], heads + ntiles + 1);
+  hipLaunchKernelGGL(k_lin_tile<true>, dim3((unsigned)ntiles), dim3(kT), 0, s, src, m, lt, (const Fr*)heads, dst);
+  hipLaunchKernelGGL(k_div_check, dim3(1), dim3(64), 0, s, src, p0_adjust, dst, ht.dp[1], flags.p, flag_bit);
   NZ_HIP(hipGetLastError());
 }
 
@@ -1731,14 +1773,15 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
                        root_lo.p, root_hi.p, pa, Z.p, ntot, dtot);
     hipLaunchKernelGGL(k_perm_factors, dim3(1), dim3(1024), 0, s, (const Fr*)ntot, (const Fr*)dtot, (int)ntiles,
                        fac, totals);
-    hipLaunchKernelGGL(k_apply_tiles, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, Z.p, (size_t)n,
-                       (const Fr*)fac);
     NZ_HIP(hipGetLastError());
-    // Z[n] = prod num / prod den must be 1
+    // Z[n] = prod num / prod den must be 1; 1 / prod den scales the tiles
     Fr tt[2];
     NZ_HIP(hipMemcpyAsync(tt, totals, sizeof(tt), hipMemcpyDeviceToHost, s));
     NZ_HIP(hipStreamSynchronize(s));
     if (tt[0] != tt[1]) throw Error(NZCB_ERR_COPY, "Copy constraints does not match");
+    hipLaunchKernelGGL(k_apply_tiles, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, Z.p, (size_t)n,
+                       (const Fr*)fac, inverse(tt[1]));
+    NZ_HIP(hipGetLastError());
     const int bz[3] = {9, 8, 7};
     NZ_HIP(hipStreamWaitEvent(s, side_done, 0));  // A, B, C's NTTs (same scratch) are done
     // Z's commitment needs only its coefficients: its MSM starts before the 4n coset NTT,
@@ -1833,7 +1876,11 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       const size_t lens[7] = {n + 2, n + 2, n + 2, n, n, 3 * (size_t)n + 6, n + 3};
       const Fr xs[7] = {xi, xi, xi, xi, xi, xi, xi * wn};
       Fr ev[7];
-      eval_many(7, polys, lens, xs, ev);
+      // round 5's divPol1 tables (d = xi, xi w) on the host while the evaluations run
+      eval_many(7, polys, lens, xs, ev, [&] {
+        lin_tables(0, xi);
+        lin_tables(1, xi * wn);
+      });
       ea = ev[0];
       eb = ev[1];
       ec = ev[2];
@@ -1899,10 +1946,10 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     hipLaunchKernelGGL(k_pol_wxi, dim3(grid_for(n + 6, kT, 1u << 30)), dim3(kT), 0, s, t.p, pol_r.p, pol_a.p,
                        pol_b.p, pol_c.p, sigma.p, sigma.p + 5 * (size_t)n, (size_t)n, wa, T.p);
     NZ_HIP(hipGetLastError());
-    div_pol1(T.p, n + 6, xi, Fr::zero(), pol_wxi.p, 4u);
+    div_pol1(T.p, n + 6, 0, Fr::zero(), pol_wxi.p, 4u);
     lg("multiexp Wxi");
     commit_start(0, pol_wxi.p, n + 6);
-    div_pol1(pol_z.p, n + 3, xi * wn, ezw, pol_wxiw.p, 4u);
+    div_pol1(pol_z.p, n + 3, 1, ezw, pol_wxiw.p, 4u);
     lg("multiexp Wxiw");
     commit_start(1, pol_wxiw.p, n + 3);
     uint32_t f = 0;
