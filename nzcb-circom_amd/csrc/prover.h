@@ -88,7 +88,9 @@ struct Prover {
   DevBuf<Fr> pol_r, pol_wxi, pol_wxiw;    // n+3, n+6, n+3
   DevBuf<Fr> blind;               // 12 (index 0 unused)
   DevBuf<Fr> scan_tmp;            // tile totals / heads of the round-2 and round-5 scans, and their levels
-  DevBuf<Fr> lin_tab;             // 2 x LinTab (prover.hip): divPol1's power tables for xi, xi w
+  DevBuf<Fr> lin_tab;             // 2 x LinTab (prover.hip) + tile powers: divPol1's tables for xi, xi w
+  size_t lin_qn = 0;              // tile-power entries per table (n / kTileN + 3)
+  Fr* lin_tile_pows(int k);       // Q then Qinv of slot k
   std::vector<Fr> lin_host;       // their host copies (Fr-sized words)
   DevBuf<Fr> eval_part;           // partial sums of polynomial evaluations
   DevBuf<uint32_t> flags;
@@ -133,8 +135,6 @@ struct Prover {
   // np <= 8 evaluations p_j(x_j) (two launches, one host round trip)
   void eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out,
                  const std::function<void()>& overlap = nullptr);
-  void prefix_product(Fr* x, size_t m, Fr* level_tmp);
-  void suffix_linear(Fr* x, size_t m, const Fr& d, Fr* level_tmp);
   // y_i = x_i + d y_(i+1) with d from lin_tables slot `tab` (round 4 builds slots 0, 1 = xi, xi w)
   void div_pol1(const Fr* src, size_t m, int tab, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit);
   void lin_tables(int k, const Fr& d);

@@ -30,7 +30,6 @@ namespace nzcb {
 
 static constexpr int kT = 256;
 static constexpr uint32_t kZeroRef = 0xffffffffu;
-static constexpr int kScanChunk = 32;
 
 // ----------------------------------------------------------------------------
 // kernels
@@ -128,7 +127,7 @@ static F29 fr29_operand(Fr c) {
 // 32-byte elements) on the HBM side, and with one word of padding per 4 elements (word
 // 8 e + e / 4 + w) both the coalesced pass and the per-thread pass hit 32 distinct banks per
 // 32-lane half for kPer = 2 and 4 (ds_read_b32 / ds_write_b32 bank by (a / 4) mod 32).
-// The chunk-per-thread scans these replace (kScanChunk = 32 elements per thread read
+// The chunk-per-thread scans these replace (32 elements per thread read
 // straight from HBM, 1 KB apart per lane) ran at 0.06-0.3 of the HBM rate.
 // kPer = 4 (175 VGPRs, no scratch, 2 waves per SIMD) against 2 (132 VGPRs, 48 B of scratch
 // in k_perm_tile): bench +0.9 % on one box (profiles/r4_window_ab.txt); -DNZ_KPER=2 for A/B
@@ -290,8 +289,14 @@ k_perm_tile(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __rest
     if (k == 2) col = C;
     stage_use([&](size_t g) { return col[g]; }, base, n, stg,
               [&](int j, const Fr& x) {
-                Fr kbw = perm_bw(rlo, rhi, e0 + j, n, op);
-                if (k23 && k) kbw = k == 1 ? kbw + kbw : kbw + kbw + kbw;
+                // b w^i once per element when k1, k2 = 2, 3 (v[] holds it until the scans)
+                Fr kbw;
+                if (k23 && k) {
+                  kbw = k == 1 ? v[j] + v[j] : v[j] + v[j] + v[j];
+                } else {
+                  kbw = perm_bw(rlo, rhi, e0 + j, n, op);
+                  if (k23) v[j] = kbw;
+                }
                 const Fr f = x + kbw + gamma;
                 num[j] = k ? num[j] * f : f;
                 u[j] = x + gamma;
@@ -407,6 +412,8 @@ struct LinTab {
   Fr Pinv[kT + 1];  // d^(-kPer t) (0 for t > 0 when d = 0)
   Fr dp[kPer + 1];  // d^j
 };
+// ... and per tile T (Prover::lin_tables, after the LinTab): Q[T] = D^T, Qinv[T] = D^(-T) with
+// D = d^kTileN, so the tile heads h_T chain the same way: H_T = Qinv[T] sum_(T' >= T) h_T' Q[T']
 static_assert(sizeof(LinTab) % sizeof(Fr) == 0, "LinTab is stored as Fr words");
 
 template <bool kWrite>
@@ -429,7 +436,7 @@ k_lin_tile(const Fr* __restrict__ src, size_t m, const LinTab* __restrict__ tab,
   Fr total;
   Fr ex = block_sum_excl_suffix(y * tab->P[tid], sh, total);
   if (!kWrite) {
-    if (tid == 0) out[blockIdx.x] = total;
+    if (tid == 0) out[blockIdx.x] = total;  // h_T
     return;
   }
   if (carry) ex = ex + carry[blockIdx.x + 1] * tab->P[kT];
@@ -439,96 +446,57 @@ k_lin_tile(const Fr* __restrict__ src, size_t m, const LinTab* __restrict__ tab,
   stage_out(x, base, m, stg, out);
 }
 
+// Q[T] = D^T and Qinv[T] = Di^T for T < count (square-and-multiply per thread)
+__global__ void k_pow_tiles(Fr D, Fr Di, int count, Fr* __restrict__ Q, Fr* __restrict__ Qinv) {
+  const int T = blockIdx.x * blockDim.x + threadIdx.x;
+  if (T >= count) return;
+  Fr a = Fr::one(), b = Fr::one(), pa = D, pb = Di;
+  for (int e = T; e; e >>= 1) {
+    if (e & 1) {
+      a = a * pa;
+      b = b * pb;
+    }
+    pa = sqr(pa);
+    pb = sqr(pb);
+  }
+  Q[T] = a;
+  Qinv[T] = b;
+}
+
+// the true tile heads from the tile-local ones: H_T = Qinv[T] sum_(T' >= T) h_T' Q[T'] for
+// T < m, H_m = 0 (one workgroup: each thread a run of tiles, then a suffix sum of additions
+// over the threads); h[T] is replaced by H_T
+__global__ void __launch_bounds__(1024) k_tile_heads(Fr* __restrict__ h, int m, const Fr* __restrict__ Q,
+                                                     const Fr* __restrict__ Qinv) {
+  __shared__ Fr sh[1024];
+  const int tid = threadIdx.x;
+  const int per = (m + 1023) / 1024;
+  const int t0 = min(tid * per, m), t1 = min(t0 + per, m);
+  Fr run = Fr::zero();
+  for (int T = t0; T < t1; T++) run = run + h[T] * Q[T];
+  // exclusive suffix sum of the runs over the threads
+  sh[tid] = run;
+  __syncthreads();
+  Fr acc = run;
+  for (int d = 1; d < 1024; d <<= 1) {
+    const Fr o = tid + d < 1024 ? sh[tid + d] : Fr::zero();
+    __syncthreads();
+    acc = acc + o;
+    sh[tid] = acc;
+    __syncthreads();
+  }
+  Fr suf = tid + 1 < 1024 ? sh[tid + 1] : Fr::zero();
+  for (int T = t1 - 1; T >= t0; T--) {
+    suf = suf + h[T] * Q[T];
+    h[T] = suf * Qinv[T];
+  }
+  if (tid == 0) h[m] = Fr::zero();
+}
+
 // contiguous sigma_k(w^i) = the 4n evaluation at 4 i (once per context)
 __global__ void k_stride4(const Fr* __restrict__ src, size_t n, Fr* __restrict__ dst) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) dst[i] = src[4 * i];
-}
-
-// exclusive prefix products: chunk products, small single-block scan, apply
-__global__ void k_chunk_prod(const Fr* __restrict__ x, size_t m, Fr* __restrict__ out) {
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t s = t * kScanChunk;
-  if (s >= m) return;
-  size_t e = s + kScanChunk < m ? s + kScanChunk : m;
-  Fr p = Fr::one();
-  for (size_t i = s; i < e; i++) p = p * x[i];
-  out[t] = p;
-}
-
-// in place exclusive product scan of m <= 1024 values; total -> *total
-__global__ void __launch_bounds__(1024) k_scan_mul_small(Fr* x, int m, Fr* total) {
-  __shared__ Fr buf[1024];
-  int i = threadIdx.x;
-  Fr v = i < m ? x[i] : Fr::one();
-  buf[i] = v;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {
-    Fr o = (i >= d) ? buf[i - d] : Fr::one();
-    __syncthreads();
-    if (i >= d) buf[i] = buf[i] * o;
-    __syncthreads();
-  }
-  // buf[i] = inclusive product; exclusive = buf[i-1]
-  if (i < m) x[i] = (i == 0) ? Fr::one() : buf[i - 1];
-  if (i == 1023) *total = buf[1023];
-}
-
-__global__ void k_apply_prod(Fr* __restrict__ x, size_t m, const Fr* __restrict__ pref) {
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t s = t * kScanChunk;
-  if (s >= m) return;
-  size_t e = s + kScanChunk < m ? s + kScanChunk : m;
-  Fr p = pref[t];
-  for (size_t i = s; i < e; i++) {
-    Fr v = x[i];
-    x[i] = p;
-    p = p * v;
-  }
-}
-
-// suffix linear recurrence y_i = x_i + d*y_{i+1} (y_m = 0), chunk-local pass
-__global__ void k_lin_local(Fr* __restrict__ x, size_t m, Fr d, Fr* __restrict__ heads) {
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t s = t * kScanChunk;
-  if (s >= m) return;
-  size_t e = s + kScanChunk < m ? s + kScanChunk : m;
-  Fr y = Fr::zero();
-  for (size_t i = e; i-- > s;) {
-    y = x[i] + d * y;
-    x[i] = y;
-  }
-  heads[t] = y;
-}
-
-__global__ void __launch_bounds__(1024) k_lin_small(Fr* x, int m, Fr d) {
-  __shared__ Fr buf[1024];
-  int i = threadIdx.x;
-  buf[i] = i < m ? x[i] : Fr::zero();
-  Fr dk = d;
-  __syncthreads();
-  for (int k = 1; k < 1024; k <<= 1) {
-    Fr o = (i + k < 1024) ? buf[i + k] : Fr::zero();
-    __syncthreads();
-    buf[i] = buf[i] + dk * o;
-    dk = sqr(dk);
-    __syncthreads();
-  }
-  if (i < m) x[i] = buf[i];
-}
-
-// add the carry from the next chunk: y_i += d^(e-i) * Y_e
-__global__ void k_lin_apply(Fr* __restrict__ x, size_t m, Fr d, const Fr* __restrict__ heads, size_t nheads) {
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t s = t * kScanChunk;
-  if (s >= m || t + 1 >= nheads) return;
-  size_t e = s + kScanChunk < m ? s + kScanChunk : m;
-  Fr carry = heads[t + 1];
-  Fr pw = d;
-  for (size_t i = e; i-- > s;) {
-    x[i] = x[i] + pw * carry;
-    pw = pw * d;
-  }
 }
 
 struct QArgs {
@@ -1212,8 +1180,10 @@ void Prover::alloc_workspace() {
   pol_r.alloc(n + 3); pol_wxi.alloc(n + 6); pol_wxiw.alloc(n + 3);
   blind.alloc(13);  // b1..b11 (index 0 unused), then the 32-bit check flags in slot 12
   // tile totals / heads (n / kTileN + 2) and the small scans' levels over them
-  scan_tmp.alloc(3 * ((size_t)n / kTileN + 2) + 4096);
-  lin_tab.alloc(2 * sizeof(LinTab) / sizeof(Fr));  // round 5's divPol1 tables (d = xi, xi w)
+  scan_tmp.alloc(3 * ((size_t)n / kTileN + 2) + 64);
+  // round 5's divPol1 tables (d = xi, xi w): 2 LinTab, then per d the tile powers Q, Qinv
+  lin_qn = (size_t)n / kTileN + 3;
+  lin_tab.alloc(2 * sizeof(LinTab) / sizeof(Fr) + 4 * lin_qn);
   lin_host.resize(2 * sizeof(LinTab) / sizeof(Fr));
   size_t nblocks = ((size_t)3 * n + 6 + (size_t)kT * kEvalChunk2 - 1) / ((size_t)kT * kEvalChunk2) + 1;
   eval_part.alloc((size_t)kEvalMax * nblocks + kEvalMax);  // eval_many: kEvalMax rows + results
@@ -1523,35 +1493,6 @@ void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const
   for (int j = 0; j < np; j++) out[j] = host_part[j];
 }
 
-void Prover::prefix_product(Fr* x, size_t m, Fr* level_tmp) {
-  hipStream_t s = st();
-  if (m <= 1024) {
-    hipLaunchKernelGGL(k_scan_mul_small, dim3(1), dim3(1024), 0, s, x, (int)m, level_tmp + 1024);
-    NZ_HIP(hipGetLastError());
-    return;
-  }
-  size_t nc = (m + kScanChunk - 1) / kScanChunk;
-  hipLaunchKernelGGL(k_chunk_prod, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, level_tmp);
-  prefix_product(level_tmp, nc, level_tmp + nc);
-  hipLaunchKernelGGL(k_apply_prod, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, level_tmp);
-  NZ_HIP(hipGetLastError());
-}
-
-void Prover::suffix_linear(Fr* x, size_t m, const Fr& d, Fr* level_tmp) {
-  hipStream_t s = st();
-  if (m <= 1024) {
-    hipLaunchKernelGGL(k_lin_small, dim3(1), dim3(1024), 0, s, x, (int)m, d);
-    NZ_HIP(hipGetLastError());
-    return;
-  }
-  size_t nc = (m + kScanChunk - 1) / kScanChunk;
-  hipLaunchKernelGGL(k_lin_local, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, d, level_tmp);
-  // heads obey Y_c = h_c + d^K * Y_{c+1}
-  suffix_linear(level_tmp, nc, pow_u64(d, kScanChunk), level_tmp + nc);
-  hipLaunchKernelGGL(k_lin_apply, dim3(grid_for(nc, kT, 1u << 30)), dim3(kT), 0, s, x, m, d, level_tmp, nc);
-  NZ_HIP(hipGetLastError());
-}
-
 // divPol1's power tables for d (k_lin_tile's LinTab) into slot k of lin_tab: host products,
 // uploaded on the prover's stream (round 4 builds both while its evaluations run)
 void Prover::lin_tables(int k, const Fr& d) {
@@ -1565,19 +1506,26 @@ void Prover::lin_tables(int k, const Fr& d) {
     t.Pinv[i] = t.Pinv[i - 1] * dki;
   }
   NZ_HIP(hipMemcpyAsync((LinTab*)lin_tab.p + k, &t, sizeof(LinTab), hipMemcpyHostToDevice, st()));
+  Fr* q = lin_tile_pows(k);
+  const int qn = (int)lin_qn;
+  hipLaunchKernelGGL(k_pow_tiles, dim3((qn + 255) / 256), dim3(256), 0, st(), t.P[kT], t.Pinv[kT], qn, q, q + qn);
+  NZ_HIP(hipGetLastError());
 }
+
+Fr* Prover::lin_tile_pows(int k) { return lin_tab.p + 2 * sizeof(LinTab) / sizeof(Fr) + (size_t)k * 2 * lin_qn; }
 
 void Prover::div_pol1(const Fr* src, size_t m, int tab, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit) {
   hipStream_t s = st();
   const size_t ntiles = (m + kTileN - 1) / kTileN;
   const LinTab* lt = (const LinTab*)lin_tab.p + tab;
   const LinTab& ht = ((const LinTab*)lin_host.data())[tab];
+  if (ntiles + 1 > lin_qn) throw Error(NZCB_ERR_INTERNAL, "divPol1: more tiles than its power tables");
   Fr* heads = scan_tmp.p;  // ntiles + 1 (the last one 0: the carry into the last tile)
-  NZ_HIP(hipMemsetAsync(heads + ntiles, 0, sizeof(Fr), s));
   hipLaunchKernelGGL(k_lin_tile<false>, dim3((unsigned)ntiles), dim3(kT), 0, s, src, m, lt, (const Fr*)nullptr, heads);
+  // true heads: H_T = h_T + d^kTileN H_(T+1), by the tile power tables (additions)
+  const Fr* q = lin_tile_pows(tab);
+  hipLaunchKernelGGL(k_tile_heads, dim3(1), dim3(1024), 0, s, heads, (int)ntiles, q, q + lin_qn);
   NZ_HIP(hipGetLastError());
-  // true heads: H_T = h_T + d^kTileN H_(T+1)
-  suffix_linear(heads, ntiles, ht.P[kT], heads + ntiles + 1);
   hipLaunchKernelGGL(k_lin_tile<true>, dim3((unsigned)ntiles), dim3(kT), 0, s, src, m, lt, (const Fr*)heads, dst);
   hipLaunchKernelGGL(k_div_check, dim3(1), dim3(64), 0, s, src, p0_adjust, dst, ht.dp[1], flags.p, flag_bit);
   NZ_HIP(hipGetLastError());

@@ -39,9 +39,12 @@ def main():
             ph = eng.time_msm_phases(bases, sc, n, True, fixed, args.reps)
             ms = ph["wall"]
             gbs = 96 * n / (ms / 1e3) / 1e9
-            phases = {k: round(v, 4) for k, v in ph.items() if k not in ("wall", "entries", "table_build")}
+            phases = {k: round(v, 4) for k, v in ph.items()
+                      if k not in ("wall", "entries", "table_build", "host_enqueue", "host_sort_call")}
             print(json.dumps({"kernel": "msm_fixed_base" if fixed else "msm", "log_n": lg, "ms": round(ms, 4),
                               "phases_ms": phases, "phase_sum_ms": round(sum(phases.values()), 4),
+                              "host_enqueue_ms": round(ph.get("host_enqueue", 0), 4),
+                              "host_sort_call_ms": round(ph.get("host_sort_call", 0), 4),
                               "table_build_ms": round(ph.get("table_build", 0), 2), "entries": int(ph.get("entries", 0)),
                               "points_per_s": round(n / (ms / 1e3), 1), "GBs": round(gbs, 1),
                               "frac": round(gbs / PEAK, 5)}), flush=True)
