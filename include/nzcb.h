@@ -127,7 +127,9 @@ int nzcb_prove_logged(nzcb_ctx* ctx, const void* witness, size_t n, int kind, co
 /* Proof lanes (default 1): each extra lane is a per-proof working set + streams on
  * the context's device (~6.5 GB at n = 2^21) sharing the HBM-resident proving key,
  * so nzcb_prove_batch keeps `lanes` proofs in flight and one proof's latency-bound
- * phases (Fiat-Shamir host steps, bucket reductions) overlap another's compute. */
+ * phases (Fiat-Shamir host steps, bucket reductions) overlap another's compute. A change
+ * of the count waits for the proofs in flight (it rebuilds the lane pool); setting the
+ * count the context already has returns at once. */
 int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err);
 int nzcb_ctx_lanes(const nzcb_ctx* ctx);
 

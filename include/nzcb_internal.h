@@ -71,7 +71,9 @@ int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table,
  * out[0] wall ms, out[1..7] keys, sort, offsets, accumulate, finalize, reduce, sums,
  * out[8] table build ms (fixed_base only), out[9] bucket entries per MSM (nonzero digits),
  * out[10] host ms per MSM from the device results' arrival to the affine result (the
- * window combination on the CPU: the Horner over the window slots). out holds 11 doubles. */
+ * window combination on the CPU: the Horner over the window slots), out[11] host ms of the
+ * enqueue (kernel launches), out[12] of which the library radix sort's host call (generic
+ * schedule). out holds 13 doubles. */
 int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
                           int fixed_base, int reps, double* out, nzcb_err* err);
 /* Field self-test helpers: out[i] = a[i] * b[i] (Montgomery, device), n elements. */

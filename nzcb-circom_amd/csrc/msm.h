@@ -66,7 +66,9 @@ struct MsmScratch {
   bool prof = false, prof_phases = false;
   double prof_ms = 0;
   double phase_ms[7] = {0, 0, 0, 0, 0, 0, 0};
-  double host_ms = 0;  // msm_finish's CPU part (prof_phases)
+  double host_ms = 0;          // msm_finish's CPU part (prof_phases)
+  double enqueue_ms = 0;       // msm_enqueue's host time (prof_phases)
+  double sort_host_ms = 0;     // of which the library radix sort's host call (generic schedule)
   uint64_t prof_launches = 0, prof_points = 0, prof_entries = 0;
   hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipEvent_t done = nullptr;  // recorded after the window sums' copy to host_win (msm_finish waits on it)

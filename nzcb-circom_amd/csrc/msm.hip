@@ -1369,6 +1369,15 @@ static void fixed_bucketing(MsmScratch& sc, const MsmPlan& p, const Fr* scalars,
 
 void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, bool mont, hipStream_t st,
                  const MsmBaseTable* table) {
+  const auto t_enq = std::chrono::steady_clock::now();
+  struct EnqueueClock {  // host time of the enqueue, for the phase timing (nzcb_engine_time_msm2)
+    MsmScratch& sc;
+    std::chrono::steady_clock::time_point t0;
+    ~EnqueueClock() {
+      if (sc.prof && sc.prof_phases)
+        sc.enqueue_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+  } enqueue_clock{sc, t_enq};
   sc.cur_n = n;
   if (n == 0) return;
   if (!sc.done) NZ_HIP(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming));
@@ -1408,7 +1417,10 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     size_t tmp = sc.sort_tmp_bytes;
     int end_bit = 1;
     while ((1u << end_bit) <= p.nkeys) end_bit++;
+    const auto t_sort = std::chrono::steady_clock::now();
     radix_sort(sc.sort_tmp.p, tmp, sc.keys_in.p, sc.keys_out.p, sc.vals_in.p, sc.sorted.p, p.entries, end_bit, st);
+    if (phases)
+      sc.sort_host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sort).count();
     mark(2);
     hipLaunchKernelGGL(msm_offsets_kernel, dim3(grid_for((size_t)p.nkeys + 1, kMsmThreads, 1u << 30)),
                        dim3(kMsmThreads), 0, st, sc.keys_out.p, p.entries, p.nkeys, sc.offsets.p);

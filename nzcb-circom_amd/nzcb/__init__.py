@@ -334,13 +334,15 @@ class Engine:
     def time_msm_phases(self, dev_bases: int, dev_scalars: int, n: int, scalars_mont: bool, fixed_base: bool,
                         reps: int) -> dict:
         """Wall ms per MSM and HIP-event ms per phase (generic or fixed-base schedule)."""
-        out = (c_double * 11)()
+        out = (c_double * 13)()
         err = _Err()
         _check(self.lib.nzcb_engine_time_msm2(self.h, dev_bases, dev_scalars, n, int(scalars_mont), int(fixed_base),
                                               reps, out, ctypes.byref(err)), err)
         d = {"wall": out[0], "table_build": out[8], "entries": out[9]}
         d.update({k: out[1 + i] for i, k in enumerate(self.MSM_PHASES)})
         d["host_finish"] = out[10]
+        d["host_enqueue"] = out[11]     # host time, overlapping the device phases
+        d["host_sort_call"] = out[12]
         return d
 
     def msm_fixed_dev(self, dev_bases: int, n_table: int, dev_scalars: int, n: int, scalars_mont: bool) -> bytes:

@@ -42,10 +42,11 @@ def test_ntt(engine, log_n, inverse):
     assert got == want
 
 
-@pytest.mark.parametrize("log_n", [21, 23, 24])
+@pytest.mark.parametrize("log_n", [17, 18, 20, 21, 22, 23, 24])
 def test_ntt_full_size_properties(log_n):
-    """The prover's NTT sizes (n = 2^21, 4n = 2^23) and the top of BASELINE configs[1]
-    (2^24), size-independent properties on pseudo-random Montgomery inputs:
+    """The prover's NTT sizes (n = 2^21, 4n = 2^23), the top of BASELINE configs[1] (2^24)
+    and the other sizes of the two-pass plan (2048-element tiles, 17 <= log n <= 22),
+    size-independent properties on pseudo-random Montgomery inputs:
     iNTT(NTT(x)) = x bit-exactly; NTT(x)[0] = sum x; NTT(x)[n/2] = alternating sum;
     NTT(x)[1] and NTT(x)[n-1] against Horner at w and w^-1 (every twiddle contributes;
     at 2^21 and 2^24). All linear, so the checks run on the raw Montgomery values."""
