@@ -54,6 +54,41 @@ def test_repeat_proofs_same_context():
         assert proof.hex() == exp["proof_bin"]
 
 
+def test_concurrent_calls_on_lanes_bit_exact():
+    """Host threads proving on one context at the same time (the lane pool of
+    nzcb_prove_logged: each call takes a free lane, a fifth waits): every proof equals the
+    golden one, with the golden blinding and with a per-thread one against sequential
+    proofs; the lane count set again unchanged returns at once, as a Node caller does."""
+    import threading
+    meta, zkey, wtns = _gold("p8")
+    exp = meta["proofs"]["fixed"]
+    bl = bytes.fromhex(exp["blinding"])
+    ctx = nzcb.ProverContext(zkey)
+    try:
+        ctx.set_lanes(4)
+        others = [bytes([(k * 37 + i) % 251 for i in range(352)]) for k in range(5)]
+        want = [ctx.prove_raw(wtns, b)[0] for b in others]       # sequential
+        res, errs = {}, []
+
+        def worker(k):
+            try:
+                ctx.set_lanes(4)                                     # no change: returns at once
+                res[("gold", k)] = ctx.prove_raw(wtns, bl)[0]
+                res[("other", k)] = ctx.prove_raw(wtns, others[k])[0]
+            except Exception as e:  # noqa: BLE001 (reported below)
+                errs.append(e)
+        threads = [threading.Thread(target=worker, args=(k,)) for k in range(5)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(120)
+        assert not errs, errs
+        assert all(res[("gold", k)].hex() == exp["proof_bin"] for k in range(5))
+        assert [res[("other", k)] for k in range(5)] == want
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("power,seed,npub,nin", [(4, 11, 1, 2), (6, 12, 3, 5), (10, 13, 3, 8), (11, 14, 5, 16),
                                                  (7, 16, 8, 10), (7, 17, 10, 12)])
 def test_live_oracle(power, seed, npub, nin):
