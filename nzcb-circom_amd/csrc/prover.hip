@@ -189,65 +189,86 @@ __device__ __forceinline__ void stage_out(const Fr (&v)[kPer], size_t base, size
   __syncthreads();
 }
 
-// exclusive product scan of v over the workgroup's threads (Kogge-Stone in LDS, 8 steps);
-// total = the product of all kT values
+// Workgroup scans (exclusive, over the kT threads in thread order) in two levels: a
+// Kogge-Stone over each wave's 64 lanes by shuffles (no barrier), then the kT / 64 wave
+// totals through LDS (one barrier pair). Round 3's form, a Kogge-Stone over all kT threads in
+// LDS, paid two barriers per step (32 per product scan pair of k_perm_tile).
+__device__ __forceinline__ Fr shfl_fr(const Fr& v, int src) {
+  Fr o;
+#pragma unroll
+  for (int w = 0; w < 8; w++) o.v[w] = __shfl(v.v[w], src, 64);
+  return o;
+}
+struct MulOp {
+  __device__ Fr operator()(const Fr& a, const Fr& b) const { return a * b; }
+  __device__ static Fr id() { return Fr::one(); }
+};
+struct AddOp {
+  __device__ Fr operator()(const Fr& a, const Fr& b) const { return a + b; }
+  __device__ static Fr id() { return Fr::zero(); }
+};
+// kSuffix = false: op of v_t' over t' < t; true: over t' > t, for the NT threads of the
+// workgroup. sh: >= NT / 64 entries. *total (when given) = op over all NT values, valid in
+// thread 0. Up to 4 waves the wave totals are combined directly (wave-uniform branches); past
+// that the first wave scans them by shuffles (k_perm_factors' 16 waves).
+template <bool kSuffix, class Op, int NT = kT>
+__device__ __forceinline__ Fr block_scan_excl(const Fr& v, Fr* sh, Fr* total) {
+  constexpr int NW = NT / 64;
+  static_assert(NW >= 1 && NW <= 64 && NT % 64 == 0, "whole waves, at most 64");
+  const Op op;
+  const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+  Fr inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int src = kSuffix ? lane + d : lane - d;
+    const Fr o = shfl_fr(inc, src & 63);
+    if (kSuffix ? lane + d < 64 : lane >= d) inc = op(inc, o);
+  }
+  Fr ex = shfl_fr(inc, (kSuffix ? lane + 1 : lane - 1) & 63);
+  if (kSuffix ? lane == 63 : lane == 0) ex = Op::id();
+  if (kSuffix ? lane == 0 : lane == 63) sh[wv] = inc;  // the wave's total
+  __syncthreads();
+  if constexpr (NW <= 4) {
+#pragma unroll
+    for (int k = 0; k < NW; k++)  // wave-uniform: the other waves' totals on this side
+      if (kSuffix ? k > wv : k < wv) ex = op(ex, sh[k]);
+    if (total && threadIdx.x == 0) {
+      Fr t = sh[0];
+#pragma unroll
+      for (int k = 1; k < NW; k++) t = op(t, sh[k]);
+      *total = t;
+    }
+    __syncthreads();
+  } else {
+    Fr tot_all = Op::id();
+    if (wv == 0) {  // exclusive scan of the NW wave totals in lanes < NW, back into sh
+      Fr w = lane < NW ? sh[lane] : Op::id();
+#pragma unroll
+      for (int d = 1; d < NW; d <<= 1) {
+        const int src = kSuffix ? lane + d : lane - d;
+        const Fr o = shfl_fr(w, src & 63);
+        if (kSuffix ? lane + d < NW : (lane >= d && lane < NW)) w = op(w, o);
+      }
+      Fr wex = shfl_fr(w, (kSuffix ? lane + 1 : lane - 1) & 63);
+      if (kSuffix ? lane == NW - 1 : lane == 0) wex = Op::id();
+      tot_all = shfl_fr(w, kSuffix ? 0 : NW - 1);
+      if (lane < NW) sh[lane] = wex;  // no other wave reads sh before the barrier below
+    }
+    __syncthreads();
+    ex = op(ex, sh[wv]);
+    if (total && threadIdx.x == 0) *total = tot_all;
+    __syncthreads();
+  }
+  return ex;
+}
 __device__ __forceinline__ Fr block_prod_excl(const Fr& v, Fr* sh, Fr& total) {
-  const int tid = threadIdx.x;
-  sh[tid] = v;
-  __syncthreads();
-  Fr acc = v;
-#pragma unroll 1
-  for (int d = 1; d < kT; d <<= 1) {
-    const Fr o = tid >= d ? sh[tid - d] : Fr::one();
-    __syncthreads();
-    acc = acc * o;
-    sh[tid] = acc;
-    __syncthreads();
-  }
-  total = sh[kT - 1];
-  const Fr ex = tid ? sh[tid - 1] : Fr::one();
-  __syncthreads();
-  return ex;
+  return block_scan_excl<false, MulOp>(v, sh, &total);
 }
-
-// exclusive suffix product scan of v over the workgroup's threads (Kogge-Stone in LDS)
 __device__ __forceinline__ Fr block_prod_excl_suffix(const Fr& v, Fr* sh) {
-  const int tid = threadIdx.x;
-  sh[tid] = v;
-  __syncthreads();
-  Fr acc = v;
-#pragma unroll 1
-  for (int d = 1; d < kT; d <<= 1) {
-    const Fr o = tid + d < kT ? sh[tid + d] : Fr::one();
-    __syncthreads();
-    acc = acc * o;
-    sh[tid] = acc;
-    __syncthreads();
-  }
-  const Fr ex = tid + 1 < kT ? sh[tid + 1] : Fr::one();
-  __syncthreads();
-  return ex;
+  return block_scan_excl<true, MulOp>(v, sh, nullptr);
 }
-
-// exclusive suffix sum of v over the workgroup's threads, sum_{t' > t} v_t' (Kogge-Stone in
-// LDS, additions only); total = the sum of all kT values
 __device__ __forceinline__ Fr block_sum_excl_suffix(const Fr& v, Fr* sh, Fr& total) {
-  const int tid = threadIdx.x;
-  sh[tid] = v;
-  __syncthreads();
-  Fr acc = v;
-#pragma unroll 1
-  for (int d = 1; d < kT; d <<= 1) {
-    const Fr o = tid + d < kT ? sh[tid + d] : Fr::zero();
-    __syncthreads();
-    acc = acc + o;
-    sh[tid] = acc;
-    __syncthreads();
-  }
-  total = sh[0];
-  const Fr ex = tid + 1 < kT ? sh[tid + 1] : Fr::zero();
-  __syncthreads();
-  return ex;
+  return block_scan_excl<true, AddOp>(v, sh, &total);
 }
 
 // Round 2 without a single inversion per element or per workgroup:
@@ -272,7 +293,7 @@ k_perm_tile(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __rest
             const Fr* __restrict__ sig_h, size_t n, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi,
             PermArgs pa, Fr* __restrict__ Z, Fr* __restrict__ ntot, Fr* __restrict__ dtot) {
   __shared__ uint32_t stg[kStageWords];
-  __shared__ Fr sh[kT];
+  __shared__ Fr sh[kT / 64];  // the scans' wave totals
   const int tid = threadIdx.x;
   const size_t base = (size_t)blockIdx.x * kTileN;
   const size_t e0 = base + (size_t)kPer * tid;
@@ -337,7 +358,7 @@ k_perm_tile(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __rest
 __global__ void __launch_bounds__(1024)
 k_perm_factors(const Fr* __restrict__ ntot, const Fr* __restrict__ dtot, int ntiles, Fr* __restrict__ F,
                Fr* __restrict__ totals) {
-  __shared__ Fr sh[1024];
+  __shared__ Fr sh[1024 / 64];  // the scans' wave totals
   const int tid = threadIdx.x;
   const int per = (ntiles + 1023) / 1024;
   const int t0 = min(tid * per, ntiles), t1 = min(t0 + per, ntiles);
@@ -347,30 +368,9 @@ k_perm_factors(const Fr* __restrict__ ntot, const Fr* __restrict__ dtot, int nti
     pd = pd * dtot[t];
   }
   // exclusive prefix of pn, exclusive suffix of pd over the 1024 threads
-  Fr an = pn, ad = pd;
-  sh[tid] = an;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {
-    const Fr o = tid >= d ? sh[tid - d] : Fr::one();
-    __syncthreads();
-    an = an * o;
-    sh[tid] = an;
-    __syncthreads();
-  }
-  const Fr nall = sh[1023];
-  const Fr npre = tid ? sh[tid - 1] : Fr::one();
-  __syncthreads();
-  sh[tid] = ad;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {
-    const Fr o = tid + d < 1024 ? sh[tid + d] : Fr::one();
-    __syncthreads();
-    ad = ad * o;
-    sh[tid] = ad;
-    __syncthreads();
-  }
-  const Fr dall = sh[0];
-  const Fr dsuf = tid + 1 < 1024 ? sh[tid + 1] : Fr::one();
+  Fr nall, dall;
+  const Fr npre = block_scan_excl<false, MulOp, 1024>(pn, sh, &nall);
+  const Fr dsuf = block_scan_excl<true, MulOp, 1024>(pd, sh, &dall);
   if (tid == 0) {
     totals[0] = nall;
     totals[1] = dall;
@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(kT)
 k_lin_tile(const Fr* __restrict__ src, size_t m, const LinTab* __restrict__ tab, const Fr* __restrict__ carry,
            Fr* __restrict__ out) {
   __shared__ uint32_t stg[kStageWords];
-  __shared__ Fr sh[kT];
+  __shared__ Fr sh[kT / 64];  // the scan's wave totals
   const int tid = threadIdx.x;
   const size_t base = (size_t)blockIdx.x * kTileN;
   Fr x[kPer];
@@ -468,24 +468,14 @@ __global__ void k_pow_tiles(Fr D, Fr Di, int count, Fr* __restrict__ Q, Fr* __re
 // over the threads); h[T] is replaced by H_T
 __global__ void __launch_bounds__(1024) k_tile_heads(Fr* __restrict__ h, int m, const Fr* __restrict__ Q,
                                                      const Fr* __restrict__ Qinv) {
-  __shared__ Fr sh[1024];
+  __shared__ Fr sh[1024 / 64];  // the scan's wave totals
   const int tid = threadIdx.x;
   const int per = (m + 1023) / 1024;
   const int t0 = min(tid * per, m), t1 = min(t0 + per, m);
   Fr run = Fr::zero();
   for (int T = t0; T < t1; T++) run = run + h[T] * Q[T];
   // exclusive suffix sum of the runs over the threads
-  sh[tid] = run;
-  __syncthreads();
-  Fr acc = run;
-  for (int d = 1; d < 1024; d <<= 1) {
-    const Fr o = tid + d < 1024 ? sh[tid + d] : Fr::zero();
-    __syncthreads();
-    acc = acc + o;
-    sh[tid] = acc;
-    __syncthreads();
-  }
-  Fr suf = tid + 1 < 1024 ? sh[tid + 1] : Fr::zero();
+  Fr suf = block_scan_excl<true, AddOp, 1024>(run, sh, nullptr);
   for (int T = t1 - 1; T >= t0; T--) {
     suf = suf + h[T] * Q[T];
     h[T] = suf * Qinv[T];
