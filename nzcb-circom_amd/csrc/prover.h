@@ -93,6 +93,7 @@ struct Prover {
   Fr* lin_tile_pows(int k);       // Q then Qinv of slot k
   std::vector<Fr> lin_host;       // their host copies (Fr-sized words)
   DevBuf<Fr> eval_part;           // partial sums of polynomial evaluations
+  DevBuf<F29> eval_pw;            // the evaluation points' powers x^t, t < 256
   DevBuf<uint32_t> flags;
   std::vector<Fr> host_part;
 

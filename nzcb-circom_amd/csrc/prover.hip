@@ -695,6 +695,7 @@ struct EvalSet {
   uint64_t len[kEvalMax];
   Fr x[kEvalMax];
   F29 x29[kEvalMax];  // x as the mul_fr29 operand
+  F29 y29[kEvalMax];  // x^kT: the strided Horner's step (k_eval_multi)
   int np;
 };
 
@@ -704,43 +705,60 @@ __device__ __forceinline__ F29 fr29_operand_dev(Fr c) {
   return split29(c);
 }
 
-// NP interleaved evaluations per thread (independent Horner chains side by side), a
-// chunk of kEvalChunk2 coefficients each
+// A workgroup evaluates the 4096 coefficients [4096 b, 4096 b + 4096) of each polynomial:
+// thread t takes the coefficients 4096 b + t + 256 m (m < kEvalChunk2), so every load of a
+// wave is 64 consecutive coefficients (round 3 gave each thread 16 consecutive ones, loads
+// 512 B apart per lane), by Horner in y = x^256 over m; times x^t (k_eval_pows' table) the
+// thread's terms carry their true power, and the workgroup adds them. NP evaluations side
+// by side (independent chains).
 static constexpr int kEvalChunk2 = 16;
 static constexpr int kEvalLogChunk2 = 4;
 
-template <int NP>
-__global__ void __launch_bounds__(kT) k_eval_multi(EvalSet es, Fr* __restrict__ partial, int nblocks) {
-  __shared__ Fr sh[kT];      // one evaluation's tree at a time (8 KB: many workgroups per CU)
-  __shared__ F29 yl[NP][8];  // kT = 2^8 threads: y^(2^l), l < 8
-  if (threadIdx.x < NP) {
-    Fr y = es.x[threadIdx.x];
-    for (int k = 0; k < kEvalLogChunk2; k++) y = y * y;
-    for (int l = 0; l < 8; l++) {
-      yl[threadIdx.x][l] = fr29_operand_dev(y);
-      y = y * y;
-    }
+// x_j^t for t < kT as mul_fr29 operands, one workgroup per evaluation point
+__global__ void __launch_bounds__(kT) k_eval_pows(EvalSet es, F29* __restrict__ pw) {
+  const int j = blockIdx.x, t = threadIdx.x;
+  Fr a = Fr::one(), q = es.x[j];
+  for (int e = t; e; e >>= 1) {
+    if (e & 1) a = a * q;
+    q = q * q;
   }
-  const size_t s = ((size_t)blockIdx.x * kT + threadIdx.x) * kEvalChunk2;
+  pw[(size_t)j * kT + t] = fr29_operand_dev(a);
+}
+
+// sum of v over the workgroup's threads, in thread 0 (wave butterflies, then the wave totals)
+__device__ __forceinline__ Fr block_sum_fr(const Fr& v, Fr* sh) {
+  Fr x = v;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x = x + shfl_fr(x, (int)(threadIdx.x & 63) ^ m);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+  __syncthreads();
+  Fr t = sh[0];
+#pragma unroll
+  for (int k = 1; k < kT / 64; k++) t = t + sh[k];
+  __syncthreads();
+  return t;
+}
+
+template <int NP>
+__global__ void __launch_bounds__(kT) k_eval_multi(EvalSet es, const F29* __restrict__ pw, Fr* __restrict__ partial,
+                                                   int nblocks) {
+  __shared__ Fr sh[kT / 64];
+  const size_t s = (size_t)blockIdx.x * kT * kEvalChunk2 + threadIdx.x;
   Fr acc[NP];
 #pragma unroll
   for (int j = 0; j < NP; j++) acc[j] = Fr::zero();
-  for (int i = kEvalChunk2 - 1; i >= 0; i--) {
+  // from the top coefficient down: indices past a polynomial's length are its top ones, so
+  // skipping them (acc still 0) is Horner over zeros
+  for (int m = kEvalChunk2 - 1; m >= 0; m--) {
+    const size_t i = s + (size_t)m * kT;
 #pragma unroll
     for (int j = 0; j < NP; j++)
-      if (s + i < es.len[j]) acc[j] = mul_fr29(acc[j], es.x29[j]) + es.p[j][s + i];
+      if (i < es.len[j]) acc[j] = mul_fr29(acc[j], es.y29[j]) + es.p[j][i];
   }
 #pragma unroll
   for (int j = 0; j < NP; j++) {
-    sh[threadIdx.x] = acc[j];
-    __syncthreads();
-    for (int l = 0; l < 8; l++) {
-      const unsigned st = 1u << l;
-      if ((threadIdx.x & (2 * st - 1)) == 0) sh[threadIdx.x] = sh[threadIdx.x] + mul_fr29(sh[threadIdx.x + st], yl[j][l]);
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) partial[(size_t)j * nblocks + blockIdx.x] = sh[0];
-    __syncthreads();
+    const Fr r = block_sum_fr(mul_fr29(acc[j], pw[(size_t)j * kT + threadIdx.x]), sh);
+    if (threadIdx.x == 0) partial[(size_t)j * nblocks + blockIdx.x] = r;
   }
 }
 
@@ -1177,6 +1195,7 @@ void Prover::alloc_workspace() {
   lin_host.resize(2 * sizeof(LinTab) / sizeof(Fr));
   size_t nblocks = ((size_t)3 * n + 6 + (size_t)kT * kEvalChunk2 - 1) / ((size_t)kT * kEvalChunk2) + 1;
   eval_part.alloc((size_t)kEvalMax * nblocks + kEvalMax);  // eval_many: kEvalMax rows + results
+  eval_pw.alloc((size_t)kEvalMax * kT);                       // x_j^t, t < kT (k_eval_pows)
   host_part.resize(std::max<size_t>(nblocks, kEvalMax));
   flags.p = (uint32_t*)(blind.p + 12);  // a view: the blinding upload also clears the flags
   flags.n = 1;
@@ -1462,16 +1481,20 @@ void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const
     es.len[j] = lens[j];
     es.x[j] = xs[j];
     es.x29[j] = fr29_operand(xs[j]);
+    es.y29[j] = fr29_operand(pow_u64(xs[j], kT));
     maxlen = std::max(maxlen, lens[j]);
   }
   es.np = np;
   const size_t nblocks = (maxlen + (size_t)kT * kEvalChunk2 - 1) / ((size_t)kT * kEvalChunk2);
   if ((size_t)np * nblocks + kEvalMax > eval_part.n) throw Error(NZCB_ERR_INTERNAL, "eval partial buffer too small");
   Fr* res = eval_part.p + (size_t)np * nblocks;
+  hipLaunchKernelGGL(k_eval_pows, dim3((unsigned)np), dim3(kT), 0, s, es, eval_pw.p);
   if (np == 7)
-    hipLaunchKernelGGL(k_eval_multi<7>, dim3((unsigned)nblocks), dim3(kT), 0, s, es, eval_part.p, (int)nblocks);
+    hipLaunchKernelGGL(k_eval_multi<7>, dim3((unsigned)nblocks), dim3(kT), 0, s, es, (const F29*)eval_pw.p,
+                       eval_part.p, (int)nblocks);
   else if (np == 1)
-    hipLaunchKernelGGL(k_eval_multi<1>, dim3((unsigned)nblocks), dim3(kT), 0, s, es, eval_part.p, (int)nblocks);
+    hipLaunchKernelGGL(k_eval_multi<1>, dim3((unsigned)nblocks), dim3(kT), 0, s, es, (const F29*)eval_pw.p,
+                       eval_part.p, (int)nblocks);
   else
     throw Error(NZCB_ERR_INTERNAL, "eval_many: 1 or 7 evaluations");
   NZ_HIP(hipGetLastError());
