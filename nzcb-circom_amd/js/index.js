@@ -473,4 +473,5 @@ module.exports = {
   version: addon.version,
   deviceCount: addon.deviceCount,
   _addon: addon,
+  _programInputBuffer: programInputBuffer,  // tests: the input signals' 32-byte encoding
 };

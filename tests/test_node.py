@@ -31,6 +31,22 @@ def test_addon_exports():
 
 
 @needs_node
+def test_program_input_encoding():
+    """fullProve's input signals as 32-byte LE field elements (js/index.js putSignal): small
+    numbers take a direct path, everything else (numbers past 2^48, strings, BigInts,
+    negatives) is reduced mod r, as circom's calculator reduces them; arrays flatten."""
+    R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+    vals = [0, 1, 255, (1 << 48) - 1, 1 << 48, (1 << 53) - 1, -1, -7]
+    strs = ["12345678901234567890123456789", str(R + 5), str(R - 1)]
+    script = ("const m=require('./'); const meta={names:[['a',%d],['b',%d],['c',1]]};"
+              "const buf=m._programInputBuffer({a:%s, b:%s, c:BigInt('%d')}, meta);"
+              "console.log(buf.toString('hex'))" % (len(vals), len(strs), json.dumps(vals), json.dumps(strs), R + 9))
+    got = bytes.fromhex(run_node(script).strip())
+    want = b"".join((int(x) % R).to_bytes(32, "little") for x in vals + strs + [R + 9])
+    assert got == want
+
+
+@needs_node
 def test_node_zkey_export_past_2gib(tmp_path):
     """zKey.exportVerificationKey / exportSolidityVerifier on a zkey file past
     Node's 2 GiB readFileSync limit (nzcp_live_final.zkey is ~3.9 GB): a golden zkey grown to
