@@ -288,7 +288,9 @@ __device__ __forceinline__ Fr perm_bw(const Fr* rlo, const Fr* rhi, size_t e, si
   return e < n ? mul_fr29(root4(rlo, rhi, 4 * e), op) : Fr::zero();
 }
 
-__global__ void __launch_bounds__(kT)
+// 3 waves per SIMD (168 VGPRs, 100 B scratch) instead of the compiler's 2 (222 VGPRs):
+// 0.696 -> 0.597 ms isolated, bench unchanged (profiles/r4_perm_waves_ab.txt)
+__global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3, 8)))
 k_perm_tile(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
             const Fr* __restrict__ sig_h, size_t n, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi,
             PermArgs pa, Fr* __restrict__ Z, Fr* __restrict__ ntot, Fr* __restrict__ dtot) {
@@ -685,10 +687,8 @@ static F29 f29_exp(Fr v, int extra) {  // split29 of v * 2^extra (host)
 
 // Round 4, all evaluations of one point set in two launches and one host round trip
 // (eight separately synchronised Horner launches took 1.05 ms + 8 syncs per proof,
-// profiles/r3_single_lane_phases.txt). Block b, thread i: Horner over coefficients
-// [K t, K t + K) (t = b kT + i) in radix 2^29 products, then a tree over the block's
-// threads with level factors y^(2^l), y = x^K (sum_i h_i y^i); k_eval_comb folds the
-// block sums the same way in z = x^(K kT).
+// profiles/r3_single_lane_phases.txt): k_eval_pows, k_eval_multi (one partial sum per
+// workgroup and point, below), k_eval_comb (the partial sums folded in z = x^4096).
 static constexpr int kEvalMax = 8;
 struct EvalSet {
   const Fr* p[kEvalMax];
