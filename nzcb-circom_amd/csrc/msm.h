@@ -54,6 +54,7 @@ struct MsmScratch {
   DevBuf<G1xyzz> parts;       // generic: per (set, sum slot, part): partial plain sums
   DevBuf<G1xyzz> win;         // per (set, sum slot): see msm_sums_kernel / msm_slots29_kernel
   G1xyzz* host_win = nullptr;  // pinned
+  uint32_t* host_total = nullptr;  // pinned (after host_win's slots): the entry count (prof)
   size_t host_win_cap = 0;
   // shape of the MSM in flight (set by msm_enqueue, used by msm_finish)
   int cur_c = 0, cur_nsets = 0, cur_nbits = 0, cur_seglen = 0;

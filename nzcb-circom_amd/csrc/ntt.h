@@ -47,7 +47,9 @@ struct NttIo {
 // out = NTT(in) (inverse: out = (1/N) * iNTT(in)), N = 2^log_n <= 2^max_log.
 // Natural order in and out; in != out required (first pass gathers in bit-reversed order).
 // scale (optional, Montgomery) multiplies every input element on load.
+// scratch29 (optional): 9 << log_n words for the inter-pass values instead of t.scratch29,
+// so that transforms on two streams can run at once (the prover's round 2).
 void ntt(const NttTables& t, const Fr* in, Fr* out, int log_n, bool inverse, hipStream_t st,
-         const Fr* scale = nullptr, const NttIo* io = nullptr);
+         const Fr* scale = nullptr, const NttIo* io = nullptr, uint32_t* scratch29 = nullptr);
 
 }  // namespace nzcb

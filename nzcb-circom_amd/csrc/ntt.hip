@@ -498,7 +498,7 @@ static int ntt29_tile() {
 // stages per pass through the F29 scratch; the last pass writes canonical Fr.
 template <int TILE>
 static void ntt29_passes(const NttTables& t, const Fr* in, Fr* out, const F29* tw, int L, const F29& sc29,
-                         int do_scale, const NttIo& io, bool sparse_ok, int swz, hipStream_t st) {
+                         int do_scale, const NttIo& io, bool sparse_ok, int swz, hipStream_t st, F29* scr) {
   constexpr int T = TILE / 4;
   const int q1 = L < 8 ? L : 8;
   const int cols = 1 << (L - q1);
@@ -509,7 +509,6 @@ static void ntt29_passes(const NttTables& t, const Fr* in, Fr* out, const F29* t
   // tiles past the first skip stages 0-1 (a 4n coset NTT of an n+3-term polynomial)
   const int sparse4 = sparse_ok && L >= 2 && q1 >= 2 && !(q1 & 1) &&
                       io.in_len <= ((size_t)1 << (L - 2)) + ((size_t)1 << logC1);
-  F29* scr = (F29*)t.scratch29.p;
   if (q1 == L) {
     hipLaunchKernelGGL((ntt29_pass_kernel<false, false, TILE>), dim3((unsigned)tiles), dim3(T), 0, st, in,
                        (const F29*)nullptr, out, (F29*)nullptr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4, swz);
@@ -537,7 +536,7 @@ static void ntt29_passes(const NttTables& t, const Fr* in, Fr* out, const F29* t
 }
 
 void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hipStream_t st, const Fr* scale,
-         const NttIo* iop) {
+         const NttIo* iop, uint32_t* scratch29) {
   const NttIo io = iop ? *iop : NttIo();
   if (L > t.max_log) throw Error(NZCB_ERR_ARG, "ntt size exceeds table");
   if (in == out) throw Error(NZCB_ERR_ARG, "ntt requires in != out");
@@ -575,12 +574,13 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   }();
   const int sparse4 = sparse_ok && L >= 2 && q1 >= 2 && !(q1 & 1) &&
                       io.in_len <= ((size_t)1 << (L - 2)) + ((size_t)1 << logC1);
-  if (ntt29_enabled() && (q1 == L || t.scratch29.n >= ((size_t)9 << L))) {
+  if (ntt29_enabled() && (q1 == L || scratch29 || t.scratch29.n >= ((size_t)9 << L))) {
     const int swz = ntt29_swizzle();
+    F29* scr = (F29*)(scratch29 ? scratch29 : t.scratch29.p);
     if (ntt29_tile() == 1024)
-      ntt29_passes<1024>(t, in, out, tw, L, sc29, do_scale, io, sparse_ok, swz, st);
+      ntt29_passes<1024>(t, in, out, tw, L, sc29, do_scale, io, sparse_ok, swz, st, scr);
     else
-      ntt29_passes<2048>(t, in, out, tw, L, sc29, do_scale, io, sparse_ok, swz, st);
+      ntt29_passes<2048>(t, in, out, tw, L, sc29, do_scale, io, sparse_ok, swz, st, scr);
     return;
   }
   hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)tiles), dim3(kNttThreads), lds, st, in, out, tw, L, 0, q1, logC1,

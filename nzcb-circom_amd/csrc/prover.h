@@ -47,8 +47,9 @@ struct Prover {
   hipStream_t aux[kSlots] = {nullptr, nullptr, nullptr};
   hipEvent_t ready[kSlots] = {nullptr, nullptr, nullptr};
   bool slot_local[kSlots] = {false, false, false};  // slot's MSM stays on this device (Lagrange basis)
-  // round 1's interpolations of A, B, C run on aux[2] (overlapping round 2's grand product)
-  hipEvent_t side_ready = nullptr, side_done = nullptr;
+  // round 1's interpolations of A, B, C (and the gate check) run on aux[2], overlapping
+  // round 2; round 3 waits for side_done. pows_done: round 4's divPol1 tile powers (aux[2])
+  hipEvent_t side_ready = nullptr, side_done = nullptr, pows_done = nullptr;
   ~Prover();
   // resident zkey data (LEM, as in the file)
   DevBuf<G1Affine> ptau;
@@ -96,6 +97,11 @@ struct Prover {
   DevBuf<F29> eval_pw;            // the evaluation points' powers x^t, t < 256
   DevBuf<uint32_t> flags;
   std::vector<Fr> host_part;
+  DevBuf<uint32_t> ntt_scr2;      // Z's transforms' inter-pass scratch (beside A, B, C's on aux[2])
+  // pinned: the top six coefficients of A, B, C and Z for round 3's t recombination, then
+  // the check flags
+  Fr* top_host = nullptr;
+  static constexpr int kTopWords = 4 * 6 + 1;
 
   // timings of the last proof (ms)
   double tm[9] = {0};
@@ -127,9 +133,11 @@ struct Prover {
   void init_slots();
   void alloc_workspace();
   void to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int nb, hipStream_t s = nullptr);
-  void to4t_coefs(const Fr* evals, Fr* coefs, const int* bidx, int nb, hipStream_t s);
-  void to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s);
+  void to4t_coefs(const Fr* evals, Fr* coefs, const int* bidx, int nb, hipStream_t s, uint32_t* scr = nullptr);
+  void to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s, uint32_t* scr = nullptr);
   void round3_quot3(const Fr& beta, const Fr& gamma, const Fr& alpha, hipStream_t s);
+  void launch_gate_check(hipStream_t s);
+  void copy_tops(hipStream_t s);  // the tops and flags into top_host; throws on a gate failure
   void commit_start(int slot, const Fr* scalars, size_t len, const MsmBaseTable* tab = nullptr,
                     const G1Affine* bases = nullptr, bool on_main = false);
   G1Affine commit_finish(int slot);
@@ -138,7 +146,7 @@ struct Prover {
                  const std::function<void()>& overlap = nullptr);
   // y_i = x_i + d y_(i+1) with d from lin_tables slot `tab` (round 4 builds slots 0, 1 = xi, xi w)
   void div_pol1(const Fr* src, size_t m, int tab, const Fr& p0_adjust, Fr* dst, uint32_t flag_bit);
-  void lin_tables(int k, const Fr& d);
+  void lin_tables(int k, const Fr& d, hipStream_t s);
   double ms_since(std::chrono::steady_clock::time_point t0);
   double msm_ms = 0, ntt_ms = 0;
 };

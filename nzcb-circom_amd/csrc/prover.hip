@@ -688,15 +688,18 @@ static F29 f29_exp(Fr v, int extra) {  // split29 of v * 2^extra (host)
 // Round 4, all evaluations of one point set in two launches and one host round trip
 // (eight separately synchronised Horner launches took 1.05 ms + 8 syncs per proof,
 // profiles/r3_single_lane_phases.txt): k_eval_pows, k_eval_multi (one partial sum per
-// workgroup and point, below), k_eval_comb (the partial sums folded in z = x^4096).
+// workgroup and point, already times x^(4096 b)), k_eval_sum (the partial sums added).
 static constexpr int kEvalMax = 8;
+static constexpr int kEvalBits = 16;  // workgroup index bits (<= 2^16 workgroups of 4096 coefficients)
 struct EvalSet {
   const Fr* p[kEvalMax];
   uint64_t len[kEvalMax];
   Fr x[kEvalMax];
+  Fr x4096[kEvalMax];  // x^4096 (host), the base of the workgroup powers
   F29 x29[kEvalMax];  // x as the mul_fr29 operand
   F29 y29[kEvalMax];  // x^kT: the strided Horner's step (k_eval_multi)
   int np;
+  int nbits;  // bits of the largest workgroup index
 };
 
 __device__ __forceinline__ F29 fr29_operand_dev(Fr c) {
@@ -712,10 +715,10 @@ __device__ __forceinline__ F29 fr29_operand_dev(Fr c) {
 // thread's terms carry their true power, and the workgroup adds them. NP evaluations side
 // by side (independent chains).
 static constexpr int kEvalChunk2 = 16;
-static constexpr int kEvalLogChunk2 = 4;
 
-// x_j^t for t < kT as mul_fr29 operands, one workgroup per evaluation point
-__global__ void __launch_bounds__(kT) k_eval_pows(EvalSet es, F29* __restrict__ pw) {
+// x_j^t for t < kT as mul_fr29 operands, and x_j^(4096 2^k) for k < nbits (pw2), one
+// workgroup per evaluation point
+__global__ void __launch_bounds__(kT) k_eval_pows(EvalSet es, F29* __restrict__ pw, Fr* __restrict__ pw2) {
   const int j = blockIdx.x, t = threadIdx.x;
   Fr a = Fr::one(), q = es.x[j];
   for (int e = t; e; e >>= 1) {
@@ -723,6 +726,11 @@ __global__ void __launch_bounds__(kT) k_eval_pows(EvalSet es, F29* __restrict__ 
     q = q * q;
   }
   pw[(size_t)j * kT + t] = fr29_operand_dev(a);
+  if (t < es.nbits) {
+    Fr z = es.x4096[j];
+    for (int k = 0; k < t; k++) z = z * z;
+    pw2[j * kEvalBits + t] = z;
+  }
 }
 
 // sum of v over the workgroup's threads, in thread 0 (wave butterflies, then the wave totals)
@@ -740,9 +748,19 @@ __device__ __forceinline__ Fr block_sum_fr(const Fr& v, Fr* sh) {
 }
 
 template <int NP>
-__global__ void __launch_bounds__(kT) k_eval_multi(EvalSet es, const F29* __restrict__ pw, Fr* __restrict__ partial,
-                                                   int nblocks) {
+__global__ void __launch_bounds__(kT) k_eval_multi(EvalSet es, const F29* __restrict__ pw, const Fr* __restrict__ pw2,
+                                                   Fr* __restrict__ partial, int nblocks) {
+  static_assert(NP <= kEvalMax && kEvalMax <= 4 * (kT / 64), "one 16-lane group per point");
   __shared__ Fr sh[kT / 64];
+  __shared__ Fr bpow[kEvalMax];  // x_j^(4096 b): the product of pw2[j][k] over the set bits k of b
+  __shared__ Fr bsum[kEvalMax];
+  {
+    const int l = (int)(threadIdx.x & 63), k = l & 15, j = 4 * (int)(threadIdx.x >> 6) + (l >> 4);
+    Fr f = Fr::one();
+    if (j < NP && k < es.nbits && ((blockIdx.x >> k) & 1u)) f = pw2[j * kEvalBits + k];
+    for (int m = 8; m >= 1; m >>= 1) f = f * shfl_fr(f, l ^ m);
+    if (j < NP && k == 0) bpow[j] = f;
+  }
   const size_t s = (size_t)blockIdx.x * kT * kEvalChunk2 + threadIdx.x;
   Fr acc[NP];
 #pragma unroll
@@ -758,42 +776,20 @@ __global__ void __launch_bounds__(kT) k_eval_multi(EvalSet es, const F29* __rest
 #pragma unroll
   for (int j = 0; j < NP; j++) {
     const Fr r = block_sum_fr(mul_fr29(acc[j], pw[(size_t)j * kT + threadIdx.x]), sh);
-    if (threadIdx.x == 0) partial[(size_t)j * nblocks + blockIdx.x] = r;
+    if (threadIdx.x == 0) bsum[j] = r;
   }
+  // (block_sum_fr's barriers made bpow visible) the point j's product in lane j
+  if (threadIdx.x < NP) partial[(size_t)threadIdx.x * nblocks + blockIdx.x] = bsum[threadIdx.x] * bpow[threadIdx.x];
 }
 
-// block per evaluation: sum_b partial_b z^b (z = x^(kEvalChunk2 kT) = x^(2^12)), each of the
-// 1024 threads Horner over q consecutive block sums, then a tree with factors (z^q)^(2^l)
-__global__ void __launch_bounds__(1024) k_eval_comb(EvalSet es, const Fr* __restrict__ partial, int nblocks,
-                                                    Fr* __restrict__ out) {
-  __shared__ Fr sh[1024];
-  __shared__ F29 zl[11];  // [0] = z, [1 + l] = w^(2^l), w = z^q, l < 10
+// block per evaluation: the sum of its workgroups' partial sums
+__global__ void __launch_bounds__(kT) k_eval_sum(const Fr* __restrict__ partial, int nblocks, Fr* __restrict__ out) {
+  __shared__ Fr sh[kT / 64];
   const int j = blockIdx.x;
-  const int q = (nblocks + 1023) / 1024;
-  if (threadIdx.x == 0) {
-    Fr z = es.x[j];
-    for (int k = 0; k < kEvalLogChunk2 + 8; k++) z = z * z;
-    zl[0] = fr29_operand_dev(z);
-    Fr w = Fr::one();
-    for (int k = 0; k < q; k++) w = w * z;
-    for (int l = 0; l < 10; l++) {
-      zl[1 + l] = fr29_operand_dev(w);
-      w = w * w;
-    }
-  }
-  __syncthreads();
   Fr acc = Fr::zero();
-  const int b0 = (int)threadIdx.x * q;
-  for (int b = b0 + q; b-- > b0;)
-    if (b < nblocks) acc = mul_fr29(acc, zl[0]) + partial[(size_t)j * nblocks + b];
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int l = 0; l < 10; l++) {
-    const unsigned st = 1u << l;
-    if ((threadIdx.x & (2 * st - 1)) == 0) sh[threadIdx.x] = sh[threadIdx.x] + mul_fr29(sh[threadIdx.x + st], zl[1 + l]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[j] = sh[0];
+  for (int b = (int)threadIdx.x; b < nblocks; b += kT) acc = acc + partial[(size_t)j * nblocks + b];
+  const Fr r = block_sum_fr(acc, sh);
+  if (threadIdx.x == 0) out[j] = r;
 }
 
 struct RArgs {
@@ -900,6 +896,8 @@ Prover::~Prover() {
   }
   if (side_ready) (void)hipEventDestroy(side_ready);
   if (side_done) (void)hipEventDestroy(side_done);
+  if (pows_done) (void)hipEventDestroy(pows_done);
+  if (top_host) (void)hipHostFree(top_host);
 }
 
 MsmShard::~MsmShard() {
@@ -1172,6 +1170,9 @@ void Prover::init_slots() {
   }
   NZ_HIP(hipEventCreateWithFlags(&side_ready, hipEventDisableTiming));
   NZ_HIP(hipEventCreateWithFlags(&side_done, hipEventDisableTiming));
+  NZ_HIP(hipEventCreateWithFlags(&pows_done, hipEventDisableTiming));
+  NZ_HIP(hipHostMalloc((void**)&top_host, kTopWords * sizeof(Fr), hipHostMallocDefault));
+  std::memset((void*)top_host, 0, kTopWords * sizeof(Fr));
 }
 
 // per-proof working set (one per lane)
@@ -1195,11 +1196,16 @@ void Prover::alloc_workspace() {
   lin_host.resize(2 * sizeof(LinTab) / sizeof(Fr));
   size_t nblocks = ((size_t)3 * n + 6 + (size_t)kT * kEvalChunk2 - 1) / ((size_t)kT * kEvalChunk2) + 1;
   eval_part.alloc((size_t)kEvalMax * nblocks + kEvalMax);  // eval_many: kEvalMax rows + results
-  eval_pw.alloc((size_t)kEvalMax * kT);                       // x_j^t, t < kT (k_eval_pows)
+  // x_j^t, t < kT (F29), then x_j^(4096 2^k), k < kEvalBits (Fr), both from k_eval_pows
+  eval_pw.alloc((size_t)kEvalMax * kT + (kEvalMax * kEvalBits * sizeof(Fr) + sizeof(F29) - 1) / sizeof(F29));
   host_part.resize(std::max<size_t>(nblocks, kEvalMax));
   flags.p = (uint32_t*)(blind.p + 12);  // a view: the blinding upload also clears the flags
   flags.n = 1;
   flags.owned = false;
+  // Z's interpolation and coset transforms (round 2) run while A, B, C's still use the
+  // engine's scratch on aux[2]
+  const int zlog = quot3 ? power : power + 2;
+  if (zlog > 8) ntt_scr2.alloc((size_t)9 << zlog);
 }
 
 // An extra proof lane on the primary's device: shares the HBM-resident proving key
@@ -1250,8 +1256,30 @@ Prover::Prover(const Prover& pk, int) {
 // t mod (X^n - d_j); k_t_combine solves for the quarters of t. The divisibility check of
 // the 4n path (coefficients >= 3n + 6 of the 4n iNTT) becomes the gate check on H.
 // Same t, bit for bit: t is unique.
+// the gate check on H (t's divisibility, flag bit 1), and the copies t's recombination
+// needs: A, B, C's coefficients n-4 .. n+1, Z's n-3 .. n+2 and the flags, into top_host
+void Prover::launch_gate_check(hipStream_t s) {
+  hipLaunchKernelGGL(k_gate_h, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, qm.p, ql.p, qr.p,
+                     qo.p, qc.p, (size_t)n, nPublic, flags.p);
+  NZ_HIP(hipGetLastError());
+}
+
+void Prover::copy_tops(hipStream_t s) {
+  const Fr* src[4] = {pol_a.p + (n - 4), pol_b.p + (n - 4), pol_c.p + (n - 4), pol_z.p + (n - 3)};
+  for (int k = 0; k < 4; k++)
+    NZ_HIP(hipMemcpyAsync(top_host + 6 * k, src[k], 6 * sizeof(Fr), hipMemcpyDeviceToHost, s));
+  NZ_HIP(hipMemcpyAsync(top_host + 24, flags.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  NZ_HIP(hipStreamSynchronize(s));
+  if (*(const uint32_t*)(top_host + 24) & 1u) throw Error(NZCB_ERR_T_DIV, "T Polynomial is not divisible");
+}
+
 void Prover::round3_quot3(const Fr& beta, const Fr& gamma, const Fr& alpha, hipStream_t s) {
   const size_t n3 = (size_t)3 * n;
+  // Lagrange commitments: round 1 ran the gate check on aux[2] (s waits for side_done), so
+  // the one host round trip (tops and flag) comes first, while the GPU is idle anyway, and
+  // none sits between the quotient and t's recombination
+  const bool side = lcommit;
+  if (side) copy_tops(s);
   QArgs29 q29;
   q29.beta = f29_exp(beta, 5);
   q29.k23 = k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0;
@@ -1264,9 +1292,7 @@ void Prover::round3_quot3(const Fr& beta, const Fr& gamma, const Fr& alpha, hipS
   q29.alpha = f29_exp(alpha, 20);
   hipLaunchKernelGGL((k_quotient_coset29<true>), dim3(grid_for(n3, kT, 1u << 30)), dim3(kT), 0, s, A4.p, B4.p, C4.p,
                      Z4.p, cq3.p, cs3.p, cl3.p, nPublic, A.p, (size_t)n, x_lo.p, root_hi.p, q29, T.p);
-  hipLaunchKernelGGL(k_gate_h, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, qm.p, ql.p, qr.p,
-                     qo.p, qc.p, (size_t)n, nPublic, flags.p);
-  NZ_HIP(hipGetLastError());
+  if (!side) launch_gate_check(s);
   for (int j = 0; j < 3; j++) {  // v_j = (t mod (X^n - d_j)) / 4
     NttIo io;
     io.out_f = itw3.p + (size_t)j * n;
@@ -1274,15 +1300,9 @@ void Prover::round3_quot3(const Fr& beta, const Fr& gamma, const Fr& alpha, hipS
     ntt(eng->ntt_tables, T.p + (size_t)j * n, Tz.p + (size_t)j * n, power, true, s, nullptr, &io);
   }
   NZ_HIP(hipGetLastError());
+  if (!side) copy_tops(s);
   Fr top[4][6];  // coefficients n-4 .. n+1 of A, B, C and n-3 .. n+2 of Z
-  uint32_t f = 0;
-  NZ_HIP(hipMemcpyAsync(top[0], pol_a.p + (n - 4), 6 * sizeof(Fr), hipMemcpyDeviceToHost, s));
-  NZ_HIP(hipMemcpyAsync(top[1], pol_b.p + (n - 4), 6 * sizeof(Fr), hipMemcpyDeviceToHost, s));
-  NZ_HIP(hipMemcpyAsync(top[2], pol_c.p + (n - 4), 6 * sizeof(Fr), hipMemcpyDeviceToHost, s));
-  NZ_HIP(hipMemcpyAsync(top[3], pol_z.p + (n - 3), 6 * sizeof(Fr), hipMemcpyDeviceToHost, s));
-  NZ_HIP(hipMemcpyAsync(&f, flags.p, 4, hipMemcpyDeviceToHost, s));
-  NZ_HIP(hipStreamSynchronize(s));
-  if (f & 1u) throw Error(NZCB_ERR_T_DIV, "T Polynomial is not divisible");
+  std::memcpy(top, top_host, sizeof(top));
   // factor coefficients by offset u from the top degree (A, B, C: n + 1; Z: n + 2)
   Fr p1[4][6], p2[4][6];
   const Fr w = wn, wi = inverse(wn);
@@ -1333,9 +1353,9 @@ void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int n
 }
 
 // the blinded coefficients (what the commitment needs) ...
-void Prover::to4t_coefs(const Fr* evals, Fr* coefs, const int* bidx, int nb, hipStream_t s) {
+void Prover::to4t_coefs(const Fr* evals, Fr* coefs, const int* bidx, int nb, hipStream_t s, uint32_t* scr) {
   auto t0 = std::chrono::steady_clock::now();
-  ntt(eng->ntt_tables, evals, coefs, power, true, s);
+  ntt(eng->ntt_tables, evals, coefs, power, true, s, nullptr, nullptr, scr);
   BlindIdx bi;
   bi.count = nb;
   for (int k = 0; k < nb; k++) bi.idx[k] = bidx[k];
@@ -1345,7 +1365,7 @@ void Prover::to4t_coefs(const Fr* evals, Fr* coefs, const int* bidx, int nb, hip
 }
 
 // ... and their 4n coset evaluations (what round 3's quotient needs)
-void Prover::to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s) {
+void Prover::to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s, uint32_t* scr) {
   auto t0 = std::chrono::steady_clock::now();
   // evaluations of the *blinded* polynomial on the coset g*<w4> (round-3 quotient input)
   if (quot3) {  // on c_j H, j < 3: the nb top coefficients folded in (x^n = d_j there)
@@ -1356,7 +1376,7 @@ void Prover::to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s) {
       io.fold_len = (size_t)nb;
       io.fold_n = n;
       io.fold_f = fr29_operand(d3[j]);
-      ntt(eng->ntt_tables, coefs, evals4 + (size_t)j * n, power, false, s, nullptr, &io);
+      ntt(eng->ntt_tables, coefs, evals4 + (size_t)j * n, power, false, s, nullptr, &io, scr);
     }
     NZ_HIP(hipGetLastError());
     ntt_ms += ms_since(t0);
@@ -1365,7 +1385,7 @@ void Prover::to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s) {
   NttIo io;  // coset shift g^j and the zero padding fused into the NTT's first pass
   io.in_len = (size_t)n + nb;
   io.in_f = g29.p;
-  ntt(eng->ntt_tables, coefs, evals4, power + 2, false, s, nullptr, &io);
+  ntt(eng->ntt_tables, coefs, evals4, power + 2, false, s, nullptr, &io, scr);
   NZ_HIP(hipGetLastError());
   ntt_ms += ms_since(t0);  // host enqueue time only (kernels run asynchronously)
 }
@@ -1482,23 +1502,29 @@ void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const
     es.x[j] = xs[j];
     es.x29[j] = fr29_operand(xs[j]);
     es.y29[j] = fr29_operand(pow_u64(xs[j], kT));
+    es.x4096[j] = pow_u64(xs[j], (uint64_t)kT * kEvalChunk2);
     maxlen = std::max(maxlen, lens[j]);
   }
   es.np = np;
   const size_t nblocks = (maxlen + (size_t)kT * kEvalChunk2 - 1) / ((size_t)kT * kEvalChunk2);
+  if (nblocks > ((size_t)1 << kEvalBits)) throw Error(NZCB_ERR_INTERNAL, "eval_many: polynomial too long");
+  es.nbits = 1;
+  while (((size_t)1 << es.nbits) < nblocks) es.nbits++;
   if ((size_t)np * nblocks + kEvalMax > eval_part.n) throw Error(NZCB_ERR_INTERNAL, "eval partial buffer too small");
   Fr* res = eval_part.p + (size_t)np * nblocks;
-  hipLaunchKernelGGL(k_eval_pows, dim3((unsigned)np), dim3(kT), 0, s, es, eval_pw.p);
+  F29* pw = eval_pw.p;
+  Fr* pw2 = (Fr*)(eval_pw.p + (size_t)kEvalMax * kT);
+  hipLaunchKernelGGL(k_eval_pows, dim3((unsigned)np), dim3(kT), 0, s, es, pw, pw2);
   if (np == 7)
-    hipLaunchKernelGGL(k_eval_multi<7>, dim3((unsigned)nblocks), dim3(kT), 0, s, es, (const F29*)eval_pw.p,
+    hipLaunchKernelGGL(k_eval_multi<7>, dim3((unsigned)nblocks), dim3(kT), 0, s, es, (const F29*)pw, (const Fr*)pw2,
                        eval_part.p, (int)nblocks);
   else if (np == 1)
-    hipLaunchKernelGGL(k_eval_multi<1>, dim3((unsigned)nblocks), dim3(kT), 0, s, es, (const F29*)eval_pw.p,
+    hipLaunchKernelGGL(k_eval_multi<1>, dim3((unsigned)nblocks), dim3(kT), 0, s, es, (const F29*)pw, (const Fr*)pw2,
                        eval_part.p, (int)nblocks);
   else
     throw Error(NZCB_ERR_INTERNAL, "eval_many: 1 or 7 evaluations");
   NZ_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_eval_comb, dim3(np), dim3(1024), 0, s, es, (const Fr*)eval_part.p, (int)nblocks, res);
+  hipLaunchKernelGGL(k_eval_sum, dim3(np), dim3(kT), 0, s, (const Fr*)eval_part.p, (int)nblocks, res);
   NZ_HIP(hipGetLastError());
   NZ_HIP(hipMemcpyAsync(host_part.data(), res, np * sizeof(Fr), hipMemcpyDeviceToHost, s));
   if (overlap) overlap();  // host work beside the evaluation kernels
@@ -1507,8 +1533,8 @@ void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const
 }
 
 // divPol1's power tables for d (k_lin_tile's LinTab) into slot k of lin_tab: host products,
-// uploaded on the prover's stream (round 4 builds both while its evaluations run)
-void Prover::lin_tables(int k, const Fr& d) {
+// uploaded on stream s (round 4 builds both on aux[2] while its evaluations run)
+void Prover::lin_tables(int k, const Fr& d, hipStream_t s) {
   LinTab& t = ((LinTab*)lin_host.data())[k];
   t.dp[0] = Fr::one();
   for (int j = 1; j <= kPer; j++) t.dp[j] = t.dp[j - 1] * d;
@@ -1518,10 +1544,10 @@ void Prover::lin_tables(int k, const Fr& d) {
     t.P[i] = t.P[i - 1] * dk;
     t.Pinv[i] = t.Pinv[i - 1] * dki;
   }
-  NZ_HIP(hipMemcpyAsync((LinTab*)lin_tab.p + k, &t, sizeof(LinTab), hipMemcpyHostToDevice, st()));
+  NZ_HIP(hipMemcpyAsync((LinTab*)lin_tab.p + k, &t, sizeof(LinTab), hipMemcpyHostToDevice, s));
   Fr* q = lin_tile_pows(k);
   const int qn = (int)lin_qn;
-  hipLaunchKernelGGL(k_pow_tiles, dim3((qn + 255) / 256), dim3(256), 0, st(), t.P[kT], t.Pinv[kT], qn, q, q + qn);
+  hipLaunchKernelGGL(k_pow_tiles, dim3((qn + 255) / 256), dim3(256), 0, s, t.P[kT], t.Pinv[kT], qn, q, q + qn);
   NZ_HIP(hipGetLastError());
 }
 
@@ -1673,6 +1699,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       to4t(A.p, pol_a.p, A4.p, ba, 2, ss);
       to4t(B.p, pol_b.p, B4.p, bb, 2, ss);
       to4t(C.p, pol_c.p, C4.p, bc, 2, ss);
+      if (quot3) launch_gate_check(ss);  // t's divisibility from round 1's data (round 3 reads the flag)
       NZ_HIP(hipEventRecord(side_done, ss));
     } else {
       to4t(A.p, pol_a.p, A4.p, ba, 2);
@@ -1744,13 +1771,13 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
                        (const Fr*)fac, inverse(tt[1]));
     NZ_HIP(hipGetLastError());
     const int bz[3] = {9, 8, 7};
-    NZ_HIP(hipStreamWaitEvent(s, side_done, 0));  // A, B, C's NTTs (same scratch) are done
-    // Z's commitment needs only its coefficients: its MSM starts before the 4n coset NTT,
-    // which runs beside it on the main stream (single-proof round 2: -1 ms)
-    to4t_coefs(Z.p, pol_z.p, bz, 3, s);
+    // Z's transforms use their own scratch (ntt_scr2), so they need not wait for A, B, C's
+    // on aux[2] (round 3 does). Z's commitment needs only its coefficients: its MSM starts
+    // before the coset NTTs, which run beside it on the main stream (single-proof round 2: -1 ms)
+    to4t_coefs(Z.p, pol_z.p, bz, 3, s, ntt_scr2.p);
     lg("multiexp Z");
     commit_start(0, pol_z.p, n + 3);
-    to4t_evals4(pol_z.p, Z4.p, 3, s);
+    to4t_evals4(pol_z.p, Z4.p, 3, s, ntt_scr2.p);
     pZ = commit_finish(0);
   }
   tm[3] = ms_since(t2);
@@ -1775,6 +1802,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     q.bk2 = beta * k2;
     for (int k = 0; k < 4; k++) q.zhinv[k] = zh_inv[k];
     auto tq = std::chrono::steady_clock::now();
+    NZ_HIP(hipStreamWaitEvent(s, side_done, 0));  // A, B, C's coset evaluations (aux[2], round 1)
     if (quot3) {
       round3_quot3(beta, gamma, alpha, s);
     } else if (nPublic <= kQ29MaxPub) {
@@ -1839,9 +1867,11 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       Fr ev[7];
       // round 5's divPol1 tables (d = xi, xi w) on the host while the evaluations run
       eval_many(7, polys, lens, xs, ev, [&] {
-        lin_tables(0, xi);
-        lin_tables(1, xi * wn);
+        lin_tables(0, xi, aux[2]);
+        lin_tables(1, xi * wn, aux[2]);
+        NZ_HIP(hipEventRecord(pows_done, aux[2]));
       });
+      NZ_HIP(hipStreamWaitEvent(s, pows_done, 0));  // round 5's divPol1 reads them
       ea = ev[0];
       eb = ev[1];
       ec = ev[2];

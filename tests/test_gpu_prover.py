@@ -267,11 +267,14 @@ def test_msm_split_live_oracle():
     assert got == plonk.proof_to_bytes(proof)
 
 
-@pytest.mark.parametrize("quot3", ["0", "1"])
-def test_quotient_schedules_same_proof(quot3):
+@pytest.mark.parametrize("quot3,lcommit", [("0", "1"), ("1", "1"), ("1", "0")])
+def test_quotient_schedules_same_proof(quot3, lcommit):
     """The three-coset quotient (default, n >= 64) and the 4n coset one (NZCB_QUOT3=0; also
     every n < 64, e.g. p5 above) prove p8 bit for bit, and both report a broken gate as
-    snarkjs's "T Polynomial is not divisible" (a fresh process: the switch is read once)."""
+    snarkjs's "T Polynomial is not divisible" (a fresh process: the switch is read once).
+    Under the three-coset quotient the gate check runs on round 1's side stream with the
+    Lagrange-basis commitments (default) and in round 3 without them
+    (NZCB_LAGRANGE_COMMIT=0); after the error the context proves bit for bit again."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -290,7 +293,9 @@ def test_quotient_schedules_same_proof(quot3):
         "    ctx.prove_raw(binfmt.write_wtns(w)); raise SystemExit('no error')\n"
         "except nzcb.NzcbError as e:\n"
         "    assert str(e) == 'T Polynomial is not divisible', str(e)\n"
+        "proof, _ = ctx.prove_raw(wtns, bytes.fromhex(exp['blinding']))\n"
+        "assert proof.hex() == exp['proof_bin'], 'proof differs after the error'\n"
         "print('ok')\n" % (os.path.join(root, "nzcb-circom_amd"), root, GOLD))
-    env = dict(os.environ, NZCB_QUOT3=quot3)
+    env = dict(os.environ, NZCB_QUOT3=quot3, NZCB_LAGRANGE_COMMIT=lcommit)
     p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stdout + p.stderr
