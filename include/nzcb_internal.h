@@ -14,7 +14,8 @@ extern "C" {
 
 /* HIP-event timing of the MSM bucket-accumulation kernel (the dominant kernel):
  * out = {total ms, launches, MSM points, bucket entries} accumulated since the last
- * reset; enable = 1 / 0 turns timing on / off and resets, -1 only reads. */
+ * reset; enable = 1 / 0 turns timing on / off and resets, -1 only reads. Timing adds no
+ * host synchronisation (the entry count is copied with the MSM's window sums). */
 int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]);
 
 /* ---- Synthetic circuit + setup ------- */

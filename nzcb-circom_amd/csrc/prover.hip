@@ -577,8 +577,10 @@ __device__ __forceinline__ F29 q29_pi(const Fr* __restrict__ cl, const Fr* __res
 // i = j n + m (x = g w4^(4m + j), Z(w x) at j n + (m + 1) mod n, 1/Z_H by j); otherwise
 // the 4n coset g<w4> in natural order (x_i = g w4^i, Z(w x) at i + 4, 1/Z_H by i mod 4).
 // Every array holds npts = 3n or 4n points per polynomial.
+// 4 waves per SIMD (128 VGPRs, 24 B scratch) instead of the compiler's 3 (130 VGPRs):
+// 1.084 -> 1.011 ms isolated, bench unchanged (profiles/r4_env_q4_ab.txt)
 template <bool THREE>
-__global__ void __launch_bounds__(kT)
+__global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(4, 8)))
 k_quotient_coset29(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
                    const Fr* __restrict__ Z, const Fr* __restrict__ cq, const Fr* __restrict__ cs,
                    const Fr* __restrict__ cl, uint32_t npub, const Fr* __restrict__ Apub, size_t n,

@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 bash nzcb-circom_amd/tools/r4_envab.sh "$@" || exit 1
 shift 2
 i=0
-for cfg in "$@"; do
+for cfg in "$1" "${@: -1}"; do   # the first and the last setting only
   d=gpurun_out/${tag}_tl$i; rm -rf $d
   env $cfg timeout -k 10 240 rocprofv3 --kernel-trace --marker-trace -d $d -o run --output-format csv \
     -- python3 bench.py --lanes 1 --steps 6 --warmup 2 --no-cpu-baseline --no-probe > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
