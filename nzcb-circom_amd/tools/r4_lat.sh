@@ -7,7 +7,7 @@ tag=$1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread \
-  tests/test_gpu_prover.py tests/test_gpu_fullsize.py > gpurun_out/${tag}_pytest.log 2>&1 || { tail -30 gpurun_out/${tag}_pytest.log; exit 1; }
+  tests/test_gpu_prover.py tests/test_gpu_fullsize.py tests/test_gpu_wvm.py > gpurun_out/${tag}_pytest.log 2>&1 || { tail -30 gpurun_out/${tag}_pytest.log; exit 1; }
 tail -2 gpurun_out/${tag}_pytest.log
 bash nzcb-circom_amd/tools/r4_libab.sh "$@"
 # single-lane timeline of this build (tools/timeline.py)
