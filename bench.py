@@ -147,6 +147,49 @@ def cpu_baseline_sample(zkey_raw, wtns: bytes, n: int):
     return out
 
 
+def launch_plan(gpus: int, env) -> str:
+    """How `bench.py --gpus N` runs:
+    * "local": this process is the whole job (N = 1 without a launcher) or one rank of a
+      launcher's job whose WORLD_SIZE equals N;
+    * "spawn": N > 1 and no launcher; start N fresh ranks under torch.distributed.run.
+    A launcher's world that differs from --gpus is an error (exit 2): the line would
+    otherwise label one world with another's size."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != gpus:
+            print(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+            raise SystemExit(2)
+        return "local"
+    return "spawn" if gpus > 1 else "local"
+
+
+def spawn_ranks(gpus: int, argv) -> int:
+    """Start `gpus` ranks of this script under torch.distributed.run (127.0.0.1, a free
+    port) as a CHILD process and return its exit code. Called before anything in this
+    process imports torch or touches HIP, so the ranks are fresh processes that each
+    initialise their own GPU; rank 0's JSON line reaches stdout through the child."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def launch_check(world: int, rank: int, device: int, backend: str, dist) -> None:
+    """--launch-check: the launcher's decision without a proof. Every rank reports its rank
+    and device to rank 0, which prints one JSON line with n_gpus = dist's world size."""
+    got = [None] * world
+    dist.all_gather_object(got, {"rank": rank, "device": device})
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": dist.get_world_size(), "backend": backend,
+                          "ranks": got}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -163,7 +206,13 @@ def main():
                          "MSM split by point range over all ranks (scatter of scalar slices + gather of partials)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the isolated accumulation-kernel probe")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, report world size and devices, and exit (no GPU work)")
     args = ap.parse_args()
+
+    # before torch / nzcb / any HIP call: --gpus N > 1 without a launcher starts N ranks
+    if launch_plan(args.gpus, os.environ) == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -176,11 +225,35 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(device)
         if backend == "nccl":
+            # one GPU per rank: a world larger than the node's devices cannot be measured
+            if torch.cuda.device_count() < world:
+                print(f"bench.py: {world} ranks over RCCL need {world} GPUs, this node has "
+                      f"{torch.cuda.device_count()}", file=sys.stderr)
+                sys.exit(2)
+            torch.cuda.set_device(device)
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
+            if not args.launch_check:
+                torch.cuda.set_device(device)
             dist.init_process_group(backend)
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the process group has {dist.get_world_size()} ranks",
+                  file=sys.stderr)
+            sys.exit(2)
+        world = dist.get_world_size()
+    rank_devices = [device]
+    if dist is not None and not args.launch_check:
+        rank_devices = [None] * world
+        dist.all_gather_object(rank_devices, device)
+    if args.launch_check:
+        if dist is not None:
+            launch_check(world, rank, device, backend, dist)
+            dist.destroy_process_group()
+        else:
+            print(json.dumps({"launch_check": True, "n_gpus": 1, "backend": None,
+                              "ranks": [{"rank": 0, "device": device}]}), flush=True)
+        return
 
     import nzcb
     from nzcb import nzcplive
@@ -359,6 +432,8 @@ def main():
                                 else f"batch-shard x{world} (no collective)"),
                 "proofs_in_flight_per_gpu": args.lanes,
                 "msm_devices": msm_devices or None,
+                "rank_devices": rank_devices,
+                "dist_backend": backend if dist is not None else None,
             },
             "roofline": {
                 "kernel": "msm_accumulate29_kernel (fixed-base Pippenger bucket accumulation, c=17, 2^21+6 points)",

@@ -18,6 +18,22 @@ extern "C" {
  * host synchronisation (the entry count is copied with the MSM's window sums). */
 int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]);
 
+/* Guard words (csrc/common.h GuardScope): every device buffer a prover context allocates
+ * (proving key, lanes' working sets, MSM and NTT scratch) carries 4 KiB of a known pattern
+ * past its end. nzcb_debug_guard_check reads every guard on `device` (-1: all) back: 0
+ * when all are intact, NZCB_ERR_INTERNAL with the damaged buffers in err otherwise
+ * (checked / damaged: counts). Call it with no proof in flight. nzcb_debug_guard_selftest
+ * writes one word past a fresh guarded buffer and checks that exactly that is found. */
+int nzcb_debug_guard_check(int device, size_t* checked, int* damaged, nzcb_err* err);
+int nzcb_debug_guard_selftest(int device, nzcb_err* err);
+
+/* Fault injection (tests of the prover's own checks): the next proof on each lane of ctx
+ * perturbs its quotient t after round 3 (kind NZCB_FAULT_QUOTIENT: t[1] += 1), which
+ * the xi check must report as NZCB_ERR_INTERNAL "quotient check failed". One-shot per
+ * lane; kind 0 clears it. */
+#define NZCB_FAULT_QUOTIENT 1
+int nzcb_debug_inject_fault(nzcb_ctx* ctx, int kind);
+
 /* ---- Synthetic circuit + setup ------- */
 /* Builds the seeded synthetic circuit of oracle/synth.py and its snarkjs-0.4
  * PLONK zkey with trapdoor tau (32-byte LE normal) on `device`. Buffers are

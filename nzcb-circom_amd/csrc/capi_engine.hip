@@ -1,7 +1,9 @@
 // C-ABI: engine, device memory and kernel-level entry points (include/nzcb.h).
 #include <chrono>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../../include/nzcb_internal.h"
@@ -25,6 +27,63 @@ void set_err(nzcb_err* err, int code, const char* msg) {
   if (!err) return;
   err->code = code;
   std::snprintf(err->msg, sizeof(err->msg), "%s", msg);
+}
+
+// ---- guard words past device buffers (common.h GuardScope) ---------------------------
+thread_local int g_guard_scope = 0;
+namespace {
+struct GuardRec {
+  size_t bytes;
+  int device;
+};
+std::mutex g_guard_mu;
+std::map<void*, GuardRec>& guard_map() {
+  static std::map<void*, GuardRec> m;
+  return m;
+}
+}  // namespace
+
+void guard_register(void* base, size_t bytes) {
+  NZ_HIP(hipMemset((uint8_t*)base + bytes, kGuardByte, kGuardBytes));
+  int dev = 0;
+  NZ_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_guard_mu);
+  guard_map()[base] = GuardRec{bytes, dev};
+}
+
+void guard_unregister(void* base) {
+  std::lock_guard<std::mutex> lk(g_guard_mu);
+  guard_map().erase(base);
+}
+
+int guard_check(int device, size_t* checked, std::string* report) {
+  std::vector<std::pair<void*, GuardRec>> recs;
+  {
+    std::lock_guard<std::mutex> lk(g_guard_mu);
+    for (auto& kv : guard_map())
+      if (device < 0 || kv.second.device == device) recs.push_back(kv);
+  }
+  std::vector<uint8_t> h(kGuardBytes);
+  int bad = 0;
+  for (auto& r : recs) {
+    NZ_HIP(hipMemcpy(h.data(), (uint8_t*)r.first + r.second.bytes, kGuardBytes, hipMemcpyDeviceToHost));
+    size_t k = 0;
+    while (k < kGuardBytes && h[k] == kGuardByte) k++;
+    if (k == kGuardBytes) continue;
+    bad++;
+    if (report && bad <= 8) {
+      char line[160];
+      std::snprintf(line, sizeof(line), "%sbuffer %p (%zu bytes, device %d): guard byte %zu overwritten",
+                    report->empty() ? "" : "; ", r.first, r.second.bytes, r.second.device, k);
+      *report += line;
+    }
+  }
+  if (checked) *checked = recs.size();
+  return bad;
+}
+
+__global__ void k_guard_poke(uint32_t* p, size_t at) {
+  if (threadIdx.x == 0) p[at] = 0;
 }
 
 }  // namespace nzcb
@@ -393,5 +452,40 @@ int nzcb_msm_table_run(nzcb_msm_table* t, const void* dev_scalars, size_t count,
 }
 
 void nzcb_msm_table_destroy(nzcb_msm_table* t) { delete t; }
+
+int nzcb_debug_guard_check(int device, size_t* checked, int* damaged, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  std::string report;
+  const int bad = guard_check(device, checked, &report);
+  if (damaged) *damaged = bad;
+  if (bad) throw Error(NZCB_ERR_INTERNAL, std::to_string(bad) + " damaged guard(s): " + report);
+  if (err) err->code = 0;
+  return 0;
+  NZ_GUARD_END(err)
+}
+
+int nzcb_debug_guard_selftest(int device, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  NZ_HIP(hipSetDevice(device));
+  size_t before = 0;
+  guard_check(device, &before, nullptr);
+  int bad = 0;
+  {
+    GuardScope gs;
+    DevBuf<uint32_t> b(1000);
+    // one word written 7 words past the end: inside the guard, so legal memory, and found
+    hipLaunchKernelGGL(k_guard_poke, dim3(1), dim3(64), 0, nullptr, b.p, (size_t)1007);
+    NZ_HIP(hipGetLastError());
+    NZ_HIP(hipDeviceSynchronize());
+    bad = guard_check(device, nullptr, nullptr);
+  }
+  const int after = guard_check(device, nullptr, nullptr);
+  if (bad != 1 || after != 0)
+    throw Error(NZCB_ERR_INTERNAL, "guard self-test: overrun found " + std::to_string(bad) + " time(s), " +
+                                       std::to_string(after) + " left after release");
+  if (err) err->code = 0;
+  return 0;
+  NZ_GUARD_END(err)
+}
 
 }  // extern "C"

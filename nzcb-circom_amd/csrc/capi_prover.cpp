@@ -244,14 +244,29 @@ int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err) {
       }
     }
     std::unique_lock<std::shared_mutex> lk(ctx->cfg);
-    while (ctx->lanes() > (size_t)lanes) {
-      ctx->extra.pop_back();
-      for (auto& de : ctx->dev_extra) de.pop_back();
-    }
-    while (ctx->lanes() < (size_t)lanes) {
-      const int l = (int)ctx->lanes();
-      ctx->extra.emplace_back(new Prover(*ctx->p, l));
-      for (size_t d = 0; d < ctx->dev_p.size(); d++) ctx->dev_extra[d].emplace_back(new Prover(*ctx->dev_p[d], l));
+    const size_t before = ctx->lanes();
+    // trim every device's lane list to `k` lanes (a failed growth can leave device 0 one
+    // lane ahead of the others)
+    auto trim = [&](size_t k) {
+      while (ctx->extra.size() + 1 > k) ctx->extra.pop_back();
+      for (auto& de : ctx->dev_extra)
+        while (de.size() + 1 > k) de.pop_back();
+    };
+    try {
+      trim((size_t)lanes);
+      while (ctx->lanes() < (size_t)lanes) {
+        const int l = (int)ctx->lanes();
+        ctx->extra.emplace_back(new Prover(*ctx->p, l));
+        for (size_t d = 0; d < ctx->dev_p.size(); d++)
+          ctx->dev_extra[d].emplace_back(new Prover(*ctx->dev_p[d], l));
+      }
+    } catch (...) {
+      // growth failed (out of HBM): back to the previous count on every device, so the
+      // pool, lanes() and the allocations agree
+      trim(std::min(before, ctx->lanes()));
+      ctx->reset_pool();
+      (void)hipSetDevice(ctx->p->eng->device);
+      throw;
     }
     ctx->reset_pool();
     NZ_HIP(hipSetDevice(ctx->p->eng->device));
@@ -405,16 +420,22 @@ int prove_one(nzcb_ctx* ctx, const void* witness, size_t n, int kind, const uint
       nw = w.nWitness;
     }
     std::shared_lock<std::shared_mutex> lk(ctx->cfg);
+    // a lane of a device-set context may be on another GPU: Prover::prove selects its
+    // device, and the caller's current device is restored here
+    int caller_dev = 0;
+    NZ_HIP(hipGetDevice(&caller_dev));
     Prover* pr = ctx->acquire(log, log_user);
     try {
       pr->prove(values, nw, blinding, proof_out, pub_out, kind == NZCB_WITNESS_DEVICE);
     } catch (...) {
       pr->log = nullptr;
       ctx->release(pr);
+      (void)hipSetDevice(caller_dev);
       throw;
     }
     pr->log = nullptr;
     ctx->release(pr);
+    NZ_HIP(hipSetDevice(caller_dev));
     if (err) err->code = 0;
     return 0;
   } catch (const Error& e) {
@@ -459,6 +480,9 @@ int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap) {
 
 int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
   if (!ctx) return NZCB_ERR_ARG;
+  // exclusive: no proof is between msm_enqueue and msm_finish while `prof` flips (ADVICE
+  // r4: finish would time events that enqueue never recorded), and no set_lanes runs
+  std::unique_lock<std::shared_mutex> lk(ctx->cfg);
   if (out) {
     for (int i = 0; i < 4; i++) out[i] = 0;
     for (Prover* q : ctx->all())
@@ -477,6 +501,13 @@ int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
         m->prof_launches = m->prof_points = m->prof_entries = 0;
       }
   }
+  return 0;
+}
+
+int nzcb_debug_inject_fault(nzcb_ctx* ctx, int kind) {
+  if (!ctx || (kind != 0 && kind != NZCB_FAULT_QUOTIENT)) return NZCB_ERR_ARG;
+  std::unique_lock<std::shared_mutex> lk(ctx->cfg);
+  for (Prover* q : ctx->all()) q->fault = kind;
   return 0;
 }
 

@@ -30,25 +30,60 @@ void set_err(nzcb_err* err, int code, const char* msg);
                                                     __FILE__ + ":" + std::to_string(__LINE__)); \
   } while (0)
 
+// Guard words past the end of device buffers (the round-4 overrun of the
+// three-coset quotient buffer surfaced as an illegal access two kernels later). While a
+// GuardScope is alive on the calling thread (the prover's lane and proving-key
+// allocations), every DevBuf::alloc adds kGuardBytes of kGuardByte past the end and
+// registers them; guard_check() reads every registered guard back (capi_engine.hip).
+constexpr size_t kGuardBytes = 4096;
+constexpr unsigned char kGuardByte = 0xA5;
+extern thread_local int g_guard_scope;
+struct GuardScope {
+  GuardScope() { g_guard_scope++; }
+  ~GuardScope() { g_guard_scope--; }
+  GuardScope(const GuardScope&) = delete;
+  GuardScope& operator=(const GuardScope&) = delete;
+};
+void guard_register(void* base, size_t bytes);  // writes the pattern (synchronously)
+void guard_unregister(void* base);
+// every registered guard on `device` (-1: all devices): the number found damaged; `report`
+// lists them (address, buffer bytes, first damaged offset)
+int guard_check(int device, size_t* checked, std::string* report);
+
 // Plain owning device buffer.
 template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
   bool owned = true;  // false: a view of another buffer (shared proving-key data)
+  bool guarded = false;
   DevBuf() = default;
   explicit DevBuf(size_t count) { alloc(count); }
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
-  DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n), owned(o.owned) { o.p = nullptr; o.n = 0; }
+  DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n), owned(o.owned), guarded(o.guarded) {
+    o.p = nullptr;
+    o.n = 0;
+    o.guarded = false;
+  }
   DevBuf& operator=(DevBuf&& o) noexcept {
-    if (this != &o) { release(); p = o.p; n = o.n; owned = o.owned; o.p = nullptr; o.n = 0; }
+    if (this != &o) {
+      release();
+      p = o.p; n = o.n; owned = o.owned; guarded = o.guarded;
+      o.p = nullptr; o.n = 0; o.guarded = false;
+    }
     return *this;
   }
   ~DevBuf() { release(); }
   void alloc(size_t count) {
     release();
-    if (count) NZ_HIP(hipMalloc(&p, count * sizeof(T)));
+    if (g_guard_scope > 0) {
+      NZ_HIP(hipMalloc(&p, count * sizeof(T) + kGuardBytes));
+      guard_register(p, count * sizeof(T));
+      guarded = true;
+    } else if (count) {
+      NZ_HIP(hipMalloc(&p, count * sizeof(T)));
+    }
     n = count;
     owned = true;
   }
@@ -59,9 +94,13 @@ struct DevBuf {
     owned = false;
   }
   void release() {
-    if (p && owned) (void)hipFree(p);
+    if (p && owned) {
+      if (guarded) guard_unregister(p);
+      (void)hipFree(p);
+    }
     p = nullptr;
     n = 0;
+    guarded = false;
   }
   size_t bytes() const { return n * sizeof(T); }
 };

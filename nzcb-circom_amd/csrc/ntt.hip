@@ -12,22 +12,18 @@
 // read + one write of the array (algorithmic 64 B per element per pass).
 //
 // The pass is bound by Montgomery products (one per butterfly), so the kernel is
-// shaped for issue rate: 512 threads per 64 KiB tile (2 tiles per CU -> 4 waves
+// shaped for issue rate: 256 threads per 1024-element tile (4 tiles per CU -> 4 waves
 // per SIMD), stages are done two at a time as radix-4 groups held in registers
 // (4 elements per thread: half the LDS traffic and barriers of radix-2), twiddles
 // come from per-stage compact tables (consecutive butterflies -> consecutive
 // twiddles), and stage 0's unit twiddles are skipped.
 #include "ntt.h"
 
-#include <cstdlib>
 #include <vector>
 
 namespace nzcb {
 
-static constexpr int kTileElems = 2048;  // 64 KiB of Fr per workgroup
-static constexpr int kNttThreads = 512;
-static constexpr int kBfPerThread = kTileElems / 2 / kNttThreads;  // 2
-static_assert(kTileElems / 4 == kNttThreads, "one radix-4 group per thread");
+static constexpr int kTile = 1024;  // elements per LDS tile: 9 x 4 KiB of 29-bit limbs, 256 threads
 
 Fr fr_root_of_unity(int k) {
   Fr w;
@@ -76,8 +72,7 @@ void NttTables::init(int L, hipStream_t st) {
   if (L > 8) scratch29.alloc((size_t)9 << L);  // the 9x29 pipeline's inter-pass values
   const size_t half = L >= 1 ? (size_t(1) << (L - 1)) : 1;
   const size_t total = (size_t(1) << L) - 1;
-  fwd.alloc(total ? total : 1);
-  inv.alloc(total ? total : 1);
+  DevBuf<Fr> stage(total ? total : 1);  // one direction's Montgomery-256 stage table
   fwd29.alloc(total ? total : 1);
   inv29.alloc(total ? total : 1);
   DevBuf<Fr> full(half);
@@ -97,148 +92,12 @@ void NttTables::init(int L, hipStream_t st) {
                        half);
     if (total) {
       hipLaunchKernelGGL(ntt_stage_table_kernel, dim3(grid_for(total, 256, 1u << 30)), dim3(256), 0, st,
-                         dir ? inv.p : fwd.p, full.p, L, total);
+                         stage.p, full.p, L, total);
       hipLaunchKernelGGL(ntt_tw29_kernel, dim3(grid_for(total, 256, 1u << 30)), dim3(256), 0, st,
-                         dir ? inv29.p : fwd29.p, dir ? inv.p : fwd.p, total);
+                         dir ? inv29.p : fwd29.p, stage.p, total);
     }
     NZ_HIP(hipGetLastError());
     NZ_HIP(hipStreamSynchronize(st));
-  }
-}
-
-// One pass: stages [s, s+q) on tiles of (2^q rows) x (2^logC columns).
-__global__ void __launch_bounds__(kNttThreads)
-ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s, int q, int logC, int first,
-                F29 scale29, int do_scale, int last, NttIo io, int sparse4) {
-  extern __shared__ Fr tile[];
-  const int C = 1 << logC;
-  const int rows = 1 << q;
-  const int n_el = rows << logC;
-  const int tid = threadIdx.x;
-  const size_t t = blockIdx.x;
-  size_t base = 0, c0 = 0, lo0 = 0;
-  if (first) {
-    c0 = t << logC;
-    for (int e = tid; e < n_el; e += kNttThreads) {
-      int j = e >> logC, c = e & (C - 1);
-      size_t src = ((size_t)bit_rev((uint32_t)j, q) << (L - q)) + c0 + c;
-      Fr v = Fr::zero();
-      if (src < io.in_len) {
-        v = in[src];
-        if (src < io.fold_len) v = v + mul_fr29(in[src + io.fold_n], io.fold_f);
-        if (io.in_f) v = mul_fr29(v, io.in_f[src]);
-        if (do_scale) v = mul_fr29(v, scale29);
-      }
-      tile[e] = v;
-    }
-  } else {
-    size_t groups_lo = ((size_t)1 << s) >> logC;
-    size_t hi = t / groups_lo;
-    lo0 = (t % groups_lo) << logC;
-    base = (hi << (s + q)) + lo0;
-    for (int e = tid; e < n_el; e += kNttThreads) {
-      int j = e >> logC, c = e & (C - 1);
-      tile[e] = in[base + ((size_t)j << s) + c];
-    }
-  }
-  __syncthreads();
-  const int nbf = n_el >> 1;
-  int st = 0;
-  if (sparse4 && blockIdx.x != 0) {
-    // zero-padded input (only the first N/4 entries nonzero, past tile 0): of every four
-    // bit-reversed rows 4m..4m+3 only row 4m is nonzero, and stages 0-1 map (x, 0, 0, 0)
-    // to (x, x, x, x) whatever the twiddles, so the first radix-4 step is a copy
-    for (int e = tid; e < n_el; e += kNttThreads) {
-      const int j = e >> logC;
-      if (j & 3) tile[e] = tile[((j & ~3) << logC) + (e & (C - 1))];
-    }
-    __syncthreads();
-    st = 2;
-  } else if (q & 1) {  // odd stage count: one radix-2 stage, then radix-4 pairs of stages
-    const int g = s;
-    const F29* __restrict__ twg = tw + (((size_t)1 << g) - 1);
-#pragma unroll
-    for (int u = 0; u < kBfPerThread; u++) {
-      const int b = tid + u * kNttThreads;
-      if (b >= nbf) continue;
-      const int c = b & (C - 1);
-      const int j0 = b >> logC;  // stage span 1: pairs (2 pr, 2 pr + 1)
-      const int i0 = ((2 * j0) << logC) + c, i1 = ((2 * j0 + 1) << logC) + c;
-      const size_t k = first ? 0 : (lo0 + c);
-      const Fr x0 = tile[i0];
-      const Fr x1 = g ? mul_fr29(tile[i1], twg[k]) : tile[i1];
-      tile[i0] = x0 + x1;
-      tile[i1] = x0 - x1;
-    }
-    __syncthreads();
-    st = 1;
-  }
-  // radix-4: stages st and st+1 on 4 elements per thread (half the LDS round trips and
-  // barriers of two radix-2 stages); twiddles: stage g at low, stage g+1 at low, low+h
-  const int ngroups = n_el >> 2;
-#pragma unroll 1
-  for (; st < q; st += 2) {
-    const int h = 1 << st;
-    const int g = s + st;
-    const F29* __restrict__ twa = tw + (((size_t)1 << g) - 1);
-    const F29* __restrict__ twb = tw + (((size_t)1 << (g + 1)) - 1);
-    const int b = tid;
-    if (b < ngroups) {
-      const int c = b & (C - 1);
-      const int pr = b >> logC;
-      const int low = pr & (h - 1);
-      const int j = ((pr >> st) << (st + 2)) | low;
-      const size_t ka = first ? (size_t)low : (((size_t)low << s) + lo0 + c);
-      const size_t kc = first ? (size_t)(low + h) : (((size_t)(low + h) << s) + lo0 + c);
-      const F29 wb = twb[ka];
-      const F29 wc = twb[kc];
-      const int i0 = (j << logC) + c, i1 = ((j + h) << logC) + c, i2 = ((j + 2 * h) << logC) + c,
-                i3 = ((j + 3 * h) << logC) + c;
-      const Fr x0 = tile[i0], x1 = tile[i1], x2 = tile[i2], x3 = tile[i3];
-      // x2 +- w x3 only feed the products by wb, wc: they stay in radix 2^29, unreduced
-      // (w x3 < r + 2^249 with limbs < 2^29; x2 + 2r - w x3 < 3r with limbs < 2^30.6,
-      // which mul29 accepts against a canonical twiddle, f29.h), saving a join, two
-      // 8 x 32 modular add/subs and two splits per group
-      Fr t1 = x1;
-      F29 t3 = split29(x3);
-      if (g) {
-        const F29 wa = twa[ka];
-        t1 = mul_fr29(x1, wa);
-        t3 = mul29<Fr29>(t3, wa);
-      }
-      const Fr y0 = x0 + t1, y1 = x0 - t1;
-      const F29 x2s = split29(x2);
-      F29 y2;
-#pragma unroll
-      for (int l = 0; l < 9; l++) y2.v[l] = x2s.v[l] + t3.v[l];
-      const F29 y3 = sub29_nn(x2s, t3, Fr29::K2);
-      const Fr u2 = join_fr29(mul29<Fr29>(y2, wb)), u3 = join_fr29(mul29<Fr29>(y3, wc));
-      tile[i0] = y0 + u2;
-      tile[i2] = y0 - u2;
-      tile[i1] = y1 + u3;
-      tile[i3] = y1 - u3;
-    }
-    __syncthreads();
-  }
-  // final store, with the optional epilogue on the transform's last pass
-  auto store = [&](size_t dst, Fr v) {
-    if (last) {
-      if (io.out_f) v = mul_fr29(v, io.out_f[dst]);
-      if (io.out_flags && dst >= io.out_limit && !v.is_zero()) atomicOr(io.out_flags, 1u);
-    }
-    out[dst] = v;
-  };
-  if (first) {
-    for (int e = tid; e < n_el; e += kNttThreads) {
-      int j = e & (rows - 1), c = e >> q;
-      size_t dst = ((size_t)bit_rev((uint32_t)(c0 + c), L - q) << q) + j;
-      store(dst, tile[(j << logC) + c]);
-    }
-  } else {
-    for (int e = tid; e < n_el; e += kNttThreads) {
-      int j = e >> logC, c = e & (C - 1);
-      store(base + ((size_t)j << s) + c, tile[e]);
-    }
   }
 }
 
@@ -262,10 +121,9 @@ ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s,
 //    (v_8 = the top limb, bits 232..), v - q r < r + (q + 1) 2^232 < 2r, then one
 //    conditional subtraction (join_fr29); with an output factor the product < 1.4 r is
 //    joined directly.
-// elements per tile: 1024 (9 x 4 KiB of limbs = 36 KiB LDS, 256 threads, 4 tiles per CU) or
-// 2048 (72 KiB, 512 threads, 2 tiles per CU; NZCB_NTT_TILE=2048): the same 4 waves per SIMD,
-// in twice as many independent barrier domains with the smaller tile; one radix-4 group per
-// thread either way
+// elements per tile: 1024 (9 x 4 KiB of limbs = 36 KiB LDS, 256 threads, 4 tiles per CU), one
+// radix-4 group per thread; 2048-element tiles (72 KiB, 2 per CU) give the same 4 waves per
+// SIMD in half as many barrier domains and measured slower (profiles/r3_ntt_tile_ab.txt)
 
 // LDS slot of tile element e: bits 0-4 XORed with a function of bits 5-7, a bijection on
 // every 32-element block. ds_read_b32 / ds_write_b32 bank by (address / 4) mod 32 per
@@ -274,23 +132,20 @@ ntt_pass_kernel(const Fr* in, Fr* out, const F29* __restrict__ tw, int L, int s,
 // element stride 32) 8 banks (4-way); swizzled, every access pattern of the kernel
 // (row-major loads/stores, all radix-4 operand sets at each stage, the odd radix-2
 // stage, the sparse copy) is conflict-free (checked exhaustively for q = 6, 7, 8).
-// swz = ~0 (default) or 0 (NZCB_NTT_SWIZZLE=0: the linear layout, for A/B runs)
-__device__ __forceinline__ int tile_slot(int e, int swz) {
-  return e ^ (swz & ((((e >> 5) & 3) << 3) | ((e >> 5) & 7)));
+__device__ __forceinline__ int tile_slot(int e) {
+  return e ^ ((((e >> 5) & 3) << 3) | ((e >> 5) & 7));
 }
-template <int TILE>
-__device__ __forceinline__ F29 tile_ld(const uint32_t* sl, int e, int swz) {
-  const int p = tile_slot(e, swz);
+__device__ __forceinline__ F29 tile_ld(const uint32_t* sl, int e) {
+  const int p = tile_slot(e);
   F29 x;
 #pragma unroll
-  for (int l = 0; l < 9; l++) x.v[l] = sl[l * TILE + p];
+  for (int l = 0; l < 9; l++) x.v[l] = sl[l * kTile + p];
   return x;
 }
-template <int TILE>
-__device__ __forceinline__ void tile_st(uint32_t* sl, int e, const F29& x, int swz) {
-  const int p = tile_slot(e, swz);
+__device__ __forceinline__ void tile_st(uint32_t* sl, int e, const F29& x) {
+  const int p = tile_slot(e);
 #pragma unroll
-  for (int l = 0; l < 9; l++) sl[l * TILE + p] = x.v[l];
+  for (int l = 0; l < 9; l++) sl[l * kTile + p] = x.v[l];
 }
 __device__ __forceinline__ F29 add_nn29(const F29& a, const F29& b) {
   F29 r;
@@ -320,12 +175,12 @@ __device__ __forceinline__ Fr canon_fr29(const F29& x) {  // normalized x < 64 r
 // One pass of stages [s, s+q) on tiles of (2^q rows) x (2^logC columns). IN29: values from
 // the F29 scratch (else the Fr input, first pass only); OUT29: values to the F29 scratch
 // (else canonical Fr to `out`, last pass only).
-template <bool IN29, bool OUT29, int TILE>
-__global__ void __launch_bounds__(TILE / 4)
+template <bool IN29, bool OUT29>
+__global__ void __launch_bounds__(kTile / 4)
 ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29* __restrict__ tw, int L, int s,
-                  int q, int logC, F29 scale29, int do_scale, NttIo io, int sparse4, int swz) {
-  constexpr int T = TILE / 4;  // threads
-  __shared__ uint32_t sl[9 * TILE];
+                  int q, int logC, F29 scale29, int do_scale, NttIo io, int sparse4) {
+  constexpr int T = kTile / 4;  // threads
+  __shared__ uint32_t sl[9 * kTile];
   const int C = 1 << logC;
   const int rows = 1 << q;
   const int n_el = rows << logC;
@@ -354,7 +209,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
         if (io.in_f) x = mul29<Fr29>(x, io.in_f[src]);
         if (do_scale) x = mul29<Fr29>(x, scale29);
       }
-      tile_st<TILE>(sl, e, x, swz);
+      tile_st(sl, e, x);
     }
   } else {
     const size_t groups_lo = ((size_t)1 << s) >> logC;
@@ -363,7 +218,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
     base = (hi << (s + q)) + lo0;
     for (int e = tid; e < n_el; e += T) {
       const int j = e >> logC, c = e & (C - 1);
-      tile_st<TILE>(sl, e, in29[base + ((size_t)j << s) + c], swz);
+      tile_st(sl, e, in29[base + ((size_t)j << s) + c]);
     }
   }
   __syncthreads();
@@ -376,7 +231,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
     // is a copy
     for (int e = tid; e < n_el; e += T) {
       const int j = e >> logC;
-      if (j & 3) tile_st<TILE>(sl, e, tile_ld<TILE>(sl, ((j & ~3) << logC) + (e & (C - 1)), swz), swz);
+      if (j & 3) tile_st(sl, e, tile_ld(sl, ((j & ~3) << logC) + (e & (C - 1))));
     }
     __syncthreads();
     st = 2;
@@ -391,14 +246,14 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       const int j0 = b >> logC;
       const int i0 = ((2 * j0) << logC) + c, i1 = ((2 * j0 + 1) << logC) + c;
       const size_t k = first ? 0 : (lo0 + c);
-      const F29 x0 = tile_ld<TILE>(sl, i0, swz);
-      const F29 x1 = tile_ld<TILE>(sl, i1, swz);
+      const F29 x0 = tile_ld(sl, i0);
+      const F29 x1 = tile_ld(sl, i1);
       const F29 tt = g ? mul29<Fr29>(x1, twg[k]) : x1;
       F29 y0 = add_nn29(x0, tt), y1 = sub2r_nn29(x0, tt);
       norm29(y0);
       norm29(y1);
-      tile_st<TILE>(sl, i0, y0, swz);
-      tile_st<TILE>(sl, i1, y1, swz);
+      tile_st(sl, i0, y0);
+      tile_st(sl, i1, y1);
     }
     __syncthreads();
     st = 1;
@@ -420,7 +275,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       const size_t kc = first ? (size_t)(low + h) : (((size_t)(low + h) << s) + lo0 + c);
       const int i0 = (j << logC) + c, i1 = ((j + h) << logC) + c, i2 = ((j + 2 * h) << logC) + c,
                 i3 = ((j + 3 * h) << logC) + c;
-      F29 t1 = tile_ld<TILE>(sl, i1, swz), t3 = tile_ld<TILE>(sl, i3, swz);
+      F29 t1 = tile_ld(sl, i1), t3 = tile_ld(sl, i3);
       if (g) {
         const F29 wa = twa[ka];
         F29 p1, p3;
@@ -428,7 +283,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
         t1 = p1;
         t3 = p3;
       }
-      const F29 x0 = tile_ld<TILE>(sl, i0, swz), x2 = tile_ld<TILE>(sl, i2, swz);
+      const F29 x0 = tile_ld(sl, i0), x2 = tile_ld(sl, i2);
       const F29 y0 = add_nn29(x0, t1), y1 = sub2r_nn29(x0, t1);
       const F29 y2 = add_nn29(x2, t3), y3 = sub2r_nn29(x2, t3);
       F29 u2, u3;
@@ -438,10 +293,10 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       norm29(z1);
       norm29(z2);
       norm29(z3);
-      tile_st<TILE>(sl, i0, z0, swz);
-      tile_st<TILE>(sl, i1, z1, swz);
-      tile_st<TILE>(sl, i2, z2, swz);
-      tile_st<TILE>(sl, i3, z3, swz);
+      tile_st(sl, i0, z0);
+      tile_st(sl, i1, z1);
+      tile_st(sl, i2, z2);
+      tile_st(sl, i3, z3);
     }
     __syncthreads();
   }
@@ -458,78 +313,51 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
     for (int e = tid; e < n_el; e += T) {
       const int j = e & (rows - 1), c = e >> q;
       const size_t dst = ((size_t)bit_rev((uint32_t)(c0 + c), L - q) << q) + j;
-      store(dst, tile_ld<TILE>(sl, (j << logC) + c, swz));
+      store(dst, tile_ld(sl, (j << logC) + c));
     }
   } else {
     for (int e = tid; e < n_el; e += T) {
       const int j = e >> logC, c = e & (C - 1);
-      store(base + ((size_t)j << s) + c, tile_ld<TILE>(sl, e, swz));
+      store(base + ((size_t)j << s) + c, tile_ld(sl, e));
     }
   }
 }
 
-static int ntt29_swizzle() {  // NZCB_NTT_SWIZZLE=0: linear LDS tiles (A/B runs)
-  static const int m = [] {
-    const char* e = std::getenv("NZCB_NTT_SWIZZLE");
-    return (e && e[0] == '0') ? 0 : ~0;
-  }();
-  return m;
-}
-
-static bool ntt29_enabled() {  // NZCB_NTT29=0: the 8x32 pipeline (ntt_pass_kernel) for A/B runs
-  static const bool on = [] {
-    const char* e = std::getenv("NZCB_NTT29");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// 1024-element tiles by default: 2^23 forward 1.074 -> 1.054 ms, 2^21 0.282 -> 0.275 ms on
-// one box (profiles/r3_ntt_tile_ab.txt); NZCB_NTT_TILE=2048 restores 72 KiB tiles (A/B runs)
-static int ntt29_tile() {
-  static const int v = [] {
-    const char* e = std::getenv("NZCB_NTT_TILE");
-    return (e && std::atoi(e) == 2048) ? 2048 : 1024;
-  }();
-  return v;
-}
-
 // The 9x29 pipeline's passes: stages [0, q1) with the bit-reversed gather, then <= 8
 // stages per pass through the F29 scratch; the last pass writes canonical Fr.
-template <int TILE>
-static void ntt29_passes(const NttTables& t, const Fr* in, Fr* out, const F29* tw, int L, const F29& sc29,
-                         int do_scale, const NttIo& io, bool sparse_ok, int swz, hipStream_t st, F29* scr) {
-  constexpr int T = TILE / 4;
+static void ntt29_passes(const Fr* in, Fr* out, const F29* tw, int L, const F29& sc29, int do_scale,
+                         const NttIo& io, hipStream_t st, F29* scr) {
+  constexpr int T = kTile / 4;
   const int q1 = L < 8 ? L : 8;
   const int cols = 1 << (L - q1);
   int logC1 = 0;
-  while ((1 << (logC1 + 1)) <= cols && ((1 << (q1 + logC1 + 1)) <= TILE)) logC1++;
+  while ((1 << (logC1 + 1)) <= cols && ((1 << (q1 + logC1 + 1)) <= kTile)) logC1++;
   const size_t tiles = (size_t)cols >> logC1;
   // inputs nonzero only below N/4 (+ a few in tile 0's columns: the blinding terms):
   // tiles past the first skip stages 0-1 (a 4n coset NTT of an n+3-term polynomial)
-  const int sparse4 = sparse_ok && L >= 2 && q1 >= 2 && !(q1 & 1) &&
+  const int sparse4 = L >= 2 && q1 >= 2 && !(q1 & 1) &&
                       io.in_len <= ((size_t)1 << (L - 2)) + ((size_t)1 << logC1);
   if (q1 == L) {
-    hipLaunchKernelGGL((ntt29_pass_kernel<false, false, TILE>), dim3((unsigned)tiles), dim3(T), 0, st, in,
-                       (const F29*)nullptr, out, (F29*)nullptr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4, swz);
+    hipLaunchKernelGGL((ntt29_pass_kernel<false, false>), dim3((unsigned)tiles), dim3(T), 0, st, in,
+                       (const F29*)nullptr, out, (F29*)nullptr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4);
     NZ_HIP(hipGetLastError());
     return;
   }
-  hipLaunchKernelGGL((ntt29_pass_kernel<false, true, TILE>), dim3((unsigned)tiles), dim3(T), 0, st, in,
-                     (const F29*)nullptr, (Fr*)nullptr, scr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4, swz);
+  hipLaunchKernelGGL((ntt29_pass_kernel<false, true>), dim3((unsigned)tiles), dim3(T), 0, st, in,
+                     (const F29*)nullptr, (Fr*)nullptr, scr, tw, L, 0, q1, logC1, sc29, do_scale, io, sparse4);
   NZ_HIP(hipGetLastError());
   int s = q1;
   while (s < L) {
     const int q = (L - s) < 8 ? (L - s) : 8;
     int logC = 0;
-    while (logC + 1 <= s && (1 << (q + logC + 1)) <= TILE) logC++;
+    while (logC + 1 <= s && (1 << (q + logC + 1)) <= kTile) logC++;
     const size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
     if (s + q == L)
-      hipLaunchKernelGGL((ntt29_pass_kernel<true, false, TILE>), dim3((unsigned)ntiles), dim3(T), 0, st,
-                         (const Fr*)nullptr, (const F29*)scr, out, (F29*)nullptr, tw, L, s, q, logC, sc29, 0, io, 0, swz);
+      hipLaunchKernelGGL((ntt29_pass_kernel<true, false>), dim3((unsigned)ntiles), dim3(T), 0, st,
+                         (const Fr*)nullptr, (const F29*)scr, out, (F29*)nullptr, tw, L, s, q, logC, sc29, 0, io, 0);
     else
-      hipLaunchKernelGGL((ntt29_pass_kernel<true, true, TILE>), dim3((unsigned)ntiles), dim3(T), 0, st,
-                         (const Fr*)nullptr, (const F29*)scr, (Fr*)nullptr, scr, tw, L, s, q, logC, sc29, 0, io, 0, swz);
+      hipLaunchKernelGGL((ntt29_pass_kernel<true, true>), dim3((unsigned)ntiles), dim3(T), 0, st,
+                         (const Fr*)nullptr, (const F29*)scr, (Fr*)nullptr, scr, tw, L, s, q, logC, sc29, 0, io, 0);
     NZ_HIP(hipGetLastError());
     s += q;
   }
@@ -540,6 +368,8 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   const NttIo io = iop ? *iop : NttIo();
   if (L > t.max_log) throw Error(NZCB_ERR_ARG, "ntt size exceeds table");
   if (in == out) throw Error(NZCB_ERR_ARG, "ntt requires in != out");
+  F29* scr = (F29*)(scratch29 ? scratch29 : t.scratch29.p);
+  if (L > 8 && !scratch29 && t.scratch29.n < ((size_t)9 << L)) throw Error(NZCB_ERR_INTERNAL, "ntt: no scratch");
   const F29* tw = inverse_dir ? t.inv29.p : t.fwd29.p;
   Fr sc = Fr::one();
   int do_scale = 0;
@@ -553,51 +383,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
     do_scale = 1;
   }
   for (int k = 0; k < 5; k++) sc = sc + sc;  // Montgomery-261 operand of mul_fr29
-  const F29 sc29 = split29(sc);
-  if (L == 0) {
-    hipLaunchKernelGGL(ntt_pass_kernel, dim3(1), dim3(kNttThreads), sizeof(Fr), st, in, out, tw, 0, 0, 0, 0, 1, sc29,
-                       do_scale, 1, io, 0);
-    NZ_HIP(hipGetLastError());
-    return;
-  }
-  int q1 = L < 8 ? L : 8;
-  int cols = 1 << (L - q1);
-  int logC1 = 0;
-  while ((1 << (logC1 + 1)) <= cols && ((1 << (q1 + logC1 + 1)) <= kTileElems)) logC1++;
-  size_t tiles = (size_t)cols >> logC1;
-  size_t lds = (size_t(1) << (q1 + logC1)) * sizeof(Fr);
-  // inputs nonzero only below N/4 (+ a few in tile 0's columns: the blinding terms):
-  // tiles past the first skip stages 0-1 (a 4n coset NTT of an n+3-term polynomial)
-  static const bool sparse_ok = [] {  // NZCB_NTT_SPARSE=0 disables (A/B measurements)
-    const char* e = std::getenv("NZCB_NTT_SPARSE");
-    return !(e && e[0] == '0');
-  }();
-  const int sparse4 = sparse_ok && L >= 2 && q1 >= 2 && !(q1 & 1) &&
-                      io.in_len <= ((size_t)1 << (L - 2)) + ((size_t)1 << logC1);
-  if (ntt29_enabled() && (q1 == L || scratch29 || t.scratch29.n >= ((size_t)9 << L))) {
-    const int swz = ntt29_swizzle();
-    F29* scr = (F29*)(scratch29 ? scratch29 : t.scratch29.p);
-    if (ntt29_tile() == 1024)
-      ntt29_passes<1024>(t, in, out, tw, L, sc29, do_scale, io, sparse_ok, swz, st, scr);
-    else
-      ntt29_passes<2048>(t, in, out, tw, L, sc29, do_scale, io, sparse_ok, swz, st, scr);
-    return;
-  }
-  hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)tiles), dim3(kNttThreads), lds, st, in, out, tw, L, 0, q1, logC1,
-                     1, sc29, do_scale, q1 == L ? 1 : 0, io, sparse4);
-  NZ_HIP(hipGetLastError());
-  int s = q1;
-  while (s < L) {
-    int q = (L - s) < 8 ? (L - s) : 8;
-    int logC = 0;
-    while (logC + 1 <= s && (1 << (q + logC + 1)) <= kTileElems) logC++;
-    size_t ntiles = ((size_t)1 << (L - s - q)) * (((size_t)1 << s) >> logC);
-    size_t lds2 = (size_t(1) << (q + logC)) * sizeof(Fr);
-    hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)ntiles), dim3(kNttThreads), lds2, st, out, out, tw, L, s, q,
-                       logC, 0, sc29, 0, s + q == L ? 1 : 0, io, 0);
-    NZ_HIP(hipGetLastError());
-    s += q;
-  }
+  ntt29_passes(in, out, tw, L, split29(sc), do_scale, io, st, scr);
 }
 
 }  // namespace nzcb

@@ -63,6 +63,7 @@ struct Prover {
   DevBuf<Fr> qm, ql, qr, qo, qc;  // [n coefs | 4n evals]
   DevBuf<Fr> sigma;               // 3 x [n | 4n]
   DevBuf<Fr> sig_h;               // 3 x n: sigma_k(w^i), contiguous (round 2)
+  DevBuf<Fr> q_h;                 // 5 x n: qm..qc(w^i), contiguous (the gate check on H, quot3)
   DevBuf<Fr> lagrange;            // nLagrange x [n | 4n]
   DevBuf<uint32_t> amap, bmap, cmap;
   DevBuf<AddRec> adds;
@@ -103,6 +104,7 @@ struct Prover {
   Fr* top_host = nullptr;
   static constexpr int kTopWords = 4 * 6 + 1;
 
+  int fault = 0;  // nzcb_debug_inject_fault: NZCB_FAULT_* for this lane's next proof
   // timings of the last proof (ms)
   double tm[9] = {0};
 

@@ -633,17 +633,16 @@ k_quotient_coset29(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr*
 
 // The three-coset quotient's divisibility check: N vanishes on H iff every gate holds
 // there (the permutation part vanishes on H once round 2's copy check passed, z(1) = 1 by
-// construction), i.e. qm a b + ql a + qr b + qo c + qc - PI = 0 at every w^m; the zkey's
-// 4n evaluations (plain domain) hold the selectors on H at stride 4
+// construction), i.e. qm a b + ql a + qr b + qo c + qc - PI = 0 at every w^m. The selectors
+// on H are the zkey's 4n evaluations at stride 4, copied once per context into q_h
+// (5 x n, contiguous: the stride-4 reads fetched a 128-byte line per 32-byte value)
 __global__ void __launch_bounds__(kT)
-k_gate_h(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C, const Fr* __restrict__ qm,
-         const Fr* __restrict__ ql, const Fr* __restrict__ qr, const Fr* __restrict__ qo, const Fr* __restrict__ qc,
+k_gate_h(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C, const Fr* __restrict__ qh,
          size_t n, uint32_t npub, uint32_t* __restrict__ flags) {
   const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= n) return;
-  const size_t e = n + 4 * m;
   const Fr a = A[m], b = B[m], c = C[m];
-  Fr g = qm[e] * a * b + ql[e] * a + qr[e] * b + qo[e] * c + qc[e];
+  Fr g = qh[m] * a * b + qh[n + m] * a + qh[2 * n + m] * b + qh[3 * n + m] * c + qh[4 * n + m];
   if (m < npub) g = g - a;  // PI(w^m) = -pub_m, pub_m = A(w^m)
   if (!g.is_zero()) atomicOr(flags, 1u);
 }
@@ -671,6 +670,11 @@ k_t_combine(const Fr* __restrict__ V, size_t n, T3Args a, Fr* __restrict__ t) {
   t[n + k] = dl * a.two_over_d;
   t[2 * n + k] = (sm - v12 + im) * a.inv_d2;
   if (k < 6) t[3 * n + k] = a.q3[k];  // t has 3n + 6 coefficients (its buffer no more)
+}
+
+// fault injection (nzcb_debug_inject_fault): one coefficient + 1
+__global__ void k_fault_bump(Fr* x) {
+  if (threadIdx.x == 0) x[0] = x[0] + Fr::one();
 }
 
 // x <- x * 2^e (mod r), canonical in and out: the exponent pre-scaling of kQ29
@@ -912,6 +916,7 @@ MsmShard::~MsmShard() {
 }
 
 void Prover::set_msm_devices(const std::vector<int>& devices) {
+  GuardScope guards;
   if (devices.empty() || devices[0] != eng->device)
     throw Error(NZCB_ERR_ARG, "msm devices must start with the context's device");
   shards.clear();
@@ -952,6 +957,7 @@ double Prover::ms_since(std::chrono::steady_clock::time_point t0) {
 // context creation: parse + upload the zkey once
 // ----------------------------------------------------------------------------
 Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
+  GuardScope guards;  // every device buffer of the proving key and lane 0 (common.h)
   Zkey z = parse_zkey(zkey_bytes, len);
   n = z.domainSize;
   n4 = 4 * n;
@@ -1081,6 +1087,14 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     }
   }
   alloc_workspace();
+  if (quot3) {  // the gate check on H reads the selectors on H contiguously (k_gate_h)
+    q_h.alloc((size_t)5 * n);
+    const DevBuf<Fr>* qs[5] = {&qm, &ql, &qr, &qo, &qc};
+    for (int k = 0; k < 5; k++)
+      hipLaunchKernelGGL(k_stride4, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, qs[k]->p + n, (size_t)n,
+                         q_h.p + (size_t)k * n);
+    NZ_HIP(hipGetLastError());
+  }
   if (quot3) {  // three-coset quotient: per-coset twists c_j^k and untwists c_j^-k / 4n, j < 3
     const size_t nhi3 = (n + 4095) / 4096;
     tw3.alloc((size_t)3 * n);
@@ -1214,6 +1228,7 @@ void Prover::alloc_workspace() {
 // (zkey sections, shifted PTau table, coset evaluations, root tables) read-only and
 // owns its streams, MSM scratch and per-proof working set.
 Prover::Prover(const Prover& pk, int) {
+  GuardScope guards;  // the lane's working set, MSM and NTT scratch (common.h)
   n = pk.n; n4 = pk.n4; nVars = pk.nVars; nPublic = pk.nPublic; nAdditions = pk.nAdditions;
   nConstraints = pk.nConstraints; nWit = pk.nWit; power = pk.power;
   k1 = pk.k1; k2 = pk.k2; wn = pk.wn; w2 = pk.w2;
@@ -1232,7 +1247,7 @@ Prover::Prover(const Prover& pk, int) {
   ltab.q.alias(pk.ltab.q);
   ltab.n = pk.ltab.n; ltab.stride = pk.ltab.stride; ltab.c = pk.ltab.c; ltab.nw = pk.ltab.nw;
   qm.alias(pk.qm); ql.alias(pk.ql); qr.alias(pk.qr); qo.alias(pk.qo); qc.alias(pk.qc);
-  sigma.alias(pk.sigma); sig_h.alias(pk.sig_h); lagrange.alias(pk.lagrange);
+  sigma.alias(pk.sigma); sig_h.alias(pk.sig_h); q_h.alias(pk.q_h); lagrange.alias(pk.lagrange);
   amap.alias(pk.amap); bmap.alias(pk.bmap); cmap.alias(pk.cmap); adds.alias(pk.adds);
   root_lo.alias(pk.root_lo); root_hi.alias(pk.root_hi); x_lo.alias(pk.x_lo);
   g_lo.alias(pk.g_lo); g_hi.alias(pk.g_hi); gi_lo.alias(pk.gi_lo); gi_hi.alias(pk.gi_hi);
@@ -1261,8 +1276,8 @@ Prover::Prover(const Prover& pk, int) {
 // the gate check on H (t's divisibility, flag bit 1), and the copies t's recombination
 // needs: A, B, C's coefficients n-4 .. n+1, Z's n-3 .. n+2 and the flags, into top_host
 void Prover::launch_gate_check(hipStream_t s) {
-  hipLaunchKernelGGL(k_gate_h, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, qm.p, ql.p, qr.p,
-                     qo.p, qc.p, (size_t)n, nPublic, flags.p);
+  hipLaunchKernelGGL(k_gate_h, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, A.p, B.p, C.p, q_h.p, (size_t)n,
+                     nPublic, flags.p);
   NZ_HIP(hipGetLastError());
 }
 
@@ -1839,6 +1854,11 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       if (f & 1u) throw Error(NZCB_ERR_T_DIV, "T Polynomial is not divisible");
     }
     ntt_ms += ms_since(tq);
+    if (fault == NZCB_FAULT_QUOTIENT) {  // nzcb_debug_inject_fault: t[1] += 1, once
+      fault = 0;
+      hipLaunchKernelGGL(k_fault_bump, dim3(1), dim3(64), 0, s, t.p + 1);
+      NZ_HIP(hipGetLastError());
+    }
     lg("multiexp T1");
     commit_start(0, t.p, n);
     lg("multiexp T2");

@@ -680,6 +680,9 @@ __device__ __forceinline__ void wave_op(const Prog& P, Fr* W, const Op& op, uint
 // One workgroup per pass; per level: the thread segment spread over threads, the wave
 // segment over waves, the workgroup segment (SHA blocks) one op at a time, one barrier.
 // Ops of one level are independent, so the three segments need no barrier between them.
+// 512 threads per pass (the size the level segments are cut for; the 256 / 1024 variants
+// were A/B switches without tests and were removed in round 5).
+static constexpr int kWvmThreads = 512;
 template <int NT>
 __global__ void __launch_bounds__(NT) wvm_kernel(Prog P, const Fr* __restrict__ inputs, Fr* witness,
                                                  size_t stride_elems, uint32_t* status,
@@ -1016,15 +1019,8 @@ void run(Program* P, const void* dev_inputs, int count, void* dev_witness, size_
     lclk.alloc(((size_t)P->n_levels + 1) * kClockSlots);
     NZ_HIP(hipMemsetAsync(lclk.p, 0, ((size_t)P->n_levels + 1) * kClockSlots * 8, s));
   }
-  // NZCB_WVM_THREADS = 256 | 512 | 1024 workgroup size (A/B runs; default 512)
-  static const int nt = [] {
-    const char* v = std::getenv("NZCB_WVM_THREADS");
-    const int t = v ? std::atoi(v) : 512;
-    return t == 256 || t == 1024 ? t : 512;
-  }();
-  auto kern = nt == 256 ? wvm_kernel<256> : (nt == 1024 ? wvm_kernel<1024> : wvm_kernel<512>);
-  hipLaunchKernelGGL(kern, dim3((unsigned)count), dim3(nt), 0, s, g, (const Fr*)dev_inputs, run_dst, run_stride,
-                     R->status.p, lclk.p);
+  hipLaunchKernelGGL(wvm_kernel<kWvmThreads>, dim3((unsigned)count), dim3(kWvmThreads), 0, s, g,
+                     (const Fr*)dev_inputs, run_dst, run_stride, R->status.p, lclk.p);
   NZ_HIP(hipGetLastError());
   if (P->n_target) {
     const unsigned gx = (unsigned)std::min<size_t>(((size_t)P->n_target + 255) / 256, 1024);

@@ -44,7 +44,25 @@ EXPORTED_SYMBOLS = [
     "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_engine_lagrange_basis", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d",
     "nzcb_plonk_setup", "nzcb_prove_batch_status", "nzcb_wprog_remap", "nzcb_prove_logged", "nzcb_memcpy_d2d_async",
+    "nzcb_debug_guard_check", "nzcb_debug_guard_selftest", "nzcb_debug_inject_fault",
 ]
+
+NZCB_FAULT_QUOTIENT = 1  # include/nzcb_internal.h
+
+
+def guard_check(device: int = -1) -> int:
+    """Every guard word past the prover contexts' device buffers on `device` (-1: all) is
+    intact; returns how many guards were checked, raises NzcbError listing the damaged
+    buffers otherwise (include/nzcb_internal.h nzcb_debug_guard_check)."""
+    err, checked, bad = _Err(), c_size_t(0), c_int(0)
+    _check(load().nzcb_debug_guard_check(device, ctypes.byref(checked), ctypes.byref(bad), ctypes.byref(err)), err)
+    return checked.value
+
+
+def guard_selftest(device: int = 0) -> None:
+    """A one-word overrun past a fresh guarded buffer is found, and only it."""
+    err = _Err()
+    _check(load().nzcb_debug_guard_selftest(device, ctypes.byref(err)), err)
 
 
 class NzcbError(RuntimeError):
@@ -179,6 +197,9 @@ def load(path: str | None = None):
         "nzcb_wprog_run": (c_int, [c_void_p, ctypes.c_char_p, c_int, u8p, POINTER(ctypes.c_int32), POINTER(_Err)]),
         "nzcb_wprog_remap": (c_int, [ctypes.c_char_p, c_size_t, ctypes.c_char_p, c_size_t, ctypes.c_char_p, c_size_t,
                                      POINTER(POINTER(c_uint8)), POINTER(c_size_t), POINTER(c_uint32), POINTER(_Err)]),
+        "nzcb_debug_guard_check": (c_int, [c_int, POINTER(c_size_t), POINTER(c_int), POINTER(_Err)]),
+        "nzcb_debug_guard_selftest": (c_int, [c_int, POINTER(_Err)]),
+        "nzcb_debug_inject_fault": (c_int, [c_void_p, c_int]),
     }
     lib.missing_symbols = []
     for name, (res, args) in sigs.items():
@@ -589,6 +610,11 @@ class ProverContext:
         P, Q = bytes(proofs), bytes(pubs)
         return [(P[i * PROOF_BYTES:(i + 1) * PROOF_BYTES], Q[i * stride:i * stride + 32 * self.n_public])
                 for i in range(count)]
+
+    def inject_fault(self, kind: int = NZCB_FAULT_QUOTIENT) -> None:
+        """The next proof on each lane perturbs its quotient t (tests of the xi check)."""
+        if self.lib.nzcb_debug_inject_fault(self.h, kind) != 0:
+            raise ValueError(f"bad fault kind {kind}")
 
     def kernel_stats(self, enable: int = -1):
         """MSM bucket-accumulation kernel timing: (ms, launches, points, entries); enable 1/0 resets."""

@@ -86,6 +86,53 @@ def test_batch_shards_prove_gloo():
     assert all(v == want for v in merged.values())
 
 
+def test_launch_plan_decisions():
+    """--gpus N > 1 without a launcher spawns N ranks; under a launcher
+    the world must equal --gpus."""
+    assert bench.launch_plan(1, {}) == "local"
+    assert bench.launch_plan(8, {}) == "spawn"
+    assert bench.launch_plan(8, {"WORLD_SIZE": "8"}) == "local"
+    assert bench.launch_plan(1, {"WORLD_SIZE": "1"}) == "local"
+    for gpus, env in ((2, {"WORLD_SIZE": "1"}), (1, {"WORLD_SIZE": "2"}), (8, {"WORLD_SIZE": "4"})):
+        with pytest.raises(SystemExit) as e:
+            bench.launch_plan(gpus, env)
+        assert e.value.code == 2
+    with pytest.raises(SystemExit):
+        bench.launch_plan(0, {})
+
+
+def _bench_env(**extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env.update(NZCB_DIST_BACKEND="gloo", **extra)
+    return env
+
+
+def test_bench_gpus2_spawns_two_ranks_gloo():
+    """`bench.py --gpus 2` with no launcher starts two fresh ranks (torch.distributed.run as
+    a child) and rank 0 reports n_gpus = 2 from the process group."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
+                       env=_bench_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(s) for s in r.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1
+    assert lines[0]["n_gpus"] == 2 and lines[0]["backend"] == "gloo"
+    assert sorted(x["rank"] for x in lines[0]["ranks"]) == [0, 1]
+    assert [x["device"] for x in sorted(lines[0]["ranks"], key=lambda x: x["rank"])] == [0, 1]
+
+
+def test_bench_world_mismatch_exits_nonzero():
+    """A launcher's world that differs from --gpus is refused before any work."""
+    import subprocess
+    env = _bench_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=1" in r.stderr
+
+
 def test_shard_edge_cases():
     assert [list(bench.shard(3, r, 8)) for r in range(8)] == [[0], [1], [2], [], [], [], [], []]
     assert list(bench.shard(0, 0, 1)) == []

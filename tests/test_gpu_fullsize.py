@@ -76,6 +76,12 @@ def test_nzcp_live_2p21_bit_exact_vs_c_port():
         # third lane: other blinding, same statement as pass 2 -> a different valid proof
         assert res[2][0] not in (refs[0][0], refs[1][0])
         assert all(nzcb.verify(ctx.vk, p, q) for p, q in res)
+        # round 4's overrun (k_t_combine writing t[3n..4n) into the 3n + 6
+        # quotient buffer) surfaced two kernels later as an illegal access in this test.
+        # Every buffer of the context (proving key, 3 lanes' working sets, MSM and NTT
+        # scratch) carries guard words: all intact after the 3-lane batch and the single proof
+        checked = nzcb.guard_check(0)
+        assert checked >= 3 * 40
         ctx.close()
     finally:
         nzcb.free_raw(raw)

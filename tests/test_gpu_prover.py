@@ -299,3 +299,74 @@ def test_quotient_schedules_same_proof(quot3, lcommit):
     env = dict(os.environ, NZCB_QUOT3=quot3, NZCB_LAGRANGE_COMMIT=lcommit)
     p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stdout + p.stderr
+
+
+@pytest.mark.parametrize("name", ["p5", "p8"])
+def test_quotient_fault_is_caught_then_proves_again(name):
+    """the xi check (prover.hip, round 4) is the only check on the
+    three-coset t (p8; p5's n < 64 takes the 4n coset). A one-coefficient fault injected
+    into t after round 3 is reported as NZCB_ERR_INTERNAL "quotient check failed", and the
+    context's next proof is bit-exact again."""
+    meta, zkey, wtns = _gold(name)
+    exp = meta["proofs"]["fixed"]
+    bl = bytes.fromhex(exp["blinding"])
+    ctx = nzcb.ProverContext(zkey)
+    try:
+        ctx.inject_fault(nzcb.NZCB_FAULT_QUOTIENT)
+        with pytest.raises(nzcb.NzcbError) as ei:
+            ctx.prove_raw(wtns, bl)
+        assert ei.value.name == "INTERNAL"
+        assert str(ei.value).startswith("quotient check failed")
+        proof, _ = ctx.prove_raw(wtns, bl)
+        assert proof.hex() == exp["proof_bin"]
+        ctx.inject_fault(0)   # set and cleared: nothing fires
+        proof, _ = ctx.prove_raw(wtns, bl)
+        assert proof.hex() == exp["proof_bin"]
+    finally:
+        ctx.close()
+    ctx = nzcb.ProverContext(zkey)
+    try:
+        with pytest.raises(ValueError):
+            ctx.inject_fault(7)
+    finally:
+        ctx.close()
+
+
+def test_guard_words_selftest_and_lane_buffers():
+    """The guard words behind every context buffer (common.h GuardScope): a one-word
+    overrun past a fresh guarded buffer is found, and after proofs on 3 lanes and a lane
+    count change every guard is intact."""
+    nzcb.guard_selftest(0)
+    meta, zkey, wtns = _gold("p8")
+    exp = meta["proofs"]["fixed"]
+    ctx = nzcb.ProverContext(zkey)
+    try:
+        ctx.set_lanes(3)
+        wit = b"".join(x.to_bytes(32, "little") for x in binfmt.read_wtns(wtns)["witness"])
+        res = ctx.prove_batch_raw([wit] * 6, blindings=[bytes.fromhex(exp["blinding"])] * 6)
+        assert all(p.hex() == exp["proof_bin"] for p, _ in res)
+        ctx.set_lanes(2)
+        assert nzcb.guard_check(0) > 0
+    finally:
+        ctx.close()
+
+
+def test_serial_profiling_mode_same_proof():
+    """NZCB_SERIAL (profiling: every commitment MSM synchronised as it is enqueued) proves p8
+    bit for bit in a fresh process, as the default does (test_golden_proof_bits)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = (
+        "import sys, json; sys.path[:0] = [%r, %r]\n"
+        "import nzcb\n"
+        "g = %r\n"
+        "meta = json.load(open(g + '/p8.json')); exp = meta['proofs']['fixed']\n"
+        "zkey = open(g + '/p8.zkey', 'rb').read(); wtns = open(g + '/p8.wtns', 'rb').read()\n"
+        "ctx = nzcb.ProverContext(zkey)\n"
+        "proof, _ = ctx.prove_raw(wtns, bytes.fromhex(exp['blinding']))\n"
+        "assert proof.hex() == exp['proof_bin'], 'proof differs'\n"
+        "print('ok')\n" % (os.path.join(root, "nzcb-circom_amd"), root, GOLD))
+    env = dict(os.environ, NZCB_SERIAL="1")
+    p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stdout + p.stderr

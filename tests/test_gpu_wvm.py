@@ -196,3 +196,40 @@ def test_remapped_programs_on_gpu():
         ctx.close()
     ref_proof, ref_pub, _ = cbind.prove(zkey, nzcplive.wtns_file(raw), bl, npub=1)
     assert proof == ref_proof and pub == ref_pub[:32]
+
+
+def test_level_clock_probe_same_witness(programs, tmp_path):
+    """NZCB_WVM_LEVEL_CLOCK (tools/wvm_bench.py --levels): with the per-level clock on, the
+    example pass's witness is the one computed without it, and the clock file holds one
+    record block per level (fresh process: the switch is read at the run)."""
+    import subprocess
+    import sys
+    import nzcb
+    c, prog = programs["example"]
+    gold = json.load(open(GOLD))
+    case = next(cs for cs in gold["cases"] if not cs["params"]["is_live"])
+    inputs = C.case_input_bytes(case)
+    pp, ip, op = tmp_path / "p.nzwp", tmp_path / "in.bin", tmp_path / "w.bin"
+    pp.write_bytes(prog)
+    ip.write_bytes(inputs)
+    wp = nzcb.WitnessProgram(prog)
+    try:
+        want, st = wp.run(inputs, 1)
+        n_levels = wp.n_levels
+    finally:
+        wp.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    clock = tmp_path / "clock.bin"
+    script = ("import sys; sys.path[:0] = [%r]\n"
+              "import nzcb\n"
+              "wp = nzcb.WitnessProgram(open(%r, 'rb').read())\n"
+              "raw, st = wp.run(open(%r, 'rb').read(), 1)\n"
+              "open(%r, 'wb').write(raw)\n"
+              "print('ok', list(st))\n" % (os.path.join(root, "nzcb-circom_amd"), str(pp), str(ip), str(op)))
+    p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, NZCB_WVM_LEVEL_CLOCK=str(clock)))
+    assert p.returncode == 0 and "ok" in p.stdout, p.stdout + p.stderr
+    assert f"ok {list(st)}" in p.stdout
+    assert op.read_bytes() == want
+    size = clock.stat().st_size
+    assert size > 0 and size % (8 * (n_levels + 1)) == 0
