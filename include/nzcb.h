@@ -173,9 +173,12 @@ int nzcb_prove_batch_status(nzcb_ctx* ctx, const void* const* witnesses, size_t 
                             int witness_on_device, const uint8_t* blindings, uint8_t* proofs_out, uint8_t* pubs_out,
                             size_t pub_stride, int* status_out, nzcb_err* err);
 
-/* Wall-clock milliseconds of the last proof's phases:
- * [0] total [1] witness upload+additions+ABC [2] round1 [3] round2 [4] round3 [5] round4 [6] round5
- * [7] all MSMs [8] all NTTs. Returns the number of values written. */
+/* Milliseconds of the last proof's phases. Host wall clock: [0] total [1] witness
+ * upload+additions+ABC [2] round1 [3] round2 [4] round3 [5] round4 [6] round5, [7] host time
+ * inside the MSM calls (enqueue + waiting for their results), [8] host time enqueueing the
+ * transforms. GPU time (HIP events around each commitment MSM / each transform on its
+ * stream, only while nzcb_ctx_kernel_stats is on, else -1): [9] MSMs [10] transforms.
+ * Returns the number of values written (cap <= 11). */
 int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap);
 
 /* snarkjs-format JSON ({proof}, [publicSignals]) from the binary outputs. */
@@ -323,6 +326,9 @@ void nzcb_free(void* p);
 
 /* ---- HBM buffers (witnesses for nzcb_prove_device / nzcb_prove_batch on device) ---- */
 void* nzcb_dev_alloc(size_t bytes);
+/* The same on `device`; the calling thread's current device is left as it was (the N-API
+ * addon's per-call threads allocate witness buffers on the witness program's device). */
+void* nzcb_dev_alloc_on(int device, size_t bytes);
 void nzcb_dev_free(void* p);
 int nzcb_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int nzcb_memcpy_d2h(void* dst, const void* src, size_t bytes);

@@ -173,6 +173,14 @@ void* nzcb_dev_alloc(size_t bytes) {
   if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
   return p;
 }
+void* nzcb_dev_alloc_on(int device, size_t bytes) {
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(device) != hipSuccess) return nullptr;
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) p = nullptr;
+  (void)hipSetDevice(cur);
+  return p;
+}
 void nzcb_dev_free(void* p) {
   if (p) (void)hipFree(p);
 }

@@ -59,7 +59,7 @@ struct nzcb_ctx {
   std::mutex pool_mu;
   std::condition_variable pool_cv;
   std::vector<Prover*> idle;  // lanes not proving; rebuilt by reset_pool (cfg held exclusively)
-  double last_tm[9] = {0};    // phases of the last finished proof (nzcb_ctx_last_timings)
+  double last_tm[11] = {0};   // phases of the last finished proof (nzcb_ctx_last_timings)
   Prover* lane(size_t i) { return i == 0 ? p.get() : extra[i - 1].get(); }
   size_t lanes() const { return 1 + extra.size(); }  // per device
   // every lane of every device (batch workers), device-interleaved so that a short batch
@@ -472,7 +472,7 @@ int nzcb_prove_logged(nzcb_ctx* ctx, const void* witness, size_t n, int kind, co
 
 int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap) {
   if (!ctx || !ms) return 0;
-  int k = cap < 9 ? cap : 9;
+  int k = cap < 11 ? cap : 11;
   std::lock_guard<std::mutex> lk(const_cast<nzcb_ctx*>(ctx)->pool_mu);
   for (int i = 0; i < k; i++) ms[i] = ctx->last_tm[i];
   return k;
@@ -494,12 +494,14 @@ int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
       }
   }
   if (enable >= 0) {
-    for (Prover* q : ctx->all())
+    for (Prover* q : ctx->all()) {
+      q->prof_gpu = enable != 0;
       for (auto& m : q->msc) {
         m->prof = enable != 0;
         m->prof_ms = 0;
         m->prof_launches = m->prof_points = m->prof_entries = 0;
       }
+    }
   }
   return 0;
 }

@@ -53,6 +53,19 @@ struct Fr29 {
   // 2r in borrowed form (every limb >= 2^29 - 1), for sub29
   static constexpr uint32_t K2[9] = {0x20000002u, 0x3e1f593eu, 0x3cb848a0u, 0x2fa121e5u, 0x2b0ba505u,
                                      0x25b68180u, 0x214dc281u, 0x3cb84c67u, 0x0060c89bu};
+  static constexpr uint32_t ONE[9] = {0x0fffff57u, 0x1ea70ab4u, 0x052c068bu, 0x17504f49u, 0x0aa8075bu,
+                                      0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};  // 2^261 mod r
+  static constexpr uint32_t C256[9] = {0x0ffffffbu, 0x04b1a0e2u, 0x18334a6bu, 0x18ed2b3eu, 0x1462e36fu,
+                                       0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0x000e0a77u};  // 2^256 mod r
+  // 4r in borrowed form: the NTT butterflies' a + 4r - b for Shoup products b < 3r
+  static constexpr uint32_t K4[9] = {0x20000004u, 0x3c3eb27du, 0x39709142u, 0x3f4243ccu, 0x36174a0bu,
+                                     0x2b6d0301u, 0x229b8503u, 0x397098cfu, 0x00c19138u};
+  // 2^261 - r (mul_shoup: x w - q r = x w + q (2^261 - r) mod 2^261)
+  static constexpr uint32_t RP[9] = {0x0fffffffu, 0x00f05360u, 0x11a3dbafu, 0x182f6f0cu, 0x0a7a2d7cu,
+                                     0x1d24bf3fu, 0x1f591ebeu, 0x11a3d9cbu, 0x1fcf9bb1u};
+  // -r^-1 mod 2^261 (the Shoup quotient of a twiddle from its Montgomery-261 form, ntt.hip)
+  static constexpr uint32_t NINV[9] = {0x0fffffffu, 0x170fac9fu, 0x1a446cf0u, 0x0d0c9698u, 0x02391658u,
+                                       0x0c144c83u, 0x06cb8e6au, 0x03a1b068u, 0x1273f82fu};
 };
 
 // acc + x * y as one v_mad_u64_u32 with acc as its addend. Written as asm so the
@@ -89,6 +102,96 @@ NZ_HD void mad29cx2(uint64_t& acc, uint32_t x, uint64_t& bcc, uint32_t u, uint32
   bcc += (uint64_t)u * y;
 }
 #endif
+
+NZ_HD F29 f29_const(const uint32_t (&c)[9]);
+
+// Shoup's product by a fixed factor (the NTT twiddles): w < r and ws = floor(w 2^261 / r),
+// both normalized; x < 2^261 with limbs < 2^30.6. q = floor(x ws / 2^261) from the product
+// columns 7..16 only (the dropped columns 0..6 sum to < 2^237, so q is off by at most 1 from
+// the exact floor, which is itself floor(x w / r) or one less: x ws / 2^261 > x w / r - 1),
+// then x w - q r = x w + q (2^261 - r) mod 2^261 from the low columns 0..8 alone, the exact
+// value since it is < 3r < 2^261. Result < 3r, normalized. 143 v_mad_u64_u32 (45 + 53 + 45)
+// and no v_mul_lo_u32 against the Montgomery product's 162 + 9 (round 5, the NTT's twiddles).
+// A column of the low half is <= 9 (2^59.6 + 2^58) + 2^35 < 2^64, of x ws <= 9 2^59.6 + 2^35.
+template <int N>
+NZ_HD void mul_shoup_n(const F29 (&x)[N], const F29 (&w)[N], const F29 (&ws)[N], F29 (&out)[N]) {
+  using Q = Fr29;
+  uint32_t q[N][9];
+  uint64_t acc[N];
+#pragma unroll
+  for (int t = 0; t < N; t++) acc[t] = 0;
+#pragma unroll
+  for (int c = 7; c < 17; c++) {
+#pragma unroll
+    for (int j = c > 8 ? c - 8 : 0; j <= (c < 8 ? c : 8); j++) {
+      if constexpr (N == 2) {
+        mad29x2(acc[0], x[0].v[j], ws[0].v[c - j], acc[1], x[1].v[j], ws[1].v[c - j]);
+      } else {
+#pragma unroll
+        for (int t = 0; t < N; t++) mad29(acc[t], x[t].v[j], ws[t].v[c - j]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < N; t++) {
+      if (c >= 9) q[t][c - 9] = (uint32_t)acc[t] & Q::MASK;
+      acc[t] >>= 29;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < N; t++) {
+    q[t][8] = (uint32_t)acc[t];
+    acc[t] = 0;
+  }
+#pragma unroll
+  for (int c = 0; c < 9; c++) {
+#pragma unroll
+    for (int j = 0; j <= c; j++) {
+      if constexpr (N == 2) {
+        mad29x2(acc[0], x[0].v[j], w[0].v[c - j], acc[1], x[1].v[j], w[1].v[c - j]);
+        mad29cx2(acc[0], q[0][j], acc[1], q[1][j], Q::RP[c - j]);
+      } else {
+#pragma unroll
+        for (int t = 0; t < N; t++) {
+          mad29(acc[t], x[t].v[j], w[t].v[c - j]);
+          mad29c(acc[t], q[t][j], Q::RP[c - j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < N; t++) {
+      out[t].v[c] = (uint32_t)acc[t] & Q::MASK;
+      acc[t] >>= 29;
+    }
+  }
+}
+NZ_HD F29 mul_shoup(const F29& x, const F29& w, const F29& ws) {
+  const F29 xa[1] = {x}, wa[1] = {w}, sa[1] = {ws};
+  F29 o[1];
+  mul_shoup_n<1>(xa, wa, sa, o);
+  return o[0];
+}
+// two independent Shoup products interleaved (two mad chains side by side, as mul29x2)
+NZ_HD void mul_shoup_x2(const F29& x, const F29& w, const F29& ws, const F29& y, const F29& v, const F29& vs, F29& r1,
+                        F29& r2) {
+  const F29 xa[2] = {x, y}, wa[2] = {w, v}, sa[2] = {ws, vs};
+  F29 o[2];
+  mul_shoup_n<2>(xa, wa, sa, o);
+  r1 = o[0];
+  r2 = o[1];
+}
+// the low 261 bits of a b (normalized a, b)
+NZ_HD F29 mul_lo261(const F29& a, const F29& b) {
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int c = 0; c < 9; c++) {
+#pragma unroll
+    for (int j = 0; j <= c; j++) mad29(acc, a.v[j], b.v[c - j]);
+    r.v[c] = (uint32_t)acc & Fr29::MASK;
+    acc >>= 29;
+  }
+  return r;
+}
 
 NZ_HD F29 f29_const(const uint32_t (&c)[9]) {
   F29 r;
@@ -506,6 +609,26 @@ NZ_HD Fr from_mont_fr29(const Fr& a) {
   r.v[8] = (uint32_t)acc;
   return join_fr29(r);
 }
+
+// Montgomery-256 Fr -> the same value at exponent 261 (x 2^5 < 32 r, normalized): the
+// 261-bit shift of the limbs, no product (x < 2^254, so the top limb stays < 2^27)
+NZ_HD F29 fr_to261(const Fr& x) {
+  const F29 r = split29(x);
+  F29 o;
+  o.v[0] = (r.v[0] << 5) & Fr29::MASK;
+#pragma unroll
+  for (int l = 1; l < 9; l++) o.v[l] = ((r.v[l] << 5) & Fr29::MASK) | (r.v[l - 1] >> 24);
+  return o;
+}
+NZ_HD F29 add3_29(const F29& a, const F29& b, const F29& c) {  // normalized
+  F29 r;
+#pragma unroll
+  for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + b.v[l] + c.v[l];
+  norm29(r);
+  return r;
+}
+// exponent 261 -> canonical Montgomery-256 Fr (one product by 2^256 mod r)
+NZ_HD Fr fr_from261(const F29& x) { return join_fr29(mul29<Fr29>(x, f29_const(Fr29::C256))); }
 
 // Montgomery-261 value (any F29 < 2^257) -> canonical Montgomery-256 Fq (csrc/field.h)
 NZ_HD Fq to_fq256(const F29& x) { return reduce_once(join29(mul29(x, f29_const(Fq29::C256)))); }

@@ -65,6 +65,23 @@ static uint32_t chunk_for(size_t entries) {
   while (entries / c > (size_t(1) << 20)) c *= 2;
   return c;
 }
+// Fixed base (round 5): entries per accumulation thread from the bucketed entry count M.
+// The grid is launched for the plan's bound (nthr = bound / chunk), and a sparse MSM (the
+// Lagrange-basis commitments of mostly small witness values: M ~ 7 % of the bound) spreads
+// its entries over the whole grid in chunks of at least kMinChunk instead of leaving 93 %
+// of it idle behind 48-long addition chains (round 4: 0.83 ms per commitment in round 1 of a
+// single proof). Random scalars keep chunk (M ~ the bound). Every kernel that maps entry
+// positions to chunks derives the same value from offsets[nkeys]; nthr = 0: chunk as given.
+static constexpr uint32_t kMinChunk = 8;
+#ifndef NZ_DYN_CHUNK
+#define NZ_DYN_CHUNK 1
+#endif
+__device__ __forceinline__ uint32_t fb_chunk(uint32_t chunk, uint32_t M, size_t nthr) {
+  if (!nthr || !NZ_DYN_CHUNK) return chunk;
+  uint32_t c = (uint32_t)(((size_t)M + nthr - 1) / nthr);
+  c = c < kMinChunk ? kMinChunk : c;
+  return c < chunk ? c : chunk;
+}
 static constexpr int kSegLen = 8;
 static constexpr int kSumThreads = 256;  // level-1 sums: block size
 static constexpr int kSumPer = 4;        // level-1 sums: sequential adds per thread
@@ -79,7 +96,7 @@ static constexpr int kLargeBlocks = 32;  // finalize: workgroups for the longer 
 // fixed base: workgroups over the pieces of the longer runs, and over their buckets (grid-
 // stride; random scalars list none, and under 5 proof lanes every launched workgroup waits
 // for a CU slot first, so the grids are kept small)
-static constexpr int kLargePieceBlocks = 128;
+static constexpr int kLargePieceBlocks = 256;
 static constexpr int kLargeFinalBlocks = 128;
 static constexpr int kLargeFinalThreads = 64;
 
@@ -631,17 +648,19 @@ __device__ __forceinline__ G1xyzz load_point(const Xyzz29& a) {
 static constexpr uint32_t kLdsStride = kMsmThreads + 1;  // slot-major rows, +1: conflict-free fill
 template <bool kLdsIdx>
 __global__ void __launch_bounds__(kMsmThreads) __attribute__((amdgpu_waves_per_eu(3, 8)))
-msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
+msm_accumulate29_kernel(uint32_t chunk_max, const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
                         const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
                         Xyzz29* __restrict__ buckets, Xyzz29* __restrict__ carry_own,
                         Xyzz29* __restrict__ carry_cont) {
   __shared__ uint32_t sidx[kLdsIdx ? kChunk * kLdsStride : 1];
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t M = offsets[nkeys];
+  const uint32_t chunk = fb_chunk(chunk_max, M, nthreads);  // <= kChunk when kLdsIdx
   if (kLdsIdx) {  // every thread of the workgroup takes part before any exits
-    const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * kChunk;
-    for (uint32_t j = threadIdx.x; j < kMsmThreads * kChunk; j += kMsmThreads) {
-      const uint32_t thr = j / kChunk, slot = j - thr * kChunk;
+    const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * chunk;
+    const uint32_t rcp = 0xFFFFFFFFu / chunk + 1u;  // j / chunk = umulhi(j, rcp) for j < 2^16
+    for (uint32_t j = threadIdx.x; j < kMsmThreads * chunk; j += kMsmThreads) {
+      const uint32_t thr = __umulhi(j, rcp), slot = j - thr * chunk;
       sidx[slot * kLdsStride + thr] = wg0 + j < M ? sorted[wg0 + j] : 0u;
     }
     __syncthreads();
@@ -754,11 +773,12 @@ __device__ __forceinline__ G1xyzz sum_run(const G1xyzz* carry_own, const G1xyzz*
 // multi-chunk sums go into the accumulation's own bucket array out29, in radix 2^29.
 template <class P>
 __global__ void __launch_bounds__(kMsmThreads)
-msm_bucket_finalize_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys, uint32_t span,
-                           const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
+msm_bucket_finalize_kernel(uint32_t chunk_max, size_t nthr, const uint32_t* __restrict__ offsets, uint32_t nkeys,
+                           uint32_t span, const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
                            G1xyzz* __restrict__ buckets, uint32_t* __restrict__ large, Xyzz29* __restrict__ out29) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nkeys) return;
+  const uint32_t chunk = fb_chunk(chunk_max, offsets[nkeys], nthr);
   const uint32_t s = offsets[k], e = offsets[k + 1];
   if (e == s) return;
   const uint32_t c0 = s / chunk, c1 = (e - 1) / chunk;
@@ -881,9 +901,10 @@ __device__ __forceinline__ uint32_t carry_span(uint32_t chunk, const uint32_t* o
 
 // off[i] = pieces of the listed buckets before i, off[count] = all (one workgroup)
 __global__ void __launch_bounds__(1024)
-msm_large_scan_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
-                      uint32_t* __restrict__ off) {
+msm_large_scan_kernel(uint32_t chunk_max, size_t nthr, uint32_t nkeys, const uint32_t* __restrict__ offsets,
+                      const uint32_t* __restrict__ large, uint32_t* __restrict__ off) {
   __shared__ uint32_t sh[1024];
+  const uint32_t chunk = fb_chunk(chunk_max, offsets[nkeys], nthr);
   const uint32_t count = large[0];
   const uint32_t tid = threadIdx.x;
   const uint32_t per = (count + 1023u) / 1024u;
@@ -912,10 +933,12 @@ msm_large_scan_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, cons
 }
 
 __global__ void __launch_bounds__(kSumThreads)
-msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
-                         const uint32_t* __restrict__ off, const Xyzz29* __restrict__ carry_own,
-                         const Xyzz29* __restrict__ carry_cont, Xyzz29* __restrict__ part) {
+msm_large_piece29_kernel(uint32_t chunk_max, size_t nthr, uint32_t nkeys, const uint32_t* __restrict__ offsets,
+                         const uint32_t* __restrict__ large, const uint32_t* __restrict__ off,
+                         const Xyzz29* __restrict__ carry_own, const Xyzz29* __restrict__ carry_cont,
+                         Xyzz29* __restrict__ part) {
   __shared__ Xyzz29 sh[kSumThreads];
+  const uint32_t chunk = fb_chunk(chunk_max, offsets[nkeys], nthr);
   const uint32_t count = large[0];
   const uint32_t total = off[count];
   for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
@@ -1072,6 +1095,49 @@ msm_tile29_kernel(const Xyzz29* __restrict__ buckets, const uint32_t* __restrict
     rowp[(size_t)(ht * kTileSide + tid) * ltiles + lt] = sh[tid * 16];
   else if (tid < 2 * kTileSide)
     colp[(size_t)(lt * kTileSide + tid - kTileSide) * htiles + ht] = sh[256 + tid - kTileSide];
+}
+
+// The same first level for the wide windows (c >= 19, 2^18+ buckets; round 5): strips
+// instead of LDS tiles. Row partials: thread (h, j), j < RJ = 2^a / kStrip, adds the buckets
+// (h, j + RJ t), t < kStrip, so consecutive threads read consecutive buckets; column partials:
+// thread (i, l), i < CI = 2^hb / kStrip, adds (i + CI t, l), consecutive threads consecutive
+// l. Every bucket is read and added twice, as in the tiles, with every lane busy and no LDS or
+// barrier: at 2^19 buckets the tile kernel's 55 KB of LDS per workgroup kept the bucket
+// accumulation's third workgroup off a CU whenever the two shared one (5 proof lanes).
+// rowp[h RJ + j], colp[l CI + i]: the layout msm_lines29_kernel reads (RJ, CI partials a line).
+static constexpr int kStrip = 16;
+static constexpr int kStripMinC = 19;  // the tiles stay for c <= 18 (2^16 buckets: 0.046 ms, shorter chains)
+__global__ void __launch_bounds__(256)
+msm_strips29_kernel(const Xyzz29* __restrict__ buckets, const uint32_t* __restrict__ offsets, int a, int hb,
+                    Xyzz29* __restrict__ rowp, Xyzz29* __restrict__ colp) {
+  const int RJ = (1 << a) / kStrip, CI = (1 << hb) / kStrip;
+  const size_t nrow = (size_t)RJ << hb, ncol = (size_t)CI << a;
+  const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= nrow + ncol) return;
+  uint32_t k, step;
+  size_t dst;
+  Xyzz29* out;
+  if (g < nrow) {
+    const uint32_t h = (uint32_t)(g / RJ), j = (uint32_t)(g % RJ);
+    k = (h << a) + j;
+    step = (uint32_t)RJ;
+    dst = g;
+    out = rowp;
+  } else {
+    const size_t u = g - nrow;
+    const uint32_t i = (uint32_t)(u >> a), l = (uint32_t)(u & ((1u << a) - 1));
+    k = (i << a) + l;
+    step = (uint32_t)CI << a;
+    dst = (size_t)l * CI + i;
+    out = colp;
+  }
+  Xyzz29 acc = pinf<Xyzz29>();
+#pragma unroll 1
+  for (int t = 0; t < kStrip; t++, k += step) {
+    const Xyzz29 y = offsets[k + 1] != offsets[k] ? buckets[k] : pinf<Xyzz29>();
+    acc = add29(acc, y);
+  }
+  out[dst] = acc;
 }
 
 __device__ __forceinline__ Xyzz29 shfl_xor29(const Xyzz29& v, int m) {
@@ -1447,28 +1513,37 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[4], st));
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
   if (table) {  // the large list's count was zeroed by msm_lo_scan_kernel
-    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p,
-                       p.nkeys, kSeqSpan29, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p,
-                       (G1xyzz*)nullptr, sc.large.p, sc.buckets29.p);
+    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, nthreads,
+                       sc.offsets.p, p.nkeys, kSeqSpan29, (const Xyzz29*)sc.carry_own29.p,
+                       (const Xyzz29*)sc.carry_cont29.p, (G1xyzz*)nullptr, sc.large.p, sc.buckets29.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, sc.offsets.p, sc.large.p,
-                       sc.large_off.p);
+    hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, nthreads, p.nkeys, sc.offsets.p,
+                       sc.large.p, sc.large_off.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_large_piece29_kernel, dim3(kLargePieceBlocks), dim3(kSumThreads), 0, st, chunk, sc.offsets.p,
-                       sc.large.p, sc.large_off.p, (const Xyzz29*)sc.carry_own29.p,
+    hipLaunchKernelGGL(msm_large_piece29_kernel, dim3(kLargePieceBlocks), dim3(kSumThreads), 0, st, chunk, nthreads,
+                       p.nkeys, sc.offsets.p, sc.large.p, sc.large_off.p, (const Xyzz29*)sc.carry_own29.p,
                        (const Xyzz29*)sc.carry_cont29.p, sc.large_part.p);
     NZ_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_large_final29_kernel, dim3(kLargeFinalBlocks), dim3(kLargeFinalThreads), 0, st, sc.large.p,
                        sc.large_off.p, sc.large_part.p, sc.buckets29.p);
     NZ_HIP(hipGetLastError());
     mark(5);
-    hipLaunchKernelGGL(msm_tile29_kernel, dim3((unsigned)(p.ltiles * p.htiles)), dim3(256), 0, st,
-                       (const Xyzz29*)sc.buckets29.p, sc.offsets.p, p.a, p.ltiles, p.htiles, sc.rowp29.p, sc.colp29.p);
+    int lparts = p.ltiles, hparts = p.htiles;  // partials per row / per column
+    if (p.c >= kStripMinC) {
+      lparts = (1 << p.a) / kStrip;
+      hparts = (1 << p.hb) / kStrip;
+      const size_t nthr = ((size_t)lparts << p.hb) + ((size_t)hparts << p.a);
+      hipLaunchKernelGGL(msm_strips29_kernel, dim3(grid_for(nthr, 256, 1u << 30)), dim3(256), 0, st,
+                         (const Xyzz29*)sc.buckets29.p, sc.offsets.p, p.a, p.hb, sc.rowp29.p, sc.colp29.p);
+    } else {
+      hipLaunchKernelGGL(msm_tile29_kernel, dim3((unsigned)(p.ltiles * p.htiles)), dim3(256), 0, st,
+                         (const Xyzz29*)sc.buckets29.p, sc.offsets.p, p.a, p.ltiles, p.htiles, sc.rowp29.p, sc.colp29.p);
+    }
     NZ_HIP(hipGetLastError());
     mark(6);
     const int nrows = 1 << p.hb, ncols = 1 << p.a;
     hipLaunchKernelGGL(msm_lines29_kernel, dim3(grid_for((size_t)(nrows + ncols) * kLineThreads, 256)), dim3(256), 0,
-                       st, (const Xyzz29*)sc.rowp29.p, p.ltiles, (const Xyzz29*)sc.colp29.p, p.htiles, nrows, ncols,
+                       st, (const Xyzz29*)sc.rowp29.p, lparts, (const Xyzz29*)sc.colp29.p, hparts, nrows, ncols,
                        sc.lines29.p);
     NZ_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_slots29_kernel, dim3(p.hb + p.a + 1), dim3(kSumThreads), 0, st,
@@ -1482,7 +1557,8 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     return;
   }
   NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));
-  hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
+  hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, chunk, (size_t)0,
+                     sc.offsets.p, p.nkeys,
                      kSeqSpan, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p, sc.buckets.p, sc.large.p,
                      (Xyzz29*)nullptr);
   NZ_HIP(hipGetLastError());

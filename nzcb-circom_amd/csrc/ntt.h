@@ -13,9 +13,13 @@ struct NttTables {
   // Per-stage compact twiddles: stage g (butterfly span 2^g) uses w_{2^(g+1)}^k,
   // k < 2^g, stored contiguously at offset 2^g - 1, so the twiddles of consecutive
   // butterflies of a stage are consecutive in memory (coalesced loads); 2^max_log - 1
-  // entries each, as split29 of their Montgomery-261 form (w * 2^261 mod r), the operand
-  // of mul_fr29 (f29.h) in the butterflies
-  DevBuf<F29> fwd29, inv29;
+  // entries each, as the operand pair of f29.h's Shoup product: the twiddle's value w
+  // (canonical, not Montgomery: x in Montgomery-256 times w stays Montgomery-256) and
+  // ws = floor(w 2^261 / r)
+  struct Tw {
+    F29 w, ws;
+  };
+  DevBuf<Tw> fwd29, inv29;
   // Inter-pass scratch of the 9x29 pipeline (ntt29_pass_kernel): limb-major [9][2^max_log]
   // u32, the transform's values between its HBM passes (one transform at a time: every
   // caller runs its NTTs on one stream)

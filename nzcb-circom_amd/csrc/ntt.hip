@@ -19,6 +19,10 @@
 // twiddles), and stage 0's unit twiddles are skipped.
 #include "ntt.h"
 
+#ifndef NZ_NTT_SHOUP
+#define NZ_NTT_SHOUP 1  // Shoup twiddle products (round 5); 0 = the round-4 Montgomery products, A/B builds only
+#endif
+
 #include <vector>
 
 namespace nzcb {
@@ -57,14 +61,25 @@ ntt_stage_table_kernel(Fr* __restrict__ out, const Fr* __restrict__ full, int L,
   out[i] = full[k << (L - g - 1)];
 }
 
-// out[i] = split29(tw[i] * 2^5): Montgomery-256 -> Montgomery-261 twiddles
-__global__ void __launch_bounds__(256) ntt_tw29_kernel(F29* __restrict__ out, const Fr* __restrict__ tw, size_t count) {
+// the Shoup operand pair of a twiddle given in Montgomery-256 form (s = w 2^256 mod r):
+// w = from_mont(s), and ws = floor(w 2^261 / r) from m = w 2^261 mod r (= s 2^5 mod r):
+// w 2^261 = ws r + m, so ws = -m r^-1 mod 2^261 (exact; ws < 2^261), a low-half product
+__global__ void __launch_bounds__(256) ntt_tw29_kernel(NttTables::Tw* __restrict__ out, const Fr* __restrict__ tw,
+                                                       size_t count) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
-  Fr w = tw[i];
+  Fr m = tw[i];
 #pragma unroll
-  for (int k = 0; k < 5; k++) w = w + w;
-  out[i] = split29(w);
+  for (int k = 0; k < 5; k++) m = m + m;
+  NttTables::Tw t;
+#if NZ_NTT_SHOUP
+  t.w = split29(from_mont(tw[i]));
+  t.ws = mul_lo261(split29(m), f29_const(Fr29::NINV));
+#else
+  t.w = split29(m);  // the Montgomery-261 operand of mul29 (A/B builds)
+  t.ws = t.w;
+#endif
+  out[i] = t;
 }
 
 void NttTables::init(int L, hipStream_t st) {
@@ -101,26 +116,27 @@ void NttTables::init(int L, hipStream_t st) {
   }
 }
 
-// ---- 9x29-bit pipeline (default) ----------------------------------------------------
+// ---- 9x29-bit pipeline ----------------------------------------------------------------
 // The transform's values stay in the redundant radix 2^29 of f29.h from the first pass's
 // load to the last pass's store: LDS tiles, registers and the inter-pass HBM scratch hold
-// 9 x 29-bit limbs, so a butterfly is one mul29 plus limb adds, with none of the 8x32
-// split / join / modular add-sub chains of ntt_pass_kernel.
-// Bounds (r = the BN254 scalar modulus):
-//  * every twiddle product is mul29<Fr29>(x, w) with w < r canonical: for x < 2^261 the
-//    result is < x r / 2^261 + r < 1.4 r, limbs normalized; x may have limbs < 2^31.6
-//    (column sum 9 (2^60.6 + 2^58) + 2^35 < 2^64, f29.h);
-//  * a butterfly y0 = x0 + t, y1 = x0 + 2r - t (Fr29::K2 borrowed: every limb >= t's) adds
-//    at most 2r to the value bound of its inputs, so after the L <= 24 stages of a
-//    transform from inputs < 1.4 r the values are < 50 r < 2^260 (every product input
-//    < 2^261 holds throughout, no value reduction is ever needed);
-//  * limbs: a radix-4 group's outputs are < 2^31.4 before normalisation; they are
-//    normalized (norm29) once per group (and after the odd radix-2 stage), so every
-//    group starts from limbs < 2^29;
-//  * the last pass maps v < 50 r to canonical Fr: q = floor(v_8 / (r_8 + 1)) <= v / r
+// 9 x 29-bit limbs, so a butterfly is one twiddle product plus limb adds.
+// Twiddle products (round 5) are Shoup products by the fixed twiddle (f29.h mul_shoup: 143
+// mads and no v_mul_lo_u32 against the Montgomery product's 162 + 9; NttTables::Tw holds
+// w and floor(w 2^261 / r)). Bounds (r = the BN254 scalar modulus):
+//  * a twiddle product of x < 2^261 (limbs < 2^30.7) is < 3r, limbs normalized;
+//  * a butterfly y0 = x0 + t, y1 = x0 + 4r - t (Fr29::K4 borrowed: every limb, the top one
+//    included, >= t's) adds at most 4r to the value bound of its inputs, so after the L <= 24
+//    stages of a transform from inputs < 2.4 r the values are < 99 r < 2^260.3 (every
+//    product input < 2^261 holds throughout, no value reduction is ever needed);
+//  * limbs: a radix-4 group's outputs are < 2^31.3 before normalisation, its products'
+//    inputs < 2^30.7; the outputs are normalized (norm29) once per group (and after the
+//    odd radix-2 stage), so every group starts from limbs < 2^29;
+//  * the last pass maps v < 128 r to canonical Fr: q = floor(v_8 / (r_8 + 1)) <= v / r
 //    (v_8 = the top limb, bits 232..), v - q r < r + (q + 1) 2^232 < 2r, then one
-//    conditional subtraction (join_fr29); with an output factor the product < 1.4 r is
-//    joined directly.
+//    conditional subtraction (join_fr29); with an output factor (a Montgomery product by
+//    the per-index out_f) the product < x r / 2^261 + r < 1.6 r is joined directly.
+// Until round 4 the twiddles were Montgomery-261 operands of mul29 (products < 1.4 r,
+// butterflies + 2r, values < 50 r).
 // elements per tile: 1024 (9 x 4 KiB of limbs = 36 KiB LDS, 256 threads, 4 tiles per CU), one
 // radix-4 group per thread; 2048-element tiles (72 KiB, 2 per CU) give the same 4 waves per
 // SIMD in half as many barrier domains and measured slower (profiles/r3_ntt_tile_ab.txt)
@@ -153,13 +169,29 @@ __device__ __forceinline__ F29 add_nn29(const F29& a, const F29& b) {
   for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + b.v[l];
   return r;
 }
-__device__ __forceinline__ F29 sub2r_nn29(const F29& a, const F29& b) {  // a + 2r - b, b < 2r normalized
+// the twiddle product (NZ_NTT_SHOUP=0: the round-4 Montgomery product, for A/B builds only)
+__device__ __forceinline__ F29 tw_mul(const F29& x, const NttTables::Tw& w) {
+#if NZ_NTT_SHOUP
+  return mul_shoup(x, w.w, w.ws);
+#else
+  return mul29<Fr29>(x, w.w);
+#endif
+}
+__device__ __forceinline__ void tw_mul2(const F29& x, const NttTables::Tw& w, const F29& y, const NttTables::Tw& v,
+                                        F29& r1, F29& r2) {
+#if NZ_NTT_SHOUP
+  mul_shoup_x2(x, w.w, w.ws, y, v.w, v.ws, r1, r2);
+#else
+  mul29x2<Fr29>(x, w.w, y, v.w, r1, r2);
+#endif
+}
+__device__ __forceinline__ F29 sub4r_nn29(const F29& a, const F29& b) {  // a + 4r - b, b < 3r normalized
   F29 r;
 #pragma unroll
-  for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + Fr29::K2[l] - b.v[l];
+  for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + Fr29::K4[l] - b.v[l];
   return r;
 }
-__device__ __forceinline__ Fr canon_fr29(const F29& x) {  // normalized x < 64 r -> canonical Fr
+__device__ __forceinline__ Fr canon_fr29(const F29& x) {  // normalized x < 128 r -> canonical Fr
   const uint32_t q = x.v[8] / (Fr29::P[8] + 1u);
   F29 y;
   int64_t carry = 0;
@@ -177,7 +209,7 @@ __device__ __forceinline__ Fr canon_fr29(const F29& x) {  // normalized x < 64 r
 // (else canonical Fr to `out`, last pass only).
 template <bool IN29, bool OUT29>
 __global__ void __launch_bounds__(kTile / 4)
-ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29* __restrict__ tw, int L, int s,
+ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const NttTables::Tw* __restrict__ tw, int L, int s,
                   int q, int logC, F29 scale29, int do_scale, NttIo io, int sparse4) {
   constexpr int T = kTile / 4;  // threads
   __shared__ uint32_t sl[9 * kTile];
@@ -237,7 +269,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
     st = 2;
   } else if (q & 1) {  // odd stage count: one radix-2 stage first
     const int g = s;
-    const F29* __restrict__ twg = tw + (((size_t)1 << g) - 1);
+    const NttTables::Tw* __restrict__ twg = tw + (((size_t)1 << g) - 1);
 #pragma unroll
     for (int u = 0; u < 2; u++) {
       const int b = tid + u * T;
@@ -248,8 +280,8 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
       const size_t k = first ? 0 : (lo0 + c);
       const F29 x0 = tile_ld(sl, i0);
       const F29 x1 = tile_ld(sl, i1);
-      const F29 tt = g ? mul29<Fr29>(x1, twg[k]) : x1;
-      F29 y0 = add_nn29(x0, tt), y1 = sub2r_nn29(x0, tt);
+      const F29 tt = g ? tw_mul(x1, twg[k]) : x1;
+      F29 y0 = add_nn29(x0, tt), y1 = sub4r_nn29(x0, tt);
       norm29(y0);
       norm29(y1);
       tile_st(sl, i0, y0);
@@ -263,8 +295,8 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
   for (; st < q; st += 2) {
     const int h = 1 << st;
     const int g = s + st;
-    const F29* __restrict__ twa = tw + (((size_t)1 << g) - 1);
-    const F29* __restrict__ twb = tw + (((size_t)1 << (g + 1)) - 1);
+    const NttTables::Tw* __restrict__ twa = tw + (((size_t)1 << g) - 1);
+    const NttTables::Tw* __restrict__ twb = tw + (((size_t)1 << (g + 1)) - 1);
     const int b = tid;
     if (b < ngroups) {
       const int c = b & (C - 1);
@@ -277,18 +309,19 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
                 i3 = ((j + 3 * h) << logC) + c;
       F29 t1 = tile_ld(sl, i1), t3 = tile_ld(sl, i3);
       if (g) {
-        const F29 wa = twa[ka];
+        const NttTables::Tw wa = twa[ka];
         F29 p1, p3;
-        mul29x2<Fr29>(t1, wa, t3, wa, p1, p3);
+        tw_mul2(t1, wa, t3, wa, p1, p3);
         t1 = p1;
         t3 = p3;
       }
       const F29 x0 = tile_ld(sl, i0), x2 = tile_ld(sl, i2);
-      const F29 y0 = add_nn29(x0, t1), y1 = sub2r_nn29(x0, t1);
-      const F29 y2 = add_nn29(x2, t3), y3 = sub2r_nn29(x2, t3);
+      const F29 y0 = add_nn29(x0, t1), y1 = sub4r_nn29(x0, t1);
+      const F29 y2 = add_nn29(x2, t3), y3 = sub4r_nn29(x2, t3);
       F29 u2, u3;
-      mul29x2<Fr29>(y2, twb[ka], y3, twb[kc], u2, u3);
-      F29 z0 = add_nn29(y0, u2), z2 = sub2r_nn29(y0, u2), z1 = add_nn29(y1, u3), z3 = sub2r_nn29(y1, u3);
+      const NttTables::Tw wb = twb[ka], wc = twb[kc];
+      tw_mul2(y2, wb, y3, wc, u2, u3);
+      F29 z0 = add_nn29(y0, u2), z2 = sub4r_nn29(y0, u2), z1 = add_nn29(y1, u3), z3 = sub4r_nn29(y1, u3);
       norm29(z0);
       norm29(z1);
       norm29(z2);
@@ -325,7 +358,7 @@ ntt29_pass_kernel(const Fr* in, const F29* in29, Fr* out, F29* out29, const F29*
 
 // The 9x29 pipeline's passes: stages [0, q1) with the bit-reversed gather, then <= 8
 // stages per pass through the F29 scratch; the last pass writes canonical Fr.
-static void ntt29_passes(const Fr* in, Fr* out, const F29* tw, int L, const F29& sc29, int do_scale,
+static void ntt29_passes(const Fr* in, Fr* out, const NttTables::Tw* tw, int L, const F29& sc29, int do_scale,
                          const NttIo& io, hipStream_t st, F29* scr) {
   constexpr int T = kTile / 4;
   const int q1 = L < 8 ? L : 8;
@@ -370,7 +403,7 @@ void ntt(const NttTables& t, const Fr* in, Fr* out, int L, bool inverse_dir, hip
   if (in == out) throw Error(NZCB_ERR_ARG, "ntt requires in != out");
   F29* scr = (F29*)(scratch29 ? scratch29 : t.scratch29.p);
   if (L > 8 && !scratch29 && t.scratch29.n < ((size_t)9 << L)) throw Error(NZCB_ERR_INTERNAL, "ntt: no scratch");
-  const F29* tw = inverse_dir ? t.inv29.p : t.fwd29.p;
+  const NttTables::Tw* tw = inverse_dir ? t.inv29.p : t.fwd29.p;
   Fr sc = Fr::one();
   int do_scale = 0;
   if (inverse_dir && !io.out_f_has_scale) {

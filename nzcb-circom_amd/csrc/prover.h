@@ -64,6 +64,7 @@ struct Prover {
   DevBuf<Fr> sigma;               // 3 x [n | 4n]
   DevBuf<Fr> sig_h;               // 3 x n: sigma_k(w^i), contiguous (round 2)
   DevBuf<Fr> q_h;                 // 5 x n: qm..qc(w^i), contiguous (the gate check on H, quot3)
+  DevBuf<Fr> w_h;                 // n: w^i (round 2's grand product)
   DevBuf<Fr> lagrange;            // nLagrange x [n | 4n]
   DevBuf<uint32_t> amap, bmap, cmap;
   DevBuf<AddRec> adds;
@@ -105,8 +106,18 @@ struct Prover {
   static constexpr int kTopWords = 4 * 6 + 1;
 
   int fault = 0;  // nzcb_debug_inject_fault: NZCB_FAULT_* for this lane's next proof
-  // timings of the last proof (ms)
-  double tm[9] = {0};
+  // timings of the last proof (ms): [0..6] host wall clock of the whole proof and its
+  // phases, [7] host time in the MSM calls (enqueue + waiting for results), [8] host time
+  // enqueueing transforms, and with kernel statistics on (prof_gpu) the GPU time of [9] the
+  // commitment MSMs and [10] the transforms: HIP event pairs around each one on its stream
+  double tm[11] = {0};
+  bool prof_gpu = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> span_ev;  // event pairs, created on first use
+  std::vector<int> span_kind;                               // per pair in use: 0 MSM, 1 transform
+  size_t spans_used = 0;
+  size_t span_begin(int kind, hipStream_t s);
+  void span_end(size_t i, hipStream_t s);
+  void span_totals(double* msm_ms, double* ntt_ms);
 
   Prover(const uint8_t* zkey, size_t len, int device);
   Prover(const Prover& primary, int lane);  // extra lane sharing primary's proving key

@@ -108,9 +108,9 @@ __device__ __forceinline__ Fr root4(const Fr* __restrict__ lo, const Fr* __restr
 }
 
 struct PermArgs {
-  Fr beta, gamma, k1, k2;
-  F29 beta29, k1beta29, k2beta29;  // beta, k1 beta, k2 beta as mul_fr29 operands
-  int k23;                         // k1 = 2, k2 = 3 (snarkjs getK1K2 for BN254): k beta w by additions
+  F29 beta266, k1beta266, k2beta266;  // beta, k1 beta, k2 beta at exponent 266 (x exponent 256 -> 261)
+  F29 gamma261;                       // gamma at exponent 261
+  int k23;                            // k1 = 2, k2 = 3 (snarkjs getK1K2 for BN254): k beta w by additions
 };
 
 // c * 2^5 split into the 9x29 radix: the Montgomery-261 operand of mul_fr29 for a
@@ -199,32 +199,49 @@ __device__ __forceinline__ Fr shfl_fr(const Fr& v, int src) {
   for (int w = 0; w < 8; w++) o.v[w] = __shfl(v.v[w], src, 64);
   return o;
 }
+__device__ __forceinline__ F29 shfl_fr(const F29& v, int src) {
+  F29 o;
+#pragma unroll
+  for (int w = 0; w < 9; w++) o.v[w] = __shfl(v.v[w], src, 64);
+  return o;
+}
 struct MulOp {
+  using T = Fr;
   __device__ Fr operator()(const Fr& a, const Fr& b) const { return a * b; }
   __device__ static Fr id() { return Fr::one(); }
 };
 struct AddOp {
+  using T = Fr;
   __device__ Fr operator()(const Fr& a, const Fr& b) const { return a + b; }
   __device__ static Fr id() { return Fr::zero(); }
+};
+// products of Montgomery-261 values in the 9x29 radix (F29 of v 2^261 mod r, the one
+// exponent that a product of any number of factors keeps: mul29 takes 2^261 off)
+struct Mul29Op {
+  using T = F29;
+  __device__ F29 operator()(const F29& a, const F29& b) const { return mul29<Fr29>(a, b); }
+  __device__ static F29 id() { return f29_const(Fr29::ONE); }
 };
 // kSuffix = false: op of v_t' over t' < t; true: over t' > t, for the NT threads of the
 // workgroup. sh: >= NT / 64 entries. *total (when given) = op over all NT values, valid in
 // thread 0. Up to 4 waves the wave totals are combined directly (wave-uniform branches); past
 // that the first wave scans them by shuffles (k_perm_factors' 16 waves).
 template <bool kSuffix, class Op, int NT = kT>
-__device__ __forceinline__ Fr block_scan_excl(const Fr& v, Fr* sh, Fr* total) {
+__device__ __forceinline__ typename Op::T block_scan_excl(const typename Op::T& v, typename Op::T* sh,
+                                                          typename Op::T* total) {
+  using T = typename Op::T;
   constexpr int NW = NT / 64;
   static_assert(NW >= 1 && NW <= 64 && NT % 64 == 0, "whole waves, at most 64");
   const Op op;
   const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
-  Fr inc = v;
+  T inc = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const int src = kSuffix ? lane + d : lane - d;
-    const Fr o = shfl_fr(inc, src & 63);
+    const T o = shfl_fr(inc, src & 63);
     if (kSuffix ? lane + d < 64 : lane >= d) inc = op(inc, o);
   }
-  Fr ex = shfl_fr(inc, (kSuffix ? lane + 1 : lane - 1) & 63);
+  T ex = shfl_fr(inc, (kSuffix ? lane + 1 : lane - 1) & 63);
   if (kSuffix ? lane == 63 : lane == 0) ex = Op::id();
   if (kSuffix ? lane == 0 : lane == 63) sh[wv] = inc;  // the wave's total
   __syncthreads();
@@ -233,23 +250,23 @@ __device__ __forceinline__ Fr block_scan_excl(const Fr& v, Fr* sh, Fr* total) {
     for (int k = 0; k < NW; k++)  // wave-uniform: the other waves' totals on this side
       if (kSuffix ? k > wv : k < wv) ex = op(ex, sh[k]);
     if (total && threadIdx.x == 0) {
-      Fr t = sh[0];
+      T t = sh[0];
 #pragma unroll
       for (int k = 1; k < NW; k++) t = op(t, sh[k]);
       *total = t;
     }
     __syncthreads();
   } else {
-    Fr tot_all = Op::id();
+    T tot_all = Op::id();
     if (wv == 0) {  // exclusive scan of the NW wave totals in lanes < NW, back into sh
-      Fr w = lane < NW ? sh[lane] : Op::id();
+      T w = lane < NW ? sh[lane] : Op::id();
 #pragma unroll
       for (int d = 1; d < NW; d <<= 1) {
         const int src = kSuffix ? lane + d : lane - d;
-        const Fr o = shfl_fr(w, src & 63);
+        const T o = shfl_fr(w, src & 63);
         if (kSuffix ? lane + d < NW : (lane >= d && lane < NW)) w = op(w, o);
       }
-      Fr wex = shfl_fr(w, (kSuffix ? lane + 1 : lane - 1) & 63);
+      T wex = shfl_fr(w, (kSuffix ? lane + 1 : lane - 1) & 63);
       if (kSuffix ? lane == NW - 1 : lane == 0) wex = Op::id();
       tot_all = shfl_fr(w, kSuffix ? 0 : NW - 1);
       if (lane < NW) sh[lane] = wex;  // no other wave reads sh before the barrier below
@@ -284,72 +301,75 @@ __device__ __forceinline__ Fr block_sum_excl_suffix(const Fr& v, Fr* sh, Fr& tot
 // come from contiguous copies (Prover::sig_h), not at stride 4 from the 4n evaluations.
 // Round 3 ran a batch inversion per 32-element chunk per thread (1.24 ms at 2^21, the
 // chunks 1 KB apart per lane, den / prefix arrays written and read back through HBM).
-__device__ __forceinline__ Fr perm_bw(const Fr* rlo, const Fr* rhi, size_t e, size_t n, const F29& op) {
-  return e < n ? mul_fr29(root4(rlo, rhi, 4 * e), op) : Fr::zero();
-}
-
-// 3 waves per SIMD (168 VGPRs, 100 B scratch) instead of the compiler's 2 (222 VGPRs):
-// 0.696 -> 0.597 ms isolated, bench unchanged (profiles/r4_perm_waves_ab.txt)
-__global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3, 8)))
+#ifndef NZ_PERM_WAVES
+#define NZ_PERM_WAVES 3  // waves per SIMD the grand-product tile kernel is compiled for
+#endif
+// Every product runs in the 9x29 radix at exponent 261 (round 5; until round 4 the factors'
+// products and both scans were 8x32 products, 13 of them per element): the witness values
+// and the sigmas are shifted to exponent 261 by fr_to261 or by their product with
+// beta 2^266, w^i comes from the per-context table w_h (no root-table product), and only
+// the outputs (Z, the tile totals) return to Montgomery-256.
+__global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(NZ_PERM_WAVES, 8)))
 k_perm_tile(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
-            const Fr* __restrict__ sig_h, size_t n, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi,
-            PermArgs pa, Fr* __restrict__ Z, Fr* __restrict__ ntot, Fr* __restrict__ dtot) {
+            const Fr* __restrict__ sig_h, size_t n, const Fr* __restrict__ w_h, PermArgs pa, Fr* __restrict__ Z,
+            Fr* __restrict__ ntot, Fr* __restrict__ dtot) {
   __shared__ uint32_t stg[kStageWords];
-  __shared__ Fr sh[kT / 64];  // the scans' wave totals
+  __shared__ F29 sh[kT / 64];  // the scans' wave totals
   const int tid = threadIdx.x;
   const size_t base = (size_t)blockIdx.x * kTileN;
   const size_t e0 = base + (size_t)kPer * tid;
-  const F29 beta29 = pa.beta29, k1beta29 = pa.k1beta29, k2beta29 = pa.k2beta29;  // no byval copy in scratch
-  const Fr gamma = pa.gamma;
+  const F29 beta266 = pa.beta266, gamma261 = pa.gamma261;  // no byval copy in scratch
   const bool k23 = pa.k23 != 0;
-  Fr num[kPer], den[kPer], v[kPer], u[kPer];
+  F29 num[kPer], den[kPer], bw[kPer], bs[kPer];
 #pragma unroll 1
   for (int k = 0; k < 3; k++) {
+    // sigma_k first: bs = b s_k (exponent 261), for den *= x + b s_k + g below
+    stage_use([&](size_t g) { return sig_h[(size_t)k * n + g]; }, base, n, stg,
+              [&](int j, const Fr& x) { bs[j] = mul29<Fr29>(split29(x), beta266); });
     // witness column: num *= x + k b w + g (k b w: b w, 2 b w, 3 b w when k1, k2 = 2, 3, what
-    // snarkjs getK1K2 finds for BN254); the value stays for the denominator
-    const F29 op = k23 || k == 0 ? beta29 : (k == 1 ? k1beta29 : k2beta29);
+    // snarkjs getK1K2 finds for BN254: bw[] keeps b w^i), den *= x + b s_k + g
+    const F29 kb = k == 0 ? beta266 : (k == 1 ? pa.k1beta266 : pa.k2beta266);
     const Fr* col = k == 0 ? A : B;
     if (k == 2) col = C;
     stage_use([&](size_t g) { return col[g]; }, base, n, stg,
               [&](int j, const Fr& x) {
-                // b w^i once per element when k1, k2 = 2, 3 (v[] holds it until the scans)
-                Fr kbw;
+                F29 kbw;
                 if (k23 && k) {
-                  kbw = k == 1 ? v[j] + v[j] : v[j] + v[j] + v[j];
+                  kbw = k == 1 ? add29(bw[j], bw[j]) : add3_29(bw[j], bw[j], bw[j]);
                 } else {
-                  kbw = perm_bw(rlo, rhi, e0 + j, n, op);
-                  if (k23) v[j] = kbw;
+                  kbw = mul29<Fr29>(split29(e0 + j < n ? w_h[e0 + j] : Fr::zero()), kb);
+                  if (k23) bw[j] = kbw;
                 }
-                const Fr f = x + kbw + gamma;
-                num[j] = k ? num[j] * f : f;
-                u[j] = x + gamma;
+                const F29 x261 = fr_to261(x);
+                const F29 f = add3_29(x261, kbw, gamma261);   // < 38 r
+                const F29 g = add3_29(x261, bs[j], gamma261);  // < 35 r
+                num[j] = k ? mul29<Fr29>(num[j], f) : f;
+                den[j] = k ? mul29<Fr29>(den[j], g) : g;
               });
-    // sigma_k: den *= x + b s_k + g
-    stage_use([&](size_t g) { return sig_h[(size_t)k * n + g]; }, base, n, stg, [&](int j, const Fr& x) {
-      const Fr g = u[j] + mul_fr29(x, beta29);
-      den[j] = k ? den[j] * g : g;
-    });
   }
+  const F29 one = f29_const(Fr29::ONE);
 #pragma unroll
   for (int j = 0; j < kPer; j++)  // past n: factor 1
-    if (e0 + j >= n) num[j] = den[j] = Fr::one();
-  // thread-local: v = exclusive prefix of num, u = inclusive suffix of den
-  v[0] = Fr::one();
+    if (e0 + j >= n) num[j] = den[j] = one;
+  // thread-local: bw = exclusive prefix of num, bs = inclusive suffix of den
+  bw[0] = one;
 #pragma unroll
-  for (int j = 1; j < kPer; j++) v[j] = v[j - 1] * num[j - 1];
-  u[kPer - 1] = den[kPer - 1];
+  for (int j = 1; j < kPer; j++) bw[j] = mul29<Fr29>(bw[j - 1], num[j - 1]);
+  bs[kPer - 1] = den[kPer - 1];
 #pragma unroll
-  for (int j = kPer - 2; j >= 0; j--) u[j] = u[j + 1] * den[j];
-  Fr nt;
-  const Fr np = block_prod_excl(v[kPer - 1] * num[kPer - 1], sh, nt);
-  const Fr ds = block_prod_excl_suffix(u[0], sh);
-  const Fr c = np * ds;
+  for (int j = kPer - 2; j >= 0; j--) bs[j] = mul29<Fr29>(bs[j + 1], den[j]);
+  F29 nt;
+  const F29 np = block_scan_excl<false, Mul29Op>(mul29<Fr29>(bw[kPer - 1], num[kPer - 1]), sh, &nt);
+  const F29 ds = block_scan_excl<true, Mul29Op>(bs[0], sh, nullptr);
+  // c at exponent 256: the last product of each element lands in Montgomery-256
+  const F29 c = mul29<Fr29>(mul29<Fr29>(np, ds), f29_const(Fr29::C256));
+  Fr out[kPer];
 #pragma unroll
-  for (int j = 0; j < kPer; j++) v[j] = v[j] * u[j] * c;
-  stage_out(v, base, n, stg, Z);
+  for (int j = 0; j < kPer; j++) out[j] = join_fr29(mul29<Fr29>(mul29<Fr29>(bw[j], bs[j]), c));
+  stage_out(out, base, n, stg, Z);
   if (tid == 0) {
-    ntot[blockIdx.x] = nt;
-    dtot[blockIdx.x] = ds * u[0];  // thread 0: its own suffix times the others'
+    ntot[blockIdx.x] = fr_from261(nt);
+    dtot[blockIdx.x] = fr_from261(mul29<Fr29>(ds, bs[0]));  // thread 0: its own suffix times the others'
   }
 }
 
@@ -672,6 +692,12 @@ k_t_combine(const Fr* __restrict__ V, size_t n, T3Args a, Fr* __restrict__ t) {
   if (k < 6) t[3 * n + k] = a.q3[k];  // t has 3n + 6 coefficients (its buffer no more)
 }
 
+// w^i = w4^(4 i), i < n (Prover::w_h)
+__global__ void k_root_n(Fr* __restrict__ out, const Fr* __restrict__ rlo, const Fr* __restrict__ rhi, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = root4(rlo, rhi, 4 * i);
+}
+
 // fault injection (nzcb_debug_inject_fault): one coefficient + 1
 __global__ void k_fault_bump(Fr* x) {
   if (threadIdx.x == 0) x[0] = x[0] + Fr::one();
@@ -904,6 +930,35 @@ Prover::~Prover() {
   if (side_done) (void)hipEventDestroy(side_done);
   if (pows_done) (void)hipEventDestroy(pows_done);
   if (top_host) (void)hipHostFree(top_host);
+  for (auto& e : span_ev) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+}
+
+// GPU time spans of the last proof (prof_gpu): a start event before and an end event after
+// one transform or one commitment MSM, on the stream it runs on
+size_t Prover::span_begin(int kind, hipStream_t s) {
+  if (spans_used == span_ev.size()) {
+    hipEvent_t a, b;
+    NZ_HIP(hipEventCreate(&a));
+    NZ_HIP(hipEventCreate(&b));
+    span_ev.emplace_back(a, b);
+    span_kind.push_back(0);
+  }
+  span_kind[spans_used] = kind;
+  NZ_HIP(hipEventRecord(span_ev[spans_used].first, s));
+  return spans_used++;
+}
+void Prover::span_end(size_t i, hipStream_t s) { NZ_HIP(hipEventRecord(span_ev[i].second, s)); }
+void Prover::span_totals(double* msm_ms, double* ntt_ms) {
+  *msm_ms = *ntt_ms = 0;
+  for (size_t i = 0; i < spans_used; i++) {
+    NZ_HIP(hipEventSynchronize(span_ev[i].second));
+    float ms = 0;
+    NZ_HIP(hipEventElapsedTime(&ms, span_ev[i].first, span_ev[i].second));
+    (span_kind[i] ? *ntt_ms : *msm_ms) += ms;
+  }
 }
 
 MsmShard::~MsmShard() {
@@ -998,6 +1053,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   up(qc, z.qc);
   up(sigma, z.sigma);
   sig_h.alloc((size_t)3 * n);  // sigma_k on H, contiguous (round 2's grand product)
+  w_h.alloc(n);                // w^i, i < n (round 2's grand product; built with the root tables below)
   for (int k = 0; k < 3; k++)
     hipLaunchKernelGGL(k_stride4, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, sigma.p + (size_t)k * 5 * n + n,
                        (size_t)n, sig_h.p + (size_t)k * n);
@@ -1057,6 +1113,9 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
   };
   table(root_lo, nlo, w4, one);
   table(root_hi, nhi, pow_u64(w4, 4096), one);
+  hipLaunchKernelGGL(k_root_n, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, w_h.p, root_lo.p, root_hi.p,
+                     (size_t)n);
+  NZ_HIP(hipGetLastError());
   // coset g*<w4>, g = 5 (the Fr multiplicative generator, ffjavascript's nqr): x_i = g*w4^i,
   // g^j and g^-j for coset (un)scaling, and 1/Z_H(x_i) = 1/(g^n w4^(i n) - 1), by i mod 4
   const Fr g = fr_small(5), gi = inverse(g);
@@ -1247,7 +1306,7 @@ Prover::Prover(const Prover& pk, int) {
   ltab.q.alias(pk.ltab.q);
   ltab.n = pk.ltab.n; ltab.stride = pk.ltab.stride; ltab.c = pk.ltab.c; ltab.nw = pk.ltab.nw;
   qm.alias(pk.qm); ql.alias(pk.ql); qr.alias(pk.qr); qo.alias(pk.qo); qc.alias(pk.qc);
-  sigma.alias(pk.sigma); sig_h.alias(pk.sig_h); q_h.alias(pk.q_h); lagrange.alias(pk.lagrange);
+  sigma.alias(pk.sigma); sig_h.alias(pk.sig_h); q_h.alias(pk.q_h); w_h.alias(pk.w_h); lagrange.alias(pk.lagrange);
   amap.alias(pk.amap); bmap.alias(pk.bmap); cmap.alias(pk.cmap); adds.alias(pk.adds);
   root_lo.alias(pk.root_lo); root_hi.alias(pk.root_hi); x_lo.alias(pk.x_lo);
   g_lo.alias(pk.g_lo); g_hi.alias(pk.g_hi); gi_lo.alias(pk.gi_lo); gi_hi.alias(pk.gi_hi);
@@ -1314,7 +1373,11 @@ void Prover::round3_quot3(const Fr& beta, const Fr& gamma, const Fr& alpha, hipS
     NttIo io;
     io.out_f = itw3.p + (size_t)j * n;
     io.out_f_has_scale = true;
-    ntt(eng->ntt_tables, T.p + (size_t)j * n, Tz.p + (size_t)j * n, power, true, s, nullptr, &io);
+    {
+      const size_t sp = prof_gpu ? span_begin(1, s) : 0;
+      ntt(eng->ntt_tables, T.p + (size_t)j * n, Tz.p + (size_t)j * n, power, true, s, nullptr, &io);
+      if (prof_gpu) span_end(sp, s);
+    }
   }
   NZ_HIP(hipGetLastError());
   if (!side) copy_tops(s);
@@ -1372,7 +1435,11 @@ void Prover::to4t(const Fr* evals, Fr* coefs, Fr* evals4, const int* bidx, int n
 // the blinded coefficients (what the commitment needs) ...
 void Prover::to4t_coefs(const Fr* evals, Fr* coefs, const int* bidx, int nb, hipStream_t s, uint32_t* scr) {
   auto t0 = std::chrono::steady_clock::now();
-  ntt(eng->ntt_tables, evals, coefs, power, true, s, nullptr, nullptr, scr);
+  {
+    const size_t sp = prof_gpu ? span_begin(1, s) : 0;
+    ntt(eng->ntt_tables, evals, coefs, power, true, s, nullptr, nullptr, scr);
+    if (prof_gpu) span_end(sp, s);
+  }
   BlindIdx bi;
   bi.count = nb;
   for (int k = 0; k < nb; k++) bi.idx[k] = bidx[k];
@@ -1393,7 +1460,11 @@ void Prover::to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s, uin
       io.fold_len = (size_t)nb;
       io.fold_n = n;
       io.fold_f = fr29_operand(d3[j]);
-      ntt(eng->ntt_tables, coefs, evals4 + (size_t)j * n, power, false, s, nullptr, &io, scr);
+      {
+        const size_t sp = prof_gpu ? span_begin(1, s) : 0;
+        ntt(eng->ntt_tables, coefs, evals4 + (size_t)j * n, power, false, s, nullptr, &io, scr);
+        if (prof_gpu) span_end(sp, s);
+      }
     }
     NZ_HIP(hipGetLastError());
     ntt_ms += ms_since(t0);
@@ -1402,7 +1473,11 @@ void Prover::to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s, uin
   NttIo io;  // coset shift g^j and the zero padding fused into the NTT's first pass
   io.in_len = (size_t)n + nb;
   io.in_f = g29.p;
-  ntt(eng->ntt_tables, coefs, evals4, power + 2, false, s, nullptr, &io, scr);
+  {
+    const size_t sp = prof_gpu ? span_begin(1, s) : 0;
+    ntt(eng->ntt_tables, coefs, evals4, power + 2, false, s, nullptr, &io, scr);
+    if (prof_gpu) span_end(sp, s);
+  }
   NZ_HIP(hipGetLastError());
   ntt_ms += ms_since(t0);  // host enqueue time only (kernels run asynchronously)
 }
@@ -1439,7 +1514,9 @@ void Prover::commit_start(int slot, const Fr* coefs, size_t len, const MsmBaseTa
       throw Error(NZCB_ERR_INTERNAL, "msm split: sending the scalars to the other ranks failed");
     len = std::min(len, split_own);
   }
+  const size_t sp = prof_gpu ? span_begin(0, ms) : 0;
   msm_enqueue(*msc[slot], bases ? bases : ptau.p, coefs, len, true, ms, tab ? tab : &ptab);
+  if (prof_gpu) span_end(sp, ms);
   static const bool serial = std::getenv("NZCB_SERIAL") != nullptr;  // profiling: one kernel at a time
   if (serial) NZ_HIP(hipStreamSynchronize(ms));
 }
@@ -1641,6 +1718,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   NZ_HIP(hipSetDevice(eng->device));
   hipStream_t s = st();
   msm_ms = ntt_ms = 0;
+  spans_used = 0;
   // a previous proof that failed in round 2 may have left the side stream's NTTs running
   // on this lane's buffers (blind, A, B, C)
   if (side_done) NZ_HIP(hipEventSynchronize(side_done));
@@ -1766,7 +1844,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     lg("gamma: " + fr_dec(gamma));
   }
   {
-    PermArgs pa{beta, gamma, k1, k2, fr29_operand(beta), fr29_operand(k1 * beta), fr29_operand(k2 * beta),
+    PermArgs pa{f29_exp(beta, 10), f29_exp(k1 * beta, 10), f29_exp(k2 * beta, 10), f29_exp(gamma, 5),
                 k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0};
     const size_t ntiles = (n + kTileN - 1) / kTileN;
     if (ntiles > 1024 * 64) throw Error(NZCB_ERR_INTERNAL, "round 2: domain too large for the tile factors");
@@ -1775,7 +1853,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     Fr* fac = dtot + ntiles;
     Fr* totals = fac + ntiles;
     hipLaunchKernelGGL(k_perm_tile, dim3((unsigned)ntiles), dim3(kT), 0, s, A.p, B.p, C.p, sig_h.p, (size_t)n,
-                       root_lo.p, root_hi.p, pa, Z.p, ntot, dtot);
+                       w_h.p, pa, Z.p, ntot, dtot);
     hipLaunchKernelGGL(k_perm_factors, dim3(1), dim3(1024), 0, s, (const Fr*)ntot, (const Fr*)dtot, (int)ntiles,
                        fac, totals);
     NZ_HIP(hipGetLastError());
@@ -1846,7 +1924,11 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       io.out_f_has_scale = true;
       io.out_limit = (size_t)3 * n + 6;
       io.out_flags = flags.p;
-      ntt(eng->ntt_tables, T.p, t.p, power + 2, true, s, nullptr, &io);
+      {
+        const size_t sp = prof_gpu ? span_begin(1, s) : 0;
+        ntt(eng->ntt_tables, T.p, t.p, power + 2, true, s, nullptr, &io);
+        if (prof_gpu) span_end(sp, s);
+      }
       NZ_HIP(hipGetLastError());
       uint32_t f = 0;
       NZ_HIP(hipMemcpyAsync(&f, flags.p, 4, hipMemcpyDeviceToHost, s));
@@ -1976,6 +2058,8 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   tm[0] = ms_since(T0);
   tm[7] = msm_ms;
   tm[8] = ntt_ms;
+  tm[9] = tm[10] = -1;  // not measured
+  if (prof_gpu) span_totals(&tm[9], &tm[10]);
 
   // ---------------- output ----------------
   const G1Affine* pts[9] = {&pA, &pB, &pC, &pZ, &pT1, &pT2, &pT3, &pWxi, &pWxiw};

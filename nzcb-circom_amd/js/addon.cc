@@ -73,6 +73,21 @@ napi_value CreateContext(napi_env env, napi_callback_info info) {
   return ext;
 }
 
+// releaseContext(ctx): frees the context's HBM now instead of at garbage collection (a
+// context whose lane setup failed is dropped this way; the external must not be used after)
+napi_value ReleaseContext(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+  Ctx* c = nullptr;
+  CHECK(napi_get_value_external(env, argv[0], reinterpret_cast<void**>(&c)));
+  if (c && c->ctx) {
+    nzcb_ctx_destroy(c->ctx);
+    c->ctx = nullptr;
+  }
+  return nullptr;
+}
+
 // a JS string argument as UTF-8 (false if it is not a string)
 bool str_arg(napi_env env, napi_value v, std::string* out) {
   napi_valuetype t;
@@ -261,28 +276,31 @@ napi_value SetLanes(napi_env env, napi_callback_info info) {
 // ---- witness programs (nzcb_wprog_*): circom's witness calculator on the GPU ----------
 struct Wprog {
   nzcb_wprog* p = nullptr;
+  int device = 0;  // the program's GPU: its witness buffers live there
 };
 
 // HBM buffers reused across fullProveDevice calls (a witness of nzcp_live is 19.2 MB; a
-// hipMalloc per proof would cost more than the witness program's run)
+// hipMalloc per proof would cost more than the witness program's run), keyed by (device,
+// bytes): a call's buffers are on its witness program's device (the per-call
+// threads never selected a device, so every buffer was on device 0)
 std::mutex g_pool_mu;
-std::multimap<size_t, void*> g_pool;
-void* pool_get(size_t bytes) {
+std::multimap<std::pair<int, size_t>, void*> g_pool;
+void* pool_get(int device, size_t bytes) {
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    auto it = g_pool.find(bytes);
+    auto it = g_pool.find({device, bytes});
     if (it != g_pool.end()) {
       void* p = it->second;
       g_pool.erase(it);
       return p;
     }
   }
-  return nzcb_dev_alloc(bytes);
+  return nzcb_dev_alloc_on(device, bytes);
 }
-void pool_put(size_t bytes, void* p) {
+void pool_put(int device, size_t bytes, void* p) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(g_pool_mu);
-  g_pool.emplace(bytes, p);
+  g_pool.emplace(std::make_pair(device, bytes), p);
 }
 
 // plonk.fullProve with a witness program, everything in HBM: the input signals go up
@@ -298,8 +316,9 @@ void run_fullprove_device(ProveWork* w) {
     std::snprintf(w->err.msg, sizeof(w->err.msg), "expected %zu input signals", nin);
     return;
   }
-  void* din = pool_get(nin * 32 ? nin * 32 : 32);
-  void* dw = pool_get(nwires * 32);
+  const int dev = w->prog->device;
+  void* din = pool_get(dev, nin * 32 ? nin * 32 : 32);
+  void* dw = pool_get(dev, nwires * 32);
   if (!din || !dw || nzcb_memcpy_h2d(din, w->in, w->in_len) != 0) {
     w->rc = NZCB_ERR_HIP;
     std::snprintf(w->err.msg, sizeof(w->err.msg), "device buffers for the witness failed");
@@ -309,8 +328,8 @@ void run_fullprove_device(ProveWork* w) {
       w->rc = nzcb_prove_logged(w->c->ctx, dw, nwires, NZCB_WITNESS_DEVICE, w->has_blinding ? w->blinding : nullptr,
                                 w->proof, w->pub, sizeof(w->pub), w->tsfn ? log_trampoline : nullptr, w, &w->err);
   }
-  pool_put(nin * 32 ? nin * 32 : 32, din);
-  pool_put(nwires * 32, dw);
+  pool_put(dev, nin * 32 ? nin * 32 : 32, din);
+  pool_put(dev, nwires * 32, dw);
 }
 
 void wprog_finalize(napi_env, void* data, void*) {
@@ -337,6 +356,7 @@ napi_value CreateWitnessProgram(napi_env env, napi_callback_info info) {
   }
   Wprog* w = new Wprog();
   w->p = p;
+  w->device = device;
   napi_value ext;
   CHECK(napi_create_external(env, w, wprog_finalize, nullptr, &ext));
   return ext;
@@ -725,6 +745,7 @@ napi_value Init(napi_env env, napi_value exports) {
       {"calculateWitness", nullptr, CalculateWitness, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"fullProveDevice", nullptr, FullProveDevice, nullptr, nullptr, nullptr, napi_default, nullptr},
       {"setLanes", nullptr, SetLanes, nullptr, nullptr, nullptr, napi_default, nullptr},
+      {"releaseContext", nullptr, ReleaseContext, nullptr, nullptr, nullptr, napi_default, nullptr},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

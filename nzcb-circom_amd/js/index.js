@@ -50,27 +50,59 @@ function randomBlinding() {
 // One HBM-resident context per (zkey, device): the zkey is uploaded once. A file name is
 // memory-mapped by the library (nzcb_ctx_create_file), so zkeys of nzcp_live size
 // (~3.9 GB, beyond a Node Buffer) work; buffers are keyed by content. A context has
-// `lanes` proof lanes (options.lanes, NZCB_LANES, default 5: bench.py's measured best):
-// concurrent prove / fullProve promises on it run on different lanes at the same time.
-const DEFAULT_LANES = Number(process.env.NZCB_LANES || 5);
+// `lanes` proof lanes: concurrent prove / fullProve promises on it run on different lanes at
+// the same time. options.lanes (or NZCB_LANES) asks for an exact count; by default the
+// context takes up to 5 (bench.py's measured best) as far as the device's free HBM allows
+// (~6.5 GB per extra lane at n = 2^21): a lane count that does not fit is rolled back by
+// the library and the next smaller one is tried.
+const DEFAULT_LANES = 5;
+const ENV_LANES = process.env.NZCB_LANES ? Number(process.env.NZCB_LANES) : 0;
 const contexts = new Map();
-const zkeyHashes = new WeakMap();  // zkey Buffer -> content hash (hashed once per Buffer)
+// Buffer -> {hash, probe}: the content hash is computed once per Buffer; a cheap probe
+// (length, head and tail bytes) is checked on every lookup, so a caller that reuses one
+// Buffer for another zkey or program gets it hashed again rather than the old context.
+// Mutating a Buffer in the middle is not detected: pass a fresh Buffer for new contents.
+const bufHashes = new WeakMap();
+function probeOf(buf) {
+  const k = Math.min(buf.length, 4096);
+  return crypto.createHash('sha1').update(buf.subarray(0, k)).update(buf.subarray(buf.length - k))
+    .update(String(buf.length)).digest('hex');
+}
+function contentHash(buf) {
+  const probe = probeOf(buf);
+  const e = bufHashes.get(buf);
+  if (e && e.probe === probe) return e.hash;
+  const hash = crypto.createHash('sha256').update(buf).digest('hex');
+  bufHashes.set(buf, { hash, probe });
+  return hash;
+}
+function setLanesFitting(ctx, want) {
+  for (let l = want; ; l--) {
+    try {
+      return addon.setLanes(ctx, l);
+    } catch (e) {
+      if (l <= 1) throw e;
+    }
+  }
+}
 function contextFor(zkey, device, lanes) {
   let key;
   if (typeof zkey === 'string') {
     const st = fs.statSync(zkey);
     key = `file:${path.resolve(zkey)}:${st.size}:${st.mtimeMs}:${device}`;
   } else {
-    const buf = readBin(zkey);
-    let h = zkeyHashes.get(buf);
-    if (!h) zkeyHashes.set(buf, (h = crypto.createHash('sha256').update(buf).digest('hex')));
-    key = h + ':' + device;
+    key = contentHash(readBin(zkey)) + ':' + device;
   }
+  lanes = lanes || ENV_LANES;
   let c = contexts.get(key);
   if (!c) {
-    c = { ctx: typeof zkey === 'string' ? addon.createContextFile(zkey, device) : addon.createContext(readBin(zkey), device),
-          lanes: lanes || DEFAULT_LANES };
-    addon.setLanes(c.ctx, c.lanes);
+    const ctx = typeof zkey === 'string' ? addon.createContextFile(zkey, device) : addon.createContext(readBin(zkey), device);
+    try {
+      c = { ctx, lanes: lanes ? addon.setLanes(ctx, lanes) : setLanesFitting(ctx, DEFAULT_LANES) };
+    } catch (e) {
+      addon.releaseContext(ctx);  // its HBM now, not at garbage collection
+      throw e;
+    }
     contexts.set(key, c);
   } else if (lanes && lanes !== c.lanes) {
     // a change of lane count waits for the proofs in flight (it rebuilds the lane pool)
@@ -250,14 +282,19 @@ const programs = new Map();
 const programsByBuf = new WeakMap();
 function programFor(progBuf, device) {
   let byDev = programsByBuf.get(progBuf);
+  const probe = probeOf(progBuf);
+  if (byDev && byDev.probe !== probe) byDev = null;  // the Buffer now holds other contents
   if (byDev && byDev.has(device)) return byDev.get(device);
-  const key = crypto.createHash('sha256').update(progBuf).digest('hex') + ':' + device;
+  const key = contentHash(progBuf) + ':' + device;
   let p = programs.get(key);
   if (!p) {
     p = { handle: addon.createWitnessProgram(progBuf, device), meta: programInputs(progBuf) };
     programs.set(key, p);
   }
-  if (!byDev) programsByBuf.set(progBuf, (byDev = new Map()));
+  if (!byDev) {
+    programsByBuf.set(progBuf, (byDev = new Map()));
+    byDev.probe = probe;
+  }
   byDev.set(device, p);
   return p;
 }

@@ -628,10 +628,15 @@ class ProverContext:
         return {"proof": proof_to_json(proof), "publicSignals": public_to_json(pub, self.n_public)}
 
     def last_timings(self):
-        ms = (c_double * 9)()
-        k = self.lib.nzcb_ctx_last_timings(self.h, ms, 9)
-        names = ["total", "witness", "round1", "round2", "round3", "round4", "round5", "msm", "ntt"]
-        return dict(zip(names[:k], list(ms)[:k]))
+        """The last proof's phases in ms (include/nzcb.h nzcb_ctx_last_timings): host wall
+        clock per round, host time in the MSM calls and enqueueing transforms, and (with
+        kernel_stats on) the GPU time of the MSMs and of the transforms."""
+        ms = (c_double * 11)()
+        k = self.lib.nzcb_ctx_last_timings(self.h, ms, 11)
+        names = ["total", "witness", "round1", "round2", "round3", "round4", "round5", "msm_host_wait",
+                 "ntt_host_enqueue", "msm_gpu", "ntt_gpu"]
+        out = dict(zip(names[:k], list(ms)[:k]))
+        return {key: v for key, v in out.items() if v >= 0}
 
 
 class MsmTable:

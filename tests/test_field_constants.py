@@ -38,7 +38,7 @@ def test_field_h_params(struct, mod):
 
 
 @pytest.mark.parametrize("struct,mod,ks", [("Fq29", P_MOD, {"K2": 2, "K4": 4, "K6": 6, "K8": 8}),
-                                           ("Fr29", R_MOD, {"K2": 2})])
+                                           ("Fr29", R_MOD, {"K2": 2, "K4": 4})])
 def test_f29_params(struct, mod, ks):
     c = _struct_consts("f29.h", struct)
     assert _val(c["P"], 29) == mod and all(v < (1 << 29) for v in c["P"])
@@ -52,3 +52,12 @@ def test_f29_params(struct, mod, ks):
         assert _val(c["ONE"], 29) == (1 << 261) % mod
     if "C256" in c:
         assert _val(c["C256"], 29) == (1 << 256) % mod
+
+
+def test_fr29_shoup_constants():
+    """The NTT's Shoup products (f29.h mul_shoup, round 5): RP = 2^261 - r, NINV = -r^-1 mod
+    2^261, both as 9 normalized 29-bit limbs."""
+    c = _struct_consts("f29.h", "Fr29")
+    assert _val(c["RP"], 29) == (1 << 261) - R_MOD and all(v < (1 << 29) for v in c["RP"])
+    assert (_val(c["NINV"], 29) * R_MOD) % (1 << 261) == (1 << 261) - 1
+    assert all(v < (1 << 29) for v in c["NINV"])

@@ -326,6 +326,69 @@ const m = require('./');
 
 @needs_node
 @pytest.mark.gpu
+def test_node_reused_buffer_is_rehashed(tmp_path):
+    """contexts and witness programs are cached by Buffer identity; a Buffer whose
+    contents are replaced by another zkey of the same length (same circuit, other tau) must
+    not reuse the old context: each proof verifies under its own key and not the other."""
+    import nzcb
+    import wasm_tiny
+    r1cs, prog = wasm_tiny.mul_circuit()
+    z1 = nzcb.plonk_setup(r1cs, nzcb.ptau_synth(4, 0x1234567))
+    z2 = nzcb.plonk_setup(r1cs, nzcb.ptau_synth(4, 0x7654321))
+    assert len(z1) == len(z2) and z1 != z2
+    (tmp_path / "z1.zkey").write_bytes(z1)
+    (tmp_path / "z2.zkey").write_bytes(z2)
+    (tmp_path / "mul.wprog").write_bytes(prog)
+    script = f"""
+const m = require('./');
+const fs = require('fs');
+(async () => {{
+  const buf = Buffer.from(fs.readFileSync('{tmp_path}/z1.zkey'));
+  const p = fs.readFileSync('{tmp_path}/mul.wprog');
+  const r1 = await m.plonk.fullProve({{a: 3, b: 11}}, p, buf);
+  fs.readFileSync('{tmp_path}/z2.zkey').copy(buf);          // same Buffer, other zkey
+  const r2 = await m.plonk.fullProve({{a: 3, b: 11}}, p, buf);
+  const vk1 = await m.zKey.exportVerificationKey('{tmp_path}/z1.zkey');
+  const vk2 = await m.zKey.exportVerificationKey('{tmp_path}/z2.zkey');
+  console.log(JSON.stringify({{
+    v11: await m.plonk.verify(vk1, r1.publicSignals, r1.proof), v22: await m.plonk.verify(vk2, r2.publicSignals, r2.proof),
+    v12: await m.plonk.verify(vk1, r2.publicSignals, r2.proof)}}));
+}})().catch((e) => {{ console.error(e); process.exit(1); }});
+"""
+    d = json.loads(run_node(script))
+    assert d == {"v11": True, "v22": True, "v12": False}
+
+
+@needs_node
+@pytest.mark.gpu
+def test_node_full_prove_on_second_device(tmp_path):
+    """fullProve with {device: 1} keeps the witness program, its HBM buffers and the
+    context on device 1 (the per-call thread allocates on the program's device). Skipped
+    on a one-GPU box."""
+    import nzcb
+    import wasm_tiny
+    if nzcb.device_count() < 2:
+        pytest.skip("one GPU")
+    r1cs, prog = wasm_tiny.mul_circuit()
+    (tmp_path / "mul.zkey").write_bytes(nzcb.plonk_setup(r1cs, nzcb.ptau_synth(4, 0x1234567)))
+    (tmp_path / "mul.wprog").write_bytes(prog)
+    bl = b"".join((7 * i + 3 + (i << 200)).to_bytes(32, "little") for i in range(11)).hex()
+    script = f"""
+const m = require('./');
+(async () => {{
+  const bl = Buffer.from('{bl}', 'hex');
+  const z = '{tmp_path}/mul.zkey', p = '{tmp_path}/mul.wprog';
+  const d0 = await m.plonk.fullProve({{a: 3, b: 11}}, p, z, null, {{blinding: bl}});
+  const d1 = await m.plonk.fullProve({{a: 3, b: 11}}, p, z, null, {{blinding: bl, device: 1}});
+  console.log(JSON.stringify({{d0, d1}}));
+}})().catch((e) => {{ console.error(e); process.exit(1); }});
+"""
+    d = json.loads(run_node(script))
+    assert d["d0"] == d["d1"] and d["d1"]["publicSignals"] == ["33"]
+
+
+@needs_node
+@pytest.mark.gpu
 @pytest.mark.timeout(900)
 def test_node_full_prove_nzcp_live(tmp_path):
     """plonk.fullProve of the real nzcp_live circuit from Node: the test/nzcp.js-shaped input
