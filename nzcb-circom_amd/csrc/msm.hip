@@ -65,23 +65,6 @@ static uint32_t chunk_for(size_t entries) {
   while (entries / c > (size_t(1) << 20)) c *= 2;
   return c;
 }
-// Fixed base (round 5): entries per accumulation thread from the bucketed entry count M.
-// The grid is launched for the plan's bound (nthr = bound / chunk), and a sparse MSM (the
-// Lagrange-basis commitments of mostly small witness values: M ~ 7 % of the bound) spreads
-// its entries over the whole grid in chunks of at least kMinChunk instead of leaving 93 %
-// of it idle behind 48-long addition chains (round 4: 0.83 ms per commitment in round 1 of a
-// single proof). Random scalars keep chunk (M ~ the bound). Every kernel that maps entry
-// positions to chunks derives the same value from offsets[nkeys]; nthr = 0: chunk as given.
-static constexpr uint32_t kMinChunk = 8;
-#ifndef NZ_DYN_CHUNK
-#define NZ_DYN_CHUNK 1
-#endif
-__device__ __forceinline__ uint32_t fb_chunk(uint32_t chunk, uint32_t M, size_t nthr) {
-  if (!nthr || !NZ_DYN_CHUNK) return chunk;
-  uint32_t c = (uint32_t)(((size_t)M + nthr - 1) / nthr);
-  c = c < kMinChunk ? kMinChunk : c;
-  return c < chunk ? c : chunk;
-}
 static constexpr int kSegLen = 8;
 static constexpr int kSumThreads = 256;  // level-1 sums: block size
 static constexpr int kSumPer = 4;        // level-1 sums: sequential adds per thread
@@ -96,15 +79,17 @@ static constexpr int kLargeBlocks = 32;  // finalize: workgroups for the longer 
 // fixed base: workgroups over the pieces of the longer runs, and over their buckets (grid-
 // stride; random scalars list none, and under 5 proof lanes every launched workgroup waits
 // for a CU slot first, so the grids are kept small)
-static constexpr int kLargePieceBlocks = 256;
+static constexpr int kLargePieceBlocks = 128;
 static constexpr int kLargeFinalBlocks = 128;
 static constexpr int kLargeFinalThreads = 64;
 
-// Fixed-base window of the PTau tables: c = 17 bits (15 table rows, 2^16 buckets, 15
-// entries per random scalar). c = 20 (13 rows, 2^19 buckets) accumulates 9 % faster but its
-// bucketing and window sum cost more than that (profiles/r4_window_ab.txt);
-// NZCB_FB_WINDOW = 16..20 selects another for A/B runs.
-static constexpr int kFbWindow = 17;
+// Fixed-base window of the PTau tables: c = 20 bits (13 table rows, 2^19 buckets, 13
+// entries per random scalar) since round 5, when the window sum's first level became the
+// LDS-free strip kernel (msm_strips29_kernel): same box, bench.py --steps 200, 42.50 / 42.36
+// proofs/s at c = 20 against 41.45 / 41.23 at c = 17 (profiles/r5_window_ab.txt); until round 4
+// c = 17 (15 rows, 2^16 buckets) won, its 55 KB-LDS tile kernel at 2^19 buckets costing more
+// than the 13 % fewer entries saved. NZCB_FB_WINDOW = 16..20 selects another.
+static constexpr int kFbWindow = 20;
 int fixed_base_window() {
   static const int c = [] {
     const char* e = std::getenv("NZCB_FB_WINDOW");
@@ -648,19 +633,17 @@ __device__ __forceinline__ G1xyzz load_point(const Xyzz29& a) {
 static constexpr uint32_t kLdsStride = kMsmThreads + 1;  // slot-major rows, +1: conflict-free fill
 template <bool kLdsIdx>
 __global__ void __launch_bounds__(kMsmThreads) __attribute__((amdgpu_waves_per_eu(3, 8)))
-msm_accumulate29_kernel(uint32_t chunk_max, const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
+msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, const uint32_t* __restrict__ sorted,
                         const uint32_t* __restrict__ offsets, uint32_t nkeys, size_t nthreads,
                         Xyzz29* __restrict__ buckets, Xyzz29* __restrict__ carry_own,
                         Xyzz29* __restrict__ carry_cont) {
   __shared__ uint32_t sidx[kLdsIdx ? kChunk * kLdsStride : 1];
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t M = offsets[nkeys];
-  const uint32_t chunk = fb_chunk(chunk_max, M, nthreads);  // <= kChunk when kLdsIdx
   if (kLdsIdx) {  // every thread of the workgroup takes part before any exits
-    const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * chunk;
-    const uint32_t rcp = 0xFFFFFFFFu / chunk + 1u;  // j / chunk = umulhi(j, rcp) for j < 2^16
-    for (uint32_t j = threadIdx.x; j < kMsmThreads * chunk; j += kMsmThreads) {
-      const uint32_t thr = __umulhi(j, rcp), slot = j - thr * chunk;
+    const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * kChunk;
+    for (uint32_t j = threadIdx.x; j < kMsmThreads * kChunk; j += kMsmThreads) {
+      const uint32_t thr = j / kChunk, slot = j - thr * kChunk;
       sidx[slot * kLdsStride + thr] = wg0 + j < M ? sorted[wg0 + j] : 0u;
     }
     __syncthreads();
@@ -773,12 +756,11 @@ __device__ __forceinline__ G1xyzz sum_run(const G1xyzz* carry_own, const G1xyzz*
 // multi-chunk sums go into the accumulation's own bucket array out29, in radix 2^29.
 template <class P>
 __global__ void __launch_bounds__(kMsmThreads)
-msm_bucket_finalize_kernel(uint32_t chunk_max, size_t nthr, const uint32_t* __restrict__ offsets, uint32_t nkeys,
-                           uint32_t span, const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
+msm_bucket_finalize_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys, uint32_t span,
+                           const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
                            G1xyzz* __restrict__ buckets, uint32_t* __restrict__ large, Xyzz29* __restrict__ out29) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nkeys) return;
-  const uint32_t chunk = fb_chunk(chunk_max, offsets[nkeys], nthr);
   const uint32_t s = offsets[k], e = offsets[k + 1];
   if (e == s) return;
   const uint32_t c0 = s / chunk, c1 = (e - 1) / chunk;
@@ -901,10 +883,9 @@ __device__ __forceinline__ uint32_t carry_span(uint32_t chunk, const uint32_t* o
 
 // off[i] = pieces of the listed buckets before i, off[count] = all (one workgroup)
 __global__ void __launch_bounds__(1024)
-msm_large_scan_kernel(uint32_t chunk_max, size_t nthr, uint32_t nkeys, const uint32_t* __restrict__ offsets,
-                      const uint32_t* __restrict__ large, uint32_t* __restrict__ off) {
+msm_large_scan_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
+                      uint32_t* __restrict__ off) {
   __shared__ uint32_t sh[1024];
-  const uint32_t chunk = fb_chunk(chunk_max, offsets[nkeys], nthr);
   const uint32_t count = large[0];
   const uint32_t tid = threadIdx.x;
   const uint32_t per = (count + 1023u) / 1024u;
@@ -933,12 +914,10 @@ msm_large_scan_kernel(uint32_t chunk_max, size_t nthr, uint32_t nkeys, const uin
 }
 
 __global__ void __launch_bounds__(kSumThreads)
-msm_large_piece29_kernel(uint32_t chunk_max, size_t nthr, uint32_t nkeys, const uint32_t* __restrict__ offsets,
-                         const uint32_t* __restrict__ large, const uint32_t* __restrict__ off,
-                         const Xyzz29* __restrict__ carry_own, const Xyzz29* __restrict__ carry_cont,
-                         Xyzz29* __restrict__ part) {
+msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
+                         const uint32_t* __restrict__ off, const Xyzz29* __restrict__ carry_own,
+                         const Xyzz29* __restrict__ carry_cont, Xyzz29* __restrict__ part) {
   __shared__ Xyzz29 sh[kSumThreads];
-  const uint32_t chunk = fb_chunk(chunk_max, offsets[nkeys], nthr);
   const uint32_t count = large[0];
   const uint32_t total = off[count];
   for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
@@ -1513,15 +1492,15 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[4], st));
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
   if (table) {  // the large list's count was zeroed by msm_lo_scan_kernel
-    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, nthreads,
-                       sc.offsets.p, p.nkeys, kSeqSpan29, (const Xyzz29*)sc.carry_own29.p,
-                       (const Xyzz29*)sc.carry_cont29.p, (G1xyzz*)nullptr, sc.large.p, sc.buckets29.p);
+    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p,
+                       p.nkeys, kSeqSpan29, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p,
+                       (G1xyzz*)nullptr, sc.large.p, sc.buckets29.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, nthreads, p.nkeys, sc.offsets.p,
-                       sc.large.p, sc.large_off.p);
+    hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, sc.offsets.p, sc.large.p,
+                       sc.large_off.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_large_piece29_kernel, dim3(kLargePieceBlocks), dim3(kSumThreads), 0, st, chunk, nthreads,
-                       p.nkeys, sc.offsets.p, sc.large.p, sc.large_off.p, (const Xyzz29*)sc.carry_own29.p,
+    hipLaunchKernelGGL(msm_large_piece29_kernel, dim3(kLargePieceBlocks), dim3(kSumThreads), 0, st, chunk, sc.offsets.p,
+                       sc.large.p, sc.large_off.p, (const Xyzz29*)sc.carry_own29.p,
                        (const Xyzz29*)sc.carry_cont29.p, sc.large_part.p);
     NZ_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_large_final29_kernel, dim3(kLargeFinalBlocks), dim3(kLargeFinalThreads), 0, st, sc.large.p,
@@ -1557,8 +1536,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     return;
   }
   NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));
-  hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, chunk, (size_t)0,
-                     sc.offsets.p, p.nkeys,
+  hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
                      kSeqSpan, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p, sc.buckets.p, sc.large.p,
                      (Xyzz29*)nullptr);
   NZ_HIP(hipGetLastError());

@@ -19,10 +19,6 @@
 // twiddles), and stage 0's unit twiddles are skipped.
 #include "ntt.h"
 
-#ifndef NZ_NTT_SHOUP
-#define NZ_NTT_SHOUP 1  // Shoup twiddle products (round 5); 0 = the round-4 Montgomery products, A/B builds only
-#endif
-
 #include <vector>
 
 namespace nzcb {
@@ -72,13 +68,8 @@ __global__ void __launch_bounds__(256) ntt_tw29_kernel(NttTables::Tw* __restrict
 #pragma unroll
   for (int k = 0; k < 5; k++) m = m + m;
   NttTables::Tw t;
-#if NZ_NTT_SHOUP
   t.w = split29(from_mont(tw[i]));
   t.ws = mul_lo261(split29(m), f29_const(Fr29::NINV));
-#else
-  t.w = split29(m);  // the Montgomery-261 operand of mul29 (A/B builds)
-  t.ws = t.w;
-#endif
   out[i] = t;
 }
 
@@ -169,21 +160,11 @@ __device__ __forceinline__ F29 add_nn29(const F29& a, const F29& b) {
   for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + b.v[l];
   return r;
 }
-// the twiddle product (NZ_NTT_SHOUP=0: the round-4 Montgomery product, for A/B builds only)
-__device__ __forceinline__ F29 tw_mul(const F29& x, const NttTables::Tw& w) {
-#if NZ_NTT_SHOUP
-  return mul_shoup(x, w.w, w.ws);
-#else
-  return mul29<Fr29>(x, w.w);
-#endif
-}
+// twiddle products (Shoup, f29.h): one, and two interleaved
+__device__ __forceinline__ F29 tw_mul(const F29& x, const NttTables::Tw& w) { return mul_shoup(x, w.w, w.ws); }
 __device__ __forceinline__ void tw_mul2(const F29& x, const NttTables::Tw& w, const F29& y, const NttTables::Tw& v,
                                         F29& r1, F29& r2) {
-#if NZ_NTT_SHOUP
   mul_shoup_x2(x, w.w, w.ws, y, v.w, v.ws, r1, r2);
-#else
-  mul29x2<Fr29>(x, w.w, y, v.w, r1, r2);
-#endif
 }
 __device__ __forceinline__ F29 sub4r_nn29(const F29& a, const F29& b) {  // a + 4r - b, b < 3r normalized
   F29 r;
