@@ -21,6 +21,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 KERNEL = "msm_accumulate29"
+WINDOW = 20  # csrc/msm.hip kFbWindow
 
 
 def pmc_avg(path, counter, last=10):
@@ -56,11 +57,12 @@ def valu_by_kernel(path):
     return "\n".join(lines) + "\n"
 
 
-def acc_pmc(src):
-    """SQ / GRBM counters of the isolated accumulation (tools/acc_probe.py, two passes)."""
+def acc_pmc(src, ent):
+    """SQ / GRBM counters of the isolated accumulation (tools/acc_probe.py, two passes); ent =
+    the probe's bucket entries per launch (bench.py roofline.bucket_entries_per_launch)."""
     vals, lines = {}, ["# rocprofv3 --pmc (two passes) -- python3 nzcb-circom_amd/tools/acc_probe.py",
-                       "# fixed-base MSM alone, 2^21 + 6 points of random scalars, c = 17; "
-                       "msm_accumulate29_kernel<3, false, true, true>, averages over each pass's launches"]
+                       f"# fixed-base MSM alone, 2^21 + 6 points of random scalars, c = {WINDOW}; "
+                       "msm_accumulate29_kernel<true>, averages over each pass's launches"]
     for d in ("pmcA", "pmcB"):
         agg = {}
         for f in glob.glob(os.path.join(src, d, "**", "*counter_collection.csv"), recursive=True):
@@ -71,7 +73,6 @@ def acc_pmc(src):
         for k, v in sorted(agg.items()):
             vals[k] = sum(v) / len(v)
             lines.append(f"  {k:24s} launches {len(v)}  avg {vals[k]:.6g}")
-    ent = 31457085  # nonzero digits of the probe's 2^21 + 6 random scalars (15 per scalar)
     wc = vals["SQ_WAVE_CYCLES"]
     quad = 1024 * vals["GRBM_GUI_ACTIVE"] / 8 / 4
     lines += ["derived (SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles, MI355X_MICROARCH.md):",
@@ -116,9 +117,9 @@ def main():
     nw, write_kb = pmc_avg(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     fetch_raw = fetch_kb * 1024
     traffic = {
-        "kernel": "msm_accumulate29_kernel<3, false, true, true> (fixed-base bucket accumulation: LDS-staged "
-                  "indices, paired products; 2^21+6-point MSM of random scalars, c=17: bench.py's probe, the last 10 "
-                  "launches of each pass)",
+        "kernel": "msm_accumulate29_kernel<true> (fixed-base bucket accumulation: LDS-staged indices, paired "
+                  "products; 2^21+6-point MSM of random scalars at the default window, c = %d: bench.py's probe, the "
+                  "last 10 launches of each pass)" % WINDOW,
         "command": "rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE (separate passes) -- python3 bench.py "
                    "--no-cpu-baseline --steps 8",
         "counters_kb_per_launch": {"FETCH_SIZE": {"launches": nf, "avg_kb_per_launch": round(fetch_kb, 1)},
@@ -128,7 +129,9 @@ def main():
         "fetch_bytes_per_launch_raw": int(fetch_raw),
         "bytes_per_launch": int(fetch_raw + write_kb * 1024),
         "note": "gathers are random 64 B affine table points (16 B/lane dwordx4 loads); algorithmic bytes "
-                "96 B x 2^21 points = 201 MB; gathered table bytes 64 B x 31.5 M entries = 2.0 GB",
+                "96 B x 2^21 points = 201 MB; gathered table bytes 64 B x %.1f M entries = %.2f GB"
+                % (bench["roofline"]["bucket_entries_per_launch"] / 1e6,
+                   bench["roofline"]["bucket_entries_per_launch"] * 64 / 1e9),
     }
     with open(os.path.join(out, "accumulate_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
@@ -139,7 +142,7 @@ def main():
             f.write(valu_by_kernel(pv))
     if os.path.isdir(os.path.join(src, "pmcA")) and os.path.isdir(os.path.join(src, "pmcB")):
         with open(os.path.join(out, f"{a.prefix}_acc_pmc.txt"), "w") as f:
-            f.write(acc_pmc(src))
+            f.write(acc_pmc(src, bench["roofline"]["bucket_entries_per_launch"]))
     mb = os.path.join(src, "microbench.log")
     if os.path.exists(mb):
         shutil.copy(mb, os.path.join(out, f"{a.prefix}_microbench.txt"))
