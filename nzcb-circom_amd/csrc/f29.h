@@ -72,7 +72,10 @@ struct Fr29 {
 // compiler keeps each column one accumulation chain: left to itself it restarts every
 // column at 0 and adds the previous column's carry with an extra 64-bit add (about
 // 150 v_lshl_add_u64 per XYZZ addition). mad29c takes y from an SGPR (modulus limbs).
-#if defined(__HIP_DEVICE_COMPILE__)
+#ifndef NZ_MAD_ASM
+#define NZ_MAD_ASM 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && NZ_MAD_ASM
 __device__ __forceinline__ void mad29(uint64_t& acc, uint32_t x, uint32_t y) {
   asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(x), "v"(y) : "vcc");
 }
@@ -105,6 +108,17 @@ NZ_HD void mad29cx2(uint64_t& acc, uint32_t x, uint64_t& bcc, uint32_t u, uint32
 
 NZ_HD F29 f29_const(const uint32_t (&c)[9]);
 
+#ifndef NZ_MAD_COLS
+#define NZ_MAD_COLS 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && NZ_MAD_ASM && NZ_MAD_COLS
+#include "f29_cols.h"
+#define NZ_F29_COLS 1
+#else
+#define NZ_F29_COLS 0
+#endif
+
+
 // Shoup's product by a fixed factor (the NTT twiddles): w < r and ws = floor(w 2^261 / r),
 // both normalized; x < 2^261 with limbs < 2^30.6. q = floor(x ws / 2^261) from the product
 // columns 7..16 only (the dropped columns 0..6 sum to < 2^237, so q is off by at most 1 from
@@ -115,6 +129,12 @@ NZ_HD F29 f29_const(const uint32_t (&c)[9]);
 // A column of the low half is <= 9 (2^59.6 + 2^58) + 2^35 < 2^64, of x ws <= 9 2^59.6 + 2^35.
 template <int N>
 NZ_HD void mul_shoup_n(const F29 (&x)[N], const F29 (&w)[N], const F29 (&ws)[N], F29 (&out)[N]) {
+#if NZ_F29_COLS
+  if constexpr (N == 2) {
+    mul_shoup2_cols(x[0], w[0], ws[0], x[1], w[1], ws[1], out[0], out[1]);
+    return;
+  }
+#endif
   using Q = Fr29;
   uint32_t q[N][9];
   uint64_t acc[N];
@@ -203,6 +223,9 @@ NZ_HD F29 f29_const(const uint32_t (&c)[9]) {
 // a * b * 2^-261 mod p (see the invariants above); Q = Fq29 or Fr29
 template <class Q = Fq29>
 NZ_HD F29 mul29(const F29& a, const F29& b) {
+#if NZ_F29_COLS
+  return mul29_cols<Q>(a, b);
+#endif
   uint32_t m[9];
   F29 r;
   uint64_t acc = 0;
@@ -238,6 +261,9 @@ NZ_HD F29 mul29(const F29& a, const F29& b) {
 // while one chain waits on its previous mad
 template <class Q = Fr29>
 NZ_HD void mul29x2(const F29& a, const F29& b, const F29& c, const F29& d, F29& r1, F29& r2) {
+#if NZ_F29_COLS
+  mul29x2_cols<Q>(a, b, c, d, r1, r2);
+#else
   uint32_t m[9], n[9];
   uint64_t acc = 0, bcc = 0;
 #pragma unroll
@@ -268,6 +294,7 @@ NZ_HD void mul29x2(const F29& a, const F29& b, const F29& c, const F29& d, F29& 
   }
   r1.v[8] = (uint32_t)acc;
   r2.v[8] = (uint32_t)bcc;
+#endif
 }
 
 // a^2 * 2^-261 mod p: the cross products a_j a_k (j < k) once, against 2 a_k
@@ -307,6 +334,9 @@ NZ_HD F29 sqr29(const F29& a) {
 
 // sqr29 of two independent values, interleaved as mul29x2
 NZ_HD void sqr29x2(const F29& a, const F29& c, F29& r1, F29& r2) {
+#if NZ_F29_COLS
+  sqr29x2_cols(a, c, r1, r2);
+#else
   using Q = Fq29;
   uint32_t a2[9], c2[9], m[9], n[9];
 #pragma unroll
@@ -342,12 +372,16 @@ NZ_HD void sqr29x2(const F29& a, const F29& c, F29& r1, F29& r2) {
   }
   r1.v[8] = (uint32_t)acc;
   r2.v[8] = (uint32_t)bcc;
+#endif
 }
 
 // (a b + c d) * 2^-261 mod p with one Montgomery reduction. Needs every limb < 2^29
 // (normalized or product outputs: a column is <= 27 terms < 2^58) and a, b, c, d < 2^257
 // with a b + c d < 2^515; result < 2p for the operand sizes used (see msm.hip)
 NZ_HD F29 mul2sum29(const F29& a, const F29& b, const F29& c, const F29& d) {
+#if NZ_F29_COLS
+  return mul2sum29_cols(a, b, c, d);
+#else
   using Q = Fq29;
   uint32_t m[9];
   F29 r;
@@ -378,6 +412,7 @@ NZ_HD F29 mul2sum29(const F29& a, const F29& b, const F29& c, const F29& d) {
   }
   r.v[8] = (uint32_t)acc;
   return r;
+#endif
 }
 
 // sum_k a[k] b[k] * 2^-261 mod q with one Montgomery reduction (K <= 6 keeps a column
@@ -385,6 +420,13 @@ NZ_HD F29 mul2sum29(const F29& a, const F29& b, const F29& c, const F29& d) {
 // below 4q the result is below (0.1 K + 1) q < 2q for K <= 6 (q ~ 2^253.6).
 template <class Q, int K>
 NZ_HD F29 mulsum29(const F29 (&a)[K], const F29 (&b)[K]) {
+#if NZ_F29_COLS
+  if constexpr (K == 2) return mulsum29_cols2<Q>(a, b);
+  if constexpr (K == 3) return mulsum29_cols3<Q>(a, b);
+  if constexpr (K == 4) return mulsum29_cols4<Q>(a, b);
+  if constexpr (K == 5) return mulsum29_cols5<Q>(a, b);
+  if constexpr (K == 6) return mulsum29_cols6<Q>(a, b);
+#endif
   uint32_t m[9];
   F29 r;
   uint64_t acc = 0;

@@ -101,7 +101,10 @@ int fixed_base_window() {
 
 // the Lagrange-basis table's window: its small scalars make few entries, which do not pay
 // for a larger bucket set
-int lagrange_window() { return 17; }
+#ifndef NZ_LAGRANGE_WINDOW
+#define NZ_LAGRANGE_WINDOW 17
+#endif
+int lagrange_window() { return NZ_LAGRANGE_WINDOW; }
 
 int msm_window_bits(size_t n) {
   if (n >= (size_t(1) << 18)) return 16;
@@ -482,13 +485,19 @@ msm_lo_scan_kernel(const uint32_t* __restrict__ counts, uint32_t ntiles, uint32_
   if (hb == 0 && threadIdx.x == 0) large[0] = 0;                     // the finalize's count of long runs
 }
 
-template <int LO>
-__global__ void __launch_bounds__(kLoThreads)
+// c > 17 (LO = 11: 2048 buckets per high-byte region): 1024 threads ranking 16384-entry
+// chunks in LDS (122 KB, one workgroup per CU) instead of 512 x 8. A 4096-entry chunk left
+// runs of ~2 entries per bucket, so the coalesced write-out degenerated into 8-byte pieces;
+// at 16384 they average 8 entries (isolated 2^21 MSM at c = 20: lo pass 0.269 -> 0.179 ms,
+// profiles/r5_lo_scatter_ab.txt). Grouping a region's items on one XCD measured nothing.
+template <int LO, int NT = kLoThreads, uint32_t U = kLoU>
+__global__ void __launch_bounds__(NT)
 msm_lo_scatter_kernel(const typename std::conditional<LO <= 8, uint8_t, uint16_t>::type* __restrict__ lo2,
                       const uint32_t* __restrict__ vals2, const uint32_t* __restrict__ counts, uint32_t ntiles,
                       const uint32_t* __restrict__ segoff, uint32_t* __restrict__ sorted) {
   using Lo = typename std::conditional<LO <= 8, uint8_t, uint16_t>::type;
   constexpr uint32_t NL = 1u << LO;
+  constexpr uint32_t kLoThreads = NT, kLoU = U;
   __shared__ uint32_t h[NL], lcnt[NL], lst[NL];
   __shared__ uint32_t wsum[kLoThreads / 64], rs[256], rf[257];
   __shared__ uint32_t lv[kLoU * kLoThreads];
@@ -1399,7 +1408,9 @@ static void fixed_bucketing(MsmScratch& sc, const MsmPlan& p, const Fr* scalars,
     hipLaunchKernelGGL(msm_lo_scan_kernel<LO>, dim3(256), dim3(kLoThreads), 0, st, sc.bin_counts.p, ntiles,
                        sc.lo_seg.p, p.nkeys, sc.offsets.p, sc.large.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_lo_scatter_kernel<LO>, igrid, dim3(kLoThreads), 0, st, (const Lo*)lo2, sc.vals_mid.p,
+    constexpr int sNT = LO > 8 ? 1024 : kLoThreads;
+    constexpr uint32_t sU = LO > 8 ? 16 : kLoU;
+    hipLaunchKernelGGL((msm_lo_scatter_kernel<LO, sNT, sU>), igrid, dim3(sNT), 0, st, (const Lo*)lo2, sc.vals_mid.p,
                        sc.bin_counts.p, ntiles, (const uint32_t*)sc.lo_seg.p, sc.sorted.p);
     NZ_HIP(hipGetLastError());
   };
@@ -1567,6 +1578,33 @@ G1xyzz msm_finish(MsmScratch& sc, hipStream_t st) {
   // the window sums' copy, not the whole stream: work queued on the stream after the MSM
   // (the prover's A/B/C interpolations follow C's commitment on its stream) runs on
   NZ_HIP(hipEventSynchronize(sc.done));
+#ifdef NZCB_MSM_STATS
+  if (sc.cur_fixed) {  // scratch diagnostics build: carry spans of the buckets
+    std::vector<uint32_t> off(sc.cur_nkeys + 1);
+    NZ_HIP(hipMemcpy(off.data(), sc.offsets.p, off.size() * 4, hipMemcpyDeviceToHost));
+    uint32_t cnt = 0;
+    NZ_HIP(hipMemcpy(&cnt, sc.large.p, 4, hipMemcpyDeviceToHost));
+    uint32_t pieces = 0;
+    NZ_HIP(hipMemcpy(&pieces, sc.large_off.p + cnt, 4, hipMemcpyDeviceToHost));
+    const uint32_t M = off.back(), chunk = chunk_for(sc.cur_n * (size_t)num_windows(sc.cur_c));
+    size_t h[12] = {0};
+    uint32_t mx = 0;
+    uint64_t carries_large = 0, carries_mid = 0;
+    for (uint32_t k = 0; k < sc.cur_nkeys; k++) {
+      if (off[k + 1] == off[k]) { h[0]++; continue; }
+      const uint32_t sp = (off[k + 1] - 1) / chunk - off[k] / chunk + 1;
+      mx = sp > mx ? sp : mx;
+      int b = 1;
+      while (b < 11 && sp > (1u << (b - 1))) b++;
+      h[b]++;
+      if (sp > kSeqSpan29 + 1) carries_large += sp; else if (sp > 1) carries_mid += sp;
+    }
+    fprintf(stderr, "MSMSTATS n=%zu c=%d entries=%u chunk=%u large=%u pieces=%u maxspan=%u carries_mid=%llu "
+            "carries_large=%llu spans[empty,1,2,<=4,<=8,..,<=512,>512]=", sc.cur_n, sc.cur_c, M, chunk, cnt, pieces, mx,
+            (unsigned long long)carries_mid, (unsigned long long)carries_large);
+    for (int b = 0; b < 12; b++) fprintf(stderr, "%zu%c", h[b], b == 11 ? '\n' : ',');
+  }
+#endif
   const int c = sc.cur_c, nsets = sc.cur_nsets, nslots = sc.cur_nbits + 1;
   if (sc.prof) {
     float t = 0;

@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Generates csrc/f29_cols.h: the device bodies of the paired 9x29 products of csrc/f29.h
+(mul29x2, sqr29x2) and of mul2sum29 with one inline-asm statement per product column.
+
+The compiler puts an s_nop after every inline-asm statement; with one statement per mad
+pair (f29.h mad29x2) the bucket accumulation carried 1,646 of them per loop body against
+2,506 v_mad_u64_u32. Here a statement holds a whole column of both chains: the previous
+column's m_i * P_0 pair and carry shift, then every product term of the column, so a
+product pair pays 17 of them. The Montgomery quotient digits m_i and the result limbs
+(low 32 bits of an accumulator) stay C between the statements.
+
+    python3 tools/gen_f29_cols.py > csrc/f29_cols.h
+"""
+
+
+class Blk:
+    """One asm statement: the accumulators are operands 0 (and 1), inputs follow."""
+
+    def __init__(self, naccs):
+        self.naccs = naccs
+        self.ins = []      # (constraint, expr)
+        self.lines = []
+
+    def op(self, cons, expr):
+        key = (cons, expr)
+        if key not in self.ins:
+            self.ins.append(key)
+        return "%" + str(self.naccs + self.ins.index(key))
+
+    def mad(self, acc, x, y, ycons="v"):
+        self.lines.append(f"v_mad_u64_u32 %{acc}, vcc, {self.op('v', x)}, {self.op(ycons, y)}, %{acc}")
+
+    def shift(self, acc):
+        self.lines.append(f"v_lshrrev_b64 %{acc}, 29, %{acc}")
+
+    def emit(self, accs, ind="  "):
+        if not self.lines:
+            return []
+        outs = ", ".join(f'"+v"({a})' for a in accs)
+        ins = ", ".join(f'"{c}"({e})' for c, e in self.ins)
+        body = "\\n\\t".join(self.lines)
+        return [f'{ind}asm("{body}"', f"{ind}    : {outs}", f"{ind}    : {ins}", f'{ind}    : "vcc");']
+
+
+def write_product(name, sig, pairs, sq=None, Q="Q", template="template <class Q>", pre=()):
+    """pairs: per chain, a function i -> list of (x, y) product terms of column i."""
+    chains = ["acc", "bcc"][:len(pairs)]
+    ms = ["m", "n"][:len(pairs)]
+    out = [template] if template else []
+    out.append(f"__device__ __forceinline__ {sig} {{")
+    out += ["  " + p for p in pre]
+    out.append("  " + " ".join(f"uint32_t {m}[9];" for m in ms))
+    out.append("  " + " ".join(f"uint64_t {a} = 0;" for a in chains))
+    carry = []  # lines the next statement starts with: previous m_i P_0 and/or shifts
+    for i in range(17):
+        b = Blk(len(chains))
+        for kind, c, extra in carry:
+            if kind == "mp0":
+                b.mad(c, f"{ms[c]}[{extra}]", f"{Q}::P[0]", "s")
+            else:
+                b.shift(c)
+        carry = []
+        tl = [p(i) for p in pairs]
+        for k in range(max(len(t) for t in tl)):
+            for c in range(len(chains)):
+                if k < len(tl[c]):
+                    b.mad(c, *tl[c][k])
+        jr = range(0, i) if i < 9 else range(i - 8, 9)
+        for j in jr:
+            for c in range(len(chains)):
+                b.mad(c, f"{ms[c]}[{j}]", f"{Q}::P[{i - j}]", "s")
+        out += b.emit(chains)
+        if i < 9:
+            for c, a in enumerate(chains):
+                out.append(f"  {ms[c]}[{i}] = ((uint32_t){a} * {Q}::INV) & {Q}::MASK;")
+            carry = [("mp0", c, i) for c in range(len(chains))] + [("sh", c, None) for c in range(len(chains))]
+        else:
+            for c, a in enumerate(chains):
+                out.append(f"  r{c + 1}.v[{i - 9}] = (uint32_t){a} & {Q}::MASK;")
+            carry = [("sh", c, None) for c in range(len(chains))]
+    # final limb: the accumulator after the last shift
+    b = Blk(len(chains))
+    for c in range(len(chains)):
+        b.shift(c)
+    out += b.emit(chains)
+    for c, a in enumerate(chains):
+        out.append(f"  r{c + 1}.v[8] = (uint32_t){a};")
+    return out
+
+
+def write_shoup2():
+    """mul_shoup_n<2> (f29.h): q from columns 7..16 of x ws, then x w + q (2^261 - r) over
+    columns 0..8, both products side by side (chains acc / bcc)."""
+    out = ["__device__ __forceinline__ void mul_shoup2_cols(const F29& x0, const F29& w0, const F29& s0, "
+           "const F29& x1, const F29& w1, const F29& s1, F29& r1, F29& r2) {",
+           "  using Q = Fr29;",
+           "  uint32_t q0[9], q1[9];",
+           "  uint64_t acc = 0, bcc = 0;"]
+    xs, ws, ss, qs = ["x0", "x1"], ["w0", "w1"], ["s0", "s1"], ["q0", "q1"]
+    chains = ["acc", "bcc"]
+    pend_shift = False
+    for c in range(7, 17):
+        b = Blk(2)
+        if pend_shift:
+            b.shift(0)
+            b.shift(1)
+        for j in range(max(0, c - 8), min(c, 8) + 1):
+            for t in range(2):
+                b.mad(t, f"{xs[t]}.v[{j}]", f"{ss[t]}.v[{c - j}]")
+        if c < 9:
+            b.shift(0)
+            b.shift(1)
+            out += b.emit(chains)
+            pend_shift = False
+        else:
+            out += b.emit(chains)
+            for t in range(2):
+                out.append(f"  {qs[t]}[{c - 9}] = (uint32_t){chains[t]} & Q::MASK;")
+            pend_shift = True
+    b = Blk(2)
+    b.shift(0)
+    b.shift(1)
+    out += b.emit(chains)
+    out.append("  q0[8] = (uint32_t)acc;")
+    out.append("  q1[8] = (uint32_t)bcc;")
+    out.append("  acc = 0;")
+    out.append("  bcc = 0;")
+    pend_shift = False
+    for c in range(9):
+        b = Blk(2)
+        if pend_shift:
+            b.shift(0)
+            b.shift(1)
+        for j in range(c + 1):
+            for t in range(2):
+                b.mad(t, f"{xs[t]}.v[{j}]", f"{ws[t]}.v[{c - j}]")
+            for t in range(2):
+                b.mad(t, f"{qs[t]}[{j}]", f"Q::RP[{c - j}]", "s")
+        out += b.emit(chains)
+        for t in range(2):
+            out.append(f"  r{t + 1}.v[{c}] = (uint32_t){chains[t]} & Q::MASK;")
+        pend_shift = True
+    out.append("}")
+    return out
+
+
+def main():
+    L = ["// GENERATED by tools/gen_f29_cols.py from the column schedules of csrc/f29.h's",
+         "// mul29x2 / sqr29x2 / mul2sum29 / mul_shoup_n<2> / mul29 -- do not edit. One inline-asm statement per product",
+         "// column (see the generator's docstring); included by f29.h for the device compile.",
+         "#pragma once", ""]
+    mul = lambda a, b: (lambda i: [(f"{a}.v[{j}]", f"{b}.v[{i - j}]")
+                                   for j in range(max(0, i - 8), min(i, 8) + 1)])
+    L += write_product("mul29x2_cols", "void mul29x2_cols(const F29& a, const F29& b, const F29& c, const F29& d, "
+                       "F29& r1, F29& r2)", [mul("a", "b"), mul("c", "d")])
+    L.append("}")
+    L.append("")
+
+    def sq(a, a2):
+        def t(i):
+            r = [(f"{a}.v[{j}]", f"{a2}[{i - j}]") for j in range(max(0, i - 8), 9) if 2 * j < i]
+            if i % 2 == 0 and i // 2 <= 8:
+                r.append((f"{a}.v[{i // 2}]", f"{a}.v[{i // 2}]"))
+            return r
+        return t
+    L += write_product("sqr29x2_cols", "void sqr29x2_cols(const F29& a, const F29& c, F29& r1, F29& r2)",
+                       [sq("a", "a2"), sq("c", "c2")], Q="Fq29", template=None,
+                       pre=["uint32_t a2[9], c2[9];",
+                            "#pragma unroll",
+                            "for (int i = 0; i < 9; i++) {",
+                            "  a2[i] = a.v[i] << 1;",
+                            "  c2[i] = c.v[i] << 1;",
+                            "}"])
+    L.append("}")
+    L.append("")
+
+    def two(i):
+        r = []
+        for j in range(max(0, i - 8), min(i, 8) + 1):
+            r += [(f"a.v[{j}]", f"b.v[{i - j}]"), (f"c.v[{j}]", f"d.v[{i - j}]")]
+        return r
+    body = write_product("mul2sum29_cols", "F29 mul2sum29_cols(const F29& a, const F29& b, const F29& c, const F29& d)",
+                         [two], Q="Fq29", template=None)
+    body.insert(2, "  F29 r1;")
+    L += body
+    L.append("  return r1;")
+    L.append("}")
+    L.append("")
+    body = write_product("mul29_cols", "F29 mul29_cols(const F29& a, const F29& b)", [mul("a", "b")])
+    body.insert(3, "  F29 r1;")
+    L += body
+    L.append("  return r1;")
+    L.append("}")
+    L.append("")
+    L += write_shoup2()
+    L.append("")
+    for K in range(2, 7):  # mulsum29<Q, K> (sum of K products, one reduction)
+        def terms(i, K=K):
+            r = []
+            js = range(0, i + 1) if i < 9 else range(i - 8, 9)
+            for j in js:
+                r += [(f"a[{k}].v[{j}]", f"b[{k}].v[{i - j}]") for k in range(K)]
+            return r
+        body = write_product(f"mulsum29_cols{K}", f"F29 mulsum29_cols{K}(const F29 (&a)[{K}], const F29 (&b)[{K}])",
+                             [terms])
+        body.insert(3, "  F29 r1;")
+        L += body
+        L.append("  return r1;")
+        L.append("}")
+        L.append("")
+    print("\n".join(L))
+
+
+if __name__ == "__main__":
+    main()
