@@ -100,7 +100,8 @@ int fixed_base_window() {
 }
 
 // the Lagrange-basis table's window: its small scalars make few entries, which do not pay
-// for a larger bucket set
+// for a larger bucket set (round 5, same box: c = 20 here lost 1.2-1.5 % of the bench,
+// profiles/r5_chunk_key_lw20_ab.txt)
 #ifndef NZ_LAGRANGE_WINDOW
 #define NZ_LAGRANGE_WINDOW 17
 #endif
