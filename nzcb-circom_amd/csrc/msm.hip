@@ -759,16 +759,14 @@ __device__ __forceinline__ G1xyzz sum_run(const G1xyzz* carry_own, const G1xyzz*
   return v;
 }
 
-// Buckets whose entries span several accumulation chunks: owner chunk's carry plus the
-// continuation carries of the chunks the bucket spills into (thread per bucket); runs of
-// more than `span` carries go to the large list. P = G1xyzz (generic): every bucket
-// ends up in `buckets` (single-chunk ones already there); P = Xyzz29 (fixed base): the
-// multi-chunk sums go into the accumulation's own bucket array out29, in radix 2^29.
-template <class P>
+// Buckets whose entries span several accumulation chunks (generic schedule): owner chunk's
+// carry plus the continuation carries of the chunks the bucket spills into (thread per
+// bucket), into `buckets` (single-chunk ones are already there); runs of more than `span`
+// carries go to the large list.
 __global__ void __launch_bounds__(kMsmThreads)
 msm_bucket_finalize_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys, uint32_t span,
-                           const P* __restrict__ carry_own, const P* __restrict__ carry_cont,
-                           G1xyzz* __restrict__ buckets, uint32_t* __restrict__ large, Xyzz29* __restrict__ out29) {
+                           const G1xyzz* __restrict__ carry_own, const G1xyzz* __restrict__ carry_cont,
+                           G1xyzz* __restrict__ buckets, uint32_t* __restrict__ large) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nkeys) return;
   const uint32_t s = offsets[k], e = offsets[k + 1];
@@ -779,12 +777,54 @@ msm_bucket_finalize_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets,
     large[1 + atomicAdd(&large[0], 1u)] = (uint32_t)k;
     return;
   }
-  if constexpr (std::is_same<P, Xyzz29>::value) {
-    Xyzz29 v = carry_own[c0];
-    for (uint32_t u = c0 + 1; u <= c1; u++) v = add29(v, carry_cont[u]);
-    out29[k] = v;
-  } else {
-    buckets[k] = sum_run(carry_own, carry_cont, c0, c1);
+  buckets[k] = sum_run(carry_own, carry_cont, c0, c1);
+}
+
+// The fixed-base finalize (radix 2^29). Thread per bucket, as above, but a bucket's carries
+// past the first addition are not walked by its own lane: at c = 20 (~52 entries per bucket,
+// 48-entry chunks) ~92 % of the multi-chunk buckets need exactly one addition, and a wave
+// whose longest lane needed 2-6 ran that many rounds of additions for all 64 lanes. Every
+// lane does its first addition in one round; the workgroup's buckets with more park their
+// partial sum in place (out29) and their carry range in LDS (12 B each: the kernel keeps
+// the accumulation's LDS free), and the first waves finish them after a barrier (usually
+// one wave, one more round). Isolated 2^21 MSM: 0.149 -> 0.12 ms, VALU -34 %.
+__global__ void __launch_bounds__(kMsmThreads)
+msm_finalize29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys, uint32_t span,
+                      const Xyzz29* __restrict__ carry_own, const Xyzz29* __restrict__ carry_cont,
+                      uint32_t* __restrict__ large, Xyzz29* __restrict__ out29) {
+  __shared__ uint32_t pk[kMsmThreads], pu[kMsmThreads], pe[kMsmThreads];
+  __shared__ uint32_t cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t c0 = 0, c1 = 0;
+  bool mine = false;
+  if (k < nkeys) {
+    const uint32_t s = offsets[k], e = offsets[k + 1];
+    if (e != s) {
+      c0 = s / chunk;
+      c1 = (e - 1) / chunk;
+      if (c1 - c0 > span)  // long run (skewed digits): msm_large_*
+        large[1 + atomicAdd(&large[0], 1u)] = (uint32_t)k;
+      else
+        mine = c1 > c0;  // single-chunk buckets were stored by the accumulation
+    }
+  }
+  if (mine) {
+    out29[k] = add29(carry_own[c0], carry_cont[c0 + 1]);
+    if (c1 > c0 + 1) {
+      const uint32_t i = atomicAdd(&cnt, 1u);
+      pk[i] = (uint32_t)k;
+      pu[i] = c0 + 2;
+      pe[i] = c1;
+    }
+  }
+  __syncthreads();  // (workgroup-scope fence: the parked sums are visible to the finishing lanes)
+  if (threadIdx.x < cnt) {
+    const uint32_t kk = pk[threadIdx.x], u1 = pe[threadIdx.x];
+    Xyzz29 v = out29[kk];
+    for (uint32_t u = pu[threadIdx.x]; u <= u1; u++) v = add29(v, carry_cont[u]);
+    out29[kk] = v;
   }
 }
 
@@ -1504,9 +1544,9 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[4], st));
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
   if (table) {  // the large list's count was zeroed by msm_lo_scan_kernel
-    hipLaunchKernelGGL(msm_bucket_finalize_kernel<Xyzz29>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p,
-                       p.nkeys, kSeqSpan29, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p,
-                       (G1xyzz*)nullptr, sc.large.p, sc.buckets29.p);
+    hipLaunchKernelGGL(msm_finalize29_kernel, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
+                       kSeqSpan29, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p, sc.large.p,
+                       sc.buckets29.p);
     NZ_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, sc.offsets.p, sc.large.p,
                        sc.large_off.p);
@@ -1548,9 +1588,8 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     return;
   }
   NZ_HIP(hipMemsetAsync(sc.large.p, 0, sizeof(uint32_t), st));
-  hipLaunchKernelGGL(msm_bucket_finalize_kernel<G1xyzz>, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
-                     kSeqSpan, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p, sc.buckets.p, sc.large.p,
-                     (Xyzz29*)nullptr);
+  hipLaunchKernelGGL(msm_bucket_finalize_kernel, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
+                     kSeqSpan, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p, sc.buckets.p, sc.large.p);
   NZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(msm_bucket_large_kernel, dim3(kLargeBlocks), dim3(kSumThreads), 0, st, chunk, sc.offsets.p,
                      sc.large.p, (const G1xyzz*)sc.carry_own.p, (const G1xyzz*)sc.carry_cont.p, sc.buckets.p);

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Generates csrc/f29_cols.h: the device bodies of the paired 9x29 products of csrc/f29.h
-(mul29x2, sqr29x2) and of mul2sum29 with one inline-asm statement per product column.
+"""Generates csrc/f29_cols.h: the device bodies of csrc/f29.h's 9x29 products (mul29,
+mul29x2, sqr29x2, mul2sum29, mulsum29<K>, the Shoup pair) with one inline-asm statement per
+product column.
 
 The compiler puts an s_nop after every inline-asm statement; with one statement per mad
 pair (f29.h mad29x2) the bucket accumulation carried 1,646 of them per loop body against
@@ -44,8 +45,8 @@ class Blk:
 
 def write_product(name, sig, pairs, sq=None, Q="Q", template="template <class Q>", pre=()):
     """pairs: per chain, a function i -> list of (x, y) product terms of column i."""
-    chains = ["acc", "bcc"][:len(pairs)]
-    ms = ["m", "n"][:len(pairs)]
+    chains = ["acc", "bcc", "ccc"][:len(pairs)]
+    ms = ["m", "n", "o"][:len(pairs)]
     out = [template] if template else []
     out.append(f"__device__ __forceinline__ {sig} {{")
     out += ["  " + p for p in pre]
@@ -146,7 +147,7 @@ def write_shoup2():
 
 def main():
     L = ["// GENERATED by tools/gen_f29_cols.py from the column schedules of csrc/f29.h's",
-         "// mul29x2 / sqr29x2 / mul2sum29 / mul_shoup_n<2> / mul29 -- do not edit. One inline-asm statement per product",
+         "// mul29x2 / sqr29x2 / mul2sum29 / mul_shoup_n<2> / mul29 / mulsum29 -- do not edit. One inline-asm statement per product",
          "// column (see the generator's docstring); included by f29.h for the device compile.",
          "#pragma once", ""]
     mul = lambda a, b: (lambda i: [(f"{a}.v[{j}]", f"{b}.v[{i - j}]")
