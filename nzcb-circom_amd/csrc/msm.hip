@@ -648,7 +648,7 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
                         Xyzz29* __restrict__ buckets, Xyzz29* __restrict__ carry_own,
                         Xyzz29* __restrict__ carry_cont) {
   __shared__ uint32_t sidx[kLdsIdx ? kChunk * kLdsStride : 1];
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // < 2^32 (entries / chunk)
   const uint32_t M = offsets[nkeys];
   if (kLdsIdx) {  // every thread of the workgroup takes part before any exits
     const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * kChunk;

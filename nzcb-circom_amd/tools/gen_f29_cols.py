@@ -15,93 +15,112 @@ product pair pays 17 of them. The Montgomery quotient digits m_i and the result 
 
 
 class Blk:
-    """One asm statement: the accumulators are operands 0 (and 1), inputs follow."""
+    """One asm statement. Outputs: each chain's new accumulator value (operands 0..k-1,
+    early-clobber). Inputs: each chain's previous value (unless it starts at 0), then the
+    multiplicands. The first instruction of a chain reads the previous value and writes
+    the new one (v_mad_u64_u32 and v_lshrrev_b64 are three-address), so the previous value
+    stays readable after the statement: the C extraction of its low limb needs no copy."""
 
-    def __init__(self, naccs):
-        self.naccs = naccs
-        self.ins = []      # (constraint, expr)
+    def __init__(self, olds, news):
+        self.olds, self.news = olds, news  # per chain: previous value (None: starts at 0), new value
+        self.k = len(news)
+        self.ins = [("v", o) for o in olds if o is not None]
         self.lines = []
+        self.started = set()
 
     def op(self, cons, expr):
         key = (cons, expr)
         if key not in self.ins:
             self.ins.append(key)
-        return "%" + str(self.naccs + self.ins.index(key))
+        return "%" + str(self.k + self.ins.index(key))
 
-    def mad(self, acc, x, y, ycons="v"):
-        self.lines.append(f"v_mad_u64_u32 %{acc}, vcc, {self.op('v', x)}, {self.op(ycons, y)}, %{acc}")
+    def _src(self, c):
+        if c in self.started:
+            return f"%{c}"
+        self.started.add(c)
+        return "0" if self.olds[c] is None else self.op("v", self.olds[c])
 
-    def shift(self, acc):
-        self.lines.append(f"v_lshrrev_b64 %{acc}, 29, %{acc}")
+    def mad(self, c, x, y, ycons="v"):
+        xo, yo = self.op("v", x), self.op(ycons, y)
+        self.lines.append(f"v_mad_u64_u32 %{c}, vcc, {xo}, {yo}, {self._src(c)}")
 
-    def emit(self, accs, ind="  "):
-        if not self.lines:
-            return []
-        outs = ", ".join(f'"+v"({a})' for a in accs)
+    def shift(self, c):
+        self.lines.append(f"v_lshrrev_b64 %{c}, 29, {self._src(c)}")
+
+    def emit(self, ind="  "):
+        assert self.lines and len(self.started) == self.k
+        outs = ", ".join(f'"=&v"({a})' for a in self.news)
         ins = ", ".join(f'"{c}"({e})' for c, e in self.ins)
         body = "\\n\\t".join(self.lines)
         return [f'{ind}asm("{body}"', f"{ind}    : {outs}", f"{ind}    : {ins}", f'{ind}    : "vcc");']
 
 
+class Chains:
+    """Accumulator values, one C variable per statement and chain (acc0, acc1, ...)."""
+
+    def __init__(self, names):
+        self.names, self.cur, self.n, self.decl = names, [None] * len(names), 0, []
+
+    def block(self):
+        news = [f"{nm}{self.n}" for nm in self.names]
+        self.decl += news
+        b = Blk(list(self.cur), news)
+        self.cur = news
+        self.n += 1
+        return b
+
+
 def write_product(name, sig, pairs, sq=None, Q="Q", template="template <class Q>", pre=()):
     """pairs: per chain, a function i -> list of (x, y) product terms of column i."""
-    chains = ["acc", "bcc", "ccc"][:len(pairs)]
-    ms = ["m", "n", "o"][:len(pairs)]
-    out = [template] if template else []
-    out.append(f"__device__ __forceinline__ {sig} {{")
-    out += ["  " + p for p in pre]
-    out.append("  " + " ".join(f"uint32_t {m}[9];" for m in ms))
-    out.append("  " + " ".join(f"uint64_t {a} = 0;" for a in chains))
-    carry = []  # lines the next statement starts with: previous m_i P_0 and/or shifts
+    k = len(pairs)
+    ch = Chains(["acc", "bcc", "ccc"][:k])
+    ms = ["m", "n", "o"][:k]
+    body = []
+    carry = []  # what the next statement starts with: previous m_i P_0 and/or shifts
     for i in range(17):
-        b = Blk(len(chains))
+        b = ch.block()
         for kind, c, extra in carry:
             if kind == "mp0":
                 b.mad(c, f"{ms[c]}[{extra}]", f"{Q}::P[0]", "s")
             else:
                 b.shift(c)
-        carry = []
         tl = [p(i) for p in pairs]
-        for k in range(max(len(t) for t in tl)):
-            for c in range(len(chains)):
-                if k < len(tl[c]):
-                    b.mad(c, *tl[c][k])
+        for t in range(max(len(x) for x in tl)):
+            for c in range(k):
+                if t < len(tl[c]):
+                    b.mad(c, *tl[c][t])
         jr = range(0, i) if i < 9 else range(i - 8, 9)
         for j in jr:
-            for c in range(len(chains)):
+            for c in range(k):
                 b.mad(c, f"{ms[c]}[{j}]", f"{Q}::P[{i - j}]", "s")
-        out += b.emit(chains)
+        body += b.emit()
         if i < 9:
-            for c, a in enumerate(chains):
-                out.append(f"  {ms[c]}[{i}] = ((uint32_t){a} * {Q}::INV) & {Q}::MASK;")
-            carry = [("mp0", c, i) for c in range(len(chains))] + [("sh", c, None) for c in range(len(chains))]
+            for c in range(k):
+                body.append(f"  {ms[c]}[{i}] = ((uint32_t){ch.cur[c]} * {Q}::INV) & {Q}::MASK;")
+            carry = [("mp0", c, i) for c in range(k)] + [("sh", c, None) for c in range(k)]
         else:
-            for c, a in enumerate(chains):
-                out.append(f"  r{c + 1}.v[{i - 9}] = (uint32_t){a} & {Q}::MASK;")
-            carry = [("sh", c, None) for c in range(len(chains))]
-    # final limb: the accumulator after the last shift
-    b = Blk(len(chains))
-    for c in range(len(chains)):
-        b.shift(c)
-    out += b.emit(chains)
-    for c, a in enumerate(chains):
-        out.append(f"  r{c + 1}.v[8] = (uint32_t){a};")
-    return out
+            for c in range(k):
+                body.append(f"  r{c + 1}.v[{i - 9}] = (uint32_t){ch.cur[c]} & {Q}::MASK;")
+            carry = [("sh", c, None) for c in range(k)]
+    for c in range(k):  # the top limb: the last column's carry
+        body.append(f"  r{c + 1}.v[8] = (uint32_t)({ch.cur[c]} >> 29);")
+    out = [template] if template else []
+    out.append(f"__device__ __forceinline__ {sig} {{")
+    out += ["  " + p for p in pre]
+    out.append("  " + " ".join(f"uint32_t {m}[9];" for m in ms))
+    out.append("  uint64_t " + ", ".join(ch.decl) + ";")
+    return out + body
 
 
 def write_shoup2():
     """mul_shoup_n<2> (f29.h): q from columns 7..16 of x ws, then x w + q (2^261 - r) over
-    columns 0..8, both products side by side (chains acc / bcc)."""
-    out = ["__device__ __forceinline__ void mul_shoup2_cols(const F29& x0, const F29& w0, const F29& s0, "
-           "const F29& x1, const F29& w1, const F29& s1, F29& r1, F29& r2) {",
-           "  using Q = Fr29;",
-           "  uint32_t q0[9], q1[9];",
-           "  uint64_t acc = 0, bcc = 0;"]
+    columns 0..8, both products side by side."""
     xs, ws, ss, qs = ["x0", "x1"], ["w0", "w1"], ["s0", "s1"], ["q0", "q1"]
-    chains = ["acc", "bcc"]
+    ch = Chains(["acc", "bcc"])
+    body = []
     pend_shift = False
     for c in range(7, 17):
-        b = Blk(2)
+        b = ch.block()
         if pend_shift:
             b.shift(0)
             b.shift(1)
@@ -111,24 +130,19 @@ def write_shoup2():
         if c < 9:
             b.shift(0)
             b.shift(1)
-            out += b.emit(chains)
             pend_shift = False
         else:
-            out += b.emit(chains)
-            for t in range(2):
-                out.append(f"  {qs[t]}[{c - 9}] = (uint32_t){chains[t]} & Q::MASK;")
             pend_shift = True
-    b = Blk(2)
-    b.shift(0)
-    b.shift(1)
-    out += b.emit(chains)
-    out.append("  q0[8] = (uint32_t)acc;")
-    out.append("  q1[8] = (uint32_t)bcc;")
-    out.append("  acc = 0;")
-    out.append("  bcc = 0;")
+        body += b.emit()
+        if c >= 9:
+            for t in range(2):
+                body.append(f"  {qs[t]}[{c - 9}] = (uint32_t){ch.cur[t]} & Q::MASK;")
+    for t in range(2):
+        body.append(f"  {qs[t]}[8] = (uint32_t)({ch.cur[t]} >> 29);")
+    ch.cur = [None, None]  # the second product starts at 0
     pend_shift = False
     for c in range(9):
-        b = Blk(2)
+        b = ch.block()
         if pend_shift:
             b.shift(0)
             b.shift(1)
@@ -137,12 +151,16 @@ def write_shoup2():
                 b.mad(t, f"{xs[t]}.v[{j}]", f"{ws[t]}.v[{c - j}]")
             for t in range(2):
                 b.mad(t, f"{qs[t]}[{j}]", f"Q::RP[{c - j}]", "s")
-        out += b.emit(chains)
+        body += b.emit()
         for t in range(2):
-            out.append(f"  r{t + 1}.v[{c}] = (uint32_t){chains[t]} & Q::MASK;")
+            body.append(f"  r{t + 1}.v[{c}] = (uint32_t){ch.cur[t]} & Q::MASK;")
         pend_shift = True
-    out.append("}")
-    return out
+    out = ["__device__ __forceinline__ void mul_shoup2_cols(const F29& x0, const F29& w0, const F29& s0, "
+           "const F29& x1, const F29& w1, const F29& s1, F29& r1, F29& r2) {",
+           "  using Q = Fr29;",
+           "  uint32_t q0[9], q1[9];",
+           "  uint64_t " + ", ".join(ch.decl) + ";"]
+    return out + body + ["}"]
 
 
 def main():
@@ -182,13 +200,13 @@ def main():
         return r
     body = write_product("mul2sum29_cols", "F29 mul2sum29_cols(const F29& a, const F29& b, const F29& c, const F29& d)",
                          [two], Q="Fq29", template=None)
-    body.insert(2, "  F29 r1;")
+    body.insert(body.index("  uint32_t m[9];") + 1, "  F29 r1;")
     L += body
     L.append("  return r1;")
     L.append("}")
     L.append("")
     body = write_product("mul29_cols", "F29 mul29_cols(const F29& a, const F29& b)", [mul("a", "b")])
-    body.insert(3, "  F29 r1;")
+    body.insert(body.index("  uint32_t m[9];") + 1, "  F29 r1;")
     L += body
     L.append("  return r1;")
     L.append("}")
@@ -204,7 +222,7 @@ def main():
             return r
         body = write_product(f"mulsum29_cols{K}", f"F29 mulsum29_cols{K}(const F29 (&a)[{K}], const F29 (&b)[{K}])",
                              [terms])
-        body.insert(3, "  F29 r1;")
+        body.insert(body.index("  uint32_t m[9];") + 1, "  F29 r1;")
         L += body
         L.append("  return r1;")
         L.append("}")

@@ -34,11 +34,11 @@ def _asm_terms(body):
     stmts = []
     for m in re.finditer(r'asm\("(.*?)"\n\s*: (.*?)\n\s*: (.*?)\n\s*: "vcc"\);', body, re.S):
         lines, outs, ins = m.group(1).split("\\n\\t"), m.group(2), m.group(3)
-        naccs = outs.count('"+v"')
+        naccs = outs.count('"=&v"') + outs.count('"+v"')
         ops = re.findall(r'"[vs]"\(([^()]*(?:\([^()]*\))?[^()]*)\)', ins)
         mads = []
         for ln in lines:
-            mm = re.match(r"v_mad_u64_u32 %(\d+), vcc, %(\d+), %(\d+), %\d+", ln)
+            mm = re.match(r"v_mad_u64_u32 %(\d+), vcc, %(\d+), %(\d+), (?:%\d+|0)", ln)
             if mm:
                 mads.append((int(mm.group(1)), ops[int(mm.group(2)) - naccs], ops[int(mm.group(3)) - naccs]))
         stmts.append(mads)
