@@ -302,7 +302,10 @@ __device__ __forceinline__ Fr block_sum_excl_suffix(const Fr& v, Fr* sh, Fr& tot
 // Round 3 ran a batch inversion per 32-element chunk per thread (1.24 ms at 2^21, the
 // chunks 1 KB apart per lane, den / prefix arrays written and read back through HBM).
 #ifndef NZ_PERM_WAVES
-#define NZ_PERM_WAVES 3  // waves per SIMD the grand-product tile kernel is compiled for
+// waves per SIMD the grand-product tile kernel is compiled for: at 2 it takes 223 VGPRs and
+// no scratch, at 3 (168 VGPRs) it spilled 188 B; 394 against 404 us per launch in a
+// single-lane proof, same bench (profiles/r5_perm_waves_ab.txt)
+#define NZ_PERM_WAVES 2
 #endif
 // Every product runs in the 9x29 radix at exponent 261 (round 5; until round 4 the factors'
 // products and both scans were 8x32 products, 13 of them per element): the witness values
