@@ -619,6 +619,20 @@ NZ_HD Fr join_fr29(const F29& t) {
   }
   return reduce_once(r);
 }
+// normalized x < 128 r -> canonical Fr: q = floor(x_8 / (r_8 + 1)) <= x / r, x - q r < 2r
+// (ntt.hip's last pass, round 5's k_pol_r / k_pol_wxi)
+NZ_HD Fr canon_fr29(const F29& x) {
+  const uint32_t q = x.v[8] / (Fr29::P[8] + 1u);
+  F29 y;
+  int64_t carry = 0;
+#pragma unroll
+  for (int l = 0; l < 9; l++) {
+    const int64_t t = (int64_t)x.v[l] + carry - (int64_t)((uint64_t)q * Fr29::P[l]);
+    y.v[l] = l < 8 ? ((uint32_t)t & Fr29::MASK) : (uint32_t)t;
+    carry = t >> 29;
+  }
+  return join_fr29(y);
+}
 NZ_HD Fr mul_fr29(const Fr& a, const F29& w29) {
   return join_fr29(mul29<Fr29>(split29(a), w29));  // product < 2r, limbs < 2^29
 }

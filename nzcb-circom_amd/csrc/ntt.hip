@@ -172,18 +172,6 @@ __device__ __forceinline__ F29 sub4r_nn29(const F29& a, const F29& b) {  // a + 
   for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + Fr29::K4[l] - b.v[l];
   return r;
 }
-__device__ __forceinline__ Fr canon_fr29(const F29& x) {  // normalized x < 128 r -> canonical Fr
-  const uint32_t q = x.v[8] / (Fr29::P[8] + 1u);
-  F29 y;
-  int64_t carry = 0;
-#pragma unroll
-  for (int l = 0; l < 9; l++) {
-    const int64_t t = (int64_t)x.v[l] + carry - (int64_t)((uint64_t)q * Fr29::P[l]);
-    y.v[l] = l < 8 ? ((uint32_t)t & Fr29::MASK) : (uint32_t)t;
-    carry = t >> 29;
-  }
-  return join_fr29(y);
-}
 
 // One pass of stages [s, s+q) on tiles of (2^q rows) x (2^logC columns). IN29: values from
 // the F29 scratch (else the Fr input, first pass only); OUT29: values to the F29 scratch

@@ -797,20 +797,29 @@ __global__ void __launch_bounds__(kT) k_eval_multi(EvalSet es, const F29* __rest
     if (j < NP && k == 0) bpow[j] = f;
   }
   const size_t s = (size_t)blockIdx.x * kT * kEvalChunk2 + threadIdx.x;
-  Fr acc[NP];
+  // the Horner sums stay in the 9x29 radix (round 5: no canonical Fr round trip per step):
+  // acc < 3r with limbs < 2^30 -> mul29 by y < r gives < (3r r + 2^261 r) / 2^261 < 2r, plus
+  // the coefficient (< r) -> < 3r again
+  F29 acc[NP];
 #pragma unroll
-  for (int j = 0; j < NP; j++) acc[j] = Fr::zero();
+  for (int j = 0; j < NP; j++)
+#pragma unroll
+    for (int l = 0; l < 9; l++) acc[j].v[l] = 0;
   // from the top coefficient down: indices past a polynomial's length are its top ones, so
   // skipping them (acc still 0) is Horner over zeros
   for (int m = kEvalChunk2 - 1; m >= 0; m--) {
     const size_t i = s + (size_t)m * kT;
 #pragma unroll
     for (int j = 0; j < NP; j++)
-      if (i < es.len[j]) acc[j] = mul_fr29(acc[j], es.y29[j]) + es.p[j][i];
+      if (i < es.len[j]) {
+        const F29 t = mul29<Fr29>(acc[j], es.y29[j]), c = split29(es.p[j][i]);
+#pragma unroll
+        for (int l = 0; l < 9; l++) acc[j].v[l] = t.v[l] + c.v[l];
+      }
   }
 #pragma unroll
   for (int j = 0; j < NP; j++) {
-    const Fr r = block_sum_fr(mul_fr29(acc[j], pw[(size_t)j * kT + threadIdx.x]), sh);
+    const Fr r = block_sum_fr(join_fr29(mul29<Fr29>(acc[j], pw[(size_t)j * kT + threadIdx.x])), sh);
     if (threadIdx.x == 0) bsum[j] = r;
   }
   // (block_sum_fr's barriers made bpow visible) the point j's product in lane j

@@ -1,0 +1,30 @@
+#!/bin/bash
+# End-of-round check on one box (from the repo root, GPU box): the whole -m gpu suite, smoke(),
+# the default bench.py line, and one same-box pair against the previous round's library
+# (lib/ab/libnzcb_r4.so, built from round 4's last commit) at --steps 300.
+#   bash nzcb-circom_amd/tools/final_check.sh   -> gpurun_out/final/{pytest,smoke,bench,ab_*}.log
+# Each GPU step has its own time limit; the first failure ends the call.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/final; mkdir -p $O
+step() { echo "== $1 $(date +%T)"; }
+step pytest
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; tail -1 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+step smoke
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit $?
+tail -1 $O/smoke.log
+step bench
+timeout -k 10 600 python3 -u bench.py > $O/bench.log 2>&1 || exit $?
+grep '^{"metric"' $O/bench.log | tail -1 | cut -c1-400
+R4=nzcb-circom_amd/lib/ab/libnzcb_r4.so
+if [ -f $R4 ]; then
+  for cfg in r4 r5; do
+    L=nzcb-circom_amd/lib/libnzcb.so; [ $cfg = r4 ] && L=$R4
+    step "ab $cfg"
+    NZCB_LIB=$L timeout -k 10 300 python3 -u bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-probe > $O/ab_$cfg.log 2>&1 || exit $?
+    python3 -c "import json;d=json.loads([l for l in open('$O/ab_$cfg.log') if l.startswith('{')][-1]);print('$cfg', d['value'], d['ms_per_step'], d['single_proof_latency_ms'])"
+  done
+fi
+step done
