@@ -133,6 +133,9 @@ NZ_HD void mul_shoup_n(const F29 (&x)[N], const F29 (&w)[N], const F29 (&ws)[N],
   if constexpr (N == 2) {
     mul_shoup2_cols(x[0], w[0], ws[0], x[1], w[1], ws[1], out[0], out[1]);
     return;
+  } else if constexpr (N == 1) {
+    out[0] = mul_shoup1_cols(x[0], w[0], ws[0]);
+    return;
   }
 #endif
   using Q = Fr29;

@@ -108,10 +108,19 @@ __device__ __forceinline__ Fr root4(const Fr* __restrict__ lo, const Fr* __restr
 }
 
 struct PermArgs {
-  F29 beta266, k1beta266, k2beta266;  // beta, k1 beta, k2 beta at exponent 266 (x exponent 256 -> 261)
-  F29 gamma261;                       // gamma at exponent 261
-  int k23;                            // k1 = 2, k2 = 3 (snarkjs getK1K2 for BN254): k beta w by additions
+  F29 beta, beta_s;                      // Shoup pair of beta (mul_shoup: w, floor(w 2^261 / r))
+  F29 k1beta, k1beta_s, k2beta, k2beta_s;  // ... of k1 beta, k2 beta (read only when k23 == 0)
+  F29 gamma256;                          // gamma at exponent 256 (its Montgomery-256 form)
+  int k23;                               // k1 = 2, k2 = 3 (snarkjs getK1K2 for BN254): k beta w by additions
 };
+// Shoup pair (w, ws) of a Montgomery-256 constant c: w = c's canonical value, ws = floor(w
+// 2^261 / r) from m = w 2^261 mod r = c 2^5 mod r (as ntt.hip's ntt_tw29_kernel; host)
+static void shoup_pair(const Fr& c, F29& w, F29& ws) {
+  Fr m = c;
+  for (int k = 0; k < 5; k++) m = m + m;
+  w = split29(from_mont(c));
+  ws = mul_lo261(split29(m), f29_const(Fr29::NINV));
+}
 
 // c * 2^5 split into the 9x29 radix: the Montgomery-261 operand of mul_fr29 for a
 // Montgomery-256 constant c
@@ -135,7 +144,7 @@ static F29 fr29_operand(Fr c) {
 #define NZ_KPER 4
 #endif
 static constexpr int kPer = NZ_KPER;  // elements per thread in the tile scans
-static constexpr int kTileN = kT * kPer;                // 2048
+static constexpr int kTileN = kT * kPer;                // 1024
 static constexpr int kStageWords = kTileN * 8 + kTileN / 4;
 
 __device__ __forceinline__ int stage_word(int e) { return e * 8 + e / 4; }
@@ -207,11 +216,13 @@ __device__ __forceinline__ F29 shfl_fr(const F29& v, int src) {
 }
 struct MulOp {
   using T = Fr;
+  static constexpr bool kCheap = false;
   __device__ Fr operator()(const Fr& a, const Fr& b) const { return a * b; }
   __device__ static Fr id() { return Fr::one(); }
 };
 struct AddOp {
   using T = Fr;
+  static constexpr bool kCheap = true;
   __device__ Fr operator()(const Fr& a, const Fr& b) const { return a + b; }
   __device__ static Fr id() { return Fr::zero(); }
 };
@@ -219,13 +230,16 @@ struct AddOp {
 // exponent that a product of any number of factors keeps: mul29 takes 2^261 off)
 struct Mul29Op {
   using T = F29;
+  static constexpr bool kCheap = false;
   __device__ F29 operator()(const F29& a, const F29& b) const { return mul29<Fr29>(a, b); }
   __device__ static F29 id() { return f29_const(Fr29::ONE); }
 };
 // kSuffix = false: op of v_t' over t' < t; true: over t' > t, for the NT threads of the
 // workgroup. sh: >= NT / 64 entries. *total (when given) = op over all NT values, valid in
-// thread 0. Up to 4 waves the wave totals are combined directly (wave-uniform branches); past
-// that the first wave scans them by shuffles (k_perm_factors' 16 waves).
+// thread 0. Up to 4 waves an addition scan combines the wave totals directly (wave-uniform
+// branches: wave w applies w of them, thread 0 all for the total); a product scan, and any
+// scan past 4 waves, has the first wave scan them by shuffles and every wave apply one
+// (k_perm_tile's two scans: 12 instead of 15 wave-products per workgroup).
 template <bool kSuffix, class Op, int NT = kT>
 __device__ __forceinline__ typename Op::T block_scan_excl(const typename Op::T& v, typename Op::T* sh,
                                                           typename Op::T* total) {
@@ -245,7 +259,7 @@ __device__ __forceinline__ typename Op::T block_scan_excl(const typename Op::T& 
   if (kSuffix ? lane == 63 : lane == 0) ex = Op::id();
   if (kSuffix ? lane == 0 : lane == 63) sh[wv] = inc;  // the wave's total
   __syncthreads();
-  if constexpr (NW <= 4) {
+  if constexpr (NW <= 4 && Op::kCheap) {
 #pragma unroll
     for (int k = 0; k < NW; k++)  // wave-uniform: the other waves' totals on this side
       if (kSuffix ? k > wv : k < wv) ex = op(ex, sh[k]);
@@ -302,16 +316,33 @@ __device__ __forceinline__ Fr block_sum_excl_suffix(const Fr& v, Fr* sh, Fr& tot
 // Round 3 ran a batch inversion per 32-element chunk per thread (1.24 ms at 2^21, the
 // chunks 1 KB apart per lane, den / prefix arrays written and read back through HBM).
 #ifndef NZ_PERM_WAVES
-// waves per SIMD the grand-product tile kernel is compiled for: at 2 it takes 223 VGPRs and
-// no scratch, at 3 (168 VGPRs) it spilled 188 B; 394 against 404 us per launch in a
-// single-lane proof, same bench (profiles/r5_perm_waves_ab.txt)
+// waves per SIMD the grand-product tile kernel is compiled for: at 2 it takes 247 VGPRs and
+// no scratch; the exponent-261 form before it took 223 at 2 and spilled 188 B at 3 (168
+// VGPRs): 394 against 404 us per launch in a single-lane proof, same bench
+// (profiles/r5_perm_waves_ab.txt)
 #define NZ_PERM_WAVES 2
 #endif
-// Every product runs in the 9x29 radix at exponent 261 (round 5; until round 4 the factors'
-// products and both scans were 8x32 products, 13 of them per element): the witness values
-// and the sigmas are shifted to exponent 261 by fr_to261 or by their product with
-// beta 2^266, w^i comes from the per-context table w_h (no root-table product), and only
-// the outputs (Z, the tile totals) return to Montgomery-256.
+// Every product runs in the 9x29 radix (round 5; until round 4 the factors' products and both
+// scans were 8x32 products, 13 of them per element). The factors stay at exponent 256: x is
+// the witness value's Montgomery-256 form as it is, b s_k and k b w^i are Shoup products of
+// the Montgomery-256 sigma / w^i (table w_h) by the canonical beta, k beta, and gamma is
+// Montgomery-256. Each real element's num and den then carry the same 2^-15 against their
+// exponent-261 values (three factors at 256, two Montgomery products), and every quantity
+// the proof reads is a ratio with as many num as den factors: a local Z_i holds the tile's
+// num_k (k < i) and den_k (k >= i), one each per real element, its F_T the other tiles'
+// totals, and 1 / prod den the rest (prod num = prod den, the copy-constraint check, holds
+// with both sides scaled alike). Past n the factors are the exponent-261 one. Against the
+// exponent-261 factors (fr_to261 shifts, Montgomery products by beta 2^266) this drops three
+// limb shifts and four products' 28 reduction instructions each (Shoup), and the factors of
+// the k >= 1 columns feed their product unnormalized against the normalized num / den. Their
+// limbs: x + 2 b w + g < 4 2^29 (f29.h's one factor < 2^31), x + 3 b w + g < 5 2^29, one step
+// past it: a column of that product is <= 9 (5 2^29 2^29 + 2^58) + 2^35 < 2^63.8 < 2^64.
+__device__ __forceinline__ F29 add3_nn29(const F29& a, const F29& b, const F29& c) {  // unnormalized
+  F29 r;
+#pragma unroll
+  for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + b.v[l] + c.v[l];
+  return r;
+}
 __global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(NZ_PERM_WAVES, 8)))
 k_perm_tile(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __restrict__ C,
             const Fr* __restrict__ sig_h, size_t n, const Fr* __restrict__ w_h, PermArgs pa, Fr* __restrict__ Z,
@@ -321,54 +352,69 @@ k_perm_tile(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __rest
   const int tid = threadIdx.x;
   const size_t base = (size_t)blockIdx.x * kTileN;
   const size_t e0 = base + (size_t)kPer * tid;
-  const F29 beta266 = pa.beta266, gamma261 = pa.gamma261;  // no byval copy in scratch
+  const F29 beta = pa.beta, beta_s = pa.beta_s, gamma = pa.gamma256;  // no byval copy in scratch
   const bool k23 = pa.k23 != 0;
   F29 num[kPer], den[kPer], bw[kPer], bs[kPer];
 #pragma unroll 1
   for (int k = 0; k < 3; k++) {
-    // sigma_k first: bs = b s_k (exponent 261), for den *= x + b s_k + g below
+    // sigma_k first: bs = b s_k, for den *= x + b s_k + g below
     stage_use([&](size_t g) { return sig_h[(size_t)k * n + g]; }, base, n, stg,
-              [&](int j, const Fr& x) { bs[j] = mul29<Fr29>(split29(x), beta266); });
-    // witness column: num *= x + k b w + g (k b w: b w, 2 b w, 3 b w when k1, k2 = 2, 3, what
-    // snarkjs getK1K2 finds for BN254: bw[] keeps b w^i), den *= x + b s_k + g
-    const F29 kb = k == 0 ? beta266 : (k == 1 ? pa.k1beta266 : pa.k2beta266);
+              [&](int j, const Fr& x) { bs[j] = mul_shoup(split29(x), beta, beta_s); });
+    // k b w: b w, 2 b w, 3 b w when k1, k2 = 2, 3, what snarkjs getK1K2 finds for BN254 (bw[]
+    // keeps b w^i), else one Shoup product per column
+    if (k == 0 || !k23) {
+      const F29 kb = k == 0 ? beta : (k == 1 ? pa.k1beta : pa.k2beta);
+      const F29 kbs = k == 0 ? beta_s : (k == 1 ? pa.k1beta_s : pa.k2beta_s);
+#pragma unroll
+      for (int j = 0; j < kPer; j++) bw[j] = mul_shoup(split29(e0 + j < n ? w_h[e0 + j] : Fr::zero()), kb, kbs);
+    }
+    // witness column: num *= x + k b w + g, den *= x + b s_k + g
     const Fr* col = k == 0 ? A : B;
     if (k == 2) col = C;
     stage_use([&](size_t g) { return col[g]; }, base, n, stg,
               [&](int j, const Fr& x) {
-                F29 kbw;
-                if (k23 && k) {
-                  kbw = k == 1 ? add29(bw[j], bw[j]) : add3_29(bw[j], bw[j], bw[j]);
-                } else {
-                  kbw = mul29<Fr29>(split29(e0 + j < n ? w_h[e0 + j] : Fr::zero()), kb);
-                  if (k23) bw[j] = kbw;
+                F29 kbw = bw[j];  // < 3 r
+                if (k23 && k == 1) {  // 2 b w, 3 b w unnormalized: f's limbs < 4 2^29, 5 2^29 (below)
+#pragma unroll
+                  for (int l = 0; l < 9; l++) kbw.v[l] = bw[j].v[l] << 1;
+                } else if (k23 && k == 2) {
+#pragma unroll
+                  for (int l = 0; l < 9; l++) kbw.v[l] = (bw[j].v[l] << 1) + bw[j].v[l];
                 }
-                const F29 x261 = fr_to261(x);
-                const F29 f = add3_29(x261, kbw, gamma261);   // < 38 r
-                const F29 g = add3_29(x261, bs[j], gamma261);  // < 35 r
-                num[j] = k ? mul29<Fr29>(num[j], f) : f;
-                den[j] = k ? mul29<Fr29>(den[j], g) : g;
+                const F29 xs = split29(x);
+                if (k == 0) {
+                  num[j] = add3_29(xs, kbw, gamma);   // < 5 r, normalized (k >= 1: < 11 r)
+                  den[j] = add3_29(xs, bs[j], gamma);  // < 5 r
+                } else {
+                  num[j] = mul29<Fr29>(num[j], add3_nn29(xs, kbw, gamma));
+                  den[j] = mul29<Fr29>(den[j], add3_nn29(xs, bs[j], gamma));
+                }
               });
   }
   const F29 one = f29_const(Fr29::ONE);
 #pragma unroll
   for (int j = 0; j < kPer; j++)  // past n: factor 1
     if (e0 + j >= n) num[j] = den[j] = one;
-  // thread-local: bw = exclusive prefix of num, bs = inclusive suffix of den
-  bw[0] = one;
+  // thread-local: the product of num, bs = inclusive suffix of den; after the scans the
+  // prefix of num restarts from c, so each output is one product (15 products per thread
+  // against 17 with a stored prefix times c)
+  F29 ntl = num[0];
 #pragma unroll
-  for (int j = 1; j < kPer; j++) bw[j] = mul29<Fr29>(bw[j - 1], num[j - 1]);
+  for (int j = 1; j < kPer; j++) ntl = mul29<Fr29>(ntl, num[j]);
   bs[kPer - 1] = den[kPer - 1];
 #pragma unroll
   for (int j = kPer - 2; j >= 0; j--) bs[j] = mul29<Fr29>(bs[j + 1], den[j]);
   F29 nt;
-  const F29 np = block_scan_excl<false, Mul29Op>(mul29<Fr29>(bw[kPer - 1], num[kPer - 1]), sh, &nt);
+  const F29 np = block_scan_excl<false, Mul29Op>(ntl, sh, &nt);
   const F29 ds = block_scan_excl<true, Mul29Op>(bs[0], sh, nullptr);
   // c at exponent 256: the last product of each element lands in Montgomery-256
-  const F29 c = mul29<Fr29>(mul29<Fr29>(np, ds), f29_const(Fr29::C256));
+  F29 pre = mul29<Fr29>(mul29<Fr29>(np, ds), f29_const(Fr29::C256));
   Fr out[kPer];
 #pragma unroll
-  for (int j = 0; j < kPer; j++) out[j] = join_fr29(mul29<Fr29>(mul29<Fr29>(bw[j], bs[j]), c));
+  for (int j = 0; j < kPer; j++) {
+    out[j] = join_fr29(mul29<Fr29>(pre, bs[j]));
+    if (j + 1 < kPer) pre = mul29<Fr29>(pre, num[j]);
+  }
   stage_out(out, base, n, stg, Z);
   if (tid == 0) {
     ntot[blockIdx.x] = fr_from261(nt);
@@ -413,12 +459,17 @@ k_perm_factors(const Fr* __restrict__ ntot, const Fr* __restrict__ dtot, int nti
   }
 }
 
-// Z[i] *= F[i / kTileN] / prod D (coalesced)
+// Z[i] *= F[i / kTileN] / prod D (coalesced): one workgroup per tile, F_T / prod D once per
+// thread for its kPer elements (1 + 1 / kPer products per element instead of 2)
 __global__ void __launch_bounds__(kT)
 k_apply_tiles(Fr* __restrict__ x, size_t m, const Fr* __restrict__ F, Fr inv_d) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  x[i] = x[i] * (F[i / kTileN] * inv_d);
+  const Fr f = F[blockIdx.x] * inv_d;
+  const size_t base = (size_t)blockIdx.x * kTileN + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    const size_t i = base + (size_t)k * kT;
+    if (i < m) x[i] = x[i] * f;
+  }
 }
 
 // Round 5's divPol1: y_i = x_i + d y_{i+1} over i < m, x_i =
@@ -1856,8 +1907,12 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     lg("gamma: " + fr_dec(gamma));
   }
   {
-    PermArgs pa{f29_exp(beta, 10), f29_exp(k1 * beta, 10), f29_exp(k2 * beta, 10), f29_exp(gamma, 5),
-                k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0};
+    PermArgs pa;
+    shoup_pair(beta, pa.beta, pa.beta_s);
+    shoup_pair(k1 * beta, pa.k1beta, pa.k1beta_s);
+    shoup_pair(k2 * beta, pa.k2beta, pa.k2beta_s);
+    pa.gamma256 = f29_exp(gamma, 0);
+    pa.k23 = k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0;
     const size_t ntiles = (n + kTileN - 1) / kTileN;
     if (ntiles > 1024 * 64) throw Error(NZCB_ERR_INTERNAL, "round 2: domain too large for the tile factors");
     Fr* ntot = scan_tmp.p;  // per tile: numerator / denominator totals, then the factors F_T
@@ -1874,7 +1929,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     NZ_HIP(hipMemcpyAsync(tt, totals, sizeof(tt), hipMemcpyDeviceToHost, s));
     NZ_HIP(hipStreamSynchronize(s));
     if (tt[0] != tt[1]) throw Error(NZCB_ERR_COPY, "Copy constraints does not match");
-    hipLaunchKernelGGL(k_apply_tiles, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, Z.p, (size_t)n,
+    hipLaunchKernelGGL(k_apply_tiles, dim3((unsigned)ntiles), dim3(kT), 0, s, Z.p, (size_t)n,
                        (const Fr*)fac, inverse(tt[1]));
     NZ_HIP(hipGetLastError());
     const int bz[3] = {9, 8, 7};

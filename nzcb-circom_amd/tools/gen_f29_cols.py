@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Generates csrc/f29_cols.h: the device bodies of csrc/f29.h's 9x29 products (mul29,
-mul29x2, sqr29x2, mul2sum29, mulsum29<K>, the Shoup pair) with one inline-asm statement per
+mul29x2, sqr29x2, mul2sum29, mulsum29<K>, the Shoup pair and single) with one inline-asm statement per
 product column.
 
 The compiler puts an s_nop after every inline-asm statement; with one statement per mad
@@ -112,60 +112,65 @@ def write_product(name, sig, pairs, sq=None, Q="Q", template="template <class Q>
     return out + body
 
 
-def write_shoup2():
-    """mul_shoup_n<2> (f29.h): q from columns 7..16 of x ws, then x w + q (2^261 - r) over
-    columns 0..8, both products side by side."""
-    xs, ws, ss, qs = ["x0", "x1"], ["w0", "w1"], ["s0", "s1"], ["q0", "q1"]
-    ch = Chains(["acc", "bcc"])
+def write_shoup(k):
+    """mul_shoup_n<k> (f29.h), k = 1 or 2: q from columns 7..16 of x ws, then
+    x w + q (2^261 - r) over columns 0..8, the k products side by side."""
+    xs, ws, ss, qs = ["x0", "x1"][:k], ["w0", "w1"][:k], ["s0", "s1"][:k], ["q0", "q1"][:k]
+    T = range(k)
+    ch = Chains(["acc", "bcc"][:k])
     body = []
     pend_shift = False
     for c in range(7, 17):
         b = ch.block()
         if pend_shift:
-            b.shift(0)
-            b.shift(1)
+            for t in T:
+                b.shift(t)
         for j in range(max(0, c - 8), min(c, 8) + 1):
-            for t in range(2):
+            for t in T:
                 b.mad(t, f"{xs[t]}.v[{j}]", f"{ss[t]}.v[{c - j}]")
         if c < 9:
-            b.shift(0)
-            b.shift(1)
+            for t in T:
+                b.shift(t)
             pend_shift = False
         else:
             pend_shift = True
         body += b.emit()
         if c >= 9:
-            for t in range(2):
+            for t in T:
                 body.append(f"  {qs[t]}[{c - 9}] = (uint32_t){ch.cur[t]} & Q::MASK;")
-    for t in range(2):
+    for t in T:
         body.append(f"  {qs[t]}[8] = (uint32_t)({ch.cur[t]} >> 29);")
-    ch.cur = [None, None]  # the second product starts at 0
+    ch.cur = [None] * k  # the second product starts at 0
     pend_shift = False
     for c in range(9):
         b = ch.block()
         if pend_shift:
-            b.shift(0)
-            b.shift(1)
+            for t in T:
+                b.shift(t)
         for j in range(c + 1):
-            for t in range(2):
+            for t in T:
                 b.mad(t, f"{xs[t]}.v[{j}]", f"{ws[t]}.v[{c - j}]")
-            for t in range(2):
+            for t in T:
                 b.mad(t, f"{qs[t]}[{j}]", f"Q::RP[{c - j}]", "s")
         body += b.emit()
-        for t in range(2):
+        for t in T:
             body.append(f"  r{t + 1}.v[{c}] = (uint32_t){ch.cur[t]} & Q::MASK;")
         pend_shift = True
-    out = ["__device__ __forceinline__ void mul_shoup2_cols(const F29& x0, const F29& w0, const F29& s0, "
-           "const F29& x1, const F29& w1, const F29& s1, F29& r1, F29& r2) {",
-           "  using Q = Fr29;",
-           "  uint32_t q0[9], q1[9];",
-           "  uint64_t " + ", ".join(ch.decl) + ";"]
-    return out + body + ["}"]
+    if k == 2:
+        out = ["__device__ __forceinline__ void mul_shoup2_cols(const F29& x0, const F29& w0, const F29& s0, "
+               "const F29& x1, const F29& w1, const F29& s1, F29& r1, F29& r2) {"]
+    else:
+        out = ["__device__ __forceinline__ F29 mul_shoup1_cols(const F29& x0, const F29& w0, const F29& s0) {",
+               "  F29 r1;"]
+    out += ["  using Q = Fr29;",
+            "  " + " ".join(f"uint32_t {q}[9];" for q in qs),
+            "  uint64_t " + ", ".join(ch.decl) + ";"]
+    return out + body + (["  return r1;"] if k == 1 else []) + ["}"]
 
 
 def main():
     L = ["// GENERATED by tools/gen_f29_cols.py from the column schedules of csrc/f29.h's",
-         "// mul29x2 / sqr29x2 / mul2sum29 / mul_shoup_n<2> / mul29 / mulsum29 -- do not edit. One inline-asm statement per product",
+         "// mul29x2 / sqr29x2 / mul2sum29 / mul_shoup_n<2> / mul_shoup_n<1> / mul29 / mulsum29 -- do not edit. One inline-asm statement per product",
          "// column (see the generator's docstring); included by f29.h for the device compile.",
          "#pragma once", ""]
     mul = lambda a, b: (lambda i: [(f"{a}.v[{j}]", f"{b}.v[{i - j}]")
@@ -211,7 +216,9 @@ def main():
     L.append("  return r1;")
     L.append("}")
     L.append("")
-    L += write_shoup2()
+    L += write_shoup(2)
+    L.append("")
+    L += write_shoup(1)
     L.append("")
     for K in range(2, 7):  # mulsum29<Q, K> (sum of K products, one reduction)
         def terms(i, K=K):
