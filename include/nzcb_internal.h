@@ -32,6 +32,11 @@ int nzcb_debug_guard_selftest(int device, nzcb_err* err);
  * the xi check must report as NZCB_ERR_INTERNAL "quotient check failed". One-shot per
  * lane; kind 0 clears it. */
 #define NZCB_FAULT_QUOTIENT 1
+/* Not a fault: kind NZCB_DEBUG_GENERIC_K makes the next proof's grand product form
+ * k1 beta w^i and k2 beta w^i by their own Shoup products (the path for k1, k2 other than
+ * snarkjs' 2, 3) instead of 2 beta w^i and 3 beta w^i by additions; the proof must be the
+ * same. One-shot per lane, like the fault. */
+#define NZCB_DEBUG_GENERIC_K 2
 int nzcb_debug_inject_fault(nzcb_ctx* ctx, int kind);
 
 /* ---- Synthetic circuit + setup ------- */

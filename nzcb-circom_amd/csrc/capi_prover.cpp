@@ -507,7 +507,7 @@ int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
 }
 
 int nzcb_debug_inject_fault(nzcb_ctx* ctx, int kind) {
-  if (!ctx || (kind != 0 && kind != NZCB_FAULT_QUOTIENT)) return NZCB_ERR_ARG;
+  if (!ctx || (kind != 0 && kind != NZCB_FAULT_QUOTIENT && kind != NZCB_DEBUG_GENERIC_K)) return NZCB_ERR_ARG;
   std::unique_lock<std::shared_mutex> lk(ctx->cfg);
   for (Prover* q : ctx->all()) q->fault = kind;
   return 0;

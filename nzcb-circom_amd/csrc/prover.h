@@ -105,7 +105,7 @@ struct Prover {
   Fr* top_host = nullptr;
   static constexpr int kTopWords = 4 * 6 + 1;
 
-  int fault = 0;  // nzcb_debug_inject_fault: NZCB_FAULT_* for this lane's next proof
+  int fault = 0;  // nzcb_debug_inject_fault: NZCB_FAULT_* / NZCB_DEBUG_* for this lane's next proof
   // timings of the last proof (ms): [0..6] host wall clock of the whole proof and its
   // phases, [7] host time in the MSM calls (enqueue + waiting for results), [8] host time
   // enqueueing transforms, and with kernel statistics on (prof_gpu) the GPU time of [9] the

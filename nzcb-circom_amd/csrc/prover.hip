@@ -1913,6 +1913,10 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     shoup_pair(k2 * beta, pa.k2beta, pa.k2beta_s);
     pa.gamma256 = f29_exp(gamma, 0);
     pa.k23 = k1 == fr_small(2) && k2 == fr_small(3) ? 1 : 0;
+    if (fault == NZCB_DEBUG_GENERIC_K) {  // nzcb_debug_inject_fault: the k1, k2 products path, once
+      fault = 0;
+      pa.k23 = 0;
+    }
     const size_t ntiles = (n + kTileN - 1) / kTileN;
     if (ntiles > 1024 * 64) throw Error(NZCB_ERR_INTERNAL, "round 2: domain too large for the tile factors");
     Fr* ntot = scan_tmp.p;  // per tile: numerator / denominator totals, then the factors F_T

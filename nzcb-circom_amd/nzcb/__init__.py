@@ -48,6 +48,7 @@ EXPORTED_SYMBOLS = [
 ]
 
 NZCB_FAULT_QUOTIENT = 1  # include/nzcb_internal.h
+NZCB_DEBUG_GENERIC_K = 2  # include/nzcb_internal.h
 
 
 def guard_check(device: int = -1) -> int:
@@ -612,7 +613,9 @@ class ProverContext:
                 for i in range(count)]
 
     def inject_fault(self, kind: int = NZCB_FAULT_QUOTIENT) -> None:
-        """The next proof on each lane perturbs its quotient t (tests of the xi check)."""
+        """The next proof on each lane perturbs its quotient t (NZCB_FAULT_QUOTIENT: tests of
+        the xi check) or takes the grand product's generic k1, k2 path (NZCB_DEBUG_GENERIC_K:
+        the same proof); 0 clears it."""
         if self.lib.nzcb_debug_inject_fault(self.h, kind) != 0:
             raise ValueError(f"bad fault kind {kind}")
 

@@ -332,6 +332,26 @@ def test_quotient_fault_is_caught_then_proves_again(name):
         ctx.close()
 
 
+@pytest.mark.parametrize("name", ["p5", "p8"])
+def test_grand_product_generic_k_path_same_proof(name):
+    """k_perm_tile forms k1 beta w^i and k2 beta w^i by their own Shoup products when k1, k2
+    are not snarkjs' 2, 3 (prover.hip, round 2); nzcb_debug_inject_fault(NZCB_DEBUG_GENERIC_K)
+    forces that path for one proof, which must still be the golden proof bit for bit, and so
+    must the next one (one-shot)."""
+    meta, zkey, wtns = _gold(name)
+    exp = meta["proofs"]["fixed"]
+    bl = bytes.fromhex(exp["blinding"])
+    ctx = nzcb.ProverContext(zkey)
+    try:
+        ctx.inject_fault(nzcb.NZCB_DEBUG_GENERIC_K)
+        proof, _ = ctx.prove_raw(wtns, bl)
+        assert proof.hex() == exp["proof_bin"]
+        proof, _ = ctx.prove_raw(wtns, bl)
+        assert proof.hex() == exp["proof_bin"]
+    finally:
+        ctx.close()
+
+
 def test_guard_words_selftest_and_lane_buffers():
     """The guard words behind every context buffer (common.h GuardScope): a one-word
     overrun past a fresh guarded buffer is found, and after proofs on 3 lanes and a lane
