@@ -180,6 +180,19 @@ def spawn_ranks(gpus: int, argv) -> int:
     return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
+def build_once(dist, rank: int, build):
+    """The nzcp_live r1cs / witness program (nzcplive.build, cached on disk by source hash):
+    rank 0 builds (or reads) it first while the other ranks wait at a barrier, so that on a
+    cold cache 8 ranks do not each spend the generator's minutes and 8x its host memory; the
+    others then read the cache rank 0 wrote."""
+    if dist is not None and rank != 0:
+        dist.barrier()
+    out = build()
+    if dist is not None and rank == 0:
+        dist.barrier()
+    return out
+
+
 def launch_check(world: int, rank: int, device: int, backend: str, dist) -> None:
     """--launch-check: the launcher's decision without a proof. Every rank reports its rank
     and device to rank 0, which prints one JSON line with n_gpus = dist's world size."""
@@ -261,7 +274,7 @@ def main():
     # the real statement: NZCPPubIdentity(1, 351, 0, 4, 2, 4) compiled to an r1cs and a
     # witness program (nzcb/nzcpgen.py), zkey from nzcb_plonk_setup against a seeded
     # ptau of the reference's power 21 (Makefile:59-62)
-    r1cs, program, _ = nzcplive.build()
+    r1cs, program, _ = build_once(dist, rank, nzcplive.build)
     ctx, zkey_raw = nzcplive.context(r1cs, TAU, device)
     setup_s = time.time() - t_setup
     n = ctx.domain_size
@@ -311,15 +324,22 @@ def main():
         from nzcb import msmsplit
         comm = msmsplit.Comm(dist, f"cuda:{device}" if backend == "nccl" else "cpu")
         args.lanes = 1
+        # A, B, C too, over ranges of the n + 2-point Lagrange basis (round 6; all 9 commitments)
+        n_lag = n + 2 if nzcb.lagrange_commit_enabled() else 0
         if rank == 0:
-            root = msmsplit.SplitRoot(comm, n + 6)
+            root = msmsplit.SplitRoot(comm, n + 6, n_lagrange=n_lag)
             root.install(ctx)
         else:
             addr, size = msmsplit.zkey_section(zkey_raw[0], zkey_raw[1], 14)   # PTau [tau^i]G1
             dev_ptau = nzcb.dev_alloc(size)
             nzcb.memcpy_h2d_ptr(dev_ptau, addr, size)
             lo, hi = msmsplit.point_ranges(n + 6, world)[rank]
-            backend_range = (msmsplit.GpuRange(dev_ptau, lo, hi, device), dev_ptau)
+            lag = None
+            if n_lag:   # this rank's range of the Lagrange basis, from the PTau (1.4 s at 2^21)
+                llo, lhi = msmsplit.point_ranges(n_lag, world)[rank]
+                lag = msmsplit.GpuRange(dev_ptau, llo, lhi, device, lagrange=True, ptau_n=size // 64,
+                                        log_n=n.bit_length() - 1)
+            backend_range = (msmsplit.GpuRange(dev_ptau, lo, hi, device), dev_ptau, lag)
     ctx.set_lanes(args.lanes)
     if split:
         mine = list(range(args.steps)) if rank == 0 else []
@@ -331,7 +351,7 @@ def main():
         """The step loop of this rank: proofs (and, in split mode, the STOP that ends the
         servers' loop), or serving rank 0's commitments."""
         if split and rank != 0:
-            msmsplit.serve(comm, backend_range[0], n + 6)
+            msmsplit.serve(comm, backend_range[0], n + 6, n_lag, backend_range[2])
             return []
         res = prover.full_prove_staged(count_or_none, blindings) if count_or_none else []
         if root is not None:
@@ -359,6 +379,8 @@ def main():
         ctx.set_msm_split(1, 0, None, None)
     if backend_range is not None:
         backend_range[0].close()
+        if backend_range[2] is not None:
+            backend_range[2].close()
         nzcb.dev_free(backend_range[1])
     assert len({p for p, _ in proofs}) == len(mine)  # distinct passes -> distinct proofs
     # full-size checks outside the timed region: every proof's public signals equal its
@@ -409,11 +431,15 @@ def main():
             except Exception as e:  # reported, never silently replaced
                 cpu = {"value": None, "unit": "proofs/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
         proof_gbs = PROOF_BYTES_PER_N * n / (ms_step / 1e3) / 1e9
+        # ranks sharing a device (the one-GPU rehearsal, NZCB_BENCH_DEVICE) are not that many
+        # GPUs: n_gpus counts distinct devices and the line says it is a rehearsal
+        n_devices = len(set(rank_devices))
         line = {
             "metric": METRIC,
             "value": round(value, 4),
             "unit": "proofs/s",
-            "n_gpus": world,
+            "n_gpus": n_devices,
+            "n_ranks": world,
             "steps": steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
@@ -472,6 +498,7 @@ def main():
                 "achieved_GBs": round(proof_gbs, 2),
                 "frac": round(proof_gbs / HBM_PEAK_GBS, 5),
             },
+            "rehearsal": n_devices != world,
             "proofs_verified": verified,
             "witness_program_ms_per_batch": round(witness_ms, 3),
             "single_proof_latency_ms": round(latency_ms, 3),

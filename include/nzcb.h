@@ -135,27 +135,35 @@ int nzcb_ctx_lanes(const nzcb_ctx* ctx);
 
 /* Single-proof mode across GPUs: every commitment MSM of lane 0
  * is split by point range over devices[0..ndev) (devices[0] = the context's device); each
- * other device holds the shifted-base table of its PTau range, receives its scalar slice
- * by a peer copy over xGMI and returns one 96-byte partial, which the host adds. ndev = 1
- * restores the single-device schedule. Results are bit-identical either way. */
+ * other device holds the shifted-base tables of its PTau range and of its range of the n + 2
+ * Lagrange-basis points (A, B, C's commitments, when the context commits them in that basis),
+ * receives its scalar slice by a peer copy over xGMI and returns one partial, which the host
+ * adds. ndev = 1 restores the single-device schedule. Results are bit-identical either way. */
 int nzcb_ctx_set_msm_devices(nzcb_ctx* ctx, const int* devices, int ndev, nzcb_err* err);
 
-/* The same split across processes, one rank per GPU (scalars by
- * RCCL broadcast, one 64-byte partial per rank back by all-gather; the collectives live in
- * the host runtime, e.g. torch.distributed, see nzcb/msmsplit.py). The context (rank 0)
- * computes PTau points [0, own_points) of every commitment of lane 0 and calls
+/* The same split across processes, one rank per GPU (each rank's
+ * slice of the scalars by RCCL scatter, one 64-byte partial per rank back by gather; the
+ * collectives live in the host runtime, e.g. torch.distributed, see nzcb/msmsplit.py). The
+ * context (rank 0) computes PTau points [0, own_points) of every commitment of lane 0 and,
+ * when own_lagrange > 0, Lagrange-basis points [0, own_lagrange) of A, B and C's commitments
+ * (own_lagrange = 0 keeps those three whole on this rank), and calls
  *   send(user, slot, dev_scalars, count): the commitment's `count` scalars (32-byte
  *       Montgomery Fr, HBM of the context's device) are ready; the other ranks take the
- *       points [own_points, count) of it; called when the commitment starts
+ *       points [own, count) of it; called when the commitment starts. `slot` carries
+ *       NZCB_MSM_LAGRANGE when the commitment is over the Lagrange basis (the n + 2 points
+ *       [L_k(tau)] for k < n, [tau^n] - [1], [tau^(n+1)] - [tau]; a serving rank's table of
+ *       its range comes from nzcb_msm_table_create_lagrange) rather than PTau
  *   gather(user, slot, own_partial, partials_out): returns world x 64 bytes, every rank's
  *       partial sum (affine x || y, 32-byte LE normal form, infinity = zeros) in rank
- *       order (own_partial at index 0); called when the commitment is needed
- * Up to 3 commitments (slot 0..2) are in flight at once. A callback returning non-zero
- * fails the proof. world = 1 or NULL callbacks restore the local schedule. */
+ *       order (own_partial at index 0); called when the commitment is needed, with the
+ *       same slot value as its send
+ * Up to 3 commitments (slot & 0xff = 0..2) are in flight at once. A callback returning
+ * non-zero fails the proof. world = 1 or NULL callbacks restore the local schedule. */
+#define NZCB_MSM_LAGRANGE 0x100
 typedef int (*nzcb_msm_send_fn)(void* user, int slot, const void* dev_scalars, size_t count);
 typedef int (*nzcb_msm_gather_fn)(void* user, int slot, const uint8_t* own_partial, uint8_t* partials_out);
-int nzcb_ctx_set_msm_split(nzcb_ctx* ctx, int world, size_t own_points, nzcb_msm_send_fn send,
-                           nzcb_msm_gather_fn gather, void* user, nzcb_err* err);
+int nzcb_ctx_set_msm_split(nzcb_ctx* ctx, int world, size_t own_points, size_t own_lagrange,
+                           nzcb_msm_send_fn send, nzcb_msm_gather_fn gather, void* user, nzcb_err* err);
 
 /* `count` independent proofs over the context's lanes (SURVEY.md §8b nzcb_prove_batch,
  * §8e batch mode). witnesses[i]: nWitness x 32-byte LE normal-form values, host memory,
@@ -339,12 +347,20 @@ int nzcb_memcpy_d2d_async(void* dst, const void* src, size_t bytes, void* stream
 
 /* ---- Serving side of nzcb_ctx_set_msm_split (one per serving rank) ---------------- */
 /* A resident fixed-base MSM table over n device bases (affine LEM, e.g. a PTau range),
- * the prover's c = 17 shifted-base schedule: the serving ranks of nzcb_ctx_set_msm_split
+ * the prover's shifted-base schedule for PTau (c = 20): the serving ranks of nzcb_ctx_set_msm_split
  * keep one and answer every commitment with one run. out_affine: 64 bytes, x || y normal
  * form LE (infinity = zeros); scalars: `count` <= n 32-byte values in HBM, Montgomery
  * form when scalars_mont (the prover's coefficients). */
 typedef struct nzcb_msm_table nzcb_msm_table;
 nzcb_msm_table* nzcb_msm_table_create(int device, const void* dev_bases, size_t n, nzcb_err* err);
+/* The serving side of the Lagrange-basis commitments (NZCB_MSM_LAGRANGE): the points [lo, hi)
+ * of the n + 2-point Lagrange basis of a 2^log_n domain ([L_k(tau)] for k < n, then
+ * [tau^n] - [1], [tau^(n+1)] - [tau]), computed on `device` from its PTau (ptau_n >= n + 2
+ * affine LEM points in HBM, e.g. a zkey's section 14) by the elliptic-curve inverse NTT the
+ * prover runs at context creation, and kept as a table of the Lagrange window and its
+ * schedule for small scalars. Scalars passed to nzcb_msm_table_run are the range's slice. */
+nzcb_msm_table* nzcb_msm_table_create_lagrange(int device, const void* dev_ptau, size_t ptau_n, int log_n, size_t lo,
+                                               size_t hi, nzcb_err* err);
 int nzcb_msm_table_run(nzcb_msm_table* t, const void* dev_scalars, size_t count, int scalars_mont,
                        uint8_t* out_affine, nzcb_err* err);
 void nzcb_msm_table_destroy(nzcb_msm_table* t);

@@ -14,7 +14,8 @@ extern "C" {
 
 /* HIP-event timing of the MSM bucket-accumulation kernel (the dominant kernel):
  * out = {total ms, launches, MSM points, bucket entries} accumulated since the last
- * reset; enable = 1 / 0 turns timing on / off and resets, -1 only reads. Timing adds no
+ * reset; enable = 1 / 0 turns timing on / off and resets (waiting for the proofs in flight),
+ * -1 only reads (without waiting: the totals may include a proof in flight). Timing adds no
  * host synchronisation (the entry count is copied with the MSM's window sums). */
 int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]);
 
@@ -27,15 +28,16 @@ int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]);
 int nzcb_debug_guard_check(int device, size_t* checked, int* damaged, nzcb_err* err);
 int nzcb_debug_guard_selftest(int device, nzcb_err* err);
 
-/* Fault injection (tests of the prover's own checks): the next proof on each lane of ctx
- * perturbs its quotient t after round 3 (kind NZCB_FAULT_QUOTIENT: t[1] += 1), which
- * the xi check must report as NZCB_ERR_INTERNAL "quotient check failed". One-shot per
- * lane; kind 0 clears it. */
+/* Fault injection (tests of the prover's own checks): the context's next proof, whichever
+ * lane takes it, perturbs its quotient t after round 3 (kind NZCB_FAULT_QUOTIENT: t[1] += 1),
+ * which the xi check must report as NZCB_ERR_INTERNAL "quotient check failed". One-shot per
+ * context (until round 5 per lane: the lanes that did not take it stayed armed); kind 0
+ * clears it. */
 #define NZCB_FAULT_QUOTIENT 1
 /* Not a fault: kind NZCB_DEBUG_GENERIC_K makes the next proof's grand product form
  * k1 beta w^i and k2 beta w^i by their own Shoup products (the path for k1, k2 other than
  * snarkjs' 2, 3) instead of 2 beta w^i and 3 beta w^i by additions; the proof must be the
- * same. One-shot per lane, like the fault. */
+ * same. One-shot per context, like the fault. */
 #define NZCB_DEBUG_GENERIC_K 2
 int nzcb_debug_inject_fault(nzcb_ctx* ctx, int kind);
 
@@ -85,17 +87,23 @@ int nzcb_engine_lagrange_basis(nzcb_engine* e, const void* dev_ptau, size_t ptau
 int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont, int reps,
                          double* ms, double* acc_ms, nzcb_err* err);
 /* Fixed-base schedule (the prover's): builds the shifted-base table of the first
- * n_table bases (c = 17 by default: 2^(17w) multiples, 15 rows), then runs the MSM of the first n.
- * One-shot (table and scratch freed on return); for parity tests. */
+ * n_table bases (the PTau tables' window, c = 20 by default: 2^(20w) multiples, 13 rows), then
+ * runs the MSM of the first n. One-shot (table and scratch freed on return); for parity tests. */
 int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
                               int scalars_mont, uint8_t* out_affine, nzcb_err* err);
+/* The same with the table's window (16..20, 0 = the PTau tables' default) and schedule:
+ * sparse = 1 is the Lagrange-basis table's (device-derived accumulation chunk, log-depth
+ * carry trees; msm.hip dyn_chunk). */
+int nzcb_engine_msm_table_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
+                              int scalars_mont, int window, int sparse, uint8_t* out_affine, nzcb_err* err);
 /* Per-phase MSM timing (HIP events, average over reps after three warm-up runs):
  * out[0] wall ms, out[1..7] keys, sort, offsets, accumulate, finalize, reduce, sums,
  * out[8] table build ms (fixed_base only), out[9] bucket entries per MSM (nonzero digits),
  * out[10] host ms per MSM from the device results' arrival to the affine result (the
  * window combination on the CPU: the Horner over the window slots), out[11] host ms of the
  * enqueue (kernel launches), out[12] of which the library radix sort's host call (generic
- * schedule). out holds 13 doubles. */
+ * schedule). out holds 13 doubles. fixed_base: 0 generic, 1 the PTau tables' schedule, 2 the
+ * Lagrange table's (window 17, sparse), 3 window 17 with the dense schedule. */
 int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
                           int fixed_base, int reps, double* out, nzcb_err* err);
 /* Field self-test helpers: out[i] = a[i] * b[i] (Montgomery, device), n elements. */

@@ -326,12 +326,19 @@ int nzcb_engine_time_msm(nzcb_engine* e, const void* bases, const void* scalars,
 
 int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
                               int scalars_mont, uint8_t* out_affine, nzcb_err* err) {
+  return nzcb_engine_msm_table_dev(e, bases, n_table, scalars, n, scalars_mont, 0, 0, out_affine, err);
+}
+
+int nzcb_engine_msm_table_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
+                              int scalars_mont, int window, int sparse, uint8_t* out_affine, nzcb_err* err) {
   NZ_GUARD_BEGIN
   Engine& g = e->eng;
   NZ_HIP(hipSetDevice(g.device));
   if (n > n_table) throw Error(NZCB_ERR_ARG, "msm larger than its base table");
+  if (window && (window < 16 || window > 20)) throw Error(NZCB_ERR_ARG, "msm table window: 16..20");
   MsmBaseTable t;
-  t.build((const G1Affine*)bases, n_table, fixed_base_window(), g.stream);
+  t.build((const G1Affine*)bases, n_table, window ? window : fixed_base_window(), g.stream);
+  t.sparse = sparse != 0;
   MsmScratch sc;
   sc.init(n ? n : 1, true);
   G1xyzz r = msm(sc, (const G1Affine*)bases, (const Fr*)scalars, n, scalars_mont != 0, g.stream, &t);
@@ -349,10 +356,11 @@ int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars
   std::unique_ptr<MsmScratch> own;
   MsmScratch* sc = &g.msm_scratch;
   double table_ms = 0;
-  if (fixed_base) {
+  if (fixed_base) {  // 2: the Lagrange table's schedule (window 17, sparse); 3: window 17, dense schedule
     auto t0 = std::chrono::steady_clock::now();
     t.reset(new MsmBaseTable());
-    t->build((const G1Affine*)bases, n, fixed_base_window(), g.stream);
+    t->build((const G1Affine*)bases, n, fixed_base >= 2 ? lagrange_window() : fixed_base_window(), g.stream);
+    t->sparse = fixed_base == 2;
     NZ_HIP(hipStreamSynchronize(g.stream));
     table_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     own.reset(new MsmScratch());
@@ -433,6 +441,40 @@ nzcb_msm_table* nzcb_msm_table_create(int device, const void* dev_bases, size_t 
       t->table.build((const G1Affine*)dev_bases, n, fixed_base_window(), t->st);
       t->sc.init(n, true);
       NZ_HIP(hipStreamSynchronize(t->st));
+    } catch (...) {
+      delete t;
+      throw;
+    }
+    return t;
+  } catch (const Error& e) {
+    set_err(err, e.code, e.what());
+  } catch (const std::exception& e) {
+    set_err(err, NZCB_ERR_INTERNAL, e.what());
+  }
+  return nullptr;
+}
+
+nzcb_msm_table* nzcb_msm_table_create_lagrange(int device, const void* dev_ptau, size_t ptau_n, int log_n, size_t lo,
+                                               size_t hi, nzcb_err* err) {
+  try {
+    if (!dev_ptau || log_n < 1 || log_n > 28) throw Error(NZCB_ERR_ARG, "lagrange table: bad PTau or domain");
+    const size_t nl = ((size_t)1 << log_n) + 2;
+    if (ptau_n < nl) throw Error(NZCB_ERR_ARG, "lagrange table: fewer than n + 2 PTau points");
+    if (lo >= hi || hi > nl) throw Error(NZCB_ERR_ARG, "lagrange table: bad point range");
+    NZ_HIP(hipSetDevice(device));
+    auto t = new nzcb_msm_table();
+    try {
+      t->device = device;
+      t->n = hi - lo;
+      NZ_HIP(hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking));
+      {  // the whole basis (the inverse NTT needs every point), then the range's table
+        DevBuf<G1Affine> basis(nl);
+        lagrange_basis((const G1Affine*)dev_ptau, ptau_n, log_n, basis.p, t->st);
+        t->table.build(basis.p + lo, hi - lo, lagrange_window(), t->st);
+        t->table.sparse = true;
+        NZ_HIP(hipStreamSynchronize(t->st));
+      }
+      t->sc.init(hi - lo, true);
     } catch (...) {
       delete t;
       throw;

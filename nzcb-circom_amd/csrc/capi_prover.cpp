@@ -60,6 +60,9 @@ struct nzcb_ctx {
   std::condition_variable pool_cv;
   std::vector<Prover*> idle;  // lanes not proving; rebuilt by reset_pool (cfg held exclusively)
   double last_tm[11] = {0};   // phases of the last finished proof (nzcb_ctx_last_timings)
+  // nzcb_debug_inject_fault: armed for the context's next proof, whichever lane takes it (a
+  // per-lane flag left the other lanes of a multi-lane context armed)
+  std::atomic<int> pending_fault{0};
   Prover* lane(size_t i) { return i == 0 ? p.get() : extra[i - 1].get(); }
   size_t lanes() const { return 1 + extra.size(); }  // per device
   // every lane of every device (batch workers), device-interleaved so that a short batch
@@ -100,6 +103,7 @@ struct nzcb_ctx {
       q->log = [fn, user](const std::string& m) { fn(user, m.c_str()); };
     else
       q->log = nullptr;
+    q->fault = pending_fault.exchange(0);
     return q;
   }
   void release(Prover* q) {
@@ -266,6 +270,14 @@ int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err) {
       trim(std::min(before, ctx->lanes()));
       ctx->reset_pool();
       (void)hipSetDevice(ctx->p->eng->device);
+      // the failed hipMalloc's error stays in HIP's per-thread last error until it is read:
+      // the next NZ_HIP(hipGetLastError()) on this thread (a retried growth's NTT tables, a
+      // proof) would otherwise fail with it
+      for (size_t d = 0; d <= ctx->dev_p.size(); d++) {
+        (void)hipSetDevice(d ? ctx->dev_p[d - 1]->eng->device : ctx->p->eng->device);
+        (void)hipGetLastError();
+      }
+      (void)hipSetDevice(ctx->p->eng->device);
       throw;
     }
     ctx->reset_pool();
@@ -296,12 +308,12 @@ int nzcb_ctx_set_msm_devices(nzcb_ctx* ctx, const int* devices, int ndev, nzcb_e
   }
 }
 
-int nzcb_ctx_set_msm_split(nzcb_ctx* ctx, int world, size_t own_points, nzcb_msm_send_fn send,
-                           nzcb_msm_gather_fn gather, void* user, nzcb_err* err) {
+int nzcb_ctx_set_msm_split(nzcb_ctx* ctx, int world, size_t own_points, size_t own_lagrange,
+                           nzcb_msm_send_fn send, nzcb_msm_gather_fn gather, void* user, nzcb_err* err) {
   if (!ctx || world < 1 || world > 1024) return fail(err, NZCB_ERR_ARG, "msm split: world must be in 1..1024");
   try {
     std::unique_lock<std::shared_mutex> lk(ctx->cfg);
-    ctx->p->set_msm_split(world, own_points, send, gather, user);
+    ctx->p->set_msm_split(world, own_points, own_lagrange, send, gather, user);
     ctx->reset_pool();
     if (err) err->code = 0;
     return 0;
@@ -480,9 +492,14 @@ int nzcb_ctx_last_timings(const nzcb_ctx* ctx, double* ms, int cap) {
 
 int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
   if (!ctx) return NZCB_ERR_ARG;
-  // exclusive: no proof is between msm_enqueue and msm_finish while `prof` flips (ADVICE
-  // r4: finish would time events that enqueue never recorded), and no set_lanes runs
-  std::unique_lock<std::shared_mutex> lk(ctx->cfg);
+  // switching: exclusive, so no proof is between msm_enqueue and msm_finish while `prof`
+  // flips (finish would time events that enqueue never recorded), and no
+  // set_lanes runs. A read-only query (enable < 0) takes the lock shared: it neither waits
+  // behind the proofs in flight nor deadlocks when called from a proof's log callback
+  // (ADVICE r5); its totals may then include a proof still in flight.
+  std::unique_lock<std::shared_mutex> ex(ctx->cfg, std::defer_lock);
+  std::shared_lock<std::shared_mutex> sh(ctx->cfg, std::defer_lock);
+  if (enable >= 0) ex.lock(); else sh.lock();
   if (out) {
     for (int i = 0; i < 4; i++) out[i] = 0;
     for (Prover* q : ctx->all())
@@ -509,7 +526,7 @@ int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
 int nzcb_debug_inject_fault(nzcb_ctx* ctx, int kind) {
   if (!ctx || (kind != 0 && kind != NZCB_FAULT_QUOTIENT && kind != NZCB_DEBUG_GENERIC_K)) return NZCB_ERR_ARG;
   std::unique_lock<std::shared_mutex> lk(ctx->cfg);
-  for (Prover* q : ctx->all()) q->fault = kind;
+  ctx->pending_fault = kind;
   return 0;
 }
 

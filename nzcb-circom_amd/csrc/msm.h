@@ -18,6 +18,10 @@ struct MsmBaseTable {
   // rows of 2^-256 B_i: the MSM then takes Montgomery-256 scalars as they are (mont = true
   // is required; msm.hip msm_table_kernel)
   bool mont_folded = false;
+  // the sparse schedule (msm.hip dyn_chunk: device-derived chunk, log-depth carry trees) for
+  // tables whose scalars are mostly small (the Lagrange basis: A, B, C's gate values); the
+  // result is the same point either way
+  bool sparse = false;
   void build(const G1Affine* bases, size_t n, int c, hipStream_t st, bool fold_mont = false);
 };
 
@@ -58,7 +62,7 @@ struct MsmScratch {
   size_t host_win_cap = 0;
   // shape of the MSM in flight (set by msm_enqueue, used by msm_finish)
   int cur_c = 0, cur_nsets = 0, cur_nbits = 0, cur_seglen = 0;
-  bool cur_fixed = false;
+  bool cur_fixed = false, cur_sparse = false;
   int cur_a = 0, cur_hb = 0;  // fixed base: column / row bits of the window sum
   size_t cur_n = 0;
   uint32_t cur_nkeys = 0;

@@ -78,10 +78,37 @@ static constexpr uint32_t kSeqSpan29 = 16;
 static constexpr int kLargeBlocks = 32;  // finalize: workgroups for the longer runs
 // fixed base: workgroups over the pieces of the longer runs, and over their buckets (grid-
 // stride; random scalars list none, and under 5 proof lanes every launched workgroup waits
-// for a CU slot first, so the grids are kept small)
+// for a CU slot first, so the dense tables' grids are kept small)
 static constexpr int kLargePieceBlocks = 128;
 static constexpr int kLargeFinalBlocks = 128;
-static constexpr int kLargeFinalThreads = 64;
+
+// Sparse tables (MsmBaseTable::sparse: the Lagrange basis, whose A, B, C scalars are mostly
+// 0, 1 and bytes; round 6). Their few entries (~0.7-1.5 per scalar against 13 for random
+// ones) left most of the chip idle behind 48-entry chains, and |digit| = 1 puts ~40 % of the
+// entries into one bucket whose carries went through ~80 dependent additions (48 in the
+// chain, 16 in the finalize, 12 in the pieces, ~7 in their sum). The MSM's time is its
+// depth in dependent EC additions (~15-20 us each with a wave or two per SIMD), so:
+//  * the chunk is derived on the device from the bucketed entry count M: ceil(M / 2^18)
+//    entries per thread, clamped to [kDynMin, kChunk] (every kernel that maps stream
+//    positions to chunks computes the same dyn_chunk(M));
+//  * the finalize sums runs of at most kSeqSpanSparse + 1 carries per lane;
+//  * longer runs are cut into pieces of kPieceCarries summed by log-depth LDS trees, and a
+//    bucket's pieces by another tree: ceil(log2(carries)) + 1 dependent additions.
+static constexpr uint32_t kDynThreads = 1u << 18;
+static constexpr uint32_t kDynMin = 8;
+static constexpr uint32_t kSeqSpanSparse = 3;
+static constexpr int kSparsePieceBlocks = 2048;
+static constexpr int kSparseFinalBlocks = 512;
+__host__ __device__ __forceinline__ uint32_t dyn_chunk(uint32_t m) {
+  const uint32_t c = (m + kDynThreads - 1) / kDynThreads;
+  return c < kDynMin ? kDynMin : c > kChunk ? kChunk : c;
+}
+// the most accumulation threads dyn_chunk gives for any count M <= entries: ceil(M / chunk)
+// <= 2^18 while the chunk is unclamped or kDynMin (M <= kDynMin 2^18), else ceil(M / kChunk)
+static size_t dyn_threads_bound(size_t entries) {
+  const size_t lo = std::min<size_t>(kDynThreads, (entries + kDynMin - 1) / kDynMin);
+  return std::max<size_t>(lo, (entries + kChunk - 1) / kChunk);
+}
 
 // Fixed-base window of the PTau tables: c = 20 bits (13 table rows, 2^19 buckets, 13
 // entries per random scalar) since round 5, when the window sum's first level became the
@@ -650,6 +677,7 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
   __shared__ uint32_t sidx[kLdsIdx ? kChunk * kLdsStride : 1];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // < 2^32 (entries / chunk)
   const uint32_t M = offsets[nkeys];
+  if (!kLdsIdx && !chunk) chunk = dyn_chunk(M);  // sparse tables: derived from the entry count
   if (kLdsIdx) {  // every thread of the workgroup takes part before any exits
     const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * kChunk;
     for (uint32_t j = threadIdx.x; j < kMsmThreads * kChunk; j += kMsmThreads) {
@@ -795,6 +823,7 @@ msm_finalize29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint
   __shared__ uint32_t pk[kMsmThreads], pu[kMsmThreads], pe[kMsmThreads];
   __shared__ uint32_t cnt;
   if (threadIdx.x == 0) cnt = 0;
+  if (!chunk) chunk = dyn_chunk(offsets[nkeys]);  // sparse tables
   __syncthreads();
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t c0 = 0, c1 = 0;
@@ -920,30 +949,36 @@ msm_bucket_large_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, co
   }
 }
 
-// Fixed-base schedule, long carry runs (e.g. the Lagrange-basis commitments, whose small
-// witness values put ~40 % of the entries in bucket 0: ~12 k carries): the runs are cut
-// into pieces of kPieceCarries, each summed by one workgroup in radix 2^29 (kSumPer-deep
-// sequential adds + LDS tree), then one wave per bucket adds its pieces.
-static constexpr uint32_t kPieceCarries = (uint32_t)kSumThreads * kSumPer;
+// Fixed-base schedule, long carry runs (skewed digits: the Lagrange-basis commitments'
+// |digit| = 1 bucket holds ~40 % of their entries, tens of thousands of carries; "equal"
+// scalars in the tests): the runs are cut into pieces of kPieceCarries, each summed by one
+// workgroup in an LDS tree of ceil(log2(carries)) levels, then one workgroup per bucket adds
+// its pieces by another tree (round 6; until round 5 1024-carry pieces, four sequential
+// additions per thread before an 8-level tree, and a 64-lane tree over the pieces: 20+
+// dependent additions whatever the run's length, on 128 workgroups that walked the pieces
+// one after another).
+static constexpr uint32_t kPieceCarries = (uint32_t)kSumThreads;
 
 __device__ __forceinline__ uint32_t carry_span(uint32_t chunk, const uint32_t* offsets, uint32_t k, uint32_t* c0) {
   *c0 = offsets[k] / chunk;
   return (offsets[k + 1] - 1) / chunk - *c0 + 1;
 }
 
-// off[i] = pieces of the listed buckets before i, off[count] = all (one workgroup)
+// off[i] = pieces of the listed buckets before i, off[count] = all (one workgroup).
+// chunk 0: the sparse schedule's device-derived chunk (dyn_chunk)
 __global__ void __launch_bounds__(1024)
-msm_large_scan_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
-                      uint32_t* __restrict__ off) {
+msm_large_scan_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys,
+                      const uint32_t* __restrict__ large, uint32_t* __restrict__ off) {
   __shared__ uint32_t sh[1024];
   const uint32_t count = large[0];
+  const uint32_t ch = chunk ? chunk : dyn_chunk(offsets[nkeys]);
   const uint32_t tid = threadIdx.x;
   const uint32_t per = (count + 1023u) / 1024u;
   const uint32_t i0 = tid * per < count ? tid * per : count;
   const uint32_t i1 = i0 + per < count ? i0 + per : count;
   auto pieces = [&](uint32_t i) {
     uint32_t c0;
-    return (carry_span(chunk, offsets, large[1 + i], &c0) + kPieceCarries - 1) / kPieceCarries;
+    return (carry_span(ch, offsets, large[1 + i], &c0) + kPieceCarries - 1) / kPieceCarries;
   };
   uint32_t sum = 0;
   for (uint32_t i = i0; i < i1; i++) sum += pieces(i);
@@ -963,13 +998,41 @@ msm_large_scan_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, cons
   if (tid == 1023) off[count] = sh[1023];
 }
 
+// Sum of v over the workgroup's first `cnt` threads (cnt <= kSumThreads, uniform; threads >=
+// cnt pass anything) by a tree of ceil(log2(cnt)) levels, the first level straight from the
+// registers: thread u adds u + h's value (h = the half, rounded up to a power of two) and the
+// tree continues in LDS. Result in thread 0. One addition site.
+__device__ __forceinline__ Xyzz29 tree_sum29(Xyzz29 v, uint32_t cnt, Xyzz29* sh) {
+  const uint32_t u = threadIdx.x;
+  uint32_t h = 1;
+  while (h < cnt) h <<= 1;
+  h >>= 1;  // cnt <= 1: no level
+  if (h) {
+    if (u >= h && u < cnt) sh[u] = v;
+    __syncthreads();
+  }
+  // level h reads [h, 2h) and then [h / 2, h) is written for the next level: disjoint, so
+  // one barrier per level
+  for (; h; h >>= 1) {
+    if (u < h && u + h < cnt) v = add29(v, sh[u + h]);
+    cnt = h;
+    if (h > 1) {
+      if (u >= (h >> 1) && u < h) sh[u] = v;
+      __syncthreads();
+    }
+  }
+  return v;
+}
+
 __global__ void __launch_bounds__(kSumThreads)
-msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ large,
-                         const uint32_t* __restrict__ off, const Xyzz29* __restrict__ carry_own,
-                         const Xyzz29* __restrict__ carry_cont, Xyzz29* __restrict__ part) {
+msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys,
+                         const uint32_t* __restrict__ large, const uint32_t* __restrict__ off,
+                         const Xyzz29* __restrict__ carry_own, const Xyzz29* __restrict__ carry_cont,
+                         Xyzz29* __restrict__ part) {
   __shared__ Xyzz29 sh[kSumThreads];
   const uint32_t count = large[0];
   const uint32_t total = off[count];
+  const uint32_t ch = chunk ? chunk : dyn_chunk(offsets[nkeys]);
   for (uint32_t item = blockIdx.x; item < total; item += gridDim.x) {
     uint32_t lo = 0, hi = count;  // largest i with off[i] <= item
     while (hi - lo > 1) {
@@ -977,27 +1040,24 @@ msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, c
       if (off[mid] <= item) lo = mid; else hi = mid;
     }
     uint32_t c0;
-    const uint32_t span = carry_span(chunk, offsets, large[1 + lo], &c0);
+    const uint32_t span = carry_span(ch, offsets, large[1 + lo], &c0);
     const uint32_t first = (item - off[lo]) * kPieceCarries;
     const uint32_t n = span - first < kPieceCarries ? span - first : kPieceCarries;
-    const int per = (int)((n + kSumThreads - 1) / kSumThreads);  // <= kSumPer
-    const Xyzz29 r = block_sum<kSumThreads>(per, sh, [&](int step, Xyzz29& rhs) {
-      const uint32_t u = (uint32_t)step * kSumThreads + threadIdx.x;
-      if (u >= n) return false;
-      rhs = first + u ? carry_cont[c0 + first + u] : carry_own[c0];
-      return true;
-    });
-    if (threadIdx.x == 0) part[item] = r;
-    __syncthreads();
+    const uint32_t u = first + threadIdx.x;
+    Xyzz29 v;
+    if (threadIdx.x < n) v = u ? carry_cont[c0 + u] : carry_own[c0];
+    v = tree_sum29(v, n, sh);
+    if (threadIdx.x == 0) part[item] = v;
+    __syncthreads();  // sh is reused by the next item
   }
 }
 
-// a listed bucket's pieces: one wave per bucket, a tree over up to 64 pieces at a time
-// (the hottest Lagrange bucket has ~40 pieces: 6 levels instead of 40 sequential adds)
-__global__ void __launch_bounds__(kLargeFinalThreads)
+// a listed bucket's pieces: one workgroup per bucket, a sequential add per thread while
+// there are more than kSumThreads pieces, then the tree
+__global__ void __launch_bounds__(kSumThreads)
 msm_large_final29_kernel(const uint32_t* __restrict__ large, const uint32_t* __restrict__ off,
                          const Xyzz29* __restrict__ part, Xyzz29* __restrict__ out29) {
-  __shared__ Xyzz29 sh[kLargeFinalThreads];
+  __shared__ Xyzz29 sh[kSumThreads];
   const uint32_t count = large[0];
   for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
     const uint32_t p0 = off[i], np = off[i + 1] - p0;
@@ -1005,14 +1065,11 @@ msm_large_final29_kernel(const uint32_t* __restrict__ large, const uint32_t* __r
       if (threadIdx.x == 0) out29[large[1 + i]] = part[p0];
       continue;
     }
-    const int per = (int)((np + kLargeFinalThreads - 1) / kLargeFinalThreads);
-    const Xyzz29 r = block_sum<kLargeFinalThreads>(per, sh, [&](int step, Xyzz29& rhs) {
-      const uint32_t u = (uint32_t)step * kLargeFinalThreads + threadIdx.x;
-      if (u >= np) return false;
-      rhs = part[p0 + u];
-      return true;
-    });
-    if (threadIdx.x == 0) out29[large[1 + i]] = r;
+    Xyzz29 v;
+    if (threadIdx.x < np) v = part[p0 + threadIdx.x];
+    for (uint32_t q = threadIdx.x + kSumThreads; q < np; q += kSumThreads) v = add29(v, part[p0 + q]);
+    v = tree_sum29(v, np < kSumThreads ? np : kSumThreads, sh);
+    if (threadIdx.x == 0) out29[large[1 + i]] = v;
     __syncthreads();
   }
 }
@@ -1360,7 +1417,8 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
   radix_sort(nullptr, sort_tmp_bytes, keys_in.p, keys_out.p, vals_in.p, sorted.p, max_entries, 21, nullptr);
   sort_tmp.alloc(sort_tmp_bytes + 16);
   buckets.alloc(max_keys);
-  const size_t nthreads = (max_entries + kChunk - 1) / kChunk + 1;
+  // accumulation threads: chunk_for's grid, or the sparse schedule's (dyn_threads_bound)
+  const size_t nthreads = std::max((max_entries + kChunk - 1) / kChunk, dyn_threads_bound(max_entries)) + 1;
   carry_own.alloc(nthreads);
   carry_cont.alloc(nthreads);
   large.alloc(max_keys + 1);
@@ -1525,8 +1583,12 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     NZ_HIP(hipGetLastError());
   }
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[3], st));
-  const uint32_t chunk = chunk_for(p.entries);
-  const size_t nthreads = (p.entries + chunk - 1) / chunk;
+  // sparse tables: chunk 0 = derived on the device from the bucketed entry count (dyn_chunk);
+  // the grid covers the most threads any count can ask for
+  const bool sparse = table && table->sparse;
+  sc.cur_sparse = sparse;
+  const uint32_t chunk = sparse ? 0u : chunk_for(p.entries);
+  const size_t nthreads = sparse ? dyn_threads_bound(p.entries) : (p.entries + chunk - 1) / chunk;
   const dim3 agrid(grid_for(nthreads, kMsmThreads, 1u << 30));
   const G1Affine* gather = table ? table->q.p : bases;
   if (table) {
@@ -1545,18 +1607,18 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
   if (table) {  // the large list's count was zeroed by msm_lo_scan_kernel
     hipLaunchKernelGGL(msm_finalize29_kernel, fgrid, dim3(kMsmThreads), 0, st, chunk, sc.offsets.p, p.nkeys,
-                       kSeqSpan29, (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p, sc.large.p,
-                       sc.buckets29.p);
+                       sparse ? kSeqSpanSparse : kSeqSpan29, (const Xyzz29*)sc.carry_own29.p,
+                       (const Xyzz29*)sc.carry_cont29.p, sc.large.p, sc.buckets29.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, sc.offsets.p, sc.large.p,
+    hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, sc.offsets.p, p.nkeys, sc.large.p,
                        sc.large_off.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_large_piece29_kernel, dim3(kLargePieceBlocks), dim3(kSumThreads), 0, st, chunk, sc.offsets.p,
-                       sc.large.p, sc.large_off.p, (const Xyzz29*)sc.carry_own29.p,
-                       (const Xyzz29*)sc.carry_cont29.p, sc.large_part.p);
+    hipLaunchKernelGGL(msm_large_piece29_kernel, dim3(sparse ? kSparsePieceBlocks : kLargePieceBlocks),
+                       dim3(kSumThreads), 0, st, chunk, sc.offsets.p, p.nkeys, sc.large.p, sc.large_off.p,
+                       (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p, sc.large_part.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_large_final29_kernel, dim3(kLargeFinalBlocks), dim3(kLargeFinalThreads), 0, st, sc.large.p,
-                       sc.large_off.p, sc.large_part.p, sc.buckets29.p);
+    hipLaunchKernelGGL(msm_large_final29_kernel, dim3(sparse ? kSparseFinalBlocks : kLargeFinalBlocks),
+                       dim3(kSumThreads), 0, st, sc.large.p, sc.large_off.p, sc.large_part.p, sc.buckets29.p);
     NZ_HIP(hipGetLastError());
     mark(5);
     int lparts = p.ltiles, hparts = p.htiles;  // partials per row / per column
@@ -1626,7 +1688,8 @@ G1xyzz msm_finish(MsmScratch& sc, hipStream_t st) {
     NZ_HIP(hipMemcpy(&cnt, sc.large.p, 4, hipMemcpyDeviceToHost));
     uint32_t pieces = 0;
     NZ_HIP(hipMemcpy(&pieces, sc.large_off.p + cnt, 4, hipMemcpyDeviceToHost));
-    const uint32_t M = off.back(), chunk = chunk_for(sc.cur_n * (size_t)num_windows(sc.cur_c));
+    const uint32_t M = off.back();
+    const uint32_t chunk = sc.cur_sparse ? dyn_chunk(M) : chunk_for(sc.cur_n * (size_t)num_windows(sc.cur_c));
     size_t h[12] = {0};
     uint32_t mx = 0;
     uint64_t carries_large = 0, carries_mid = 0;
@@ -1637,7 +1700,7 @@ G1xyzz msm_finish(MsmScratch& sc, hipStream_t st) {
       int b = 1;
       while (b < 11 && sp > (1u << (b - 1))) b++;
       h[b]++;
-      if (sp > kSeqSpan29 + 1) carries_large += sp; else if (sp > 1) carries_mid += sp;
+      if (sp > (sc.cur_sparse ? kSeqSpanSparse : kSeqSpan29) + 1) carries_large += sp; else if (sp > 1) carries_mid += sp;
     }
     fprintf(stderr, "MSMSTATS n=%zu c=%d entries=%u chunk=%u large=%u pieces=%u maxspan=%u carries_mid=%llu "
             "carries_large=%llu spans[empty,1,2,<=4,<=8,..,<=512,>512]=", sc.cur_n, sc.cur_c, M, chunk, cnt, pieces, mx,

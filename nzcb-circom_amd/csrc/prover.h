@@ -17,14 +17,16 @@ struct AddRec {  // one addition, reordered by dependency level
 };
 
 // one proof's MSMs split by point range over several devices
-// of this process. A shard holds the shifted-base table of its PTau range and per-slot
-// MSM scratch; the scalar slice arrives by a device-to-device copy over xGMI and the
-// 96-byte partial comes back to the host, where the partials are added.
+// of this process. A shard holds the shifted-base tables of its PTau range and of its
+// Lagrange-basis range (A, B, C) and per-slot MSM scratch; the scalar slice arrives by a
+// device-to-device copy over xGMI and the 96-byte partial comes back to the host, where the
+// partials are added.
 struct MsmShard {
   static constexpr int kSlots = 3;
   int device = 0;
-  size_t lo = 0, hi = 0;
-  MsmBaseTable table;
+  size_t lo = 0, hi = 0;    // PTau points
+  size_t llo = 0, lhi = 0;  // Lagrange-basis points (lhi = 0: none, the context commits A, B, C from coefficients)
+  MsmBaseTable table, ltable;
   std::unique_ptr<MsmScratch> sc[kSlots];
   DevBuf<Fr> scal[kSlots];
   hipStream_t st[kSlots] = {nullptr, nullptr, nullptr};
@@ -46,7 +48,8 @@ struct Prover {
   std::unique_ptr<MsmScratch> msc[kSlots];
   hipStream_t aux[kSlots] = {nullptr, nullptr, nullptr};
   hipEvent_t ready[kSlots] = {nullptr, nullptr, nullptr};
-  bool slot_local[kSlots] = {false, false, false};  // slot's MSM stays on this device (Lagrange basis)
+  bool slot_split[kSlots] = {false, false, false};  // slot's MSM went to the other ranks (commit_finish gathers)
+  bool slot_lag[kSlots] = {false, false, false};    // slot's MSM is over the Lagrange basis
   // round 1's interpolations of A, B, C (and the gate check) run on aux[2], overlapping
   // round 2; round 3 waits for side_done. pows_done: round 4's divPol1 tile powers (aux[2])
   hipEvent_t side_ready = nullptr, side_done = nullptr, pows_done = nullptr;
@@ -124,18 +127,21 @@ struct Prover {
   // Split every commitment MSM over devices[0] (this prover's device) and the others.
   void set_msm_devices(const std::vector<int>& devices);
   std::vector<std::unique_ptr<MsmShard>> shards;
-  size_t own_hi = 0;  // this device's MSM point range is [0, own_hi) when shards exist
+  size_t own_hi = 0, own_lhi = 0;  // this device's PTau / Lagrange ranges are [0, own_hi) / [0, own_lhi) with shards
   // SURVEY.md §8e config 5 across processes (one rank per GPU, RCCL over xGMI): this
-  // prover computes the points [0, split_own) of every commitment; `split_send` hands the
-  // commitment's scalars (HBM) to the other ranks as soon as they are ready and
-  // `split_gather` returns every rank's 64-byte affine partial (rank order), which are
-  // added here. Both are caller callbacks (the collectives live in the host runtime).
+  // prover computes the PTau points [0, split_own) of every commitment and, when split_own_l
+  // > 0, the Lagrange-basis points [0, split_own_l) of A, B and C; `split_send` hands the
+  // commitment's scalars (HBM) to the other ranks as soon as they are ready (the slot with
+  // NZCB_MSM_LAGRANGE for the Lagrange basis) and `split_gather` returns every rank's 64-byte
+  // affine partial (rank order), which are added here. Both are caller callbacks (the
+  // collectives live in the host runtime).
   nzcb_msm_send_fn split_send = nullptr;
   nzcb_msm_gather_fn split_gather = nullptr;
   void* split_user = nullptr;
   int split_world = 1;
-  size_t split_own = 0;
-  void set_msm_split(int world, size_t own_points, nzcb_msm_send_fn send, nzcb_msm_gather_fn gather, void* user);
+  size_t split_own = 0, split_own_l = 0;
+  void set_msm_split(int world, size_t own_points, size_t own_lagrange, nzcb_msm_send_fn send,
+                     nzcb_msm_gather_fn gather, void* user);
   // witness: nWit x 32-byte LE normal-form values; blinding: 11 x 32-byte LE or null
   // witness_on_device: `witness` is a device pointer (HBM-resident input, no PCIe copy)
   void prove(const uint8_t* witness, size_t n_witness, const uint8_t* blinding, uint8_t* proof_out,

@@ -1038,28 +1038,40 @@ void Prover::set_msm_devices(const std::vector<int>& devices) {
   if (devices.empty() || devices[0] != eng->device)
     throw Error(NZCB_ERR_ARG, "msm devices must start with the context's device");
   shards.clear();
-  own_hi = 0;
-  const size_t N = ptau.n;  // n + 6 bases
+  own_hi = own_lhi = 0;
+  const size_t N = ptau.n;                  // n + 6 bases
+  const size_t L = lcommit ? ltau.n : 0;    // n + 2 Lagrange-basis points (A, B, C)
   const size_t k = devices.size();
   if (k == 1) return;
   own_hi = N / k;
+  own_lhi = L / k;
   for (size_t i = 1; i < k; i++) {
     auto sh = std::make_unique<MsmShard>();
     sh->device = devices[i];
     sh->lo = N * i / k;
     sh->hi = N * (i + 1) / k;
-    const size_t cnt = sh->hi - sh->lo;
+    sh->llo = L * i / k;
+    sh->lhi = L * (i + 1) / k;
+    const size_t cnt = sh->hi - sh->lo, lcnt = sh->lhi - sh->llo, mx = std::max(cnt, lcnt);
     NZ_HIP(hipSetDevice(sh->device));
     for (int j = 0; j < MsmShard::kSlots; j++) {
       NZ_HIP(hipStreamCreateWithFlags(&sh->st[j], hipStreamNonBlocking));
       sh->sc[j].reset(new MsmScratch());
-      sh->sc[j]->init(cnt, true);
-      sh->scal[j].alloc(cnt);
+      sh->sc[j]->init(mx, true);
+      sh->scal[j].alloc(mx);
     }
     {  // the shard's PTau range -> its shifted-base table (built on the shard's device)
       DevBuf<G1Affine> part(cnt);
       NZ_HIP(hipMemcpyPeerAsync(part.p, sh->device, ptau.p + sh->lo, eng->device, cnt * sizeof(G1Affine), sh->st[0]));
       sh->table.build(part.p, cnt, fixed_base_window(), sh->st[0]);
+      NZ_HIP(hipStreamSynchronize(sh->st[0]));
+    }
+    if (lcnt) {  // and its range of the Lagrange basis (A, B, C: the sparse schedule)
+      DevBuf<G1Affine> part(lcnt);
+      NZ_HIP(hipMemcpyPeerAsync(part.p, sh->device, ltau.p + sh->llo, eng->device, lcnt * sizeof(G1Affine),
+                                sh->st[0]));
+      sh->ltable.build(part.p, lcnt, lagrange_window(), sh->st[0]);
+      sh->ltable.sparse = true;
       NZ_HIP(hipStreamSynchronize(sh->st[0]));
     }
     shards.push_back(std::move(sh));
@@ -1108,6 +1120,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     ltau.alloc((size_t)n + 2);
     lagrange_basis(ptau.p, ptau.n, power, ltau.p, s);
     ltab.build(ltau.p, ltau.n, lagrange_window(), s);
+    ltab.sparse = true;  // small gate values: msm.hip's sparse schedule
   }
   up(qm, z.qm);
   up(ql, z.ql);
@@ -1368,6 +1381,7 @@ Prover::Prover(const Prover& pk, int) {
   ltau.alias(pk.ltau);
   ltab.q.alias(pk.ltab.q);
   ltab.n = pk.ltab.n; ltab.stride = pk.ltab.stride; ltab.c = pk.ltab.c; ltab.nw = pk.ltab.nw;
+  ltab.sparse = pk.ltab.sparse;
   qm.alias(pk.qm); ql.alias(pk.ql); qr.alias(pk.qr); qo.alias(pk.qo); qc.alias(pk.qc);
   sigma.alias(pk.sigma); sig_h.alias(pk.sig_h); q_h.alias(pk.q_h); w_h.alias(pk.w_h); lagrange.alias(pk.lagrange);
   amap.alias(pk.amap); bmap.alias(pk.bmap); cmap.alias(pk.cmap); adds.alias(pk.adds);
@@ -1550,32 +1564,41 @@ void Prover::to4t_evals4(const Fr* coefs, Fr* evals4, int nb, hipStream_t s, uin
 // latency-bound and fill the gaps of the compute-bound bucket accumulation).
 void Prover::commit_start(int slot, const Fr* coefs, size_t len, const MsmBaseTable* tab, const G1Affine* bases,
                           bool on_main) {
+  static const char* const kEnq[kSlots] = {"mark: commit enqueue slot 0", "mark: commit enqueue slot 1",
+                                           "mark: commit enqueue slot 2"};
+  roctxMarkA(kEnq[slot]);  // host timeline of the commitments (rocprofv3 --marker-trace, tools/timeline.py)
   NZ_HIP(hipEventRecord(ready[slot], st()));
   hipStream_t ms = on_main ? st() : aux[slot];  // the stream this slot's MSM runs on
   if (!on_main) NZ_HIP(hipStreamWaitEvent(ms, ready[slot], 0));
-  // the Lagrange-basis commitments (A, B, C: mostly small scalars) are not split: the
-  // devices and ranks of a split hold PTau ranges
-  const bool local = tab != nullptr && tab != &ptab;
-  slot_local[slot] = local;
-  if (!local && !shards.empty()) {
+  // Both bases split by point range over the devices / ranks of a split: PTau (the six
+  // random-scalar commitments) and, since round 6, the Lagrange basis (A, B, C: mostly small
+  // scalars, whose |digit| = 1 bucket a point range divides as well)
+  const bool lag = tab != nullptr && tab == &ltab;
+  slot_lag[slot] = lag;
+  slot_split[slot] = false;
+  if (!shards.empty() && (!lag || own_lhi)) {
     for (auto& sh : shards) {
-      const size_t cnt = len > sh->lo ? std::min(len, sh->hi) - sh->lo : 0;
+      const size_t lo = lag ? sh->llo : sh->lo, hi = lag ? sh->lhi : sh->hi;
+      const size_t cnt = len > lo ? std::min(len, hi) - lo : 0;
       NZ_HIP(hipSetDevice(sh->device));
       if (cnt) {
         NZ_HIP(hipStreamWaitEvent(sh->st[slot], ready[slot], 0));
-        NZ_HIP(hipMemcpyPeerAsync(sh->scal[slot].p, sh->device, coefs + sh->lo, eng->device, cnt * sizeof(Fr),
+        NZ_HIP(hipMemcpyPeerAsync(sh->scal[slot].p, sh->device, coefs + lo, eng->device, cnt * sizeof(Fr),
                                   sh->st[slot]));
       }
-      msm_enqueue(*sh->sc[slot], nullptr, sh->scal[slot].p, cnt, true, sh->st[slot], &sh->table);  // cnt 0: no-op
+      msm_enqueue(*sh->sc[slot], nullptr, sh->scal[slot].p, cnt, true, sh->st[slot],
+                  lag ? &sh->ltable : &sh->table);  // cnt 0: no-op
     }
     NZ_HIP(hipSetDevice(eng->device));
-    len = std::min(len, own_hi);
+    len = std::min(len, lag ? own_lhi : own_hi);
+    slot_split[slot] = true;
   }
-  if (!local && split_send) {  // other ranks take [split_own, len): hand them the scalars once ready
+  if (split_send && (!lag || split_own_l)) {  // other ranks take [own, len): hand them the scalars once ready
     NZ_HIP(hipEventSynchronize(ready[slot]));
-    if (split_send(split_user, slot, coefs, len) != 0)
+    if (split_send(split_user, slot | (lag ? NZCB_MSM_LAGRANGE : 0), coefs, len) != 0)
       throw Error(NZCB_ERR_INTERNAL, "msm split: sending the scalars to the other ranks failed");
-    len = std::min(len, split_own);
+    len = std::min(len, lag ? split_own_l : split_own);
+    slot_split[slot] = true;
   }
   const size_t sp = prof_gpu ? span_begin(0, ms) : 0;
   msm_enqueue(*msc[slot], bases ? bases : ptau.p, coefs, len, true, ms, tab ? tab : &ptab);
@@ -1609,19 +1632,22 @@ G1xyzz xyzz_from_le(const uint8_t* in) {
 G1Affine Prover::commit_finish(int slot) {
   auto t0 = std::chrono::steady_clock::now();
   G1xyzz r = msm_finish(*msc[slot], aux[slot]);
-  const bool local = slot_local[slot];
+  static const char* const kRes[kSlots] = {"mark: commit result slot 0", "mark: commit result slot 1",
+                                           "mark: commit result slot 2"};
+  roctxMarkA(kRes[slot]);
+  const bool split = slot_split[slot];
   for (auto& sh : shards) {  // partial sums of the other devices' point ranges
-    if (local) break;
+    if (!split) break;
     NZ_HIP(hipSetDevice(sh->device));
     r = xyzz_add(r, msm_finish(*sh->sc[slot], sh->st[slot]));
   }
   if (!shards.empty()) NZ_HIP(hipSetDevice(eng->device));
-  if (!local && split_gather) {  // every rank's partial (ours included), added in rank order
+  if (split && split_gather) {  // every rank's partial (ours included), added in rank order
     const G1Affine own = xyzz_to_affine(r);
     uint8_t own_le[64];
     affine_to_le(own, own_le);
     std::vector<uint8_t> parts((size_t)split_world * 64);
-    if (split_gather(split_user, slot, own_le, parts.data()) != 0)
+    if (split_gather(split_user, slot | (slot_lag[slot] ? NZCB_MSM_LAGRANGE : 0), own_le, parts.data()) != 0)
       throw Error(NZCB_ERR_INTERNAL, "msm split: gathering the partial sums failed");
     r = G1xyzz::inf();
     for (int k = 0; k < split_world; k++) r = xyzz_add(r, xyzz_from_le(parts.data() + 64 * (size_t)k));
@@ -1630,21 +1656,26 @@ G1Affine Prover::commit_finish(int slot) {
   return xyzz_to_affine(r);
 }
 
-void Prover::set_msm_split(int world, size_t own_points, nzcb_msm_send_fn send, nzcb_msm_gather_fn gather,
-                           void* user) {
+void Prover::set_msm_split(int world, size_t own_points, size_t own_lagrange, nzcb_msm_send_fn send,
+                           nzcb_msm_gather_fn gather, void* user) {
   if (world <= 1 || !send || !gather) {
     split_send = nullptr;
     split_gather = nullptr;
     split_world = 1;
+    split_own = split_own_l = 0;
     return;
   }
   if (!shards.empty()) throw Error(NZCB_ERR_ARG, "msm split: a context splits over devices or over ranks, not both");
   if (own_points == 0 || own_points > ptau.n) throw Error(NZCB_ERR_ARG, "msm split: bad own point count");
+  if (own_lagrange > (lcommit ? ltau.n : 0))
+    throw Error(NZCB_ERR_ARG, "msm split: bad own Lagrange point count (A, B, C are committed from coefficients "
+                              "when the context has no Lagrange basis)");
   split_send = send;
   split_gather = gather;
   split_user = user;
   split_world = world;
   split_own = own_points;
+  split_own_l = own_lagrange;
 }
 
 void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out,

@@ -39,16 +39,29 @@ EXPORTED_SYMBOLS = [
     "nzcb_engine_create", "nzcb_engine_destroy", "nzcb_engine_ntt", "nzcb_engine_msm", "nzcb_dev_alloc",
     "nzcb_dev_free", "nzcb_memcpy_h2d", "nzcb_memcpy_d2h", "nzcb_engine_ntt_dev", "nzcb_engine_msm_dev",
     "nzcb_engine_time_ntt", "nzcb_engine_fr_mul", "nzcb_engine_random_fr", "nzcb_engine_fixed_base",
-    "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
+    "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_msm_table_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_from_zkey_file", "nzcb_vk_to_json", "nzcb_verify",
     "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_engine_lagrange_basis", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d",
     "nzcb_plonk_setup", "nzcb_prove_batch_status", "nzcb_wprog_remap", "nzcb_prove_logged", "nzcb_memcpy_d2d_async",
     "nzcb_debug_guard_check", "nzcb_debug_guard_selftest", "nzcb_debug_inject_fault",
+    "nzcb_msm_table_create_lagrange",
 ]
 
 NZCB_FAULT_QUOTIENT = 1  # include/nzcb_internal.h
 NZCB_DEBUG_GENERIC_K = 2  # include/nzcb_internal.h
+
+
+def lagrange_commit_enabled() -> bool:
+    """Whether prover contexts commit A, B, C over the Lagrange basis (csrc/prover.hip
+    lagrange_commit_enabled: NZCB_LAGRANGE_COMMIT unset or non-zero), which decides whether
+    the MSM split has Lagrange-basis ranges (nzcb.msmsplit)."""
+    import re
+    e = os.environ.get("NZCB_LAGRANGE_COMMIT")
+    if e is None:
+        return True
+    m = re.match(r"\s*[+-]?\d+", e)   # as C's atoi: the leading integer, 0 without one
+    return bool(m) and int(m.group()) != 0
 
 
 def guard_check(device: int = -1) -> int:
@@ -99,6 +112,7 @@ LOG_FN = ctypes.CFUNCTYPE(None, c_void_p, ctypes.c_char_p)
 # nzcb_ctx_set_msm_split callbacks (include/nzcb.h)
 MSM_SEND_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, c_void_p, c_size_t)
 MSM_GATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, POINTER(c_uint8), POINTER(c_uint8))
+MSM_LAGRANGE = 0x100   # include/nzcb.h NZCB_MSM_LAGRANGE: the slot's commitment is over the Lagrange basis
 
 _lib = None
 
@@ -174,6 +188,8 @@ def load(path: str | None = None):
                                          POINTER(c_double), POINTER(_Err)]),
         "nzcb_engine_msm_fixed_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_int, u8p,
                                               POINTER(_Err)]),
+        "nzcb_engine_msm_table_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_int, c_int, c_int,
+                                              u8p, POINTER(_Err)]),
         "nzcb_plonk_setup": (c_int, [ctypes.c_char_p, c_size_t, ctypes.c_char_p, c_size_t, c_int, POINTER(POINTER(c_uint8)),
                                      POINTER(c_size_t), POINTER(_Err)]),
         "nzcb_nzcp_input_signals": (c_size_t, [POINTER(NzcpParams)]),
@@ -184,9 +200,11 @@ def load(path: str | None = None):
                                           POINTER(c_double), POINTER(_Err)]),
         "nzcb_ctx_create_devices": (c_void_p, [u8p, c_size_t, POINTER(c_int), c_int, POINTER(_Err)]),
         "nzcb_ctx_devices": (c_int, [c_void_p]),
-        "nzcb_ctx_set_msm_split": (c_int, [c_void_p, c_int, c_size_t, MSM_SEND_FN, MSM_GATHER_FN, c_void_p,
-                                           POINTER(_Err)]),
+        "nzcb_ctx_set_msm_split": (c_int, [c_void_p, c_int, c_size_t, c_size_t, MSM_SEND_FN, MSM_GATHER_FN,
+                                           c_void_p, POINTER(_Err)]),
         "nzcb_msm_table_create": (c_void_p, [c_int, c_void_p, c_size_t, POINTER(_Err)]),
+        "nzcb_msm_table_create_lagrange": (c_void_p, [c_int, c_void_p, c_size_t, c_int, c_size_t, c_size_t,
+                                                      POINTER(_Err)]),
         "nzcb_msm_table_run": (c_int, [c_void_p, c_void_p, c_size_t, c_int, u8p, POINTER(_Err)]),
         "nzcb_msm_table_destroy": (None, [c_void_p]),
         "nzcb_ptau_synth": (c_int, [c_int, u8p, c_int, POINTER(POINTER(c_uint8)), POINTER(c_size_t), POINTER(_Err)]),
@@ -367,12 +385,18 @@ class Engine:
         d["host_sort_call"] = out[12]
         return d
 
-    def msm_fixed_dev(self, dev_bases: int, n_table: int, dev_scalars: int, n: int, scalars_mont: bool) -> bytes:
-        """Fixed-base (shifted-table) MSM of the first n of n_table device bases."""
+    def msm_fixed_dev(self, dev_bases: int, n_table: int, dev_scalars: int, n: int, scalars_mont: bool,
+                      window: int = 0, sparse: bool = False) -> bytes:
+        """Fixed-base (shifted-table) MSM of the first n of n_table device bases; window 0 = the
+        PTau tables' default, sparse = the Lagrange table's schedule (msm.hip dyn_chunk)."""
         out = _out(64)
         err = _Err()
-        _check(self.lib.nzcb_engine_msm_fixed_dev(self.h, dev_bases, n_table, dev_scalars, n, int(scalars_mont), out,
-                                                  ctypes.byref(err)), err)
+        if window or sparse:
+            _check(self.lib.nzcb_engine_msm_table_dev(self.h, dev_bases, n_table, dev_scalars, n, int(scalars_mont),
+                                                      int(window), int(sparse), out, ctypes.byref(err)), err)
+        else:
+            _check(self.lib.nzcb_engine_msm_fixed_dev(self.h, dev_bases, n_table, dev_scalars, n, int(scalars_mont),
+                                                      out, ctypes.byref(err)), err)
         return bytes(out)
 
     def msm_dev(self, dev_bases: int, dev_scalars: int, n: int, scalars_mont: bool) -> bytes:
@@ -531,13 +555,15 @@ class ProverContext:
         err = _Err()
         _check(self.lib.nzcb_ctx_set_msm_devices(self.h, arr, len(devices), ctypes.byref(err)), err)
 
-    def set_msm_split(self, world: int, own_points: int, send, gather):
+    def set_msm_split(self, world: int, own_points: int, send, gather, own_lagrange: int = 0):
         """Split every commitment MSM across ranks (nzcb_ctx_set_msm_split; nzcb.msmsplit
-        builds the callbacks). send(slot, dev_ptr, count) -> None; gather(slot, own64) ->
+        builds the callbacks): rank 0 keeps PTau points [0, own_points) and, when
+        own_lagrange > 0, Lagrange-basis points [0, own_lagrange) of A, B and C (their slot
+        carries MSM_LAGRANGE). send(slot, dev_ptr, count) -> None; gather(slot, own64) ->
         world x 64 bytes. world = 1 restores the local schedule."""
         if world <= 1:
             self._split_cbs = None
-            _check(self.lib.nzcb_ctx_set_msm_split(self.h, 1, 0, MSM_SEND_FN(), MSM_GATHER_FN(), None,
+            _check(self.lib.nzcb_ctx_set_msm_split(self.h, 1, 0, 0, MSM_SEND_FN(), MSM_GATHER_FN(), None,
                                                    ctypes.byref(_Err())), _Err())
             return
 
@@ -564,8 +590,8 @@ class ProverContext:
 
         self._split_cbs = (MSM_SEND_FN(_send), MSM_GATHER_FN(_gather))  # keep alive
         err = _Err()
-        _check(self.lib.nzcb_ctx_set_msm_split(self.h, world, own_points, self._split_cbs[0], self._split_cbs[1],
-                                               None, ctypes.byref(err)), err)
+        _check(self.lib.nzcb_ctx_set_msm_split(self.h, world, own_points, own_lagrange, self._split_cbs[0],
+                                               self._split_cbs[1], None, ctypes.byref(err)), err)
 
     @property
     def lanes(self) -> int:
@@ -645,13 +671,24 @@ class ProverContext:
 class MsmTable:
     """Resident fixed-base MSM table over device bases (include/nzcb.h nzcb_msm_table_*)."""
 
-    def __init__(self, dev_bases: int, n: int, device: int = 0):
+    def __init__(self, dev_bases: int, n: int, device: int = 0, _handle=None):
         self.lib = load()
         err = _Err()
         self.n = n
-        self.h = self.lib.nzcb_msm_table_create(device, dev_bases, n, ctypes.byref(err))
+        self.h = _handle or self.lib.nzcb_msm_table_create(device, dev_bases, n, ctypes.byref(err))
         if not self.h:
             raise NzcbError(err.code, err.msg.decode(errors="replace"))
+
+    @classmethod
+    def lagrange(cls, dev_ptau: int, ptau_n: int, log_n: int, lo: int, hi: int, device: int = 0):
+        """Points [lo, hi) of the Lagrange basis of a 2^log_n domain, from PTau in HBM
+        (nzcb_msm_table_create_lagrange): the serving side of the A, B, C commitments."""
+        lib = load()
+        err = _Err()
+        h = lib.nzcb_msm_table_create_lagrange(device, dev_ptau, ptau_n, log_n, lo, hi, ctypes.byref(err))
+        if not h:
+            raise NzcbError(err.code, err.msg.decode(errors="replace"))
+        return cls(0, hi - lo, device, _handle=h)
 
     def run(self, dev_scalars: int, count: int, scalars_mont: bool = True) -> bytes:
         out = _out(64)

@@ -3,7 +3,11 @@ one process per GPU under torch.distributed (backend "nccl" = RCCL over xGMI on 
 
 Rank 0 proves. Every commitment MSM sum_i s_i [tau^i]G1 is split by PTau point range,
 rank r taking [r N / W, (r+1) N / W) of N = n + 6 points; each rank holds the
-shifted-base table of its range resident in HBM (nzcb_msm_table). Per commitment:
+shifted-base table of its range resident in HBM (nzcb_msm_table). A, B and C are committed
+over the Lagrange basis (n + 2 points: [L_k(tau)], k < n, and the two blinding points) from
+their gate values; since round 6 they are split the same way over that basis (rank r taking
+[r L / W, (r+1) L / W) of L = n + 2; nzcb_msm_table_create_lagrange), their slot carrying
+MSM_LAGRANGE, so all nine commitments of a proof leave rank 0. Per commitment:
 
   rank 0: its scalars cut into W slices (one device copy into the send rows)
   rank 0: header (SCALARS, slot, count)                                  -- broadcast, 24 B
@@ -39,6 +43,12 @@ import ctypes
 import struct
 
 HDR_SCALARS, HDR_GATHER, HDR_STOP = 1, 2, 3
+MSM_LAGRANGE = 0x100   # include/nzcb.h NZCB_MSM_LAGRANGE (the slot of a Lagrange-basis commitment)
+
+
+def split_slot(slot: int) -> tuple:
+    """(slot 0..2, over the Lagrange basis?) of a callback's slot value."""
+    return slot & 0xFF, bool(slot & MSM_LAGRANGE)
 
 
 def point_ranges(n_points: int, world: int) -> list:
@@ -112,11 +122,14 @@ class SplitRoot:
 
     SLOTS = 3   # commitments in flight (csrc/prover.hip)
 
-    def __init__(self, comm: Comm, n_points: int, scalar_source=None):
+    def __init__(self, comm: Comm, n_points: int, scalar_source=None, n_lagrange: int = 0):
         self.comm = comm
         self.ranges = point_ranges(n_points, comm.world)
         self.own_points = self.ranges[0][1]
-        self.row = 32 * max(hi - lo for lo, hi in self.ranges)
+        # n_lagrange = n + 2 splits A, B, C over the Lagrange basis too (0: they stay on rank 0)
+        self.lranges = point_ranges(n_lagrange, comm.world) if n_lagrange else None
+        self.own_lagrange = self.lranges[0][1] if self.lranges else 0
+        self.row = 32 * max(hi - lo for lo, hi in self.ranges + (self.lranges or []))
         # scalar_source(src, lo, cnt, row_tensor): copies scalars [lo, lo + cnt) of the
         # commitment into a send row (device copy by default; tests pass host bytes)
         self.scalar_source = scalar_source or self._device_copy
@@ -136,6 +149,11 @@ class SplitRoot:
                                                             dtype=self.comm.torch.uint8))
 
     def send(self, slot: int, src, count: int):
+        wire_slot = slot
+        slot, lag = split_slot(slot)
+        ranges = self.lranges if lag else self.ranges
+        if ranges is None:
+            raise RuntimeError("msm split: a Lagrange-basis commitment, but no Lagrange ranges (n_lagrange = 0)")
         rows, work = self._rows.get(slot, (None, None))
         if rows is None:
             rows = self.comm.torch.empty((self.comm.world, max(self.row, 1)), dtype=self.comm.torch.uint8,
@@ -144,21 +162,21 @@ class SplitRoot:
             work.wait()         # RCCL: torch's stream waits for it; gloo: the host does
             self.comm.sync()    # and the host waits for torch's stream before refilling
         # fill first: if the source fails, no header is out and the servers stay in step
-        for r, ((lo, _), cnt) in enumerate(zip(self.ranges, slice_counts(count, self.ranges))):
+        for r, ((lo, _), cnt) in enumerate(zip(ranges, slice_counts(count, ranges))):
             if r and cnt:
                 self.scalar_source(src, lo, cnt, rows[r])
-        self.comm.send_header(HDR_SCALARS, slot, count)
+        self.comm.send_header(HDR_SCALARS, wire_slot, count)
         self.stopped = False        # a new serving session (serve() runs until the next STOP)
         out = self.comm.empty(self.row)
         self._rows[slot] = (rows, self.comm.scatter_rows(rows, out))
         self.sent += 1
 
     def gather(self, slot: int, own: bytes) -> bytes:
-        self.comm.send_header(HDR_GATHER, slot, 0)
+        self.comm.send_header(HDR_GATHER, split_slot(slot)[0], 0)
         return self.comm.gather64(own)
 
     def install(self, ctx):
-        ctx.set_msm_split(self.comm.world, self.own_points, self.send, self.gather)
+        ctx.set_msm_split(self.comm.world, self.own_points, self.send, self.gather, self.own_lagrange)
 
     def stop(self):
         """Ends the serving ranks' serve() loop (one STOP per serve() call they make)."""
@@ -175,11 +193,14 @@ class SplitRoot:
         return False
 
 
-def serve(comm: Comm, partial, n_points: int) -> int:
+def serve(comm: Comm, partial, n_points: int, n_lagrange: int = 0, partial_lagrange=None) -> int:
     """Ranks 1..: answer rank 0's commitments until STOP. partial(slot, slice_tensor, count)
-    -> 64 bytes over this rank's point range. Returns the commitments served."""
+    -> 64 bytes over this rank's PTau range; partial_lagrange the same over its range of the
+    n_lagrange Lagrange-basis points (A, B, C; SplitRoot's n_lagrange). Returns the
+    commitments served."""
     ranges = point_ranges(n_points, comm.world)
-    row = 32 * max(hi - lo for lo, hi in ranges)
+    lranges = point_ranges(n_lagrange, comm.world) if n_lagrange else None
+    row = 32 * max(hi - lo for lo, hi in ranges + (lranges or []))
     parts = {}
     served = 0
     while True:
@@ -187,10 +208,14 @@ def serve(comm: Comm, partial, n_points: int) -> int:
         if kind == HDR_STOP:
             return served
         if kind == HDR_SCALARS:
+            slot, lag = split_slot(slot)
+            if lag and (lranges is None or partial_lagrange is None):
+                raise RuntimeError("msm split: a Lagrange-basis commitment, but this rank serves PTau only")
             t = comm.empty(row)
             comm.scatter_rows(None, t).wait()   # the slice has arrived (RCCL: on torch's stream) ...
             comm.sync()   # ... and the host waits for that stream: the backend reads t on its own
-            parts[slot] = partial(slot, t, slice_counts(count, ranges)[comm.rank])
+            cnt = slice_counts(count, lranges if lag else ranges)[comm.rank]
+            parts[slot] = (partial_lagrange if lag else partial)(slot, t, cnt)
             served += 1
         elif kind == HDR_GATHER:
             comm.gather64(parts.pop(slot))
@@ -199,13 +224,19 @@ def serve(comm: Comm, partial, n_points: int) -> int:
 
 
 class GpuRange:
-    """A serving rank's backend: the resident fixed-base table of its PTau range."""
+    """A serving rank's backend: the resident fixed-base table of its PTau range, or (lagrange)
+    of its range of the Lagrange basis, computed from the whole PTau (ptau_n points, 2^log_n
+    domain) on this rank's GPU."""
 
-    def __init__(self, dev_ptau: int, lo: int, hi: int, device: int):
+    def __init__(self, dev_ptau: int, lo: int, hi: int, device: int, lagrange: bool = False, ptau_n: int = 0,
+                 log_n: int = 0):
         import nzcb
         self.nzcb = nzcb
         self.lo, self.hi = lo, hi
-        self.table = nzcb.MsmTable(dev_ptau + 64 * lo, hi - lo, device)
+        if lagrange:
+            self.table = nzcb.MsmTable.lagrange(dev_ptau, ptau_n, log_n, lo, hi, device)
+        else:
+            self.table = nzcb.MsmTable(dev_ptau + 64 * lo, hi - lo, device)
         self.staging = None   # HBM copy of this range's scalars when they arrive in host tensors (gloo)
 
     def __call__(self, slot: int, t, cnt: int) -> bytes:

@@ -63,7 +63,7 @@ def main():
     proofs = sorted(m for m in marks if m[2] == "plonk_prove")[-a.proofs:]
     phases = collections.defaultdict(list)     # phase -> [(s, e)] inside the selected proofs
     for s, e, name in marks:
-        if name == "plonk_prove":
+        if name == "plonk_prove" or e <= s:   # instant marks ("mark: ...") are not phases
             continue
         if any(ps <= s and e <= pe for ps, pe, _ in proofs):
             phases[name].append((s, e))

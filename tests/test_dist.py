@@ -108,19 +108,47 @@ def _bench_env(**extra):
     return env
 
 
-def test_bench_gpus2_spawns_two_ranks_gloo():
-    """`bench.py --gpus 2` with no launcher starts two fresh ranks (torch.distributed.run as
-    a child) and rank 0 reports n_gpus = 2 from the process group."""
+@pytest.mark.parametrize("gpus", [2, 8])
+def test_bench_gpus_spawns_ranks_gloo(gpus):
+    """`bench.py --gpus N` with no launcher starts N fresh ranks (torch.distributed.run as a
+    child) and rank 0 reports n_gpus = N from the process group, one device per rank. N = 8
+    is the driver's scaling run's launch, rehearsed as 8 CPU ranks."""
     import json
     import subprocess
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
-                       env=_bench_env(), capture_output=True, text=True, timeout=300)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--launch-check"],
+                       env=_bench_env(OMP_NUM_THREADS="1"), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(s) for s in r.stdout.splitlines() if s.startswith("{")]
     assert len(lines) == 1
-    assert lines[0]["n_gpus"] == 2 and lines[0]["backend"] == "gloo"
-    assert sorted(x["rank"] for x in lines[0]["ranks"]) == [0, 1]
-    assert [x["device"] for x in sorted(lines[0]["ranks"], key=lambda x: x["rank"])] == [0, 1]
+    assert lines[0]["n_gpus"] == gpus and lines[0]["backend"] == "gloo"
+    assert sorted(x["rank"] for x in lines[0]["ranks"]) == list(range(gpus))
+    assert [x["device"] for x in sorted(lines[0]["ranks"], key=lambda x: x["rank"])] == list(range(gpus))
+
+
+def _build_once_worker(rank, world, port, out):
+    import time
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+
+    def build():
+        t0 = time.time()
+        time.sleep(0.4 if rank == 0 else 0.01)   # rank 0: the cold-cache generation
+        return (t0, time.time())
+
+    out[rank] = bench.build_once(dist, rank, build)
+    dist.destroy_process_group()
+
+
+def test_build_once_rank0_first_gloo():
+    """bench.build_once: on a cold cache rank 0 builds the circuit while ranks 1..7 wait at a
+    barrier, then they build (read the cache); 8 gloo ranks."""
+    world = 8
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_build_once_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = dict(out)
+    end0 = res[0][1]
+    assert all(res[r][0] >= end0 for r in range(1, world))
 
 
 def test_bench_world_mismatch_exits_nonzero():
@@ -140,9 +168,8 @@ def test_shard_edge_cases():
 
 
 # ---- single-proof MSM split across ranks (nzcb/msmsplit.py, configs[4]) ---------------
-def _split_points(n):
+def _split_points(n, tau=0x6E7A6362746175):
     from oracle import bn254 as bn
-    tau = 0x6E7A6362746175
     pts, t = [], 1
     for _ in range(n):
         pts.append(bn.g1_to_lem(bn.g1_mul(bn.G1_GEN, t)))
@@ -150,54 +177,61 @@ def _split_points(n):
     return pts
 
 
+_LAG_TAU = 0x4C6167  # the CPU test's stand-in for the Lagrange basis: another point set
+
+
 def _split_worker(rank, world, port, n, jobs, fail, out):
     """Rank 0 drives the protocol as the prover does (sends of up to three commitments in
-    flight, then gathers); ranks 1.. serve with the CPU port's MSM over their range."""
+    flight, then gathers); ranks 1.. serve with the CPU port's MSM over their range. A batch
+    marked Lagrange (A, B, C: n - 4 = the prover's n + 2 points of another basis) travels
+    with NZCB_MSM_LAGRANGE in its slot and is served from the ranks' Lagrange ranges."""
     import torch.distributed as dist
     from nzcb import msmsplit
     from oracle import cbind
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     comm = msmsplit.Comm(dist, "cpu")
-    pts = _split_points(n)
-    ranges = msmsplit.point_ranges(n, world)
-    lo, hi = ranges[rank]
+    nl = n - 4
+    pts, lpts = _split_points(n), _split_points(nl, _LAG_TAU)
+    ranges, lranges = msmsplit.point_ranges(n, world), msmsplit.point_ranges(nl, world)
 
-    def cpu_partial(own_slice: bytes, cnt):
+    def cpu_partial(own_slice: bytes, cnt, lag=False):
         """This rank's range partial from ITS slice of the scalars (what the scatter sends)."""
         if cnt == 0:
             return bytes(64)
-        return cbind.msm(b"".join(pts[lo:lo + cnt]), own_slice[:32 * cnt], threads=1)
+        lo = (lranges if lag else ranges)[rank][0]
+        return cbind.msm(b"".join((lpts if lag else pts)[lo:lo + cnt]), own_slice[:32 * cnt], threads=1)
 
     if rank == 0:
         def source(src, first, cnt, row):
             import torch
             row[:32 * cnt].copy_(torch.frombuffer(bytearray(src[32 * first:32 * (first + cnt)]), dtype=torch.uint8))
 
-        with msmsplit.SplitRoot(comm, n, scalar_source=source) as root:
-            assert root.own_points == hi
+        with msmsplit.SplitRoot(comm, n, scalar_source=source, n_lagrange=nl) as root:
+            assert root.own_points == ranges[0][1] and root.own_lagrange == lranges[0][1]
             folded = []
-            for batch in jobs:                    # up to 3 commitments in flight, as the prover
+            for lag, batch in jobs:               # up to 3 commitments in flight, as the prover
                 owns = {}
                 for slot, sc in enumerate(batch):
                     count = len(sc) // 32
-                    root.send(slot, sc, count)
-                    owns[slot] = cpu_partial(sc, msmsplit.slice_counts(count, ranges)[0])
+                    root.send(slot | (msmsplit.MSM_LAGRANGE if lag else 0), sc, count)
+                    owns[slot] = cpu_partial(sc, msmsplit.slice_counts(count, lranges if lag else ranges)[0], lag)
                 for slot in range(len(batch)):
-                    folded.append(root.gather(slot, owns[slot]))
+                    folded.append(root.gather(slot | (msmsplit.MSM_LAGRANGE if lag else 0), owns[slot]))
             if fail:
                 # a scalar source that raises sends nothing: the servers stay in step
                 def bad(*_):
                     raise RuntimeError("scalar source failed")
                 root.scalar_source = bad
+                sc = jobs[1][1][0]
                 with pytest.raises(RuntimeError):
-                    root.send(0, jobs[0][0], len(jobs[0][0]) // 32)
+                    root.send(0, sc, len(sc) // 32)
                 root.scalar_source = source
-                sc = jobs[0][0]
                 root.send(0, sc, len(sc) // 32)
                 folded.append(root.gather(0, cpu_partial(sc, msmsplit.slice_counts(len(sc) // 32, ranges)[0])))
         out[0] = folded
     else:
-        out[rank] = msmsplit.serve(comm, lambda slot, t, cnt: cpu_partial(bytes(t.tolist()), cnt), n)
+        out[rank] = msmsplit.serve(comm, lambda slot, t, cnt: cpu_partial(bytes(t.tolist()), cnt), n, nl,
+                                   lambda slot, t, cnt: cpu_partial(bytes(t.tolist()), cnt, True))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -280,8 +314,10 @@ def test_msm_split_async_scatter_ordering_gloo():
 def test_msm_split_across_ranks_gloo(world, fail):
     """Every commitment's folded partials equal the unsplit MSM (C port), for MSM lengths
     shorter than, equal to and crossing the rank boundaries (the prover's n+2 .. n+6). Each
-    serving rank receives only its slice of the scalars. With `fail`, a send whose scalar
-    source raises leaves the protocol in step: the next commitment still folds."""
+    serving rank receives only its slice of the scalars. A proof's nine commitments: A, B, C
+    over the Lagrange basis (round 6, their own point ranges), Z, T1..T3, Wxi, Wxiw over PTau.
+    With `fail`, a send whose scalar source raises leaves the protocol in step:
+    the next commitment still folds."""
     import random
     from oracle import bn254 as bn
     from oracle import cbind
@@ -291,22 +327,25 @@ def test_msm_split_across_ranks_gloo(world, fail):
     def scal(count):
         return b"".join(bn.to_lem(rng.randrange(bn.R_MOD), bn.R_MOD) for _ in range(count))
 
-    jobs = [[scal(66), scal(66), scal(66)], [scal(67)], [scal(64), scal(64), scal(70)], [scal(1), scal(0)]]
+    jobs = [(True, [scal(66), scal(66), scal(66)]), (False, [scal(67)]), (False, [scal(64), scal(64), scal(70)]),
+            (False, [scal(70), scal(67)]), (False, [scal(1), scal(0)])]
     with mp.Manager() as m:
         out = m.dict()
         mp.spawn(_split_worker, args=(world, _free_port(), n, jobs, fail, out), nprocs=world, join=True)
         res = dict(out)
     pts = _split_points(n)
-    flat = [sc for batch in jobs for sc in batch] + ([jobs[0][0]] if fail else [])
+    lpts = _split_points(n - 4, _LAG_TAU)
+    flat = [(lag, sc) for lag, batch in jobs for sc in batch] + ([(False, jobs[1][1][0])] if fail else [])
+    assert sum(len(b) for _, b in jobs[:4]) == 9     # one proof's commitments
     assert [res[r] for r in range(1, world)] == [len(flat)] * (world - 1)
     assert len(res[0]) == len(flat)
-    for sc, parts in zip(flat, res[0]):
+    for (lag, sc), parts in zip(flat, res[0]):
         count = len(sc) // 32
         acc = None
         for r in range(world):
             p = parts[64 * r:64 * r + 64]
             x, y = bn.from_le(p[:32]), bn.from_le(p[32:])
             acc = bn.g1_add(acc, None if x == 0 and y == 0 else (x, y))
-        want = cbind.msm(b"".join(pts[:count]), sc, threads=1) if count else bytes(64)
+        want = cbind.msm(b"".join((lpts if lag else pts)[:count]), sc, threads=1) if count else bytes(64)
         wx, wy = bn.from_le(want[:32]), bn.from_le(want[32:])
         assert acc == (None if wx == 0 and wy == 0 else (wx, wy))

@@ -124,7 +124,8 @@ def test_msm_2p21_witness_scalars_schedules_agree():
     nzcp_live gate values (mostly 0, 1, -1, bytes and short sums, ~5 % full-size), so most
     digits are zero and the bucketing drops them, and bucket 0 (|digit| = 1) holds ~40 %
     of the entries (long carry runs through the finalize's workgroup path). The fixed-base
-    schedule equals the generic one, which keeps every digit, and splits linearly."""
+    schedule equals the generic one, which keeps every digit, and splits linearly; the sparse
+    schedule the prover uses for these scalars (round 6) gives the same point."""
     import random
     import numpy as np
     import nzcb
@@ -148,9 +149,14 @@ def test_msm_2p21_witness_scalars_schedules_agree():
         fixed = _affine(eng.msm_fixed_dev(bases, n, sc, n, False))
         lo = _affine(eng.msm_fixed_dev(bases, h, sc, h, False))
         hi = _affine(eng.msm_fixed_dev(bases + h * 64, n - h, sc + h * 32, n - h, False))
+        # the Lagrange table's schedule (window 17, device-derived chunk, carry trees)
+        sparse = _affine(eng.msm_fixed_dev(bases, n, sc, n, False, window=17, sparse=True))
+        slo = _affine(eng.msm_fixed_dev(bases, h, sc, h, False, window=17, sparse=True))
     finally:
         nzcb.dev_free(sc)
         nzcb.dev_free(bases)
         eng.close()
     assert generic is not None and generic == fixed
     assert bn.g1_add(lo, hi) == fixed
+    assert sparse == fixed
+    assert bn.g1_add(slo, hi) == fixed

@@ -128,8 +128,9 @@ def test_msm_duplicate_and_negated_points(engine):
     assert got == want
 
 
-def _msm_fixed(engine, pts, sc, n_table=None, mont=False):
-    """Fixed-base schedule (shifted-base table, one 2^19-bucket set) via device buffers."""
+def _msm_fixed(engine, pts, sc, n_table=None, mont=False, window=0, sparse=False):
+    """Fixed-base schedule (shifted-base table, one 2^19-bucket set) via device buffers;
+    window / sparse: another table window, the Lagrange table's sparse schedule."""
     import nzcb
     n = len(sc)
     n_table = n_table or n
@@ -140,7 +141,7 @@ def _msm_fixed(engine, pts, sc, n_table=None, mont=False):
         nzcb.h2d(db, bases)
         if scal:
             nzcb.h2d(ds, scal)
-        return _affine(engine.msm_fixed_dev(db, n_table, ds, n, mont))
+        return _affine(engine.msm_fixed_dev(db, n_table, ds, n, mont, window=window, sparse=sparse))
     finally:
         nzcb.dev_free(db)
         nzcb.dev_free(ds)
@@ -175,6 +176,38 @@ def test_msm_fixed_base(engine, n, kind):
     # table built over more bases than the MSM uses (as the prover's n+6 PTau table)
     assert _msm_fixed(engine, pts, sc, n_table=n + 5) == want
     assert _msm_fixed(engine, pts, sc, n_table=n + 5, mont=True) == want
+
+
+@pytest.mark.parametrize("n,kind", [(1, "rand"), (300, "rand"), (300, "zeros"), (3000, "ones"), (1500, "equal"),
+                                    (300, "rminus1"), (300, "top"), (3000, "witness"), (5000, "equal"),
+                                    (2000, "mixed"), (16, "equal")])
+def test_msm_sparse_schedule(engine, n, kind):
+    """The Lagrange table's schedule (round 6, msm.hip dyn_chunk): window 17, the accumulation
+    chunk derived on the device from the entry count (8 entries here), runs of more than four
+    carries through the log-depth piece and bucket trees. "ones" and "equal" put thousands of
+    entries into single buckets (1 to 3 pieces per bucket), "witness" is the A, B, C regime."""
+    rng = random.Random(4000 + n + len(kind))
+    pts = _bases(n + 2, 2 * n + 3)
+    if kind == "rand":
+        sc = [rng.randrange(R_MOD) for _ in range(n)]
+    elif kind == "zeros":
+        sc = [0] * n
+    elif kind == "ones":
+        sc = [1] * n
+    elif kind == "equal":
+        sc = [rng.randrange(R_MOD)] * n
+    elif kind == "rminus1":
+        sc = [R_MOD - 1] * n
+    elif kind == "top":
+        sc = [rng.choice([1 << 253, (1 << 240) - 1, (1 << 16) * 5, R_MOD - (1 << 16)]) for _ in range(n)]
+    elif kind == "witness":
+        sc = [rng.choice([0, 0, 1, 1, 1, R_MOD - 1, rng.randrange(256), rng.randrange(1 << 17),
+                          rng.randrange(R_MOD)]) for _ in range(n)]
+    else:
+        sc = [rng.choice([0, 1, 2, R_MOD - 1, rng.randrange(R_MOD)]) for _ in range(n)]
+    want = bn.msm(pts[:n], sc)
+    assert _msm_fixed(engine, pts, sc, n_table=n + 2, window=17, sparse=True) == want
+    assert _msm_fixed(engine, pts, sc, n_table=n + 2, mont=True, window=17, sparse=True) == want
 
 
 def test_msm_fixed_base_infinity_bases(engine):

@@ -121,18 +121,19 @@ def test_nzcp_live_full_prove_real_circuit():
     sol = nzcb.vk_to_solidity(ctx.vk, "Verifier")
     words = bytes.fromhex(nzcb.proof_to_calldata(res[0][0], b"").split(",")[0][2:])
     assert yul.run_verify_proof(sol, words, _ints(res[0][1]))[0]
-    # configs[4] on one GPU: every split commitment divided into 8 PTau ranges, ranks 1..7
-    # served in-process from resident range tables (what msmsplit.serve does per GPU), the
-    # partials folded in rank order; the proof must not change by a bit
+    # configs[4] on one GPU: every commitment divided into 8 point ranges (PTau for Z, T1..T3,
+    # Wxi, Wxiw; the Lagrange basis for A, B, C since round 6), ranks 1..7 served in-process
+    # from resident range tables (what msmsplit.serve does per GPU), the partials folded in
+    # rank order; the proof must not change by a bit
     from nzcb import msmsplit
     from tests.test_gpu_split import _LocalRanks
     ranks = _LocalRanks(nzcb, msmsplit, zkey, ctx.domain_size + 6, 8)
     try:
         ctx.set_lanes(1)
-        ctx.set_msm_split(8, ranks.ranges[0][1], ranks.send, ranks.gather)
+        ctx.set_msm_split(8, ranks.ranges[0][1], ranks.send, ranks.gather, ranks.own_lagrange)
         split_proof, split_pub = ctx.prove_witness_raw(wit0, bl)
         ctx.set_msm_split(1, 0, None, None)
-        assert ranks.calls == 6 and not ranks.pending     # Z, T1..T3, Wxi, Wxiw split; A, B, C local
+        assert ranks.calls == 9 and ranks.lagrange_calls == 3 and not ranks.pending   # all nine commitments
     finally:
         ranks.close()
     ctx.close()
