@@ -419,11 +419,17 @@ def main():
         launch_points = (n + 6) if probe else pts_per_launch
         mads_t = MADS_PER_ENTRY * launch_entries / (launch_ms / 1e3) / 1e12 if launch_ms else 0.0
         hbm_gbs = MSM_BYTES_PER_POINT * launch_points / (launch_ms / 1e3) / 1e9 if launch_ms else 0.0
-        traffic = None
+        # HBM traffic per launch is a committed PMC measurement (two separate rocprofv3 --pmc
+        # passes, FETCH_SIZE and WRITE_SIZE, tools/profile_round.sh), not this run's: the line
+        # names the file and the run it came from
+        traffic = traffic_source = None
         tf = os.environ.get("NZCB_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "accumulate_traffic.json"))
         if tf and os.path.exists(tf):
             with open(tf) as f:
-                traffic = json.load(f).get("bytes_per_launch")
+                tj = json.load(f)
+            traffic = tj.get("bytes_per_launch")
+            traffic_source = {"file": os.path.relpath(tf, ROOT), "measured": tj.get("source", "round 5 profile set"),
+                              "in_this_run": False}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -478,6 +484,7 @@ def main():
                 "unit": "T v_mad_u64_u32 lane-ops/s",
                 "frac": round(mads_t / MAD_PEAK_T, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_source,
                 "avg_launch_ms": round(launch_ms, 4),
                 "launch_ms_basis": "isolated launches (accumulate_probe, HIP events)" if iso_ms
                                    else "timed region, shared chip (probe skipped)",

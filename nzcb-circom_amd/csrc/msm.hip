@@ -39,6 +39,18 @@ namespace nzcb {
 
 static constexpr int kMsmThreads = 256;
 
+// Wave issue priority of the latency-bound MSM kernels (the fixed-base finalize, carry trees and
+// window sums, the sparse schedule's accumulation): under several proof lanes their few waves
+// share SIMDs with VALU-bound waves (other lanes' bucket accumulations, NTT passes) and got a
+// fraction of the issue slots, which stretched every dependent addition. s_setprio raises
+// them over the co-resident waves in the SIMD's arbitration (0 = off).
+#ifndef NZ_TAIL_PRIO
+#define NZ_TAIL_PRIO 0
+#endif
+__device__ __forceinline__ void tail_prio() {
+  if constexpr (NZ_TAIL_PRIO > 0) __builtin_amdgcn_s_setprio(NZ_TAIL_PRIO);
+}
+
 // Onesweep with a chosen digit width (generic schedule): the 20-bit keys take 2 passes of
 // 10 bits instead of 3 with the library's 8-bit default for gfx950 (2^21: 0.55 vs 0.69 ms)
 using SortConfig = rocprim::radix_sort_config<
@@ -677,7 +689,10 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
   __shared__ uint32_t sidx[kLdsIdx ? kChunk * kLdsStride : 1];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // < 2^32 (entries / chunk)
   const uint32_t M = offsets[nkeys];
-  if (!kLdsIdx && !chunk) chunk = dyn_chunk(M);  // sparse tables: derived from the entry count
+  if (!kLdsIdx && !chunk) {  // sparse tables: derived from the entry count
+    chunk = dyn_chunk(M);
+    tail_prio();
+  }
   if (kLdsIdx) {  // every thread of the workgroup takes part before any exits
     const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * kChunk;
     for (uint32_t j = threadIdx.x; j < kMsmThreads * kChunk; j += kMsmThreads) {
@@ -820,6 +835,7 @@ __global__ void __launch_bounds__(kMsmThreads)
 msm_finalize29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys, uint32_t span,
                       const Xyzz29* __restrict__ carry_own, const Xyzz29* __restrict__ carry_cont,
                       uint32_t* __restrict__ large, Xyzz29* __restrict__ out29) {
+  tail_prio();
   __shared__ uint32_t pk[kMsmThreads], pu[kMsmThreads], pe[kMsmThreads];
   __shared__ uint32_t cnt;
   if (threadIdx.x == 0) cnt = 0;
@@ -969,6 +985,7 @@ __device__ __forceinline__ uint32_t carry_span(uint32_t chunk, const uint32_t* o
 __global__ void __launch_bounds__(1024)
 msm_large_scan_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, uint32_t nkeys,
                       const uint32_t* __restrict__ large, uint32_t* __restrict__ off) {
+  tail_prio();
   __shared__ uint32_t sh[1024];
   const uint32_t count = large[0];
   const uint32_t ch = chunk ? chunk : dyn_chunk(offsets[nkeys]);
@@ -1029,6 +1046,7 @@ msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, u
                          const uint32_t* __restrict__ large, const uint32_t* __restrict__ off,
                          const Xyzz29* __restrict__ carry_own, const Xyzz29* __restrict__ carry_cont,
                          Xyzz29* __restrict__ part) {
+  tail_prio();
   __shared__ Xyzz29 sh[kSumThreads];
   const uint32_t count = large[0];
   const uint32_t total = off[count];
@@ -1057,6 +1075,7 @@ msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, u
 __global__ void __launch_bounds__(kSumThreads)
 msm_large_final29_kernel(const uint32_t* __restrict__ large, const uint32_t* __restrict__ off,
                          const Xyzz29* __restrict__ part, Xyzz29* __restrict__ out29) {
+  tail_prio();
   __shared__ Xyzz29 sh[kSumThreads];
   const uint32_t count = large[0];
   for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
@@ -1139,6 +1158,7 @@ static constexpr int kLineThreads = 8;  // a power of two dividing 64
 __global__ void __launch_bounds__(256)
 msm_tile29_kernel(const Xyzz29* __restrict__ buckets, const uint32_t* __restrict__ offsets, int a, int ltiles,
                   int htiles, Xyzz29* __restrict__ rowp, Xyzz29* __restrict__ colp) {
+  tail_prio();
   // [0, 256): the tile's buckets, then the row tree in place; [256, 384): the column tree
   __shared__ Xyzz29 sh[384];
   const int tid = threadIdx.x;
@@ -1196,6 +1216,7 @@ static constexpr int kStripMinC = 19;  // the tiles stay for c <= 18 (2^16 bucke
 __global__ void __launch_bounds__(256)
 msm_strips29_kernel(const Xyzz29* __restrict__ buckets, const uint32_t* __restrict__ offsets, int a, int hb,
                     Xyzz29* __restrict__ rowp, Xyzz29* __restrict__ colp) {
+  tail_prio();
   const int RJ = (1 << a) / kStrip, CI = (1 << hb) / kStrip;
   const size_t nrow = (size_t)RJ << hb, ncol = (size_t)CI << a;
   const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -1245,6 +1266,7 @@ __device__ __forceinline__ Xyzz29 shfl_xor29(const Xyzz29& v, int m) {
 __global__ void __launch_bounds__(256)
 msm_lines29_kernel(const Xyzz29* __restrict__ rowp, int ltiles, const Xyzz29* __restrict__ colp, int htiles,
                    int nrows, int ncols, Xyzz29* __restrict__ lines) {
+  tail_prio();
   constexpr int LG = kLineThreads == 8 ? 3 : kLineThreads == 4 ? 2 : kLineThreads == 16 ? 4 : 1;
   static_assert((1 << LG) == kLineThreads, "kLineThreads: 2, 4, 8 or 16");
   const int g = (int)((blockIdx.x * 256 + threadIdx.x) / kLineThreads);
@@ -1271,9 +1293,14 @@ msm_lines29_kernel(const Xyzz29* __restrict__ rowp, int ltiles, const Xyzz29* __
 }
 
 // slot s < hb: the rows with bit s set; hb <= s < hb + a: the columns with bit s - hb set;
-// s = hb + a: every column. Converted to the 8x32 layout for the host.
+// s = hb + a: every column. Converted to the 8x32 layout and written straight into the
+// scratch's pinned host_win (round 6: the copy after the kernel was one more blit dispatch per
+// MSM, queued behind the other lanes' kernels), with the bucketed entry count when total_out
+// is set (kernel statistics).
 __global__ void __launch_bounds__(kSumThreads)
-msm_slots29_kernel(const Xyzz29* __restrict__ lines, int hb, int a, G1xyzz* __restrict__ out) {
+msm_slots29_kernel(const Xyzz29* __restrict__ lines, int hb, int a, G1xyzz* __restrict__ out,
+                   const uint32_t* __restrict__ entries, uint32_t* __restrict__ total_out) {
+  tail_prio();
   __shared__ Xyzz29 sh[kSumThreads];
   const int s = blockIdx.x;
   const bool rows = s < hb;
@@ -1288,7 +1315,11 @@ msm_slots29_kernel(const Xyzz29* __restrict__ lines, int hb, int a, G1xyzz* __re
     rhs = src[plain ? q : (((q >> b) << (b + 1)) | (1 << b) | (q & ((1 << b) - 1)))];
     return true;
   });
-  if (threadIdx.x == 0) out[s] = load_point(r);
+  if (threadIdx.x == 0) {
+    out[s] = load_point(r);
+    if (s == 0 && total_out) *total_out = *entries;
+    __threadfence_system();  // host memory: complete before the kernel is
+  }
 }
 
 // Shifted-base table: row w = 2^(c*w) * B_i, thread per base (c doublings per row,
@@ -1441,7 +1472,8 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
   parts.alloc(max_parts ? max_parts : 1);
   win.alloc(max_slots);
   host_win_cap = max_slots;
-  NZ_HIP(hipHostMalloc((void**)&host_win, (max_slots + 1) * sizeof(G1xyzz), hipHostMallocDefault));
+  // coherent: the fixed-base window sums are written here by msm_slots29_kernel
+  NZ_HIP(hipHostMalloc((void**)&host_win, (max_slots + 1) * sizeof(G1xyzz), hipHostMallocCoherent));
   host_total = (uint32_t*)(host_win + max_slots);  // one more slot: the profiled entry count
 }
 
@@ -1640,12 +1672,10 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                        sc.lines29.p);
     NZ_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_slots29_kernel, dim3(p.hb + p.a + 1), dim3(kSumThreads), 0, st,
-                       (const Xyzz29*)sc.lines29.p, p.hb, p.a, sc.win.p);
+                       (const Xyzz29*)sc.lines29.p, p.hb, p.a, sc.host_win, (const uint32_t*)sc.offsets.p + p.nkeys,
+                       sc.prof ? sc.host_total : nullptr);
     NZ_HIP(hipGetLastError());
     mark(7);
-    if (sc.prof) NZ_HIP(hipMemcpyAsync(sc.host_total, sc.offsets.p + p.nkeys, 4, hipMemcpyDeviceToHost, st));
-    NZ_HIP(hipMemcpyAsync(sc.host_win, sc.win.p, (size_t)(p.hb + p.a + 1) * sizeof(G1xyzz), hipMemcpyDeviceToHost,
-                          st));
     NZ_HIP(hipEventRecord(sc.done, st));
     return;
   }

@@ -101,12 +101,20 @@ struct Prover {
   DevBuf<Fr> eval_part;           // partial sums of polynomial evaluations
   DevBuf<F29> eval_pw;            // the evaluation points' powers x^t, t < 256
   DevBuf<uint32_t> flags;
-  std::vector<Fr> host_part;
+  std::vector<Fr> host_part;  // (unused since round 6: the evaluations land in the mailbox)
   DevBuf<uint32_t> ntt_scr2;      // Z's transforms' inter-pass scratch (beside A, B, C's on aux[2])
-  // pinned: the top six coefficients of A, B, C and Z for round 3's t recombination, then
-  // the check flags
+  // The proof's mailbox (round 6): coherent pinned host memory that the
+  // kernels producing the host's small per-proof inputs write directly, instead of one
+  // hipMemcpyAsync (a blit dispatch that queued behind the other lanes' kernels) each:
+  //   [0, 24) the top coefficients of A, B, C and Z (round 3's t recombination; k_tops)
+  //   [24]    the check flags word (k_tops, k_div_check)
+  //   [25, 27) prod num / prod den (round 2's copy check; k_perm_factors)
+  //   [27, 27 + kEvalMax) evaluations (k_eval_sum)
+  //   then A's nPublic public-gate values (the beta transcript) and witness[1..nPublic]
+  //   (the public signals), both written by k_build_abc
   Fr* top_host = nullptr;
-  static constexpr int kTopWords = 4 * 6 + 1;
+  static constexpr int kMbFlags = 24, kMbTotals = 25, kMbEvals = 27, kMbEvalMax = 8;
+  size_t mb_apub = 0, mb_pubw = 0, mb_words = 0;
 
   int fault = 0;  // nzcb_debug_inject_fault: NZCB_FAULT_* / NZCB_DEBUG_* for this lane's next proof
   // timings of the last proof (ms): [0..6] host wall clock of the whole proof and its

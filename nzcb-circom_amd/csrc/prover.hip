@@ -49,11 +49,22 @@ __global__ void k_additions(const AddRec* __restrict__ recs, uint32_t count, Fr*
   wit[r.dst] = r.ac * a + r.bc * b;
 }
 
+// Host writes of small results (the prover's mailbox, coherent pinned memory): visible to the
+// host before the kernel's completion is (the fence completes the stores over the fabric)
+__device__ __forceinline__ void mailbox_fence() { __threadfence_system(); }
+
 __global__ void k_build_abc(const uint32_t* __restrict__ am, const uint32_t* __restrict__ bm,
                             const uint32_t* __restrict__ cm, uint32_t nc, uint32_t n, const Fr* __restrict__ wit,
-                            uint32_t nvars, Fr* __restrict__ A, Fr* __restrict__ B, Fr* __restrict__ C) {
+                            uint32_t nvars, Fr* __restrict__ A, Fr* __restrict__ B, Fr* __restrict__ C,
+                            uint32_t npub, Fr* __restrict__ mb_apub, Fr* __restrict__ mb_pubw) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i < npub) {  // the public signals witness[1..nPublic] into the mailbox (Prover::prove's output)
+    mb_pubw[i] = 1 + i < nvars ? wit[1 + i] : Fr::zero();
+  }
+  if (i >= n) {
+    if (i < npub) mailbox_fence();
+    return;
+  }
   Fr a = Fr::zero(), b = Fr::zero(), c = Fr::zero();
   if (i < nc) {
     uint32_t ia = am[i], ib = bm[i], ic = cm[i];
@@ -64,6 +75,27 @@ __global__ void k_build_abc(const uint32_t* __restrict__ am, const uint32_t* __r
   A[i] = a;
   B[i] = b;
   C[i] = c;
+  if (i < npub) {  // A's public-gate values: the beta transcript's public inputs (round 2)
+    mb_apub[i] = a;
+    mailbox_fence();
+  }
+}
+
+// round 3's host inputs in one dispatch: the top coefficients of A, B, C (n-4 .. n+1) and Z
+// (n-3 .. n+2) and the flags word, into the mailbox (five copies until round 6)
+__global__ void k_tops(const Fr* __restrict__ pa, const Fr* __restrict__ pb, const Fr* __restrict__ pc,
+                       const Fr* __restrict__ pz, size_t n, const uint32_t* __restrict__ flags, Fr* __restrict__ mb) {
+  const int t = threadIdx.x;  // 32 threads
+  if (t < 24) {
+    const int k = t / 6, j = t % 6;
+    const Fr* src = k == 0 ? pa + (n - 4) : k == 1 ? pb + (n - 4) : k == 2 ? pc + (n - 4) : pz + (n - 3);
+    mb[t] = src[j];
+  } else if (t == 24) {
+    Fr f = Fr::zero();
+    f.v[0] = *flags;
+    mb[24] = f;
+  }
+  mailbox_fence();
 }
 
 struct BlindIdx {
@@ -428,7 +460,7 @@ k_perm_tile(const Fr* __restrict__ A, const Fr* __restrict__ B, const Fr* __rest
 // single-lane Fermat inversion here was most of this kernel's 0.6 ms.
 __global__ void __launch_bounds__(1024)
 k_perm_factors(const Fr* __restrict__ ntot, const Fr* __restrict__ dtot, int ntiles, Fr* __restrict__ F,
-               Fr* __restrict__ totals) {
+               Fr* __restrict__ totals) {  // totals: the mailbox (host memory)
   __shared__ Fr sh[1024 / 64];  // the scans' wave totals
   const int tid = threadIdx.x;
   const int per = (ntiles + 1023) / 1024;
@@ -445,6 +477,7 @@ k_perm_factors(const Fr* __restrict__ ntot, const Fr* __restrict__ dtot, int nti
   if (tid == 0) {
     totals[0] = nall;
     totals[1] = dall;
+    mailbox_fence();
   }
   // within the run: prefix of N (forward), suffix of D (backward)
   Fr run = npre;
@@ -884,7 +917,10 @@ __global__ void __launch_bounds__(kT) k_eval_sum(const Fr* __restrict__ partial,
   Fr acc = Fr::zero();
   for (int b = (int)threadIdx.x; b < nblocks; b += kT) acc = acc + partial[(size_t)j * nblocks + b];
   const Fr r = block_sum_fr(acc, sh);
-  if (threadIdx.x == 0) out[j] = r;
+  if (threadIdx.x == 0) {
+    out[j] = r;  // the mailbox (host memory)
+    mailbox_fence();
+  }
 }
 
 struct RArgs {
@@ -926,10 +962,12 @@ __global__ void k_pol_wxi(const Fr* __restrict__ t, const Fr* __restrict__ pr, c
 
 // "Polinomial does not divide": P0 == -d * q0
 __global__ void k_div_check(const Fr* __restrict__ src, Fr p0_adjust, const Fr* __restrict__ q, Fr d,
-                            uint32_t* flags, uint32_t bit) {
+                            uint32_t* flags, uint32_t bit, uint32_t* __restrict__ mb_flags) {
   if (threadIdx.x || blockIdx.x) return;
   Fr p0 = src[0] - p0_adjust;
   if (!(p0 + d * q[0]).is_zero()) atomicOr(flags, bit);
+  *mb_flags = *flags;  // the flags word as of this check, into the mailbox
+  mailbox_fence();
 }
 
 __global__ void k_root_table(Fr* __restrict__ out, Fr base, Fr scale, size_t count) {
@@ -1120,7 +1158,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     ltau.alloc((size_t)n + 2);
     lagrange_basis(ptau.p, ptau.n, power, ltau.p, s);
     ltab.build(ltau.p, ltau.n, lagrange_window(), s);
-    ltab.sparse = true;  // small gate values: msm.hip's sparse schedule
+    ltab.sparse = std::getenv("NZCB_SPARSE") == nullptr || std::atoi(std::getenv("NZCB_SPARSE")) != 0;  // A/B (round 6)
   }
   up(qm, z.qm);
   up(ql, z.ql);
@@ -1322,8 +1360,12 @@ void Prover::init_slots() {
   NZ_HIP(hipEventCreateWithFlags(&side_ready, hipEventDisableTiming));
   NZ_HIP(hipEventCreateWithFlags(&side_done, hipEventDisableTiming));
   NZ_HIP(hipEventCreateWithFlags(&pows_done, hipEventDisableTiming));
-  NZ_HIP(hipHostMalloc((void**)&top_host, kTopWords * sizeof(Fr), hipHostMallocDefault));
-  std::memset((void*)top_host, 0, kTopWords * sizeof(Fr));
+  mb_apub = kMbEvals + kMbEvalMax;
+  mb_pubw = mb_apub + nPublic;
+  mb_words = mb_pubw + nPublic;
+  // coherent: the kernels' stores reach host memory without a cache writeback
+  NZ_HIP(hipHostMalloc((void**)&top_host, mb_words * sizeof(Fr), hipHostMallocCoherent));
+  std::memset((void*)top_host, 0, mb_words * sizeof(Fr));
 }
 
 // per-proof working set (one per lane)
@@ -1418,12 +1460,11 @@ void Prover::launch_gate_check(hipStream_t s) {
 }
 
 void Prover::copy_tops(hipStream_t s) {
-  const Fr* src[4] = {pol_a.p + (n - 4), pol_b.p + (n - 4), pol_c.p + (n - 4), pol_z.p + (n - 3)};
-  for (int k = 0; k < 4; k++)
-    NZ_HIP(hipMemcpyAsync(top_host + 6 * k, src[k], 6 * sizeof(Fr), hipMemcpyDeviceToHost, s));
-  NZ_HIP(hipMemcpyAsync(top_host + 24, flags.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  hipLaunchKernelGGL(k_tops, dim3(1), dim3(32), 0, s, pol_a.p, pol_b.p, pol_c.p, pol_z.p, (size_t)n,
+                     (const uint32_t*)flags.p, top_host);
+  NZ_HIP(hipGetLastError());
   NZ_HIP(hipStreamSynchronize(s));
-  if (*(const uint32_t*)(top_host + 24) & 1u) throw Error(NZCB_ERR_T_DIV, "T Polynomial is not divisible");
+  if (top_host[kMbFlags].v[0] & 1u) throw Error(NZCB_ERR_T_DIV, "T Polynomial is not divisible");
 }
 
 void Prover::round3_quot3(const Fr& beta, const Fr& gamma, const Fr& alpha, hipStream_t s) {
@@ -1712,12 +1753,13 @@ void Prover::eval_many(int np, const Fr* const* polys, const size_t* lens, const
   else
     throw Error(NZCB_ERR_INTERNAL, "eval_many: 1 or 7 evaluations");
   NZ_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_eval_sum, dim3(np), dim3(kT), 0, s, (const Fr*)eval_part.p, (int)nblocks, res);
+  (void)res;
+  hipLaunchKernelGGL(k_eval_sum, dim3(np), dim3(kT), 0, s, (const Fr*)eval_part.p, (int)nblocks,
+                     top_host + kMbEvals);  // the mailbox
   NZ_HIP(hipGetLastError());
-  NZ_HIP(hipMemcpyAsync(host_part.data(), res, np * sizeof(Fr), hipMemcpyDeviceToHost, s));
   if (overlap) overlap();  // host work beside the evaluation kernels
   NZ_HIP(hipStreamSynchronize(s));
-  for (int j = 0; j < np; j++) out[j] = host_part[j];
+  for (int j = 0; j < np; j++) out[j] = top_host[kMbEvals + j];
 }
 
 // divPol1's power tables for d (k_lin_tile's LinTab) into slot k of lin_tab: host products,
@@ -1754,7 +1796,8 @@ void Prover::div_pol1(const Fr* src, size_t m, int tab, const Fr& p0_adjust, Fr*
   hipLaunchKernelGGL(k_tile_heads, dim3(1), dim3(1024), 0, s, heads, (int)ntiles, q, q + lin_qn);
   NZ_HIP(hipGetLastError());
   hipLaunchKernelGGL(k_lin_tile<true>, dim3((unsigned)ntiles), dim3(kT), 0, s, src, m, lt, (const Fr*)heads, dst);
-  hipLaunchKernelGGL(k_div_check, dim3(1), dim3(64), 0, s, src, p0_adjust, dst, ht.dp[1], flags.p, flag_bit);
+  hipLaunchKernelGGL(k_div_check, dim3(1), dim3(64), 0, s, src, p0_adjust, dst, ht.dp[1], flags.p, flag_bit,
+                     (uint32_t*)(top_host + kMbFlags));
   NZ_HIP(hipGetLastError());
 }
 
@@ -1852,8 +1895,9 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       hipLaunchKernelGGL(k_additions, dim3(grid_for(a1 - a0, kT, 1u << 30)), dim3(kT), 0, s, adds.p + a0, a1 - a0,
                          wit.p);
   }
-  hipLaunchKernelGGL(k_build_abc, dim3(grid_for(n, kT, 1u << 30)), dim3(kT), 0, s, amap.p, bmap.p, cmap.p,
-                     nConstraints, n, wit.p, nVars, A.p, B.p, C.p);
+  hipLaunchKernelGGL(k_build_abc, dim3(grid_for(std::max<size_t>(n, nPublic), kT, 1u << 30)), dim3(kT), 0, s,
+                     amap.p, bmap.p, cmap.p, nConstraints, n, wit.p, nVars, A.p, B.p, C.p, nPublic,
+                     top_host + mb_apub, top_host + mb_pubw);
   NZ_HIP(hipGetLastError());
   NZ_HIP(hipStreamSynchronize(s));
   tm[1] = ms_since(T0);
@@ -1911,11 +1955,8 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   ranges.next("round2: grand product Z + commit");
   auto t2 = std::chrono::steady_clock::now();
   Fr beta, gamma;
-  std::vector<Fr> Apub(nPublic);
-  if (nPublic) {
-    NZ_HIP(hipMemcpyAsync(Apub.data(), A.p, nPublic * sizeof(Fr), hipMemcpyDeviceToHost, s));
-    NZ_HIP(hipStreamSynchronize(s));
-  }
+  // A's public-gate values came with k_build_abc (mailbox; the witness phase synchronized)
+  const Fr* Apub = top_host + mb_apub;
   {
     std::vector<uint8_t> tr;
     if (transcript_public) {
@@ -1957,12 +1998,11 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     hipLaunchKernelGGL(k_perm_tile, dim3((unsigned)ntiles), dim3(kT), 0, s, A.p, B.p, C.p, sig_h.p, (size_t)n,
                        w_h.p, pa, Z.p, ntot, dtot);
     hipLaunchKernelGGL(k_perm_factors, dim3(1), dim3(1024), 0, s, (const Fr*)ntot, (const Fr*)dtot, (int)ntiles,
-                       fac, totals);
+                       fac, top_host + kMbTotals);
     NZ_HIP(hipGetLastError());
     // Z[n] = prod num / prod den must be 1; 1 / prod den scales the tiles
-    Fr tt[2];
-    NZ_HIP(hipMemcpyAsync(tt, totals, sizeof(tt), hipMemcpyDeviceToHost, s));
     NZ_HIP(hipStreamSynchronize(s));
+    const Fr tt[2] = {top_host[kMbTotals], top_host[kMbTotals + 1]};
     if (tt[0] != tt[1]) throw Error(NZCB_ERR_COPY, "Copy constraints does not match");
     hipLaunchKernelGGL(k_apply_tiles, dim3((unsigned)ntiles), dim3(kT), 0, s, Z.p, (size_t)n,
                        (const Fr*)fac, inverse(tt[1]));
@@ -2149,9 +2189,8 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
     div_pol1(pol_z.p, n + 3, 1, ezw, pol_wxiw.p, 4u);
     lg("multiexp Wxiw");
     commit_start(1, pol_wxiw.p, n + 3);
-    uint32_t f = 0;
-    NZ_HIP(hipMemcpyAsync(&f, flags.p, 4, hipMemcpyDeviceToHost, s));
-    NZ_HIP(hipStreamSynchronize(s));
+    NZ_HIP(hipStreamSynchronize(s));  // the two division checks' flags are in the mailbox
+    const uint32_t f = top_host[kMbFlags].v[0];
     pWxi = commit_finish(0);
     pWxiw = commit_finish(1);
     if (f & 4u) throw Error(NZCB_ERR_DIVPOL, "Polinomial does not divide");
@@ -2177,19 +2216,10 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   }
   const Fr* ev[7] = {&ea, &eb, &ec, &es1, &es2, &ezw, &er};
   for (int i = 0; i < 7; i++) fr_to_le_normal(*ev[i], proof_out + 9 * 64 + 32 * i);
-  std::vector<uint8_t> pubw((size_t)nPublic * 32);
-  if (nPublic) {
-    if (witness_on_device) {
-      NZ_HIP(hipMemcpyAsync(pubw.data(), witness + 32, pubw.size(), hipMemcpyDeviceToHost, s));
-      NZ_HIP(hipStreamSynchronize(s));
-    } else {
-      std::memcpy(pubw.data(), witness + 32, pubw.size());
-    }
-  }
   for (uint32_t i = 0; i < nPublic; i++) {
-    // publicSignals = witness[1..nPublic] as given (normal form, reduced)
-    Fr m = fr_from_le_normal(pubw.data() + 32 * (size_t)i);
-    fr_to_le_normal(m, pub_out + 32 * (size_t)i);
+    // publicSignals = witness[1..nPublic] (normal form, reduced): k_build_abc wrote their
+    // Montgomery forms into the mailbox
+    fr_to_le_normal(top_host[mb_pubw + i], pub_out + 32 * (size_t)i);
   }
 }
 

@@ -4,6 +4,9 @@
 //   node cli.js plonk setup     <circuit.r1cs> <pot.ptau> <circuit.zkey>
 //   node cli.js plonk prove     <circuit.zkey> <witness.wtns> <proof.json> <public.json>
 //   node cli.js plonk fullprove <input.json> <circuit.wasm> <circuit.zkey> <proof.json> <public.json>
+//   node cli.js plonk verify    <verification_key.json> <public.json> <proof.json>
+//     (prints "OK!" and exits 0 for a valid proof, "Invalid proof" and exit code 1 otherwise,
+//     as snarkjs's CLI verb; host only, no GPU)
 // and `snarkjs zkey export verificationkey|solidityverifier|soliditycalldata` (Makefile:56-62):
 //   node cli.js zkey export verificationkey <circuit.zkey> <verification_key.json>
 //   node cli.js zkey export solidityverifier <circuit.zkey> <Verifier.sol> [contract name]
@@ -16,6 +19,7 @@ function usage() {
   console.error('usage: cli.js plonk setup <r1cs> <ptau> <zkey>\n' +
                 '       cli.js plonk prove <zkey> <wtns> <proof.json> <public.json>\n' +
                 '       cli.js plonk fullprove <input.json> <wasm> <zkey> <proof.json> <public.json>\n' +
+                '       cli.js plonk verify <verification_key.json> <public.json> <proof.json>\n' +
                 '       cli.js zkey export verificationkey <zkey> <verification_key.json>\n' +
                 '       cli.js zkey export solidityverifier <zkey> <verifier.sol> [contract name]\n' +
                 '       cli.js zkey export soliditycalldata <public.json> <proof.json>');
@@ -47,6 +51,14 @@ async function main(argv) {
   if (argv[1] === 'setup' && argv.length === 5) {
     await nz.plonk.setup(argv[2], argv[3], argv[4], logger);
     return;
+  }
+  if (argv[1] === 'verify' && argv.length === 5) {
+    const vk = JSON.parse(fs.readFileSync(argv[2], 'utf8'));
+    const pub = JSON.parse(fs.readFileSync(argv[3], 'utf8'));
+    const proof = JSON.parse(fs.readFileSync(argv[4], 'utf8'));
+    const ok = await nz.plonk.verify(vk, pub, proof, logger);
+    console.log(ok ? 'OK!' : 'Invalid proof');
+    process.exit(ok ? 0 : 1);
   }
   if (argv[1] === 'prove' && argv.length === 6) {
     res = await nz.plonk.prove(argv[2], argv[3], logger);

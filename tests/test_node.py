@@ -160,6 +160,35 @@ def test_cli_plonk_prove_verifies(tmp_path):
     assert plonk.verify_with_trapdoor(zk, pub, pt, meta["tau"])
 
 
+@needs_node
+def test_cli_plonk_verify(tmp_path):
+    """`node cli.js plonk verify <verification_key.json> <public.json> <proof.json>` (the
+    `snarkjs plonk verify` verb): the golden proof prints OK! and exits 0; a
+    tampered evaluation or public signal prints "Invalid proof" and exits 1. Host only."""
+    meta = json.load(open(os.path.join(GOLD, "p8.json")))
+    vk = tmp_path / "verification_key.json"
+    p = subprocess.run(["node", os.path.join(JS, "cli.js"), "zkey", "export", "verificationkey",
+                        os.path.join(GOLD, "p8.zkey"), str(vk)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    exp = meta["proofs"]["fixed"]
+
+    def verify(proof, pub):
+        pf, pb = tmp_path / "proof.json", tmp_path / "public.json"
+        pf.write_text(json.dumps(proof))
+        pb.write_text(json.dumps(pub))
+        return subprocess.run(["node", os.path.join(JS, "cli.js"), "plonk", "verify", str(vk), str(pb), str(pf)],
+                              capture_output=True, text=True, timeout=120)
+
+    ok = verify(exp["proof"], exp["publicSignals"])
+    assert ok.returncode == 0 and ok.stdout.strip() == "OK!", ok.stderr
+    bad_proof = dict(exp["proof"], eval_a=str((int(exp["proof"]["eval_a"]) + 1)))
+    r = verify(bad_proof, exp["publicSignals"])
+    assert r.returncode == 1 and r.stdout.strip() == "Invalid proof"
+    bad_pub = [str(int(exp["publicSignals"][0]) + 1)] + exp["publicSignals"][1:]
+    r = verify(exp["proof"], bad_pub)
+    assert r.returncode == 1 and r.stdout.strip() == "Invalid proof"
+
+
 EXAMPLE_PASS_URI = (  # /root/reference/test/nzcp.js:71 (MoH example pass)
     "NZCP:/1/2KCEVIQEIVVWK6JNGEASNICZAEP2KALYDZSGSZB2O5SWEOTOPJRXALTDN53GSZBRHEXGQZLBNR2GQLTOPICRUYMBTIFAIGTUKBAA"
     "UYTWMOSGQQDDN5XHIZLYOSBHQJTIOR2HA4Z2F4XXO53XFZ3TGLTPOJTS6MRQGE4C6Y3SMVSGK3TUNFQWY4ZPOYYXQKTIOR2HA4Z2F4XW46"
