@@ -96,6 +96,11 @@ int nzcb_engine_msm_fixed_dev(nzcb_engine* e, const void* bases, size_t n_table,
  * carry trees; msm.hip dyn_chunk). */
 int nzcb_engine_msm_table_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* scalars, size_t n,
                               int scalars_mont, int window, int sparse, uint8_t* out_affine, nzcb_err* err);
+/* `sets` (1..3) MSMs of n scalars each (device pointers scalars[0..sets)) over ONE Lagrange-window
+ * table of the first n_table bases in one schedule (msm.hip msm_enqueue_sets: the prover's A, B,
+ * C commitments since round 6); out_affine: sets x 64 bytes. */
+int nzcb_engine_msm_sets_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* const* scalars, int sets,
+                             size_t n, int scalars_mont, uint8_t* out_affine, nzcb_err* err);
 /* Per-phase MSM timing (HIP events, average over reps after three warm-up runs):
  * out[0] wall ms, out[1..7] keys, sort, offsets, accumulate, finalize, reduce, sums,
  * out[8] table build ms (fixed_base only), out[9] bucket entries per MSM (nonzero digits),

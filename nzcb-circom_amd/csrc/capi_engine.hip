@@ -347,6 +347,26 @@ int nzcb_engine_msm_table_dev(nzcb_engine* e, const void* bases, size_t n_table,
   NZ_GUARD_END(err)
 }
 
+int nzcb_engine_msm_sets_dev(nzcb_engine* e, const void* bases, size_t n_table, const void* const* scalars, int sets,
+                             size_t n, int scalars_mont, uint8_t* out_affine, nzcb_err* err) {
+  NZ_GUARD_BEGIN
+  Engine& g = e->eng;
+  NZ_HIP(hipSetDevice(g.device));
+  if (n > n_table) throw Error(NZCB_ERR_ARG, "msm larger than its base table");
+  if (sets < 1 || sets > 3 || !scalars) throw Error(NZCB_ERR_ARG, "msm sets: 1..3 scalar vectors");
+  MsmBaseTable t;
+  t.build((const G1Affine*)bases, n_table, lagrange_window(), g.stream);
+  t.sparse = true;
+  MsmScratch sc;
+  sc.init(n ? n : 1, true, 3, false);
+  G1xyzz r[3];
+  msm_enqueue_sets(sc, (const Fr* const*)scalars, sets, n, scalars_mont != 0, g.stream, &t);
+  msm_finish_sets(sc, g.stream, r);
+  for (int k = 0; k < sets; k++) affine_out(r[k], out_affine + 64 * k);
+  return 0;
+  NZ_GUARD_END(err)
+}
+
 int nzcb_engine_time_msm2(nzcb_engine* e, const void* bases, const void* scalars, size_t n, int scalars_mont,
                           int fixed_base, int reps, double* out, nzcb_err* err) {
   NZ_GUARD_BEGIN
@@ -439,7 +459,7 @@ nzcb_msm_table* nzcb_msm_table_create(int device, const void* dev_bases, size_t 
       t->n = n;
       NZ_HIP(hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking));
       t->table.build((const G1Affine*)dev_bases, n, fixed_base_window(), t->st);
-      t->sc.init(n, true);
+      t->sc.init(n, true, 1, false);
       NZ_HIP(hipStreamSynchronize(t->st));
     } catch (...) {
       delete t;
@@ -474,7 +494,7 @@ nzcb_msm_table* nzcb_msm_table_create_lagrange(int device, const void* dev_ptau,
         t->table.sparse = true;
         NZ_HIP(hipStreamSynchronize(t->st));
       }
-      t->sc.init(hi - lo, true);
+      t->sc.init(hi - lo, true, 1, false);
     } catch (...) {
       delete t;
       throw;

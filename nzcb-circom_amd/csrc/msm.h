@@ -34,6 +34,7 @@ int lagrange_window();
 
 struct MsmScratch {
   size_t max_points = 0;
+  int max_lsets = 1;  // Lagrange-table MSMs one schedule can take at once (msm_enqueue_sets)
   DevBuf<uint32_t> offsets;   // first sorted position of each bucket key, + total at the end
   DevBuf<uint32_t> sorted;    // base index | sign << 31, grouped by bucket
   DevBuf<uint32_t> keys_in, keys_out, vals_in;
@@ -64,6 +65,7 @@ struct MsmScratch {
   int cur_c = 0, cur_nsets = 0, cur_nbits = 0, cur_seglen = 0;
   bool cur_fixed = false, cur_sparse = false;
   int cur_a = 0, cur_hb = 0;  // fixed base: column / row bits of the window sum
+  int cur_msets = 1;          // fixed base: MSMs in the schedule (msm_enqueue_sets)
   size_t cur_n = 0;
   uint32_t cur_nkeys = 0;
   // optional HIP-event timing: accumulation kernel (bench.py roofline) and, with
@@ -77,7 +79,9 @@ struct MsmScratch {
   uint64_t prof_launches = 0, prof_points = 0, prof_entries = 0;
   hipEvent_t ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   hipEvent_t done = nullptr;  // recorded after the window sums' copy to host_win (msm_finish waits on it)
-  void init(size_t max_points, bool fixed_base = false);
+  // lagrange_sets: size for msm_enqueue_sets of that many MSMs over a Lagrange-window table;
+  // generic = false: table schedules only (no generic sort / 8x32 arrays)
+  void init(size_t max_points, bool fixed_base = false, int lagrange_sets = 1, bool generic = true);
   ~MsmScratch();
 };
 
@@ -91,6 +95,12 @@ int msm_window_bits(size_t n);
 void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, bool scalars_mont,
                  hipStream_t st, const MsmBaseTable* table = nullptr);
 G1xyzz msm_finish(MsmScratch& sc, hipStream_t st);
+// Several fixed-base MSMs over ONE table in one schedule (MsmScratch sized with lagrange_sets >=
+// sets): one bucketing, accumulation and carry reduction over sets x 2^(c-1) buckets, window sums
+// per set (round 6: A, B, C over the Lagrange basis). scalars[s]: n values each.
+void msm_enqueue_sets(MsmScratch& sc, const Fr* const* scalars, int sets, size_t n, bool scalars_mont,
+                      hipStream_t st, const MsmBaseTable* table);
+void msm_finish_sets(MsmScratch& sc, hipStream_t st, G1xyzz* out);
 
 inline G1xyzz msm(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, bool mont, hipStream_t st,
                   const MsmBaseTable* table = nullptr) {

@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <type_traits>
 #include <rocprim/rocprim.hpp>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 namespace nzcb {
 
@@ -259,32 +260,46 @@ __device__ __forceinline__ uint32_t bin_entries(const Fr* __restrict__ scalars, 
   return live;
 }
 
-// bucket index bits below the high byte: 8 for c <= 17 (16-bit indices), c - 9 above
-// (c = 20: 19-bit indices, 256 high-byte regions of 2048 buckets)
-template <int C> struct BinKeys {
-  static constexpr int LO = C - 9 > 8 ? C - 9 : 8;
+// bucket index bits below the high byte, for KB-bit bucket keys: 8 up to 16-bit keys (c <= 17),
+// KB - 8 above (c = 20: 19-bit keys, 256 high-byte regions of 2048 buckets; three c = 17 bucket
+// sets: 18-bit keys)
+template <int KB> struct BinKeys {
+  static constexpr int LO = KB - 8 > 8 ? KB - 8 : 8;
   using Lo = typename std::conditional<LO <= 8, uint8_t, uint16_t>::type;      // low part, per entry
-  using Full = typename std::conditional<C <= 17, uint16_t, uint32_t>::type;   // whole index, in LDS
+  using Full = typename std::conditional<KB <= 16, uint16_t, uint32_t>::type;  // whole key, in LDS
 };
 
-template <int C>
+// Several MSMs over one table in one schedule (round 6: A, B and C over the Lagrange basis):
+// set s's scalars are tiles [s tps, (s + 1) tps) of the bucketing grid and its buckets keys
+// [s nb, (s + 1) nb), so one sort, one accumulation and one carry reduction serve all of them,
+// and the window sums run per set. One set: tps = all tiles.
+static constexpr int kMaxSets = 3;
+struct BinSets {
+  const Fr* p[kMaxSets];
+  uint32_t tps;  // bucketing tiles per set
+  uint32_t nb;   // buckets per set
+};
+
+template <int C, int KB>
 __global__ void __launch_bounds__(kBinThreads)
-msm_bin_hist_kernel(const Fr* __restrict__ scalars, size_t n, int mont, uint32_t* __restrict__ counts,
-                    uint32_t ntiles) {
+msm_bin_hist_kernel(BinSets sets, size_t n, int mont, uint32_t* __restrict__ counts, uint32_t ntiles) {
   constexpr int NW = (255 + C - 1) / C;
-  constexpr int LO = BinKeys<C>::LO;
+  constexpr int LO = BinKeys<KB>::LO;
   __shared__ uint32_t h[256];
   h[threadIdx.x] = 0;
   __syncthreads();
+  const uint32_t set = blockIdx.x / sets.tps, lt = blockIdx.x - set * sets.tps;
+  const Fr* __restrict__ scalars = sets.p[set];
+  const uint32_t kbase = set * sets.nb;
 #pragma unroll
   for (int j = 0; j < kBinPer; j++) {
-    const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)j * kBinThreads + threadIdx.x;
+    const size_t i = (size_t)lt * kTileScalars + (size_t)j * kBinThreads + threadIdx.x;
     if (i < n) {
       uint32_t kk[NW], vv[NW];
       const uint32_t live = bin_entries<C, NW>(scalars, i, mont, 0, kk, vv);
 #pragma unroll
       for (int w = 0; w < NW; w++)
-        if ((live >> w) & 1u) atomicAdd(&h[kk[w] >> LO], 1u);
+        if ((live >> w) & 1u) atomicAdd(&h[(kk[w] + kbase) >> LO], 1u);
     }
   }
   __syncthreads();
@@ -334,17 +349,19 @@ msm_bin_rowscan_kernel(uint32_t* __restrict__ counts, uint32_t ntiles, uint32_t*
   if (threadIdx.x == 0) tail[blockIdx.x] = carry;
 }
 
-template <int C>
+template <int C, int KB>
 __global__ void __launch_bounds__(kBinThreads)
-msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_t stride,
-                       const uint32_t* __restrict__ counts, uint32_t ntiles, typename BinKeys<C>::Lo* __restrict__ lo2,
-                       uint32_t* __restrict__ vals2) {
+msm_bin_scatter_kernel(BinSets sets, size_t n, int mont, size_t stride, const uint32_t* __restrict__ counts,
+                       uint32_t ntiles, typename BinKeys<KB>::Lo* __restrict__ lo2, uint32_t* __restrict__ vals2) {
   constexpr int NW = (255 + C - 1) / C;
   constexpr int TE = kTileScalars * NW;  // entries per tile, at most
-  constexpr int LO = BinKeys<C>::LO;
+  constexpr int LO = BinKeys<KB>::LO;
   __shared__ uint32_t lcount[256], lstart[256], gbase[256];
   __shared__ uint32_t lval[TE];
-  __shared__ typename BinKeys<C>::Full lkey[TE];
+  __shared__ typename BinKeys<KB>::Full lkey[TE];
+  const uint32_t set = blockIdx.x / sets.tps, lt = blockIdx.x - set * sets.tps;
+  const Fr* __restrict__ scalars = sets.p[set];
+  const uint32_t kbase = set * sets.nb;
   __shared__ uint32_t wsum[4];
   const uint32_t* tail = counts + (size_t)256 * ntiles;  // row totals
   {
@@ -357,13 +374,15 @@ msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_
   uint32_t kk[kBinPer][NW], vv[kBinPer][NW], rk[kBinPer][NW], live[kBinPer];
 #pragma unroll
   for (int j = 0; j < kBinPer; j++) {
-    const size_t i = (size_t)blockIdx.x * kTileScalars + (size_t)j * kBinThreads + threadIdx.x;
+    const size_t i = (size_t)lt * kTileScalars + (size_t)j * kBinThreads + threadIdx.x;
     live[j] = 0;
     if (i < n) {
       live[j] = bin_entries<C, NW>(scalars, i, mont, stride, kk[j], vv[j]);
 #pragma unroll
-      for (int w = 0; w < NW; w++)
+      for (int w = 0; w < NW; w++) {
+        kk[j][w] += kbase;
         if ((live[j] >> w) & 1u) rk[j][w] = atomicAdd(&lcount[kk[j][w] >> LO], 1u);
+      }
     }
   }
   __syncthreads();
@@ -378,7 +397,7 @@ msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_
     for (int w = 0; w < NW; w++) {
       if ((live[j] >> w) & 1u) {
         const uint32_t q = lstart[kk[j][w] >> LO] + rk[j][w];
-        lkey[q] = (typename BinKeys<C>::Full)kk[j][w];
+        lkey[q] = (typename BinKeys<KB>::Full)kk[j][w];
         lval[q] = vv[j][w];
       }
     }
@@ -387,7 +406,7 @@ msm_bin_scatter_kernel(const Fr* __restrict__ scalars, size_t n, int mont, size_
   for (uint32_t q = threadIdx.x; q < total; q += kBinThreads) {  // runs of one high byte: coalesced
     const uint32_t key = lkey[q], hb = key >> LO;
     const uint32_t pos = gbase[hb] + (q - lstart[hb]);
-    lo2[pos] = (typename BinKeys<C>::Lo)(key & ((1u << LO) - 1u));
+    lo2[pos] = (typename BinKeys<KB>::Lo)(key & ((1u << LO) - 1u));
     vals2[pos] = lval[q];
   }
 }
@@ -1155,6 +1174,8 @@ msm_parts_kernel(const G1xyzz* __restrict__ parts, int nparts, G1xyzz* __restric
 static constexpr int kTileSide = 16;
 static constexpr int kLineThreads = 8;  // a power of two dividing 64
 
+// sets (BinSets): set s = blockIdx.y, its buckets from s 2^(a + hb), its partials from s times
+// one set's row / column partial counts
 __global__ void __launch_bounds__(256)
 msm_tile29_kernel(const Xyzz29* __restrict__ buckets, const uint32_t* __restrict__ offsets, int a, int ltiles,
                   int htiles, Xyzz29* __restrict__ rowp, Xyzz29* __restrict__ colp) {
@@ -1163,6 +1184,13 @@ msm_tile29_kernel(const Xyzz29* __restrict__ buckets, const uint32_t* __restrict
   __shared__ Xyzz29 sh[384];
   const int tid = threadIdx.x;
   const int ht = blockIdx.x / ltiles, lt = blockIdx.x - ht * ltiles;
+  {
+    const size_t per = (size_t)ltiles * htiles * kTileSide;  // row (= column) partials of one set
+    buckets += (size_t)blockIdx.y * ltiles * htiles * kTileSide * kTileSide;
+    offsets += (size_t)blockIdx.y * ltiles * htiles * kTileSide * kTileSide;
+    rowp += blockIdx.y * per;
+    colp += blockIdx.y * per;
+  }
   {
     const int i = tid >> 4, j = tid & 15;
     const uint32_t k = ((uint32_t)(ht * kTileSide + i) << a) + (uint32_t)(lt * kTileSide + j);
@@ -1267,6 +1295,10 @@ __global__ void __launch_bounds__(256)
 msm_lines29_kernel(const Xyzz29* __restrict__ rowp, int ltiles, const Xyzz29* __restrict__ colp, int htiles,
                    int nrows, int ncols, Xyzz29* __restrict__ lines) {
   tail_prio();
+  // sets: set s = blockIdx.y (one set's partials: nrows ltiles = ncols htiles; lines nrows + ncols)
+  rowp += (size_t)blockIdx.y * nrows * ltiles;
+  colp += (size_t)blockIdx.y * ncols * htiles;
+  lines += (size_t)blockIdx.y * (nrows + ncols);
   constexpr int LG = kLineThreads == 8 ? 3 : kLineThreads == 4 ? 2 : kLineThreads == 16 ? 4 : 1;
   static_assert((1 << LG) == kLineThreads, "kLineThreads: 2, 4, 8 or 16");
   const int g = (int)((blockIdx.x * 256 + threadIdx.x) / kLineThreads);
@@ -1301,6 +1333,9 @@ __global__ void __launch_bounds__(kSumThreads)
 msm_slots29_kernel(const Xyzz29* __restrict__ lines, int hb, int a, G1xyzz* __restrict__ out,
                    const uint32_t* __restrict__ entries, uint32_t* __restrict__ total_out) {
   tail_prio();
+  // sets: set = blockIdx.y (its lines from set (2^hb + 2^a), its slots from set (hb + a + 1))
+  lines += (size_t)blockIdx.y * (((size_t)1 << hb) + ((size_t)1 << a));
+  out += (size_t)blockIdx.y * (hb + a + 1);
   __shared__ Xyzz29 sh[kSumThreads];
   const int s = blockIdx.x;
   const bool rows = s < hb;
@@ -1315,10 +1350,10 @@ msm_slots29_kernel(const Xyzz29* __restrict__ lines, int hb, int a, G1xyzz* __re
     rhs = src[plain ? q : (((q >> b) << (b + 1)) | (1 << b) | (q & ((1 << b) - 1)))];
     return true;
   });
-  if (threadIdx.x == 0) {
-    out[s] = load_point(r);
-    if (s == 0 && total_out) *total_out = *entries;
-    __threadfence_system();  // host memory: complete before the kernel is
+  if (threadIdx.x == 0) {  // pinned host memory (common.h host_put)
+    host_put(out + s, load_point(r));
+    if (s == 0 && blockIdx.y == 0 && total_out) host_put(total_out, *entries);
+    host_put_done();
   }
 }
 
@@ -1375,23 +1410,33 @@ void MsmBaseTable::build(const G1Affine* bases, size_t npts, int cbits, hipStrea
   NZ_HIP(hipGetLastError());
 }
 
+// NZCB_MARK_LAUNCHES=1: a roctx mark after every launch of the fixed-base schedule, so that a
+// rocprofv3 --marker-trace shows the host time each launch takes inside a proof (round 6:
+// round 1's commitments were enqueued ~0.5-1 ms apart)
+static void lmark(const char* what) {
+  static const bool on = std::getenv("NZCB_MARK_LAUNCHES") != nullptr;
+  if (on) roctxMarkA(what);
+}
+
 // work items of the bucket_lo steps: at most one partial segment per region + entries / kLoSeg
 static size_t lo_items_bound(size_t entries) { return 256 + entries / kLoSeg + 1; }
 
 struct MsmPlan {
   int c, nw, nsets, seglen, nseg, nbits, nslots, nparts;
   int lb, a, hb, ltiles, htiles;  // fixed base: the two-dimensional window sum
+  int msets;                      // fixed base: MSMs sharing the schedule (BinSets)
   uint32_t nb, nkeys;
   size_t entries;
 };
 
-static MsmPlan make_plan(size_t n, const MsmBaseTable* t) {
+static MsmPlan make_plan(size_t n, const MsmBaseTable* t, int msets = 1) {
   MsmPlan p;
   p.c = t ? t->c : msm_window_bits(n);
   p.nw = num_windows(p.c);
   p.nsets = t ? 1 : p.nw;
+  p.msets = t ? msets : 1;
   p.nb = 1u << (p.c - 1);
-  p.nkeys = p.nb * (uint32_t)p.nsets;
+  p.nkeys = p.nb * (uint32_t)p.nsets * (uint32_t)p.msets;
   p.seglen = (int)(p.nb < (uint32_t)kSegLen ? p.nb : kSegLen);
   p.nseg = (int)(p.nb / p.seglen);
   p.nbits = 0;
@@ -1403,20 +1448,23 @@ static MsmPlan make_plan(size_t n, const MsmBaseTable* t) {
   p.hb = p.lb - p.a;
   p.ltiles = (1 << p.a) / kTileSide;
   p.htiles = (1 << p.hb) / kTileSide;
-  p.entries = n * (size_t)p.nw;
+  p.entries = n * (size_t)p.nw * (size_t)p.msets;
   return p;
 }
 
-void MsmScratch::init(size_t maxp, bool fixed_base) {
+void MsmScratch::init(size_t maxp, bool fixed_base, int lagrange_sets, bool generic) {
+  if (lagrange_sets < 1 || lagrange_sets > kMaxSets) throw Error(NZCB_ERR_ARG, "msm scratch: 1..3 Lagrange sets");
+  if (!fixed_base) generic = true;
   max_points = maxp;
+  max_lsets = lagrange_sets;
   size_t max_entries = 0, max_keys = 0, max_seg = 0, max_slots = 0, max_parts = 0, max_tiles = 0, max_lines = 0;
   auto fit = [&](const MsmPlan& p) {
     max_entries = std::max(max_entries, p.entries);
     max_keys = std::max(max_keys, (size_t)p.nkeys);
     if (p.nsets == 1) {  // fixed base
-      max_slots = std::max(max_slots, (size_t)(p.lb + 1));
-      max_tiles = std::max(max_tiles, (size_t)p.nb / kTileSide);
-      max_lines = std::max(max_lines, ((size_t)1 << p.hb) + ((size_t)1 << p.a));
+      max_slots = std::max(max_slots, (size_t)(p.lb + 1) * p.msets);
+      max_tiles = std::max(max_tiles, (size_t)p.nb / kTileSide * p.msets);
+      max_lines = std::max(max_lines, (((size_t)1 << p.hb) + ((size_t)1 << p.a)) * p.msets);
     } else {
       max_seg = std::max(max_seg, (size_t)p.nseg * p.nsets);
       max_slots = std::max(max_slots, (size_t)p.nslots * p.nsets);
@@ -1435,23 +1483,28 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
     fp = make_plan(maxp, &t);
     fit(fp);
     t.c = lagrange_window();
-    const MsmPlan lp = make_plan(maxp, &t);
+    const MsmPlan lp = make_plan(maxp, &t, lagrange_sets);
     fit(lp);
     if (lp.entries > fp.entries) fp = lp;
   }
+  // generic = false (the prover's and the serving ranks' scratches, which only run tables):
+  // none of the generic schedule's sort, 8x32 bucket and segment arrays
+  const size_t ge = generic ? max_entries : 1;
   offsets.alloc(max_keys + 1);
   sorted.alloc(max_entries);
-  keys_in.alloc(max_entries);
-  keys_out.alloc(max_entries);
-  vals_in.alloc(max_entries);
+  keys_in.alloc(ge);
+  keys_out.alloc(max_entries);  // the fixed-base bucketing's low key parts
+  vals_in.alloc(ge);
   sort_tmp_bytes = 0;
-  radix_sort(nullptr, sort_tmp_bytes, keys_in.p, keys_out.p, vals_in.p, sorted.p, max_entries, 21, nullptr);
+  if (generic) {
+    radix_sort(nullptr, sort_tmp_bytes, keys_in.p, keys_out.p, vals_in.p, sorted.p, max_entries, 21, nullptr);
+  }
   sort_tmp.alloc(sort_tmp_bytes + 16);
-  buckets.alloc(max_keys);
   // accumulation threads: chunk_for's grid, or the sparse schedule's (dyn_threads_bound)
   const size_t nthreads = std::max((max_entries + kChunk - 1) / kChunk, dyn_threads_bound(max_entries)) + 1;
-  carry_own.alloc(nthreads);
-  carry_cont.alloc(nthreads);
+  buckets.alloc(generic ? max_keys : 1);
+  carry_own.alloc(generic ? nthreads : 1);
+  carry_cont.alloc(generic ? nthreads : 1);
   large.alloc(max_keys + 1);
   if (fixed_base) {
     buckets29.alloc(max_keys);
@@ -1463,13 +1516,13 @@ void MsmScratch::init(size_t maxp, bool fixed_base) {
     rowp29.alloc(max_tiles);
     colp29.alloc(max_tiles);
     lines29.alloc(max_lines);
-    bin_counts.alloc((size_t)256 * ((maxp + kTileScalars - 1) / kTileScalars) + 256);  // + row totals
+    bin_counts.alloc((size_t)256 * ((maxp + kTileScalars - 1) / kTileScalars) * lagrange_sets + 256);  // + row totals
     vals_mid.alloc(max_entries);
-    lo_seg.alloc(lo_items_bound(max_entries) * ((size_t)1 << BinKeys<20>::LO));  // the widest low index
+    lo_seg.alloc(lo_items_bound(max_entries) * ((size_t)1 << BinKeys<19>::LO));  // the widest low index
   }
-  seg_tot.alloc(max_seg ? max_seg : 1);
-  seg_run.alloc(max_seg ? max_seg : 1);
-  parts.alloc(max_parts ? max_parts : 1);
+  seg_tot.alloc(max_seg && generic ? max_seg : 1);
+  seg_run.alloc(max_seg && generic ? max_seg : 1);
+  parts.alloc(max_parts && generic ? max_parts : 1);
   win.alloc(max_slots);
   host_win_cap = max_slots;
   // coherent: the fixed-base window sums are written here by msm_slots29_kernel
@@ -1514,49 +1567,66 @@ G1Affine xyzz_to_affine(const G1xyzz& p) {
 
 // fixed base: bucketing (msm_bin_* / msm_lo_*) into sc.offsets / sc.sorted
 template <class Mark>
-static void fixed_bucketing(MsmScratch& sc, const MsmPlan& p, const Fr* scalars, size_t n, int mdig,
+static void fixed_bucketing(MsmScratch& sc, const MsmPlan& p, const BinSets& sets, size_t n, int mdig,
                             const MsmBaseTable* table, hipStream_t st, const Mark& mark) {
-  const uint32_t ntiles = (uint32_t)((n + kTileScalars - 1) / kTileScalars);
+  const uint32_t tps = (uint32_t)((n + kTileScalars - 1) / kTileScalars);
+  const uint32_t ntiles = tps * (uint32_t)p.msets;
+  BinSets bs = sets;
+  bs.tps = tps;
+  bs.nb = p.nb;
   uint32_t* tail = sc.bin_counts.p + (size_t)256 * ntiles;
-  auto run_bins = [&](auto cc) {
+  auto run_bins = [&](auto cc, auto kb) {
     constexpr int C = decltype(cc)::value;
-    using Lo = typename BinKeys<C>::Lo;
-    constexpr int LO = BinKeys<C>::LO;
+    constexpr int KB = decltype(kb)::value;  // key bits: c - 1, + 2 for up to 3 sets
+    using Lo = typename BinKeys<KB>::Lo;
+    constexpr int LO = BinKeys<KB>::LO;
     Lo* lo2 = (Lo*)sc.keys_out.p;
-    hipLaunchKernelGGL(msm_bin_hist_kernel<C>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, mdig,
+    hipLaunchKernelGGL((msm_bin_hist_kernel<C, KB>), dim3(ntiles), dim3(kBinThreads), 0, st, bs, n, mdig,
                        sc.bin_counts.p, ntiles);
     NZ_HIP(hipGetLastError());
+    lmark("mark: L hist");
     mark(1);
     hipLaunchKernelGGL(msm_bin_rowscan_kernel, dim3(256), dim3(256), 0, st, sc.bin_counts.p, ntiles, tail);
-    hipLaunchKernelGGL(msm_bin_scatter_kernel<C>, dim3(ntiles), dim3(kBinThreads), 0, st, scalars, n, mdig,
+    lmark("mark: L rowscan");
+    hipLaunchKernelGGL((msm_bin_scatter_kernel<C, KB>), dim3(ntiles), dim3(kBinThreads), 0, st, bs, n, mdig,
                        table->stride, sc.bin_counts.p, ntiles, lo2, sc.vals_mid.p);
     NZ_HIP(hipGetLastError());
+    lmark("mark: L scatter");
     mark(2);
     const dim3 igrid((unsigned)lo_items_bound(p.entries));
     hipLaunchKernelGGL(msm_lo_count_kernel<LO>, igrid, dim3(kLoThreads), 0, st, (const Lo*)lo2, sc.bin_counts.p,
                        ntiles, sc.lo_seg.p);
     NZ_HIP(hipGetLastError());
+    lmark("mark: L lo_count");
     hipLaunchKernelGGL(msm_lo_scan_kernel<LO>, dim3(256), dim3(kLoThreads), 0, st, sc.bin_counts.p, ntiles,
                        sc.lo_seg.p, p.nkeys, sc.offsets.p, sc.large.p);
     NZ_HIP(hipGetLastError());
+    lmark("mark: L lo_scan");
     constexpr int sNT = LO > 8 ? 1024 : kLoThreads;
     constexpr uint32_t sU = LO > 8 ? 16 : kLoU;
     hipLaunchKernelGGL((msm_lo_scatter_kernel<LO, sNT, sU>), igrid, dim3(sNT), 0, st, (const Lo*)lo2, sc.vals_mid.p,
                        sc.bin_counts.p, ntiles, (const uint32_t*)sc.lo_seg.p, sc.sorted.p);
     NZ_HIP(hipGetLastError());
+    lmark("mark: L lo_scatter");
   };
+  using std::integral_constant;
+  if (p.msets > 1) {  // several MSMs: 2 more key bits (up to 4 sets; Lagrange window only)
+    if (p.c != 17) throw Error(NZCB_ERR_INTERNAL, "msm sets: the Lagrange window (17) only");
+    run_bins(integral_constant<int, 17>(), integral_constant<int, 18>());
+    return;
+  }
   switch (p.c) {
-    case 16: run_bins(std::integral_constant<int, 16>()); break;
-    case 17: run_bins(std::integral_constant<int, 17>()); break;
-    case 18: run_bins(std::integral_constant<int, 18>()); break;
-    case 19: run_bins(std::integral_constant<int, 19>()); break;
-    case 20: run_bins(std::integral_constant<int, 20>()); break;
+    case 16: run_bins(integral_constant<int, 16>(), integral_constant<int, 15>()); break;
+    case 17: run_bins(integral_constant<int, 17>(), integral_constant<int, 16>()); break;
+    case 18: run_bins(integral_constant<int, 18>(), integral_constant<int, 17>()); break;
+    case 19: run_bins(integral_constant<int, 19>(), integral_constant<int, 18>()); break;
+    case 20: run_bins(integral_constant<int, 20>(), integral_constant<int, 19>()); break;
     default: throw Error(NZCB_ERR_INTERNAL, "bad fixed-base msm window");
   }
 }
 
-void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, bool mont, hipStream_t st,
-                 const MsmBaseTable* table) {
+static void msm_enqueue_impl(MsmScratch& sc, const G1Affine* bases, const Fr* const* scalars, int msets, size_t n,
+                             bool mont, hipStream_t st, const MsmBaseTable* table) {
   const auto t_enq = std::chrono::steady_clock::now();
   struct EnqueueClock {  // host time of the enqueue, for the phase timing (nzcb_engine_time_msm2)
     MsmScratch& sc;
@@ -1576,11 +1646,14 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
     throw Error(NZCB_ERR_ARG, "msm scratch was not sized for the fixed-base schedule");
   // a folded table takes the Montgomery form's integer as the scalar (msm_table_kernel)
   const int mdig = (mont && !(table && table->mont_folded)) ? 1 : 0;
-  const MsmPlan p = make_plan(n, table);
+  if (msets < 1 || msets > kMaxSets || (msets > 1 && (!table || msets > sc.max_lsets)))
+    throw Error(NZCB_ERR_ARG, "msm sets: 1..3 over a table, within the scratch's sizing");
+  const MsmPlan p = make_plan(n, table, msets);
   if (p.entries > sc.sorted.n || p.nkeys + 1 > sc.offsets.n)
     throw Error(NZCB_ERR_ARG, "msm scratch was not sized for this schedule");
-  if (table && ((size_t)p.nb / kTileSide > sc.rowp29.n || ((size_t)1 << p.hb) + ((size_t)1 << p.a) > sc.lines29.n ||
-                (size_t)p.lb + 1 > sc.win.n))
+  if (table && ((size_t)p.nb / kTileSide * msets > sc.rowp29.n ||
+                (((size_t)1 << p.hb) + ((size_t)1 << p.a)) * msets > sc.lines29.n ||
+                (size_t)(p.lb + 1) * msets > sc.host_win_cap || (msets > 1 && p.c >= kStripMinC)))
     throw Error(NZCB_ERR_ARG, "msm scratch was not sized for this window");
   sc.cur_c = p.c;
   sc.cur_nsets = p.nsets;
@@ -1590,6 +1663,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   sc.cur_fixed = table != nullptr;
   sc.cur_a = p.a;
   sc.cur_hb = p.hb;
+  sc.cur_msets = p.msets;
   const bool phases = sc.prof && sc.prof_phases;
   if (sc.prof && !sc.ev[0])
     for (auto& e : sc.ev) NZ_HIP(hipEventCreate(&e));
@@ -1598,9 +1672,11 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   };
   mark(0);
   if (table) {
-    fixed_bucketing(sc, p, scalars, n, mdig, table, st, mark);
+    BinSets bs{};
+    for (int k = 0; k < msets; k++) bs.p[k] = scalars[k];
+    fixed_bucketing(sc, p, bs, n, mdig, table, st, mark);
   } else {
-    keys_dispatch(p.c, scalars, n, mdig, sc, st);
+    keys_dispatch(p.c, scalars[0], n, mdig, sc, st);
     mark(1);
     size_t tmp = sc.sort_tmp_bytes;
     int end_bit = 1;
@@ -1635,6 +1711,7 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                        p.nkeys, nthreads, sc.buckets.p, sc.carry_own.p, sc.carry_cont.p);
   }
   NZ_HIP(hipGetLastError());
+  lmark("mark: L accumulate");
   if (sc.prof) NZ_HIP(hipEventRecord(sc.ev[4], st));
   const dim3 fgrid(grid_for(p.nkeys, kMsmThreads, 1u << 30));
   if (table) {  // the large list's count was zeroed by msm_lo_scan_kernel
@@ -1642,16 +1719,20 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
                        sparse ? kSeqSpanSparse : kSeqSpan29, (const Xyzz29*)sc.carry_own29.p,
                        (const Xyzz29*)sc.carry_cont29.p, sc.large.p, sc.buckets29.p);
     NZ_HIP(hipGetLastError());
+    lmark("mark: L finalize");
     hipLaunchKernelGGL(msm_large_scan_kernel, dim3(1), dim3(1024), 0, st, chunk, sc.offsets.p, p.nkeys, sc.large.p,
                        sc.large_off.p);
     NZ_HIP(hipGetLastError());
+    lmark("mark: L large_scan");
     hipLaunchKernelGGL(msm_large_piece29_kernel, dim3(sparse ? kSparsePieceBlocks : kLargePieceBlocks),
                        dim3(kSumThreads), 0, st, chunk, sc.offsets.p, p.nkeys, sc.large.p, sc.large_off.p,
                        (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p, sc.large_part.p);
     NZ_HIP(hipGetLastError());
+    lmark("mark: L piece");
     hipLaunchKernelGGL(msm_large_final29_kernel, dim3(sparse ? kSparseFinalBlocks : kLargeFinalBlocks),
                        dim3(kSumThreads), 0, st, sc.large.p, sc.large_off.p, sc.large_part.p, sc.buckets29.p);
     NZ_HIP(hipGetLastError());
+    lmark("mark: L final");
     mark(5);
     int lparts = p.ltiles, hparts = p.htiles;  // partials per row / per column
     if (p.c >= kStripMinC) {
@@ -1661,20 +1742,23 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
       hipLaunchKernelGGL(msm_strips29_kernel, dim3(grid_for(nthr, 256, 1u << 30)), dim3(256), 0, st,
                          (const Xyzz29*)sc.buckets29.p, sc.offsets.p, p.a, p.hb, sc.rowp29.p, sc.colp29.p);
     } else {
-      hipLaunchKernelGGL(msm_tile29_kernel, dim3((unsigned)(p.ltiles * p.htiles)), dim3(256), 0, st,
+      hipLaunchKernelGGL(msm_tile29_kernel, dim3((unsigned)(p.ltiles * p.htiles), (unsigned)p.msets), dim3(256), 0, st,
                          (const Xyzz29*)sc.buckets29.p, sc.offsets.p, p.a, p.ltiles, p.htiles, sc.rowp29.p, sc.colp29.p);
     }
     NZ_HIP(hipGetLastError());
     mark(6);
     const int nrows = 1 << p.hb, ncols = 1 << p.a;
-    hipLaunchKernelGGL(msm_lines29_kernel, dim3(grid_for((size_t)(nrows + ncols) * kLineThreads, 256)), dim3(256), 0,
+    hipLaunchKernelGGL(msm_lines29_kernel, dim3(grid_for((size_t)(nrows + ncols) * kLineThreads, 256), (unsigned)p.msets),
+                       dim3(256), 0,
                        st, (const Xyzz29*)sc.rowp29.p, lparts, (const Xyzz29*)sc.colp29.p, hparts, nrows, ncols,
                        sc.lines29.p);
     NZ_HIP(hipGetLastError());
-    hipLaunchKernelGGL(msm_slots29_kernel, dim3(p.hb + p.a + 1), dim3(kSumThreads), 0, st,
+    lmark("mark: L lines");
+    hipLaunchKernelGGL(msm_slots29_kernel, dim3(p.hb + p.a + 1, (unsigned)p.msets), dim3(kSumThreads), 0, st,
                        (const Xyzz29*)sc.lines29.p, p.hb, p.a, sc.host_win, (const uint32_t*)sc.offsets.p + p.nkeys,
                        sc.prof ? sc.host_total : nullptr);
     NZ_HIP(hipGetLastError());
+    lmark("mark: L slots");
     mark(7);
     NZ_HIP(hipEventRecord(sc.done, st));
     return;
@@ -1703,6 +1787,39 @@ void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_
   NZ_HIP(hipMemcpyAsync(sc.host_win, sc.win.p, (size_t)p.nsets * p.nslots * sizeof(G1xyzz), hipMemcpyDeviceToHost,
                         st));
   NZ_HIP(hipEventRecord(sc.done, st));
+}
+
+void msm_enqueue(MsmScratch& sc, const G1Affine* bases, const Fr* scalars, size_t n, bool mont, hipStream_t st,
+                 const MsmBaseTable* table) {
+  const Fr* one[1] = {scalars};
+  msm_enqueue_impl(sc, bases, one, 1, n, mont, st, table);
+}
+
+void msm_enqueue_sets(MsmScratch& sc, const Fr* const* scalars, int sets, size_t n, bool mont, hipStream_t st,
+                      const MsmBaseTable* table) {
+  if (!table) throw Error(NZCB_ERR_ARG, "msm sets: a table schedule");
+  msm_enqueue_impl(sc, nullptr, scalars, sets, n, mont, st, table);
+}
+
+// the fixed-base slots of set s combined on the host: W = 2^a sum_b 2^b R_b + sum_b 2^b C_b + C
+static G1xyzz fixed_window_result(const G1xyzz* s, int hb, int a) {
+  G1xyzz acc = G1xyzz::inf();
+  for (int b = hb - 1; b >= 0; b--) acc = xyzz_add(xyzz_dbl(acc), s[b]);
+  for (int i = 0; i < a; i++) acc = xyzz_dbl(acc);
+  G1xyzz col = G1xyzz::inf();
+  for (int b = a - 1; b >= 0; b--) col = xyzz_add(xyzz_dbl(col), s[hb + b]);
+  return xyzz_add(xyzz_add(acc, col), s[hb + a]);
+}
+
+void msm_finish_sets(MsmScratch& sc, hipStream_t st, G1xyzz* out) {
+  const int msets = sc.cur_msets;
+  if (sc.cur_n == 0) {
+    for (int k = 0; k < msets; k++) out[k] = G1xyzz::inf();
+    return;
+  }
+  out[0] = msm_finish(sc, st);  // waits, timings, set 0
+  for (int k = 1; k < msets; k++) out[k] = fixed_window_result(sc.host_win + (size_t)k * (sc.cur_hb + sc.cur_a + 1),
+                                                               sc.cur_hb, sc.cur_a);
 }
 
 G1xyzz msm_finish(MsmScratch& sc, hipStream_t st) {
@@ -1768,16 +1885,7 @@ G1xyzz msm_finish(MsmScratch& sc, hipStream_t st) {
         sc.host_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
   } host_clock{sc, t_host};
-  if (sc.cur_fixed) {  // W = 2^a sum_b 2^b R_b + sum_b 2^b C_b + C (msm_slots29_kernel)
-    const int hb = sc.cur_hb, a = sc.cur_a;
-    const G1xyzz* s = sc.host_win;
-    G1xyzz acc = G1xyzz::inf();
-    for (int b = hb - 1; b >= 0; b--) acc = xyzz_add(xyzz_dbl(acc), s[b]);
-    for (int i = 0; i < a; i++) acc = xyzz_dbl(acc);
-    G1xyzz col = G1xyzz::inf();
-    for (int b = a - 1; b >= 0; b--) col = xyzz_add(xyzz_dbl(col), s[hb + b]);
-    return xyzz_add(xyzz_add(acc, col), s[hb + a]);
-  }
+  if (sc.cur_fixed) return fixed_window_result(sc.host_win, sc.cur_hb, sc.cur_a);  // set 0 (msm_slots29_kernel)
   int lg_seg = 0;
   while ((1 << lg_seg) < sc.cur_seglen) lg_seg++;
   G1xyzz res = G1xyzz::inf();

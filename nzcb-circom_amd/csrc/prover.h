@@ -168,6 +168,8 @@ struct Prover {
   void commit_start(int slot, const Fr* scalars, size_t len, const MsmBaseTable* tab = nullptr,
                     const G1Affine* bases = nullptr, bool on_main = false);
   G1Affine commit_finish(int slot);
+  void commit_start_abc(size_t len);  // A, B, C in one schedule (msm_enqueue_sets), main stream
+  void commit_finish_abc(G1Affine& a, G1Affine& b, G1Affine& c);
   // np <= 8 evaluations p_j(x_j) (two launches, one host round trip)
   void eval_many(int np, const Fr* const* polys, const size_t* lens, const Fr* xs, Fr* out,
                  const std::function<void()>& overlap = nullptr);

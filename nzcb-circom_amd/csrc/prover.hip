@@ -49,9 +49,7 @@ __global__ void k_additions(const AddRec* __restrict__ recs, uint32_t count, Fr*
   wit[r.dst] = r.ac * a + r.bc * b;
 }
 
-// Host writes of small results (the prover's mailbox, coherent pinned memory): visible to the
-// host before the kernel's completion is (the fence completes the stores over the fabric)
-__device__ __forceinline__ void mailbox_fence() { __threadfence_system(); }
+// Host writes of small results (the prover's mailbox, coherent pinned memory): common.h host_put
 
 __global__ void k_build_abc(const uint32_t* __restrict__ am, const uint32_t* __restrict__ bm,
                             const uint32_t* __restrict__ cm, uint32_t nc, uint32_t n, const Fr* __restrict__ wit,
@@ -59,10 +57,10 @@ __global__ void k_build_abc(const uint32_t* __restrict__ am, const uint32_t* __r
                             uint32_t npub, Fr* __restrict__ mb_apub, Fr* __restrict__ mb_pubw) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < npub) {  // the public signals witness[1..nPublic] into the mailbox (Prover::prove's output)
-    mb_pubw[i] = 1 + i < nvars ? wit[1 + i] : Fr::zero();
+    host_put(mb_pubw + i, 1 + i < nvars ? wit[1 + i] : Fr::zero());
   }
   if (i >= n) {
-    if (i < npub) mailbox_fence();
+    if (i < npub) host_put_done();
     return;
   }
   Fr a = Fr::zero(), b = Fr::zero(), c = Fr::zero();
@@ -76,8 +74,8 @@ __global__ void k_build_abc(const uint32_t* __restrict__ am, const uint32_t* __r
   B[i] = b;
   C[i] = c;
   if (i < npub) {  // A's public-gate values: the beta transcript's public inputs (round 2)
-    mb_apub[i] = a;
-    mailbox_fence();
+    host_put(mb_apub + i, a);
+    host_put_done();
   }
 }
 
@@ -89,13 +87,13 @@ __global__ void k_tops(const Fr* __restrict__ pa, const Fr* __restrict__ pb, con
   if (t < 24) {
     const int k = t / 6, j = t % 6;
     const Fr* src = k == 0 ? pa + (n - 4) : k == 1 ? pb + (n - 4) : k == 2 ? pc + (n - 4) : pz + (n - 3);
-    mb[t] = src[j];
+    host_put(mb + t, src[j]);
   } else if (t == 24) {
     Fr f = Fr::zero();
     f.v[0] = *flags;
-    mb[24] = f;
+    host_put(mb + 24, f);
   }
-  mailbox_fence();
+  host_put_done();
 }
 
 struct BlindIdx {
@@ -124,6 +122,15 @@ __global__ void k_abc_tail(Fr* A, Fr* B, Fr* C, size_t n, const Fr* __restrict__
   B[n + 1] = bl[3];
   C[n] = bl[6];
   C[n + 1] = bl[5];
+}
+
+// A, B, C in one MSM schedule (round 6); NZCB_ABC_SETS=0 commits them as three MSMs
+static bool abc_sets_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("NZCB_ABC_SETS");
+    return !e || std::atoi(e) != 0;
+  }();
+  return v;
 }
 
 static bool lagrange_commit_enabled() {
@@ -475,9 +482,9 @@ k_perm_factors(const Fr* __restrict__ ntot, const Fr* __restrict__ dtot, int nti
   const Fr npre = block_scan_excl<false, MulOp, 1024>(pn, sh, &nall);
   const Fr dsuf = block_scan_excl<true, MulOp, 1024>(pd, sh, &dall);
   if (tid == 0) {
-    totals[0] = nall;
-    totals[1] = dall;
-    mailbox_fence();
+    host_put(totals, nall);
+    host_put(totals + 1, dall);
+    host_put_done();
   }
   // within the run: prefix of N (forward), suffix of D (backward)
   Fr run = npre;
@@ -918,8 +925,8 @@ __global__ void __launch_bounds__(kT) k_eval_sum(const Fr* __restrict__ partial,
   for (int b = (int)threadIdx.x; b < nblocks; b += kT) acc = acc + partial[(size_t)j * nblocks + b];
   const Fr r = block_sum_fr(acc, sh);
   if (threadIdx.x == 0) {
-    out[j] = r;  // the mailbox (host memory)
-    mailbox_fence();
+    host_put(out + j, r);  // the mailbox (host memory)
+    host_put_done();
   }
 }
 
@@ -966,8 +973,8 @@ __global__ void k_div_check(const Fr* __restrict__ src, Fr p0_adjust, const Fr* 
   if (threadIdx.x || blockIdx.x) return;
   Fr p0 = src[0] - p0_adjust;
   if (!(p0 + d * q[0]).is_zero()) atomicOr(flags, bit);
-  *mb_flags = *flags;  // the flags word as of this check, into the mailbox
-  mailbox_fence();
+  host_put(mb_flags, *flags);  // the flags word as of this check, into the mailbox
+  host_put_done();
 }
 
 __global__ void k_root_table(Fr* __restrict__ out, Fr base, Fr scale, size_t count) {
@@ -1095,7 +1102,7 @@ void Prover::set_msm_devices(const std::vector<int>& devices) {
     for (int j = 0; j < MsmShard::kSlots; j++) {
       NZ_HIP(hipStreamCreateWithFlags(&sh->st[j], hipStreamNonBlocking));
       sh->sc[j].reset(new MsmScratch());
-      sh->sc[j]->init(mx, true);
+      sh->sc[j]->init(mx, true, 1, false);
       sh->scal[j].alloc(mx);
     }
     {  // the shard's PTau range -> its shifted-base table (built on the shard's device)
@@ -1353,7 +1360,8 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
 void Prover::init_slots() {
   for (int i = 0; i < kSlots; i++) {
     msc[i].reset(new MsmScratch());
-    msc[i]->init((size_t)n + 6, true);
+    // table schedules only; slot 0 also takes A, B, C's three-set schedule over the Lagrange table
+    msc[i]->init((size_t)n + 6, true, i == 0 ? 3 : 1, false);
     NZ_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
     NZ_HIP(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
   }
@@ -1646,6 +1654,9 @@ void Prover::commit_start(int slot, const Fr* coefs, size_t len, const MsmBaseTa
   if (prof_gpu) span_end(sp, ms);
   static const bool serial = std::getenv("NZCB_SERIAL") != nullptr;  // profiling: one kernel at a time
   if (serial) NZ_HIP(hipStreamSynchronize(ms));
+  static const char* const kDone[kSlots] = {"mark: commit enqueued slot 0", "mark: commit enqueued slot 1",
+                                            "mark: commit enqueued slot 2"};
+  roctxMarkA(kDone[slot]);
 }
 
 namespace {
@@ -1695,6 +1706,28 @@ G1Affine Prover::commit_finish(int slot) {
   }
   msm_ms += ms_since(t0);
   return xyzz_to_affine(r);
+}
+
+// A, B and C's commitments in one schedule over the Lagrange table (msm.hip msm_enqueue_sets),
+// on the main stream, slot 0's scratch (sized for three sets, init_slots)
+void Prover::commit_start_abc(size_t len) {
+  roctxMarkA("mark: commit enqueue A, B, C");
+  const Fr* sc[3] = {A.p, B.p, C.p};
+  const size_t sp = prof_gpu ? span_begin(0, st()) : 0;
+  msm_enqueue_sets(*msc[0], sc, 3, len, true, st(), &ltab);
+  if (prof_gpu) span_end(sp, st());
+  roctxMarkA("mark: commit enqueued A, B, C");
+}
+
+void Prover::commit_finish_abc(G1Affine& a, G1Affine& b, G1Affine& c) {
+  auto t0 = std::chrono::steady_clock::now();
+  G1xyzz r[3];
+  msm_finish_sets(*msc[0], st(), r);
+  roctxMarkA("mark: commit result A, B, C");
+  a = xyzz_to_affine(r[0]);
+  b = xyzz_to_affine(r[1]);
+  c = xyzz_to_affine(r[2]);
+  msm_ms += ms_since(t0);
 }
 
 void Prover::set_msm_split(int world, size_t own_points, size_t own_lagrange, nzcb_msm_send_fn send,
@@ -1908,16 +1941,27 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   G1Affine pA, pB, pC, pZ, pT1, pT2, pT3, pWxi, pWxiw;
   {
     const int ba[2] = {2, 1}, bb[2] = {4, 3}, bc[2] = {6, 5};
+    // one schedule for A, B, C unless the commitments are split over ranks or devices (whose
+    // protocol sends each commitment's own scalar ranges)
+    const bool abc_sets = lcommit && shards.empty() && !split_send && msc[0]->max_lsets >= 3 && abc_sets_enabled();
     if (lcommit) {
       // evaluations + blinding scalars against the Lagrange basis: the same points, and the
       // MSMs start before the interpolations (they run on the commitment streams)
       hipLaunchKernelGGL(k_abc_tail, dim3(1), dim3(64), 0, s, A.p, B.p, C.p, (size_t)n, blind.p);
       NZ_HIP(hipGetLastError());
+      if (abc_sets) {
+        // round 6: the three commitments in ONE schedule over the Lagrange table (msm_enqueue_sets:
+        // one bucketing, accumulation and carry reduction over 3 x 2^16 buckets, window sums per
+        // commitment) on the main stream, instead of three MSMs contending for the chip
+        lg("multiexp A, B, C");
+        commit_start_abc(n + 2);
+      } else {
       lg("multiexp A");
       commit_start(0, A.p, n + 2, &ltab, ltau.p);
       lg("multiexp B");
       commit_start(1, B.p, n + 2, &ltab, ltau.p);
       lg("multiexp C");
+      }
       // The interpolations and 4n coset evaluations of A, B, C are only needed by round 3's
       // quotient (and round 4), so they overlap the commitments AND round 2's grand product,
       // which reads the evaluations only (round 2 waits for them before Z's own NTTs, which
@@ -1927,7 +1971,7 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       // not on its stream.
       hipStream_t ss = aux[2];
       NZ_HIP(hipEventRecord(side_ready, s));  // A, B, C final (k_abc_tail), before C's MSM
-      commit_start(2, C.p, n + 2, &ltab, ltau.p, true);
+      if (!abc_sets) commit_start(2, C.p, n + 2, &ltab, ltau.p, true);
       NZ_HIP(hipStreamWaitEvent(ss, side_ready, 0));
       to4t(A.p, pol_a.p, A4.p, ba, 2, ss);
       to4t(B.p, pol_b.p, B4.p, bb, 2, ss);
@@ -1945,9 +1989,13 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       lg("multiexp C");
       commit_start(2, pol_c.p, n + 2);
     }
-    pA = commit_finish(0);
-    pB = commit_finish(1);
-    pC = commit_finish(2);
+    if (lcommit && abc_sets) {
+      commit_finish_abc(pA, pB, pC);
+    } else {
+      pA = commit_finish(0);
+      pB = commit_finish(1);
+      pC = commit_finish(2);
+    }
   }
   tm[2] = ms_since(t1);
 

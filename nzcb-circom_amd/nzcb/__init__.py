@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = [
     "nzcb_engine_create", "nzcb_engine_destroy", "nzcb_engine_ntt", "nzcb_engine_msm", "nzcb_dev_alloc",
     "nzcb_dev_free", "nzcb_memcpy_h2d", "nzcb_memcpy_d2h", "nzcb_engine_ntt_dev", "nzcb_engine_msm_dev",
     "nzcb_engine_time_ntt", "nzcb_engine_fr_mul", "nzcb_engine_random_fr", "nzcb_engine_fixed_base",
-    "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_msm_table_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
+    "nzcb_engine_time_msm", "nzcb_engine_msm_fixed_dev", "nzcb_engine_msm_table_dev", "nzcb_engine_msm_sets_dev", "nzcb_engine_time_msm2", "nzcb_ctx_set_lanes",
     "nzcb_ctx_lanes", "nzcb_prove_batch", "nzcb_vk_from_zkey", "nzcb_vk_from_zkey_file", "nzcb_vk_to_json", "nzcb_verify",
     "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_engine_lagrange_basis", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d",
@@ -190,6 +190,8 @@ def load(path: str | None = None):
                                               POINTER(_Err)]),
         "nzcb_engine_msm_table_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_int, c_int, c_int,
                                               u8p, POINTER(_Err)]),
+        "nzcb_engine_msm_sets_dev": (c_int, [c_void_p, c_void_p, c_size_t, POINTER(c_void_p), c_int, c_size_t, c_int,
+                                             u8p, POINTER(_Err)]),
         "nzcb_plonk_setup": (c_int, [ctypes.c_char_p, c_size_t, ctypes.c_char_p, c_size_t, c_int, POINTER(POINTER(c_uint8)),
                                      POINTER(c_size_t), POINTER(_Err)]),
         "nzcb_nzcp_input_signals": (c_size_t, [POINTER(NzcpParams)]),
@@ -398,6 +400,17 @@ class Engine:
             _check(self.lib.nzcb_engine_msm_fixed_dev(self.h, dev_bases, n_table, dev_scalars, n, int(scalars_mont),
                                                       out, ctypes.byref(err)), err)
         return bytes(out)
+
+    def msm_sets_dev(self, dev_bases: int, n_table: int, dev_scalars: list, n: int, scalars_mont: bool) -> list:
+        """len(dev_scalars) (1..3) MSMs of n scalars over one Lagrange-window table in one schedule
+        (the prover's A, B, C commitments): one 64-byte affine result per set."""
+        k = len(dev_scalars)
+        out = _out(64 * k)
+        err = _Err()
+        arr = (c_void_p * k)(*dev_scalars)
+        _check(self.lib.nzcb_engine_msm_sets_dev(self.h, dev_bases, n_table, arr, k, n, int(scalars_mont), out,
+                                                 ctypes.byref(err)), err)
+        return [bytes(out)[64 * i:64 * i + 64] for i in range(k)]
 
     def msm_dev(self, dev_bases: int, dev_scalars: int, n: int, scalars_mont: bool) -> bytes:
         out = _out(64)

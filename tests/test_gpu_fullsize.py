@@ -152,6 +152,15 @@ def test_msm_2p21_witness_scalars_schedules_agree():
         # the Lagrange table's schedule (window 17, device-derived chunk, carry trees)
         sparse = _affine(eng.msm_fixed_dev(bases, n, sc, n, False, window=17, sparse=True))
         slo = _affine(eng.msm_fixed_dev(bases, h, sc, h, False, window=17, sparse=True))
+        # and the three-set schedule (the prover's A, B, C in one MSM): the same scalars as set 0
+        # and set 2, their halves' order reversed in set 1 (other buckets, same sizes)
+        sc2 = nzcb.dev_alloc(n * 32)
+        try:
+            nzcb.h2d(sc2, raw[32 * h:] + raw[:32 * h])
+            s3 = [_affine(r) for r in eng.msm_sets_dev(bases, n, [sc, sc2, sc], n, False)]
+            rot = _affine(eng.msm_fixed_dev(bases, n, sc2, n, False, window=17, sparse=True))
+        finally:
+            nzcb.dev_free(sc2)
     finally:
         nzcb.dev_free(sc)
         nzcb.dev_free(bases)
@@ -160,3 +169,4 @@ def test_msm_2p21_witness_scalars_schedules_agree():
     assert bn.g1_add(lo, hi) == fixed
     assert sparse == fixed
     assert bn.g1_add(slo, hi) == fixed
+    assert s3[0] == fixed and s3[2] == fixed and s3[1] == rot

@@ -210,6 +210,52 @@ def test_msm_sparse_schedule(engine, n, kind):
     assert _msm_fixed(engine, pts, sc, n_table=n + 2, mont=True, window=17, sparse=True) == want
 
 
+@pytest.mark.parametrize("n,kinds", [(1, ("rand", "ones", "zeros")), (300, ("witness", "equal", "rand")),
+                                     (3000, ("ones", "witness", "mixed")), (1500, ("equal", "equal", "ones")),
+                                     (700, ("zeros", "zeros", "witness")), (2000, ("witness", "rand"))])
+def test_msm_sets_schedule(engine, n, kinds):
+    """msm_enqueue_sets (round 6: the prover's A, B, C in one schedule over the Lagrange table):
+    each set's result equals its own MSM (oracle), for sets whose buckets collide in index
+    (equal scalars in two sets), empty sets, huge single buckets (ones, equal) and the
+    witness-like regime; Montgomery and normal-form scalars."""
+    import nzcb
+    rng = random.Random(5000 + n + len(kinds))
+    pts = _bases(n + 2, 3 * n + 11)
+
+    def scal(kind):
+        if kind == "rand":
+            return [rng.randrange(R_MOD) for _ in range(n)]
+        if kind == "zeros":
+            return [0] * n
+        if kind == "ones":
+            return [1] * n
+        if kind == "equal":
+            return [rng.randrange(R_MOD)] * n
+        if kind == "witness":
+            return [rng.choice([0, 0, 1, 1, 1, R_MOD - 1, rng.randrange(256), rng.randrange(1 << 17),
+                                rng.randrange(R_MOD)]) for _ in range(n)]
+        return [rng.choice([0, 1, 2, R_MOD - 1, rng.randrange(R_MOD)]) for _ in range(n)]
+
+    sets = [scal(k) for k in kinds]
+    if kinds == ("equal", "equal", "ones"):
+        sets[1] = list(sets[0])   # the same bucket in two sets
+    want = [bn.msm(pts[:n], sc) for sc in sets]
+    bases = b"".join(bn.g1_to_lem(p) for p in pts)
+    db = nzcb.dev_alloc(len(bases))
+    ds = [nzcb.dev_alloc(32 * n) for _ in sets]
+    try:
+        nzcb.h2d(db, bases)
+        for mont in (False, True):
+            for d, sc in zip(ds, sets):
+                nzcb.h2d(d, _lem(sc, R_MOD) if mont else b"".join(bn.to_le(x) for x in sc))
+            got = [_affine(r) for r in engine.msm_sets_dev(db, n + 2, ds, n, mont)]
+            assert got == want, (mont, [g == w for g, w in zip(got, want)])
+    finally:
+        nzcb.dev_free(db)
+        for d in ds:
+            nzcb.dev_free(d)
+
+
 def test_msm_fixed_base_infinity_bases(engine):
     g = bn.g1_mul(bn.G1_GEN, 777)
     pts = [g, None, bn.g1_neg(g), g, None, g]
