@@ -1089,13 +1089,17 @@ msm_large_piece29_kernel(uint32_t chunk, const uint32_t* __restrict__ offsets, u
   }
 }
 
-// a listed bucket's pieces: one workgroup per bucket, a sequential add per thread while
-// there are more than kSumThreads pieces, then the tree
-__global__ void __launch_bounds__(kSumThreads)
+// a listed bucket's pieces: one workgroup of NT threads per bucket, a sequential add per
+// thread while there are more than NT pieces, then the tree. The dense tables' launch keeps
+// one-wave workgroups (64 threads, as until round 5): it finds nothing to do for random
+// scalars, and a 4-wave workgroup of 213 VGPRs waited longer for a free SIMD under the
+// other lanes' accumulations; the sparse tables' bucket 0 holds hundreds of pieces (256).
+template <int NT>
+__global__ void __launch_bounds__(NT)
 msm_large_final29_kernel(const uint32_t* __restrict__ large, const uint32_t* __restrict__ off,
                          const Xyzz29* __restrict__ part, Xyzz29* __restrict__ out29) {
   tail_prio();
-  __shared__ Xyzz29 sh[kSumThreads];
+  __shared__ Xyzz29 sh[NT];
   const uint32_t count = large[0];
   for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
     const uint32_t p0 = off[i], np = off[i + 1] - p0;
@@ -1105,8 +1109,8 @@ msm_large_final29_kernel(const uint32_t* __restrict__ large, const uint32_t* __r
     }
     Xyzz29 v;
     if (threadIdx.x < np) v = part[p0 + threadIdx.x];
-    for (uint32_t q = threadIdx.x + kSumThreads; q < np; q += kSumThreads) v = add29(v, part[p0 + q]);
-    v = tree_sum29(v, np < kSumThreads ? np : kSumThreads, sh);
+    for (uint32_t q = threadIdx.x + NT; q < np; q += NT) v = add29(v, part[p0 + q]);
+    v = tree_sum29(v, np < NT ? np : NT, sh);
     if (threadIdx.x == 0) out29[large[1 + i]] = v;
     __syncthreads();
   }
@@ -1729,8 +1733,12 @@ static void msm_enqueue_impl(MsmScratch& sc, const G1Affine* bases, const Fr* co
                        (const Xyzz29*)sc.carry_own29.p, (const Xyzz29*)sc.carry_cont29.p, sc.large_part.p);
     NZ_HIP(hipGetLastError());
     lmark("mark: L piece");
-    hipLaunchKernelGGL(msm_large_final29_kernel, dim3(sparse ? kSparseFinalBlocks : kLargeFinalBlocks),
-                       dim3(kSumThreads), 0, st, sc.large.p, sc.large_off.p, sc.large_part.p, sc.buckets29.p);
+    if (sparse)
+      hipLaunchKernelGGL(msm_large_final29_kernel<kSumThreads>, dim3(kSparseFinalBlocks), dim3(kSumThreads), 0, st,
+                         sc.large.p, sc.large_off.p, sc.large_part.p, sc.buckets29.p);
+    else
+      hipLaunchKernelGGL(msm_large_final29_kernel<64>, dim3(kLargeFinalBlocks), dim3(64), 0, st, sc.large.p,
+                         sc.large_off.p, sc.large_part.p, sc.buckets29.p);
     NZ_HIP(hipGetLastError());
     lmark("mark: L final");
     mark(5);

@@ -1949,11 +1949,14 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       // MSMs start before the interpolations (they run on the commitment streams)
       hipLaunchKernelGGL(k_abc_tail, dim3(1), dim3(64), 0, s, A.p, B.p, C.p, (size_t)n, blind.p);
       NZ_HIP(hipGetLastError());
+      NZ_HIP(hipEventRecord(side_ready, s));  // A, B, C final (k_abc_tail): the side stream's start
       if (abc_sets) {
         // round 6: the three commitments in ONE schedule over the Lagrange table (msm_enqueue_sets:
         // one bucketing, accumulation and carry reduction over 3 x 2^16 buckets, window sums per
         // commitment) on the main stream, instead of three MSMs contending for the chip
-        lg("multiexp A, B, C");
+        lg("multiexp A");  // snarkjs's logger lines, one per commitment
+        lg("multiexp B");
+        lg("multiexp C");
         commit_start_abc(n + 2);
       } else {
       lg("multiexp A");
@@ -1970,7 +1973,6 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
       // (round 3, profiles/r3_side_stream_ab.txt). msm_finish waits on the MSM's own event,
       // not on its stream.
       hipStream_t ss = aux[2];
-      NZ_HIP(hipEventRecord(side_ready, s));  // A, B, C final (k_abc_tail), before C's MSM
       if (!abc_sets) commit_start(2, C.p, n + 2, &ltab, ltau.p, true);
       NZ_HIP(hipStreamWaitEvent(ss, side_ready, 0));
       to4t(A.p, pol_a.p, A4.p, ba, 2, ss);
