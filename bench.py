@@ -90,6 +90,24 @@ def max_over_ranks(x: float, dist, device) -> float:
     return float(t.item())
 
 
+def rank_memory(device: int, dist) -> list:
+    """Per rank, after the timed region: HBM in use on its device (hipMemGetInfo through
+    torch: device-wide, so ranks sharing a device in a rehearsal see each other's), i.e. the
+    proving key, both fixed-base tables, every lane's working set and the witness buffers;
+    and the process's peak host RSS. DESIGN.md §6 sizes an 8-rank node from these."""
+    import resource
+    import torch
+    free, total = torch.cuda.mem_get_info(device)
+    me = {"rank": dist.get_rank() if dist is not None else 0, "device": device,
+          "hbm_used_gib": round((total - free) / 2**30, 2), "hbm_total_gib": round(total / 2**30, 1),
+          "host_peak_rss_gib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 2)}
+    if dist is None:
+        return [me]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return out
+
+
 def pass_data(i: int) -> bytes:
     """The 20 pass-through data bytes of proof i."""
     return hashlib.sha256(b"nzcb-pass" + i.to_bytes(4, "little")).digest()[:20]
@@ -395,7 +413,8 @@ def main():
     t_w = time.perf_counter()
     prover.witness_staged(len(mine))
     witness_ms = (time.perf_counter() - t_w) * 1e3
-    probe = accumulate_probe(n + 6, device) if rank == 0 and not args.no_probe else None
+    mem = rank_memory(device, dist)
+    probe =accumulate_probe(n + 6, device) if rank == 0 and not args.no_probe else None
     elapsed = max_over_ranks(elapsed, dist, f"cuda:{device}" if backend == "nccl" else "cpu")
     total_proofs = args.steps if split else (args.batch if args.batch else args.steps * world)
     steps = len(shard(args.batch, 0, world)) if args.batch and not split else args.steps
@@ -513,6 +532,7 @@ def main():
             "phase_ms_single_proof": {k: round(v, 3) for k, v in single_timings.items()},
             "pcie_inclusive_ms": round(pcie_ms, 3),
             "setup_s": round(setup_s, 2),
+            "memory_per_rank": mem,
             "cpu_baseline": cpu,
         }
         if not verified:  # never report a rate for proofs that do not verify

@@ -86,6 +86,14 @@ def acc_pmc(src, ent):
     return "\n".join(lines) + "\n"
 
 
+def head_commit() -> str:
+    try:
+        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], check=True, capture_output=True,
+                              text=True).stdout.strip()
+    except (OSError, subprocess.CalledProcessError):
+        return "unknown"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--prefix", default="r1")
@@ -106,13 +114,15 @@ def main():
     trace = os.path.join(prof, "run_kernel_trace.csv")
     psumm = subprocess.run([sys.executable, ts, trace, "--last", KERNEL, str(probe), "--durations", "--top", "12"],
                            check=True, capture_output=True, text=True).stdout
-    summ = subprocess.run([sys.executable, ts, trace, "--last", KERNEL, str(launches), "--skip-last", str(probe + 3),
+    summ = subprocess.run([sys.executable, ts, trace, "--last", KERNEL, str(launches), "--before-last", "k_fixed_base",
                            "--durations", "--top", "30"], check=True, capture_output=True, text=True).stdout
     with open(os.path.join(out, f"{a.prefix}_bench_trace_summary.txt"), "w") as f:
         f.write(f"# isolated probe: the last {probe} {KERNEL} launches of the profiled bench.py run "
                 f"(bench.py accumulate_probe; roofline.avg_launch_ms = {bench['roofline']['avg_launch_ms']} ms "
                 f"from its HIP events)\n" + psumm +
-                f"\n# timed window: the {launches} {KERNEL} launches before the probe (40 proofs x 9 MSMs)\n" + summ)
+                f"\n# timed window: the {launches} {KERNEL} launches before the probe (its random bases, k_fixed_base, start it) "
+                f"(the timed region's proofs x their MSM launches: 7 per proof since round 6, the A, B, C "
+                f"commitments being one)\n" + summ)
     nf, fetch_kb = pmc_avg(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     nw, write_kb = pmc_avg(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     fetch_raw = fetch_kb * 1024
@@ -126,6 +136,8 @@ def main():
                                    "WRITE_SIZE": {"launches": nw, "avg_kb_per_launch": round(write_kb, 1)}},
         "correction": "none: random 64-byte gathers are counted at ~1.15x their bytes, not 1/2 "
                       "(profiles/r2_fetch_calibration.txt, tools/gather_calib.hip); FETCH_SIZE + WRITE_SIZE as reported",
+        # bench.py puts this into roofline.traffic_source (the run the bytes came from)
+        "source": "tools/profile_round.sh, %s profile set, commit %s" % (a.prefix, head_commit()),
         "fetch_bytes_per_launch_raw": int(fetch_raw),
         "bytes_per_launch": int(fetch_raw + write_kb * 1024),
         "note": "gathers are random 64 B affine table points (16 B/lane dwordx4 loads); algorithmic bytes "

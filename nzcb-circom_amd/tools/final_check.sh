@@ -1,7 +1,7 @@
 #!/bin/bash
 # End-of-round check on one box (from the repo root, GPU box): the whole -m gpu suite, smoke(),
 # the default bench.py line, and one same-box pair against the previous round's library
-# (lib/ab/libnzcb_r4.so, built from round 4's last commit) at --steps 300.
+# (lib/ab/libnzcb_r5.so, built from round 5's last commit) at --steps 300; the pair runs twice.
 #   bash nzcb-circom_amd/tools/final_check.sh   -> gpurun_out/final/{pytest,smoke,bench,ab_*}.log
 # Each GPU step has its own time limit; the first failure ends the call.
 set -o pipefail
@@ -18,10 +18,10 @@ tail -1 $O/smoke.log
 step bench
 timeout -k 10 600 python3 -u bench.py > $O/bench.log 2>&1 || exit $?
 grep '^{"metric"' $O/bench.log | tail -1 | cut -c1-400
-R4=nzcb-circom_amd/lib/ab/libnzcb_r4.so
-if [ -f $R4 ]; then
-  for cfg in r4 r5; do
-    L=nzcb-circom_amd/lib/libnzcb.so; [ $cfg = r4 ] && L=$R4
+PREV=nzcb-circom_amd/lib/ab/libnzcb_r5.so
+if [ -f $PREV ]; then
+  for cfg in r5 r6 r5b r6b; do
+    L=nzcb-circom_amd/lib/libnzcb.so; [ ${cfg:0:2} = r5 ] && L=$PREV
     step "ab $cfg"
     NZCB_LIB=$L timeout -k 10 300 python3 -u bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-probe > $O/ab_$cfg.log 2>&1 || exit $?
     python3 -c "import json;d=json.loads([l for l in open('$O/ab_$cfg.log') if l.startswith('{')][-1]);print('$cfg', d['value'], d['ms_per_step'], d['single_proof_latency_ms'])"

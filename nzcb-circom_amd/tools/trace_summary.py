@@ -15,6 +15,9 @@ def main():
                     help="window from the COUNT-th last launch of a kernel whose name contains KERNEL to its last")
     ap.add_argument("--skip-last", type=int, default=0,
                     help="with --last: end the window before the kernel's last SKIP launches (e.g. a probe)")
+    ap.add_argument("--before-last", metavar="NAME", default=None,
+                    help="with --last: end the window before the last launch of a kernel whose name contains NAME "
+                         "(bench.py's probe starts with k_fixed_base, its random bases)")
     ap.add_argument("--durations", action="store_true",
                     help="with --last: also print the average duration of the KERNEL launches in the window")
     a = ap.parse_args()
@@ -31,6 +34,9 @@ def main():
     t_end = max(e for _, e, _ in rows)
     if a.last:
         hits = [r for r in rows if a.last[0] in r[2]]
+        if a.before_last:
+            cut = max(r[0] for r in rows if a.before_last in r[2])
+            hits = [r for r in hits if r[1] <= cut]
         if a.skip_last:
             hits = hits[:-a.skip_last]
         hits = hits[-int(a.last[1]):]
