@@ -91,13 +91,20 @@ def max_over_ranks(x: float, dist, device) -> float:
 
 
 def rank_memory(device: int, dist) -> list:
-    """Per rank, after the timed region: HBM in use on its device (hipMemGetInfo through
-    torch: device-wide, so ranks sharing a device in a rehearsal see each other's), i.e. the
-    proving key, both fixed-base tables, every lane's working set and the witness buffers;
-    and the process's peak host RSS. DESIGN.md §6 sizes an 8-rank node from these."""
+    """Per rank, after the timed region: HBM in use on its device (hipMemGetInfo, device-wide:
+    ranks sharing a device in a rehearsal see each other's), i.e. the proving key, both
+    fixed-base tables, every lane's working set and the witness buffers; and the process's
+    peak host RSS. DESIGN.md §6 sizes an 8-rank node from these."""
+    import ctypes
     import resource
-    import torch
-    free, total = torch.cuda.mem_get_info(device)
+    # the HIP runtime the prover library already loaded (not a second copy by name)
+    with open("/proc/self/maps") as f:
+        paths = [ln.split()[-1] for ln in f if "libamdhip64.so" in ln]
+    hip = ctypes.CDLL(paths[0] if paths else "libamdhip64.so")
+    free, total = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    if hip.hipSetDevice(ctypes.c_int(device)) != 0 or hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) != 0:
+        free.value = total.value = 0
+    free, total = free.value, total.value
     me = {"rank": dist.get_rank() if dist is not None else 0, "device": device,
           "hbm_used_gib": round((total - free) / 2**30, 2), "hbm_total_gib": round(total / 2**30, 1),
           "host_peak_rss_gib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 2)}

@@ -491,7 +491,7 @@ nzcb_msm_table* nzcb_msm_table_create_lagrange(int device, const void* dev_ptau,
         DevBuf<G1Affine> basis(nl);
         lagrange_basis((const G1Affine*)dev_ptau, ptau_n, log_n, basis.p, t->st);
         t->table.build(basis.p + lo, hi - lo, lagrange_window(), t->st);
-        t->table.sparse = true;
+        t->table.sparse = lagrange_sparse();
         NZ_HIP(hipStreamSynchronize(t->st));
       }
       t->sc.init(hi - lo, true, 1, false);

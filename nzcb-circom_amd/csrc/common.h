@@ -21,19 +21,16 @@ struct Error : std::runtime_error {
 void set_err(nzcb_err* err, int code, const char* msg);
 
 // Kernel stores into pinned host memory (the prover's mailbox, the fixed-base MSM's window
-// sums; round 6): system-scope stores, which write through the GPU caches, and a wait for their
-// completion before the wave ends, so the host sees them once it has seen the kernel complete.
-// Not __threadfence_system(): on gfx950 that is an L2 writeback plus an L2 invalidate
-// (buffer_wbl2 / buffer_inv sc0 sc1), which stalls every kernel sharing the XCD.
+// sums; round 6): plain stores, then a system-scope fence before the wave ends, so the host
+// sees them once it has seen the kernel complete. Round 6 also tried one system-scope atomic
+// store per 32-bit word and a wait for them (no L2 writeback): same box, 5-lane bench, three
+// runs each, that cost 0.8 % of proofs/s against this (profiles/r6_sets_ab.txt, r6l: 36 uncached
+// word writes per 144-byte window slot instead of nine 16-byte ones).
 template <class T>
 __device__ __forceinline__ void host_put(T* dst, const T& v) {
-  static_assert(sizeof(T) % 4 == 0, "host_put: whole 32-bit words");
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(&v);
-  uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-#pragma unroll
-  for (unsigned i = 0; i < sizeof(T) / 4; i++) __hip_atomic_store(d + i, s[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  *dst = v;
 }
-__device__ __forceinline__ void host_put_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void host_put_done() { __threadfence_system(); }
 
 
 #define NZ_HIP(call)                                                                  \

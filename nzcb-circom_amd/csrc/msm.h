@@ -25,12 +25,16 @@ struct MsmBaseTable {
   void build(const G1Affine* bases, size_t n, int c, hipStream_t st, bool fold_mont = false);
 };
 
-// Window size of the table-based (fixed-base) MSM: 17 bits by default (15 table rows,
-// 2^16 buckets); NZCB_FB_WINDOW = 16..20 overrides it.
+// Window size of the table-based (fixed-base) MSM: 20 bits by default (13 table rows,
+// 2^19 buckets; round 5); NZCB_FB_WINDOW = 16..20 overrides it.
 int fixed_base_window();
 // Window of the Lagrange-basis table (A, B, C commitments of small witness values: 17):
 // their few entries do not pay for a larger bucket set.
 int lagrange_window();
+// the Lagrange tables' schedule (round 6): the sparse one (device-derived chunk, carry trees)
+// with NZCB_SPARSE=1; off by default: on nzcp_live's A, B, C it cost 0.8-1.3 % of proofs/s
+// against the dense schedule (profiles/r6_sets_ab.txt) for no single-proof latency gain
+bool lagrange_sparse();
 
 struct MsmScratch {
   size_t max_points = 0;

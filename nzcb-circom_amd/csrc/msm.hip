@@ -146,6 +146,13 @@ int fixed_base_window() {
 #define NZ_LAGRANGE_WINDOW 17
 #endif
 int lagrange_window() { return NZ_LAGRANGE_WINDOW; }
+bool lagrange_sparse() {
+  static const bool v = [] {
+    const char* e = std::getenv("NZCB_SPARSE");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
 
 int msm_window_bits(size_t n) {
   if (n >= (size_t(1) << 18)) return 16;
@@ -685,7 +692,7 @@ __device__ __forceinline__ G1xyzz load_point(const Xyzz29& a) {
   return r;
 }
 
-// kLdsIdx (chunk == kChunk): the workgroup's kMsmThreads x kChunk slice of `sorted` is
+// kLdsIdx (chunk <= kChunk): the workgroup's kMsmThreads x chunk slice of `sorted` is
 // staged into LDS by coalesced loads before the additions. Read from HBM one index per
 // addition, each lane's chunk 192 B from its neighbour's, the index lines were evicted
 // between uses by the table gathers and fetched again (~1 GB of the 3.3 GB a launch
@@ -708,14 +715,17 @@ msm_accumulate29_kernel(uint32_t chunk, const G1Affine* __restrict__ bases, cons
   __shared__ uint32_t sidx[kLdsIdx ? kChunk * kLdsStride : 1];
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;  // < 2^32 (entries / chunk)
   const uint32_t M = offsets[nkeys];
-  if (!kLdsIdx && !chunk) {  // sparse tables: derived from the entry count
+  if (!chunk) {  // sparse tables: derived from the entry count (<= kChunk)
     chunk = dyn_chunk(M);
     tail_prio();
   }
-  if (kLdsIdx) {  // every thread of the workgroup takes part before any exits
-    const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * kChunk;
-    for (uint32_t j = threadIdx.x; j < kMsmThreads * kChunk; j += kMsmThreads) {
-      const uint32_t thr = j / kChunk, slot = j - thr * kChunk;
+  if (kLdsIdx) {  // chunk <= kChunk; every thread of the workgroup takes part before any exits
+    const uint32_t wg0 = (uint32_t)blockIdx.x * kMsmThreads * chunk;
+    if (wg0 >= M) return;  // the whole workgroup is past the stream (the sparse grids' bound)
+    // j / chunk by a multiply-high: inv = ceil(2^32 / chunk) is exact for j < 2^32 / chunk^2
+    const uint32_t inv = (uint32_t)((0x100000000ull + chunk - 1) / chunk);
+    for (uint32_t j = threadIdx.x; j < kMsmThreads * chunk; j += kMsmThreads) {
+      const uint32_t thr = __umulhi(j, inv), slot = j - thr * chunk;
       sidx[slot * kLdsStride + thr] = wg0 + j < M ? sorted[wg0 + j] : 0u;
     }
     __syncthreads();
@@ -1704,7 +1714,7 @@ static void msm_enqueue_impl(MsmScratch& sc, const G1Affine* bases, const Fr* co
   const dim3 agrid(grid_for(nthreads, kMsmThreads, 1u << 30));
   const G1Affine* gather = table ? table->q.p : bases;
   if (table) {
-    if (chunk == kChunk)
+    if (chunk == kChunk || sparse)  // sparse: chunk <= kChunk
       hipLaunchKernelGGL(msm_accumulate29_kernel<true>, agrid, dim3(kMsmThreads), 0, st, chunk, gather, sc.sorted.p,
                          sc.offsets.p, p.nkeys, nthreads, sc.buckets29.p, sc.carry_own29.p, sc.carry_cont29.p);
     else

@@ -1111,12 +1111,12 @@ void Prover::set_msm_devices(const std::vector<int>& devices) {
       sh->table.build(part.p, cnt, fixed_base_window(), sh->st[0]);
       NZ_HIP(hipStreamSynchronize(sh->st[0]));
     }
-    if (lcnt) {  // and its range of the Lagrange basis (A, B, C: the sparse schedule)
+    if (lcnt) {  // and its range of the Lagrange basis (A, B, C)
       DevBuf<G1Affine> part(lcnt);
       NZ_HIP(hipMemcpyPeerAsync(part.p, sh->device, ltau.p + sh->llo, eng->device, lcnt * sizeof(G1Affine),
                                 sh->st[0]));
       sh->ltable.build(part.p, lcnt, lagrange_window(), sh->st[0]);
-      sh->ltable.sparse = true;
+      sh->ltable.sparse = lagrange_sparse();
       NZ_HIP(hipStreamSynchronize(sh->st[0]));
     }
     shards.push_back(std::move(sh));
@@ -1165,7 +1165,7 @@ Prover::Prover(const uint8_t* zkey_bytes, size_t len, int device) {
     ltau.alloc((size_t)n + 2);
     lagrange_basis(ptau.p, ptau.n, power, ltau.p, s);
     ltab.build(ltau.p, ltau.n, lagrange_window(), s);
-    ltab.sparse = std::getenv("NZCB_SPARSE") == nullptr || std::atoi(std::getenv("NZCB_SPARSE")) != 0;  // A/B (round 6)
+    ltab.sparse = lagrange_sparse();
   }
   up(qm, z.qm);
   up(ql, z.ql);
@@ -1361,7 +1361,11 @@ void Prover::init_slots() {
   for (int i = 0; i < kSlots; i++) {
     msc[i].reset(new MsmScratch());
     // table schedules only; slot 0 also takes A, B, C's three-set schedule over the Lagrange table
+#ifdef NZCB_AB_GENERIC  // A/B (temporary): the generic schedule's arrays allocated too, as before round 6
+    msc[i]->init((size_t)n + 6, true, i == 0 ? 3 : 1, true);
+#else
     msc[i]->init((size_t)n + 6, true, i == 0 ? 3 : 1, false);
+#endif
     NZ_HIP(hipStreamCreateWithFlags(&aux[i], hipStreamNonBlocking));
     NZ_HIP(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
   }

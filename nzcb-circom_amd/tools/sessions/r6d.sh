@@ -1,0 +1,24 @@
+#!/bin/bash
+# round 6: parity of the mailbox build + same-box A/B (r5, new, new without the sparse schedule,
+# tail priority, host kernel arguments)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out; O=gpurun_out/r6d; rm -rf $O; mkdir -p $O
+echo "== pytest $(date +%T)"
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_prover.py tests/test_gpu_split.py tests/test_gpu_batch512.py -m gpu -x -v \
+  --timeout 800 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+echo "== ab $(date +%T)"
+run() {  # name lib env...
+  local name=$1 lib=$2; shift 2
+  env NZCB_LIB=$lib "$@" timeout -k 10 300 python3 -u bench.py --steps 200 --warmup 5 --no-cpu-baseline --no-probe > $O/ab_$name.log 2>&1 || return $?
+  python3 -c "import json;d=json.loads([l for l in open('$O/ab_$name.log') if l.startswith('{')][-1]);p=d['phase_ms_single_proof'];print('$name', d['value'], d['ms_per_step'], d['single_proof_latency_ms'], [p[k] for k in ('round1','round2','round3','round5')])" | tee -a $O/ab.txt
+}
+L=nzcb-circom_amd/lib/libnzcb.so; A=nzcb-circom_amd/lib/ab
+for rep in 1 2; do
+  run r5 $A/libnzcb_r5.so || exit $?
+  run new $L || exit $?
+  run nosparse $L NZCB_SPARSE=0 || exit $?
+  run prio $A/libnzcb_prio.so || exit $?
+  run hostkarg $L HIP_FORCE_DEV_KERNARG=0 || exit $?
+done
+echo done

@@ -301,6 +301,36 @@ def test_quotient_schedules_same_proof(quot3, lcommit):
     assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stdout + p.stderr
 
 
+@pytest.mark.parametrize("sparse,sets", [("0", "0"), ("0", "1"), ("1", "0"), ("1", "1")])
+def test_abc_commitment_schedules_same_proof(sparse, sets):
+    """Round 6's two switches of the A, B, C commitments, both sides each (a fresh process:
+    they are read once): NZCB_SPARSE (the Lagrange table's device-derived chunk and carry
+    trees) and NZCB_ABC_SETS (the three commitments as one 3-set MSM instead of three). p5
+    and p8 prove bit for bit, on one lane and on three lanes at once."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = (
+        "import sys, json; sys.path[:0] = [%r, %r]\n"
+        "import nzcb\n"
+        "from oracle import binfmt\n"
+        "g = %r\n"
+        "for name in ('p5', 'p8'):\n"
+        "    meta = json.load(open(g + '/' + name + '.json')); exp = meta['proofs']['fixed']\n"
+        "    zkey = open(g + '/' + name + '.zkey', 'rb').read(); wtns = open(g + '/' + name + '.wtns', 'rb').read()\n"
+        "    wit = b''.join(x.to_bytes(32, 'little') for x in binfmt.read_wtns(wtns)['witness'])\n"
+        "    ctx = nzcb.ProverContext(zkey)\n"
+        "    for lanes in (1, 3):\n"
+        "        ctx.set_lanes(lanes)\n"
+        "        res = ctx.prove_batch_raw([wit] * lanes, blindings=[bytes.fromhex(exp['blinding'])] * lanes)\n"
+        "        assert all(p.hex() == exp['proof_bin'] for p, _ in res), (name, lanes)\n"
+        "    ctx.close()\n"
+        "print('ok')\n" % (os.path.join(root, "nzcb-circom_amd"), root, GOLD))
+    env = dict(os.environ, NZCB_SPARSE=sparse, NZCB_ABC_SETS=sets)
+    p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stdout + p.stderr
+
+
 @pytest.mark.parametrize("name", ["p5", "p8"])
 def test_quotient_fault_is_caught_then_proves_again(name):
     """the xi check (prover.hip, round 4) is the only check on the
