@@ -39,7 +39,20 @@ int nzcb_debug_guard_selftest(int device, nzcb_err* err);
  * snarkjs' 2, 3) instead of 2 beta w^i and 3 beta w^i by additions; the proof must be the
  * same. One-shot per context, like the fault. */
 #define NZCB_DEBUG_GENERIC_K 2
+/* Kind NZCB_FAULT_LANE_ALLOC arms the context's next nzcb_ctx_set_lanes growth instead of a
+ * proof: after its first new lane a real device allocation larger than HBM fails (HIP's
+ * per-thread last error then holds the out-of-memory code, as after a real failed growth) and
+ * the call returns NZCB_ERR_HIP. The rollback must leave lanes() at its old value, the
+ * pool consistent and the thread's last error cleared. One-shot. */
+#define NZCB_FAULT_LANE_ALLOC 3
 int nzcb_debug_inject_fault(nzcb_ctx* ctx, int kind);
+
+/* The 9x29-bit products of csrc/f29.h as compiled for the device (the generated column asm),
+ * over `count` host items of 32-bit limb words (9 per value), for tests against exact
+ * integers. op 1: mul_shoup(x, w, ws) (27 words in, 9 out); 2: mul_shoup_x2 (54 / 18);
+ * 3: mul29<Fq29>(a, b) (18 / 9); 4: mul29x2<Fr29>(a, b, c, d) (36 / 18); 5: sqr29x2(a, c)
+ * (18 / 18); 6: mul2sum29(a, b, c, d) (36 / 9). Synchronous; count <= 2^24. */
+int nzcb_debug_f29(int device, int op, const uint32_t* in, size_t count, uint32_t* out, nzcb_err* err);
 
 /* ---- Synthetic circuit + setup ------- */
 /* Builds the seeded synthetic circuit of oracle/synth.py and its snarkjs-0.4

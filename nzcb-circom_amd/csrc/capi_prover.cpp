@@ -63,6 +63,7 @@ struct nzcb_ctx {
   // nzcb_debug_inject_fault: armed for the context's next proof, whichever lane takes it (a
   // per-lane flag left the other lanes of a multi-lane context armed)
   std::atomic<int> pending_fault{0};
+  std::atomic<int> lane_alloc_fault{0};  // NZCB_FAULT_LANE_ALLOC: the next set_lanes growth fails
   Prover* lane(size_t i) { return i == 0 ? p.get() : extra[i - 1].get(); }
   size_t lanes() const { return 1 + extra.size(); }  // per device
   // every lane of every device (batch workers), device-interleaved so that a short batch
@@ -263,6 +264,12 @@ int nzcb_ctx_set_lanes(nzcb_ctx* ctx, int lanes, nzcb_err* err) {
         ctx->extra.emplace_back(new Prover(*ctx->p, l));
         for (size_t d = 0; d < ctx->dev_p.size(); d++)
           ctx->dev_extra[d].emplace_back(new Prover(*ctx->dev_p[d], l));
+        if (ctx->lane_alloc_fault.exchange(0)) {  // nzcb_debug_inject_fault(NZCB_FAULT_LANE_ALLOC)
+          void* big = nullptr;
+          const hipError_t e = hipMalloc(&big, size_t(1) << 50);
+          if (e == hipSuccess) (void)hipFree(big);
+          throw Error(NZCB_ERR_HIP, std::string("injected lane allocation failure: ") + hipGetErrorString(e));
+        }
       }
     } catch (...) {
       // growth failed (out of HBM): back to the previous count on every device, so the
@@ -524,9 +531,16 @@ int nzcb_ctx_kernel_stats(nzcb_ctx* ctx, int enable, double out[4]) {
 }
 
 int nzcb_debug_inject_fault(nzcb_ctx* ctx, int kind) {
-  if (!ctx || (kind != 0 && kind != NZCB_FAULT_QUOTIENT && kind != NZCB_DEBUG_GENERIC_K)) return NZCB_ERR_ARG;
+  if (!ctx || (kind != 0 && kind != NZCB_FAULT_QUOTIENT && kind != NZCB_DEBUG_GENERIC_K &&
+               kind != NZCB_FAULT_LANE_ALLOC))
+    return NZCB_ERR_ARG;
   std::unique_lock<std::shared_mutex> lk(ctx->cfg);
+  if (kind == NZCB_FAULT_LANE_ALLOC) {
+    ctx->lane_alloc_fault = 1;
+    return 0;
+  }
   ctx->pending_fault = kind;
+  if (kind == 0) ctx->lane_alloc_fault = 0;
   return 0;
 }
 

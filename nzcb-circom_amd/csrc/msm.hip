@@ -190,6 +190,29 @@ __device__ __forceinline__ void for_each_digit(const Fr& s, F&& f) {
   }
 }
 
+#ifdef NZCB_MSM_STATS
+template <class F>
+static void for_each_digit_host(const Fr& s, int C, F&& f) {
+  const int NW = (255 + C - 1) / C;
+  const uint32_t MASK = (1u << C) - 1u, HALF = 1u << (C - 1);
+  uint32_t carry = 0;
+  for (int w = 0; w < NW; w++) {
+    const int bit = w * C, limb = bit >> 5, sh = bit & 31;
+    uint64_t x = s.v[limb];
+    if (limb + 1 < 8) x |= (uint64_t)s.v[limb + 1] << 32;
+    uint32_t d = ((uint32_t)(x >> sh) & MASK) + carry;
+    if (d > HALF) {
+      uint32_t mag = (MASK + 1u) - d;
+      if (mag) f(w, mag - 1u, 1u);
+      carry = 1;
+    } else {
+      if (d) f(w, d - 1u, 0u);
+      carry = 0;
+    }
+  }
+}
+#endif
+
 // generic schedule: key = w * NB + bucket, value = i | sign << 31; zero digits a sentinel
 // key that sorts after every bucket
 template <int C>
@@ -248,11 +271,35 @@ static constexpr int kLoThreads = 512;
 // the (key, value) of every window of scalar i; bit w of the result is set for the
 // windows with a nonzero digit (zero digits make no entry: a scalar of b bits costs about
 // b / C entries, which the Lagrange-basis commitments of small witness values rely on)
+// Signed scalars (round 6): s and r - s reach the same point with the base negated (every
+// base has order r), and the fixed-base schedule buckets whichever of the two is smaller, the
+// negation riding in every entry's sign bit. Random scalars lose nothing (their 13 windows stay
+// occupied); the Lagrange-basis A, B, C values, of which 13-29 % are small negatives r - k
+// (15 nonzero 17-bit digits as they stand, one as k), fall from 21.7 M to 4.7 M bucket
+// entries per proof (nzcp_live, profiles/r6_abc_scalars.txt). Values >= r (never produced)
+// are left as they are. Returns 1 when s was replaced by r - s.
+__device__ __forceinline__ uint32_t scalar_min_form(Fr& s) {
+  constexpr uint32_t H[8] = {0xf8000000u, 0xa1f0fac9u, 0x3cdcb848u, 0x9419f424u,
+                             0x40c0ac2eu, 0xdc2822dbu, 0x7098d014u, 0x18322739u};  // (r - 1) / 2
+  bool gt = false, eq = true, lt_r = false, eq_r = true;
+#pragma unroll
+  for (int l = 7; l >= 0; l--) {
+    gt = gt || (eq && s.v[l] > H[l]);
+    eq = eq && s.v[l] == H[l];
+    lt_r = lt_r || (eq_r && s.v[l] < FrParams::P[l]);
+    eq_r = eq_r && s.v[l] == FrParams::P[l];
+  }
+  if (!(gt && lt_r)) return 0u;
+  s = neg(s);
+  return 1u;
+}
+
 template <int C, int NW>
 __device__ __forceinline__ uint32_t bin_entries(const Fr* __restrict__ scalars, size_t i, int mont, size_t stride,
                                                 uint32_t (&kk)[NW], uint32_t (&vv)[NW]) {
   Fr s = scalars[i];
   if (mont) s = from_mont_fr29(s);
+  const uint32_t flip = scalar_min_form(s);
   uint32_t live = 0;
 #pragma unroll
   for (int w = 0; w < NW; w++) {
@@ -261,7 +308,7 @@ __device__ __forceinline__ uint32_t bin_entries(const Fr* __restrict__ scalars, 
   }
   for_each_digit<C>(s, [&](int w, uint32_t b, uint32_t sign) {
     kk[w] = b;
-    vv[w] = (uint32_t)((size_t)w * stride + i) | (sign << 31);
+    vv[w] = (uint32_t)((size_t)w * stride + i) | ((sign ^ flip) << 31);
     live |= 1u << w;
   });
   return live;
@@ -1663,6 +1710,38 @@ static void msm_enqueue_impl(MsmScratch& sc, const G1Affine* bases, const Fr* co
   if (msets < 1 || msets > kMaxSets || (msets > 1 && (!table || msets > sc.max_lsets)))
     throw Error(NZCB_ERR_ARG, "msm sets: 1..3 over a table, within the scratch's sizing");
   const MsmPlan p = make_plan(n, table, msets);
+#ifdef NZCB_MSM_STATS
+  if (table && !table->mont_folded) {  // scalar census (diagnostics build): nonzero c-bit digits of
+    // s and of min(s, r - s), the form a per-scalar sign flip would bucket
+    NZ_HIP(hipStreamSynchronize(st));
+    for (int k = 0; k < msets; k++) {
+      std::vector<Fr> h(n);
+      NZ_HIP(hipMemcpy(h.data(), scalars[k], n * sizeof(Fr), hipMemcpyDeviceToHost));
+      size_t e_pos = 0, e_min = 0, nneg = 0, zero = 0, hist[17] = {0};
+      const Fr half = neg(Fr::one());  // r - 1; compared as integers below via subtraction
+      for (size_t i = 0; i < n; i++) {
+        Fr v = mdig ? from_mont(h[i]) : h[i];
+        if (v.is_zero()) { zero++; continue; }
+        const Fr w = neg(v);  // r - v
+        auto digits = [&](const Fr& x) {
+          size_t d = 0;
+          for_each_digit_host(x, p.c, [&](int, uint32_t, uint32_t) { d++; });
+          return d;
+        };
+        const size_t dp = digits(v), dn = digits(w);
+        e_pos += dp;
+        e_min += dp <= dn ? dp : dn;
+        if (dn < dp) nneg++;
+        const size_t dm = dp <= dn ? dp : dn;
+        hist[dm < 16 ? dm : 16]++;
+      }
+      (void)half;
+      fprintf(stderr, "MSMSCALARS set=%d n=%zu c=%d zero=%zu entries=%zu entries_minform=%zu flipped=%zu hist_minform=",
+              k, n, p.c, zero, e_pos, e_min, nneg);
+      for (int b = 0; b < 17; b++) fprintf(stderr, "%zu%c", hist[b], b == 16 ? '\n' : ',');
+    }
+  }
+#endif
   if (p.entries > sc.sorted.n || p.nkeys + 1 > sc.offsets.n)
     throw Error(NZCB_ERR_ARG, "msm scratch was not sized for this schedule");
   if (table && ((size_t)p.nb / kTileSide * msets > sc.rowp29.n ||

@@ -44,12 +44,13 @@ EXPORTED_SYMBOLS = [
     "nzcb_proof_to_calldata", "nzcb_vk_to_solidity", "nzcb_engine_lagrange_basis", "nzcb_ctx_set_msm_devices", "nzcb_nzcp_input_signals", "nzcb_nzcp_witness",
     "nzcb_nzcp_witness_dev", "nzcb_synth_setup_ex", "nzcb_memcpy_d2d",
     "nzcb_plonk_setup", "nzcb_prove_batch_status", "nzcb_wprog_remap", "nzcb_prove_logged", "nzcb_memcpy_d2d_async",
-    "nzcb_debug_guard_check", "nzcb_debug_guard_selftest", "nzcb_debug_inject_fault",
+    "nzcb_debug_guard_check", "nzcb_debug_guard_selftest", "nzcb_debug_inject_fault", "nzcb_debug_f29",
     "nzcb_msm_table_create_lagrange",
 ]
 
 NZCB_FAULT_QUOTIENT = 1  # include/nzcb_internal.h
 NZCB_DEBUG_GENERIC_K = 2  # include/nzcb_internal.h
+NZCB_FAULT_LANE_ALLOC = 3  # include/nzcb_internal.h
 
 
 def lagrange_commit_enabled() -> bool:
@@ -71,6 +72,22 @@ def guard_check(device: int = -1) -> int:
     err, checked, bad = _Err(), c_size_t(0), c_int(0)
     _check(load().nzcb_debug_guard_check(device, ctypes.byref(checked), ctypes.byref(bad), ctypes.byref(err)), err)
     return checked.value
+
+
+F29_WORDS = {1: (27, 9), 2: (54, 18), 3: (18, 9), 4: (36, 18), 5: (18, 18), 6: (36, 9)}
+
+
+def f29_check(op: int, words, device: int = 0):
+    """Run csrc/f29.h's device product `op` (include/nzcb_internal.h nzcb_debug_f29) over
+    items of F29_WORDS[op][0] limb words each; returns the flat list of output words."""
+    win, wout = F29_WORDS[op]
+    count = len(words) // win
+    assert count * win == len(words)
+    arr = (c_uint32 * max(1, len(words)))(*words)
+    out = (c_uint32 * max(1, count * wout))()
+    err = _Err()
+    _check(load().nzcb_debug_f29(device, op, arr, count, out, ctypes.byref(err)), err)
+    return list(out)[:count * wout]
 
 
 def guard_selftest(device: int = 0) -> None:
@@ -221,6 +238,7 @@ def load(path: str | None = None):
         "nzcb_debug_guard_check": (c_int, [c_int, POINTER(c_size_t), POINTER(c_int), POINTER(_Err)]),
         "nzcb_debug_guard_selftest": (c_int, [c_int, POINTER(_Err)]),
         "nzcb_debug_inject_fault": (c_int, [c_void_p, c_int]),
+        "nzcb_debug_f29": (c_int, [c_int, c_int, POINTER(c_uint32), c_size_t, POINTER(c_uint32), POINTER(_Err)]),
     }
     lib.missing_symbols = []
     for name, (res, args) in sigs.items():
@@ -654,7 +672,8 @@ class ProverContext:
     def inject_fault(self, kind: int = NZCB_FAULT_QUOTIENT) -> None:
         """The next proof on each lane perturbs its quotient t (NZCB_FAULT_QUOTIENT: tests of
         the xi check) or takes the grand product's generic k1, k2 path (NZCB_DEBUG_GENERIC_K:
-        the same proof); 0 clears it."""
+        the same proof), or the next set_lanes growth fails after one new lane
+        (NZCB_FAULT_LANE_ALLOC: tests of the rollback); 0 clears it."""
         if self.lib.nzcb_debug_inject_fault(self.h, kind) != 0:
             raise ValueError(f"bad fault kind {kind}")
 

@@ -384,3 +384,105 @@ def test_msm_fixed_base_other_windows(window):
                         os.path.abspath(__file__), "-k", "fixed_base and not other_windows"],
                        capture_output=True, text=True, timeout=110, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
+
+
+# --- csrc/f29.h products as the device compiles them -------------------------
+_M29 = (1 << 29) - 1
+_RINV261 = {m: pow(2, -261, m) for m in (P_MOD, R_MOD)}
+
+
+def _l29(x):
+    return [(x >> (29 * i)) & _M29 for i in range(9)]
+
+
+def _v29(ws):
+    return sum(v << (29 * i) for i, v in enumerate(ws))
+
+
+def _wide29(x, rng):
+    """x's limbs with random borrows moved down (limbs above 2^29, below 2^30.7): the
+    unnormalized inputs the NTT passes hand to the Shoup product."""
+    xl = _l29(x)
+    for i in range(8, 0, -1):
+        if xl[i] and rng.random() < 0.5:
+            b = rng.randrange(0, min(xl[i], 3) + 1)
+            xl[i] -= b
+            xl[i - 1] += b << 29
+    return xl if max(xl) < int(2 ** 30.7) else _l29(x)
+
+
+def test_f29_device_products_exact():
+    """Every generated column-asm product of csrc/f29_cols.h on the GPU (nzcb_debug_f29)
+    against exact integers, at and near the bounds the kernels rely on: the Shoup twiddle
+    product (single and paired; x < 99 r < 2^261 with limbs up to 2^30.7, result = x w mod r
+    and < 3 r), the Montgomery products mod q and mod r (inputs < 2 p, result < 2 p), the
+    paired squaring and the two-product sum (inputs < 4 q, result congruent and < 4 q).
+    Output limbs are normalized (< 2^29) except the top one."""
+    import nzcb
+    rng = random.Random(0xF29C)
+    N = 2000
+    R, Q = R_MOD, P_MOD
+    edge = lambda m: [0, 1, m - 1, 2 * m - 1]
+
+    # op 1 / 2: Shoup
+    xs = [99 * R - 1, R - 1, 0] + [rng.randrange(99 * R) for _ in range(N)]
+    ws = [R - 1, R - 1, 5] + [rng.randrange(R) for _ in range(N)]
+    words, items = [], []
+    for x, w in zip(xs, ws):
+        xl = _wide29(x, rng)
+        items.append((x, w))
+        words += xl + _l29(w) + _l29((w << 261) // R)
+    out = nzcb.f29_check(1, words)
+    for i, (x, w) in enumerate(items):
+        g = out[9 * i:9 * i + 9]
+        assert max(g[:8]) <= _M29 and _v29(g) % R == x * w % R and _v29(g) < 3 * R, i
+    pairs = list(zip(items[0::2], items[1::2]))
+    words = []
+    for (x, w), (y, v) in pairs:
+        words += _wide29(x, rng) + _l29(w) + _l29((w << 261) // R) + _wide29(y, rng) + _l29(v) + _l29((v << 261) // R)
+    out = nzcb.f29_check(2, words)
+    for i, ((x, w), (y, v)) in enumerate(pairs):
+        g1, g2 = out[18 * i:18 * i + 9], out[18 * i + 9:18 * i + 18]
+        assert _v29(g1) % R == x * w % R and _v29(g1) < 3 * R, i
+        assert _v29(g2) % R == y * v % R and _v29(g2) < 3 * R, i
+
+    # op 3: mul29<Fq29>, op 4: mul29x2<Fr29>
+    for op, m in ((3, Q), (4, R)):
+        a = edge(m) + [rng.randrange(2 * m) for _ in range(N)]
+        b = edge(m)[::-1] + [rng.randrange(2 * m) for _ in range(N)]
+        k = len(a) // 2 * 2
+        words = []
+        if op == 3:
+            for x, y in zip(a, b):
+                words += _l29(x) + _l29(y)
+        else:
+            for j in range(0, k, 2):
+                words += _l29(a[j]) + _l29(b[j]) + _l29(a[j + 1]) + _l29(b[j + 1])
+        out = nzcb.f29_check(op, words)
+        cnt = len(a) if op == 3 else k
+        for i in range(cnt):
+            g = out[9 * i:9 * i + 9]
+            assert max(g[:8]) <= _M29, (op, i)
+            assert _v29(g) % m == a[i] * b[i] * _RINV261[m] % m and _v29(g) < 2 * m, (op, i)
+
+    # op 5: sqr29x2 (mod q), op 6: mul2sum29 (mod q), inputs < 4 q
+    a = [4 * Q - 1, 0, Q] + [rng.randrange(4 * Q) for _ in range(N)]
+    c = [4 * Q - 1, 1, Q - 1] + [rng.randrange(4 * Q) for _ in range(N)]
+    words = []
+    for x, y in zip(a, c):
+        words += _l29(x) + _l29(y)
+    out = nzcb.f29_check(5, words)
+    for i, (x, y) in enumerate(zip(a, c)):
+        g1, g2 = out[18 * i:18 * i + 9], out[18 * i + 9:18 * i + 18]
+        assert _v29(g1) % Q == x * x * _RINV261[Q] % Q and _v29(g1) < 4 * Q, i
+        assert _v29(g2) % Q == y * y * _RINV261[Q] % Q and _v29(g2) < 4 * Q, i
+    b = [rng.randrange(4 * Q) for _ in a]
+    d = [rng.randrange(4 * Q) for _ in a]
+    words = []
+    for w4 in zip(a, b, c, d):
+        for v in w4:
+            words += _l29(v)
+    out = nzcb.f29_check(6, words)
+    for i, (x, y, z, t) in enumerate(zip(a, b, c, d)):
+        g = out[9 * i:9 * i + 9]
+        assert _v29(g) % Q == (x * y + z * t) * _RINV261[Q] % Q and _v29(g) < 4 * Q, i

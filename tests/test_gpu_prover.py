@@ -420,3 +420,35 @@ def test_serial_profiling_mode_same_proof():
     env = dict(os.environ, NZCB_SERIAL="1")
     p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stdout + p.stderr
+
+
+def test_failed_lane_growth_rolls_back_then_proves():
+    """nzcb_ctx_set_lanes' rollback after a failed growth. NZCB_FAULT_LANE_ALLOC
+    makes the next growth fail after its first new lane with a real failed hipMalloc (HIP's
+    per-thread last error holds the out-of-memory code, as after a real one). The call
+    raises, lanes stays at its old count, and on the same thread the next proofs (one lane,
+    then a batch over the old lanes) are the golden proof bit for bit: the stale error was
+    cleared. A later growth succeeds."""
+    meta, zkey, wtns = _gold("p8")
+    exp = meta["proofs"]["fixed"]
+    bl = bytes.fromhex(exp["blinding"])
+    wit = b"".join(x.to_bytes(32, "little") for x in binfmt.read_wtns(wtns)["witness"])
+    ctx = nzcb.ProverContext(zkey)
+    try:
+        ctx.set_lanes(2)
+        ctx.inject_fault(nzcb.NZCB_FAULT_LANE_ALLOC)
+        with pytest.raises(nzcb.NzcbError) as ei:
+            ctx.set_lanes(4)
+        assert ei.value.name == "HIP" and "injected lane allocation failure" in str(ei.value)
+        assert ctx.lanes == 2
+        proof, _ = ctx.prove_raw(wtns, bl)
+        assert proof.hex() == exp["proof_bin"]
+        res = ctx.prove_batch_raw([wit] * 4, blindings=[bl] * 4)
+        assert all(p.hex() == exp["proof_bin"] for p, _ in res)
+        ctx.set_lanes(4)   # one-shot: the next growth goes through
+        assert ctx.lanes == 4
+        res = ctx.prove_batch_raw([wit] * 4, blindings=[bl] * 4)
+        assert all(p.hex() == exp["proof_bin"] for p, _ in res)
+        assert nzcb.guard_check(0) > 0
+    finally:
+        ctx.close()
