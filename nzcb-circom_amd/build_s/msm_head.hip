@@ -271,20 +271,13 @@ static constexpr int kLoThreads = 512;
 // the (key, value) of every window of scalar i; bit w of the result is set for the
 // windows with a nonzero digit (zero digits make no entry: a scalar of b bits costs about
 // b / C entries, which the Lagrange-basis commitments of small witness values rely on)
-// digit-pass flags (the `mont` argument of the bucketing kernels)
-static constexpr int kDigMont = 1;     // scalars in Montgomery form: convert first
-static constexpr int kDigMinForm = 2;  // bucket min(s, r - s) (scalar_min_form)
-
 // Signed scalars (round 6): s and r - s reach the same point with the base negated (every
 // base has order r), and the fixed-base schedule buckets whichever of the two is smaller, the
 // negation riding in every entry's sign bit. Random scalars lose nothing (their 13 windows stay
 // occupied); the Lagrange-basis A, B, C values, of which 13-29 % are small negatives r - k
 // (15 nonzero 17-bit digits as they stand, one as k), fall from 21.7 M to 4.7 M bucket
-// entries per proof (nzcp_live, profiles/r6_abc_scalars.txt). The prover's folded PTau
-// tables (random scalars: the compare and negation bought nothing and cost 0.05 G VALU
-// instructions per proof) skip it; every unfolded table (Lagrange, split ranges, engine)
-// takes it. Values >= r (never produced) are left as they are. Returns 1 when s was
-// replaced by r - s.
+// entries per proof (nzcp_live, profiles/r6_abc_scalars.txt). Values >= r (never produced)
+// are left as they are. Returns 1 when s was replaced by r - s.
 __device__ __forceinline__ uint32_t scalar_min_form(Fr& s) {
   constexpr uint32_t H[8] = {0xf8000000u, 0xa1f0fac9u, 0x3cdcb848u, 0x9419f424u,
                              0x40c0ac2eu, 0xdc2822dbu, 0x7098d014u, 0x18322739u};  // (r - 1) / 2
@@ -305,8 +298,8 @@ template <int C, int NW>
 __device__ __forceinline__ uint32_t bin_entries(const Fr* __restrict__ scalars, size_t i, int mont, size_t stride,
                                                 uint32_t (&kk)[NW], uint32_t (&vv)[NW]) {
   Fr s = scalars[i];
-  if (mont & kDigMont) s = from_mont_fr29(s);
-  const uint32_t flip = (mont & kDigMinForm) ? scalar_min_form(s) : 0u;
+  if (mont) s = from_mont_fr29(s);
+  const uint32_t flip = scalar_min_form(s);
   uint32_t live = 0;
 #pragma unroll
   for (int w = 0; w < NW; w++) {
@@ -1774,7 +1767,7 @@ static void msm_enqueue_impl(MsmScratch& sc, const G1Affine* bases, const Fr* co
   if (table) {
     BinSets bs{};
     for (int k = 0; k < msets; k++) bs.p[k] = scalars[k];
-    fixed_bucketing(sc, p, bs, n, mdig | (table->mont_folded ? 0 : kDigMinForm), table, st, mark);
+    fixed_bucketing(sc, p, bs, n, mdig, table, st, mark);
   } else {
     keys_dispatch(p.c, scalars[0], n, mdig, sc, st);
     mark(1);
