@@ -147,9 +147,25 @@ def _msm_fixed(engine, pts, sc, n_table=None, mont=False, window=0, sparse=False
         nzcb.dev_free(ds)
 
 
+def _flip_kinds(kind, n, rng):
+    """Scalars for the signed-scalar bucketing (msm.hip scalar_min_form: min(s, r - s) with
+    the base negated): "half" sits on the (r - 1) / 2 boundary on both sides, "negsmall" is
+    the A, B, C regime of small negatives r - k next to small positives and their sums with
+    equal bases' opposite signs in one bucket. None for any other kind."""
+    h = (R_MOD - 1) // 2
+    if kind == "half":
+        return [rng.choice([h, h + 1, h - 1, h + 2, R_MOD - 1, 1, R_MOD - (1 << 16), (1 << 16) + 1,
+                            rng.randrange(h - 1000, h + 1000)]) for _ in range(n)]
+    if kind == "negsmall":
+        return [rng.choice([0, 1, R_MOD - 1, R_MOD - 2, 2, rng.randrange(256), R_MOD - rng.randrange(1, 256),
+                            R_MOD - rng.randrange(1, 1 << 17), rng.randrange(1 << 17),
+                            R_MOD - rng.randrange(1, 1 << 40)]) for _ in range(n)]
+    return None
+
+
 @pytest.mark.parametrize("n,kind", [(1, "rand"), (100, "rand"), (2000, "rand"), (300, "zeros"), (300, "ones"),
                                     (300, "equal"), (300, "rminus1"), (300, "mixed"), (300, "top"),
-                                    (3000, "witness")])
+                                    (3000, "witness"), (600, "half"), (2000, "negsmall")])
 def test_msm_fixed_base(engine, n, kind):
     rng = random.Random(1000 + n + len(kind))
     pts = _bases(n + 5, n + 1)
@@ -171,6 +187,8 @@ def test_msm_fixed_base(engine, n, kind):
         sc = [rng.choice([1 << 253, (1 << 240) - 1, (1 << 239) * 3, (1 << 19) * 5, R_MOD - (1 << 19)])
               for _ in range(n)]
     else:
+        sc = _flip_kinds(kind, n, rng)
+    if sc is None:
         sc = [rng.choice([0, 1, R_MOD - 1, rng.randrange(R_MOD)]) for _ in range(n)]
     want = bn.msm(pts[:n], sc)
     # table built over more bases than the MSM uses (as the prover's n+6 PTau table)
@@ -180,7 +198,7 @@ def test_msm_fixed_base(engine, n, kind):
 
 @pytest.mark.parametrize("n,kind", [(1, "rand"), (300, "rand"), (300, "zeros"), (3000, "ones"), (1500, "equal"),
                                     (300, "rminus1"), (300, "top"), (3000, "witness"), (5000, "equal"),
-                                    (2000, "mixed"), (16, "equal")])
+                                    (2000, "mixed"), (16, "equal"), (600, "half"), (3000, "negsmall")])
 def test_msm_sparse_schedule(engine, n, kind):
     """The Lagrange table's schedule (round 6, msm.hip dyn_chunk): window 17, the accumulation
     chunk derived on the device from the entry count (8 entries here), runs of more than four
@@ -204,6 +222,8 @@ def test_msm_sparse_schedule(engine, n, kind):
         sc = [rng.choice([0, 0, 1, 1, 1, R_MOD - 1, rng.randrange(256), rng.randrange(1 << 17),
                           rng.randrange(R_MOD)]) for _ in range(n)]
     else:
+        sc = _flip_kinds(kind, n, rng)
+    if sc is None:
         sc = [rng.choice([0, 1, 2, R_MOD - 1, rng.randrange(R_MOD)]) for _ in range(n)]
     want = bn.msm(pts[:n], sc)
     assert _msm_fixed(engine, pts, sc, n_table=n + 2, window=17, sparse=True) == want
@@ -212,7 +232,8 @@ def test_msm_sparse_schedule(engine, n, kind):
 
 @pytest.mark.parametrize("n,kinds", [(1, ("rand", "ones", "zeros")), (300, ("witness", "equal", "rand")),
                                      (3000, ("ones", "witness", "mixed")), (1500, ("equal", "equal", "ones")),
-                                     (700, ("zeros", "zeros", "witness")), (2000, ("witness", "rand"))])
+                                     (700, ("zeros", "zeros", "witness")), (2000, ("witness", "rand")),
+                                     (1200, ("negsmall", "half", "negsmall"))])
 def test_msm_sets_schedule(engine, n, kinds):
     """msm_enqueue_sets (round 6: the prover's A, B, C in one schedule over the Lagrange table):
     each set's result equals its own MSM (oracle), for sets whose buckets collide in index
@@ -234,6 +255,8 @@ def test_msm_sets_schedule(engine, n, kinds):
         if kind == "witness":
             return [rng.choice([0, 0, 1, 1, 1, R_MOD - 1, rng.randrange(256), rng.randrange(1 << 17),
                                 rng.randrange(R_MOD)]) for _ in range(n)]
+        if kind in ("half", "negsmall"):
+            return _flip_kinds(kind, n, rng)
         return [rng.choice([0, 1, 2, R_MOD - 1, rng.randrange(R_MOD)]) for _ in range(n)]
 
     sets = [scal(k) for k in kinds]

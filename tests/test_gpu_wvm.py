@@ -127,6 +127,16 @@ def test_nzcp_live_full_prove_real_circuit():
     # rank order; the proof must not change by a bit
     from nzcb import msmsplit
     from tests.test_gpu_split import _LocalRanks
+    # bucket entries of one proof (kernel statistics): six dense MSMs at 13 per scalar plus
+    # A, B, C in the Lagrange basis bucketed as min(s, r - s) (msm.hip scalar_min_form): about
+    # 2.2 n for the three (21.7 M, 10.3 n, before round 6's sign flip)
+    n = ctx.domain_size
+    ctx.set_lanes(1)
+    ctx.kernel_stats(1)
+    assert ctx.prove_witness_raw(wit0, bl)[0] == res[0][0]
+    _, launches, _, entries = ctx.kernel_stats(0)
+    dense = 6 * 13 * (n + 6)
+    assert launches == 7 and dense - n < entries < dense + 3 * n, (launches, entries)
     ranks = _LocalRanks(nzcb, msmsplit, zkey, ctx.domain_size + 6, 8)
     try:
         ctx.set_lanes(1)
