@@ -1725,7 +1725,6 @@ static void msm_enqueue_impl(MsmScratch& sc, const G1Affine* bases, const Fr* co
       std::vector<Fr> h(n);
       NZ_HIP(hipMemcpy(h.data(), scalars[k], n * sizeof(Fr), hipMemcpyDeviceToHost));
       size_t e_pos = 0, e_min = 0, nneg = 0, zero = 0, hist[17] = {0};
-      const Fr half = neg(Fr::one());  // r - 1; compared as integers below via subtraction
       for (size_t i = 0; i < n; i++) {
         Fr v = mdig ? from_mont(h[i]) : h[i];
         if (v.is_zero()) { zero++; continue; }
@@ -1742,7 +1741,6 @@ static void msm_enqueue_impl(MsmScratch& sc, const G1Affine* bases, const Fr* co
         const size_t dm = dp <= dn ? dp : dn;
         hist[dm < 16 ? dm : 16]++;
       }
-      (void)half;
       fprintf(stderr, "MSMSCALARS set=%d n=%zu c=%d zero=%zu entries=%zu entries_minform=%zu flipped=%zu hist_minform=",
               k, n, p.c, zero, e_pos, e_min, nneg);
       for (int b = 0; b < 17; b++) fprintf(stderr, "%zu%c", hist[b], b == 16 ? '\n' : ',');
