@@ -31,9 +31,13 @@ def test_field_mul(engine, field_q):
     assert out == [x * y % mod for x, y in zip(a, b)]
 
 
-@pytest.mark.parametrize("log_n", [0, 1, 3, 5, 8, 9, 11, 12, 13])
+@pytest.mark.parametrize("log_n", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
 @pytest.mark.parametrize("inverse", [False, True])
 def test_ntt(engine, log_n, inverse):
+    """Against the oracle's FFT. 2^0..2^8 are one pass of log n stages, 2^9..2^14 a pass of 8
+    and one of 1..6 (7 at 2^23, test_ntt_full_size_properties): every stage plan of the pass
+    kernel (radix-8 groups of 3, radix-4 pairs, a single radix-2 stage; ntt.hip) runs, in the
+    first pass and in a later one."""
     rng = random.Random(log_n * 2 + inverse)
     n = 1 << log_n
     a = [rng.randrange(R_MOD) for _ in range(n)]
