@@ -116,6 +116,7 @@ struct Prover {
   static constexpr int kMbFlags = 24, kMbTotals = 25, kMbEvals = 27, kMbEvalMax = 8;
   size_t mb_apub = 0, mb_pubw = 0, mb_words = 0;
 
+  int lane_id = 0;  // lane index on its device (the "lane k" trace mark of each proof)
   int fault = 0;  // nzcb_debug_inject_fault: NZCB_FAULT_* / NZCB_DEBUG_* for this lane's next proof
   // timings of the last proof (ms): [0..6] host wall clock of the whole proof and its
   // phases, [7] host time in the MSM calls (enqueue + waiting for results), [8] host time

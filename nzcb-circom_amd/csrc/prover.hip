@@ -1416,8 +1416,9 @@ void Prover::alloc_workspace() {
 // An extra proof lane on the primary's device: shares the HBM-resident proving key
 // (zkey sections, shifted PTau table, coset evaluations, root tables) read-only and
 // owns its streams, MSM scratch and per-proof working set.
-Prover::Prover(const Prover& pk, int) {
+Prover::Prover(const Prover& pk, int lane) {
   GuardScope guards;  // the lane's working set, MSM and NTT scratch (common.h)
+  lane_id = lane;
   n = pk.n; n4 = pk.n4; nVars = pk.nVars; nPublic = pk.nPublic; nAdditions = pk.nAdditions;
   nConstraints = pk.nConstraints; nWit = pk.nWit; power = pk.power;
   k1 = pk.k1; k2 = pk.k2; wn = pk.wn; w2 = pk.w2;
@@ -1896,6 +1897,12 @@ void Prover::prove(const uint8_t* witness, size_t n_witness, const uint8_t* blin
   // a previous proof that failed in round 2 may have left the side stream's NTTs running
   // on this lane's buffers (blind, A, B, C)
   if (side_done) NZ_HIP(hipEventSynchronize(side_done));
+  // which lane proves (rocprofv3 --marker-trace; tools/lane_speeds.py: lanes differ in speed by
+  // the hardware queues their streams landed on, profiles/r6_drain_queues.txt)
+  static const char* kLaneMark[17] = {"lane 0", "lane 1", "lane 2", "lane 3", "lane 4", "lane 5", "lane 6", "lane 7",
+                                      "lane 8", "lane 9", "lane 10", "lane 11", "lane 12", "lane 13", "lane 14",
+                                      "lane 15", "lane 16"};
+  roctxMarkA(kLaneMark[lane_id < 16 ? lane_id : 16]);
   RoctxPhases ranges("plonk_prove");
   ranges.next("witness: calculateAdditions + buildABC");
   auto T0 = std::chrono::steady_clock::now();
